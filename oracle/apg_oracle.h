@@ -1,0 +1,78 @@
+/*
+ * apg_oracle.h — CPU restatement of the ap_gym LIDAR hot path (TEST INFRASTRUCTURE ONLY).
+ *
+ * This library is the parity oracle and the bench's `cpu_baseline` ("port").  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.  The product path
+ * (active-perception-gym_amd/) never links, loads or calls it.
+ *
+ * Pinning:
+ *   - numpy RNG restatement: pinned against numpy 2.2.6 run in the build container
+ *     (tests/golden/rng_*.npz).
+ *   - floor-map generators: pinned against the reference's own generators imported from
+ *     /root/reference (tests/golden/maps_*.npz).
+ *   - LIDAR step/reset/obs/loss control flow: pinned against the reference's
+ *     LIDARLocalization2DEnv run with an exact-rational GEOS model (tests/golden/lidar_*.npz).
+ *   - The GEOS line∩polygon semantics themselves: PARITY UNPINNED (shapely is absent).
+ */
+#ifndef APG_ORACLE_H
+#define APG_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* numpy Generator(PCG64(SeedSequence(seed))) state (numpy/random/src/pcg64). */
+typedef struct {
+  uint64_t state_hi, state_lo, inc_hi, inc_lo;
+  uint32_t has_uint32, uinteger;
+} orc_pcg64;
+
+void orc_seed(uint64_t seed, orc_pcg64 *s);
+uint64_t orc_next64(orc_pcg64 *s);
+uint32_t orc_next32(orc_pcg64 *s);
+double orc_next_double(orc_pcg64 *s);
+/* Generator.integers(lo, hi) with hi exclusive (int64 path, Lemire, not masked). */
+int64_t orc_integers(orc_pcg64 *s, int64_t lo, int64_t hi_excl);
+/* Generator.integers(0, 2**32, endpoint=True)  (inclusive range 2**32, Lemire64). */
+uint64_t orc_integers_u32_endpoint(orc_pcg64 *s);
+uint64_t orc_random_interval(orc_pcg64 *s, uint64_t max);
+int64_t orc_binomial(orc_pcg64 *s, int64_t n, double p);
+double orc_uniform(orc_pcg64 *s, double lo, double hi);
+
+/* Test helpers: a single call draws `n` values of a kind from default_rng(seed). */
+void orc_test_draws(uint64_t seed, int kind, int64_t a, int64_t b, double p, int n, double *out);
+
+/* FloorMapDatasetRooms.get_data_point / FloorMapDatasetMaze.get_data_point; out is bool[h][w]. */
+int orc_rooms_map(uint64_t idx, int h, int w, int max_rooms, int door_width, uint8_t *out);
+int orc_maze_map(uint64_t idx, int h, int w, double branching_prob, uint8_t *out);
+
+/* Exact LIDAR scan of one segment p->q against the closed union of occupied unit cells.
+ * Returns the f32 distance exactly as lidar_localization2d.py:496-536 computes it; *kind receives
+ * the GEOS result type (ORC_EMPTY .. ORC_COLLECTION). */
+enum { ORC_EMPTY = 0, ORC_LINESTRING = 1, ORC_MULTILINESTRING = 2, ORC_POINT = 3,
+       ORC_MULTIPOINT = 4, ORC_COLLECTION = 5 };
+float orc_lidar_scan(const uint8_t *map, int h, int w, float px, float py, float qx, float qy,
+                     int *kind);
+
+/* Vectorised LIDAR env (SyncVectorEnv of TimeLimit(LIDARLocalization2DEnv) restated). */
+typedef struct orc_lidar_env orc_lidar_env;
+orc_lidar_env *orc_lidar_create(int num_envs, int map_kind /*0 rooms, 1 maze*/, int h, int w,
+                                int static_map, int static_map_index, int beams, float lidar_range,
+                                int step_limit, const float *beam_dirs /*[beams][2], scaled*/);
+void orc_lidar_destroy(orc_lidar_env *e);
+/* reset(seed=seed): sub-env i seeded with seed+i. Writes obs. */
+void orc_lidar_reset(orc_lidar_env *e, uint64_t seed, float *lidar, float *odometry,
+                     float *time_step, float *map_obs /*may be NULL*/, uint64_t *map_idx);
+/* step: NEXT_STEP autoreset semantics; returns nonzero error bits (1 NaN action, 2 NaN pred). */
+int orc_lidar_step(orc_lidar_env *e, const float *action, const float *prediction, float *lidar,
+                   float *odometry, float *time_step, float *map_obs, double *reward,
+                   uint8_t *terminated, uint8_t *truncated, float *base_reward, float *target,
+                   float *loss, uint8_t *info_mask, uint64_t *map_idx);
+void orc_lidar_get_state(const orc_lidar_env *e, float *pos, float *init_pos, int32_t *elapsed,
+                         uint8_t *autoreset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

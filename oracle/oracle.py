@@ -1,0 +1,134 @@
+"""ctypes binding of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the
+checker / CPU baseline.  The product package never imports this module.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    srcs = [os.path.join(HERE, f) for f in ("apg_oracle_rng_maps.c", "apg_oracle_lidar.c", "apg_oracle.h")]
+    if force or not os.path.exists(LIB_PATH) or any(os.path.getmtime(s) > os.path.getmtime(LIB_PATH) for s in srcs):
+        subprocess.run(["make", "-s", "-C", HERE, "-B" if force else "liboracle.so"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, u64, f32, f64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_float, ctypes.c_double
+        L.orc_test_draws.argtypes = [u64, i32, ctypes.c_int64, ctypes.c_int64, f64, i32, vp]
+        L.orc_rooms_map.argtypes = [u64, i32, i32, i32, i32, vp]
+        L.orc_maze_map.argtypes = [u64, i32, i32, f64, vp]
+        L.orc_lidar_scan.restype = f32
+        L.orc_lidar_scan.argtypes = [vp, i32, i32, f32, f32, f32, f32, ctypes.POINTER(i32)]
+        L.orc_lidar_create.restype = vp
+        L.orc_lidar_create.argtypes = [i32, i32, i32, i32, i32, i32, i32, f32, i32, vp]
+        L.orc_lidar_destroy.argtypes = [vp]
+        L.orc_lidar_reset.argtypes = [vp, u64, vp, vp, vp, vp, vp]
+        L.orc_lidar_step.restype = i32
+        L.orc_lidar_step.argtypes = [vp] + [vp] * 14
+        L.orc_lidar_get_state.argtypes = [vp, vp, vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def rooms_map(idx: int, size: int) -> np.ndarray:
+    out = np.zeros((size, size), np.uint8)
+    if lib().orc_rooms_map(idx, size, size, 10, 3, _p(out)) != 0:
+        raise ValueError("rooms map must be square")
+    return out
+
+
+def maze_map(idx: int, h: int, w: int | None = None, branching_prob: float = 1.0) -> np.ndarray:
+    w = h if w is None else w
+    out = np.zeros((h, w), np.uint8)
+    if lib().orc_maze_map(idx, h, w, branching_prob, _p(out)) != 0:
+        raise ValueError("Width and height must be odd.")
+    return out
+
+
+def lidar_scan(occ: np.ndarray, p, q):
+    occ = np.ascontiguousarray(occ, dtype=np.uint8)
+    k = ctypes.c_int()
+    d = lib().orc_lidar_scan(_p(occ), occ.shape[0], occ.shape[1], float(p[0]), float(p[1]), float(q[0]),
+                             float(q[1]), ctypes.byref(k))
+    return np.float32(d), k.value
+
+
+def beam_directions(beams: int, lidar_range: float = 5) -> np.ndarray:
+    """lidar_localization2d.py:181-187, evaluated by numpy exactly like the reference."""
+    ang = np.linspace(-np.pi, np.pi, beams, dtype=np.float32, endpoint=False)
+    return np.ascontiguousarray(np.stack([np.cos(ang), np.sin(ang)], axis=-1) * lidar_range, dtype=np.float32)
+
+
+class OracleLidarVectorEnv:
+    """SyncVectorEnv(TimeLimit(LIDARLocalization2DEnv)) restated in C; numpy in/out."""
+
+    def __init__(self, num_envs, map_kind="rooms", size=32, static_map=False, static_map_index=0, beams=8,
+                 lidar_range=5, step_limit=100):
+        self.n, self.h, self.w, self.beams = num_envs, size, size, beams
+        self.static = static_map
+        self.dirs = beam_directions(beams, lidar_range)
+        self._e = lib().orc_lidar_create(num_envs, 0 if map_kind == "rooms" else 1, size, size, int(static_map),
+                                         static_map_index, beams, float(lidar_range), step_limit, _p(self.dirs))
+        if not self._e:
+            raise ValueError("invalid map configuration")
+        n = num_envs
+        self.lidar = np.zeros((n, beams), np.float32)
+        self.odometry = np.zeros((n, 2), np.float32)
+        self.time_step = np.zeros(n, np.float32)
+        self.map = None if static_map else np.zeros((n, size, size), np.float32)
+        self.map_idx = np.zeros(n, np.uint64)
+        self.reward = np.zeros(n, np.float64)
+        self.terminated = np.zeros(n, np.uint8)
+        self.truncated = np.zeros(n, np.uint8)
+        self.base_reward = np.zeros(n, np.float32)
+        self.target = np.zeros((n, 2), np.float32)
+        self.loss = np.zeros(n, np.float32)
+        self.info_mask = np.zeros(n, np.uint8)
+
+    def close(self):
+        if self._e:
+            lib().orc_lidar_destroy(self._e)
+            self._e = None
+
+    __del__ = close
+
+    def reset(self, seed: int):
+        lib().orc_lidar_reset(self._e, seed, _p(self.lidar), _p(self.odometry), _p(self.time_step), _p(self.map),
+                              _p(self.map_idx))
+
+    def step(self, action, prediction) -> int:
+        a = np.ascontiguousarray(action, np.float32)
+        p = np.ascontiguousarray(prediction, np.float32)
+        return lib().orc_lidar_step(self._e, _p(a), _p(p), _p(self.lidar), _p(self.odometry), _p(self.time_step),
+                                    _p(self.map), _p(self.reward), _p(self.terminated), _p(self.truncated),
+                                    _p(self.base_reward), _p(self.target), _p(self.loss), _p(self.info_mask),
+                                    _p(self.map_idx))
+
+    def state(self):
+        n = self.n
+        pos, ipos = np.zeros((n, 2), np.float32), np.zeros((n, 2), np.float32)
+        el, ar = np.zeros(n, np.int32), np.zeros(n, np.uint8)
+        lib().orc_lidar_get_state(self._e, _p(pos), _p(ipos), _p(el), _p(ar))
+        return dict(pos=pos, init_pos=ipos, elapsed=el, autoreset=ar)

@@ -1,0 +1,256 @@
+"""Generate the golden fixtures under tests/golden/ from the reference (build container only).
+
+    python tests/golden/make_golden.py            # all sections
+    python tests/golden/make_golden.py maps lidar # some sections
+
+Sources of truth, per fixture:
+  rng.npz          numpy 2.2.6 Generator(PCG64(SeedSequence)) itself.
+  maps.npz         the reference's FloorMapDatasetRooms / FloorMapDatasetMaze (numpy only, run as-is).
+  loss.npz         the reference's MSELossFn / CrossEntropyLossFn (normalized as the envs build them).
+  lidar_scan.npz   the reference's LIDARLocalization2DEnv.__lidar_scan (lidar_localization2d.py:496-536)
+                   with tests/golden/_stubs/shapely (exact-rational GEOS model) in place of shapely.
+  lidar_env_*.npz  the reference's LIDARLocalization2DEnv wrapped exactly as registration.py:319-356
+                   composes it (TimeLimit(100, issue_termination=True) + ActiveRegressionLogWrapper),
+                   vectorised by the gymnasium SyncVectorEnv restatement in tests/golden/_stubs.
+The fixtures hold data only (inputs and expected outputs).  See DESIGN.md §Oracle for what each pins.
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import refload  # noqa: E402
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+# --------------------------------------------------------------------------- rng
+def make_rng():
+    seeds = np.array(list(range(64)) + [2**32 - 1, 2**32, 2**40 + 7, 2**63 + 5, 2**64 - 1], dtype=np.uint64)
+    raw = np.stack([np.random.default_rng(int(s)).bit_generator.random_raw(16) for s in seeds])
+    u32e = np.stack([[np.random.default_rng(int(s)).integers(0, 2**32, endpoint=True)] for s in seeds])
+    his = np.array([2, 3, 7, 10, 61, 1000, 4096, 2**31 + 5, 2**32 - 1, 2**32], dtype=np.int64)
+    ints = np.zeros((len(seeds), len(his), 8), np.int64)
+    for i, s in enumerate(seeds):
+        for j, hi in enumerate(his):
+            g = np.random.default_rng(int(s))
+            ints[i, j] = [g.integers(0, int(hi)) for _ in range(8)]
+    binom = np.zeros((len(seeds), 9, 8), np.int64)
+    for i, s in enumerate(seeds):
+        for n in range(9):
+            g = np.random.default_rng(int(s))
+            binom[i, n] = [g.binomial(n, 0.3) for _ in range(8)]
+    unif = np.stack([np.random.default_rng(int(s)).uniform(-1, 1, 8) for s in seeds])
+    rand = np.stack([np.random.default_rng(int(s)).random(8) for s in seeds])
+    perm = np.stack([np.random.default_rng(int(s)).permutation(4) for s in seeds])
+    save("rng.npz", seeds=seeds, raw=raw, u32_endpoint=u32e, his=his, ints=ints, binom=binom,
+         uniform=unif, random=rand, perm4=perm)
+
+
+# --------------------------------------------------------------------------- maps
+def make_maps():
+    fm = refload.load("envs.floor_map")
+    out = {}
+    for m, n in ((32, 64), (64, 32), (16, 16)):
+        ds = fm.FloorMapDatasetRooms(m, m)
+        idx = np.array(list(range(n - 3)) + [123456789, 2**32 - 1, 4000000000], dtype=np.uint64)
+        out[f"rooms{m}_idx"] = idx
+        out[f"rooms{m}_bits"] = np.packbits(np.stack([ds.get_data_point(int(i)) for i in idx]), axis=-1)
+    for m, n in ((21, 32), (63, 4), (127, 3)):
+        ds = fm.FloorMapDatasetMaze(m, m)
+        idx = np.array(list(range(n - 1)) + [2**32 - 1], dtype=np.uint64)
+        out[f"maze{m}_idx"] = idx
+        out[f"maze{m}_bits"] = np.packbits(np.stack([ds.get_data_point(int(i)) for i in idx]), axis=-1)
+    save("maps.npz", **out)
+
+
+# --------------------------------------------------------------------------- loss
+def make_loss():
+    refload.load_core()
+    lf = refload.load("loss_fn")
+    are = refload.load("active_regression_env")
+    rng = np.random.default_rng(5)
+    mse, _ = are._make_mse_loss_fn_and_target_space(2, -1, 1, None)
+    pred = rng.uniform(-1.5, 1.5, (512, 2)).astype(np.float32)
+    tgt = rng.uniform(-1, 1, (512, 2)).astype(np.float32)
+    mse_out = np.stack([mse(p, t, ()) for p, t in zip(pred, tgt)])
+    out = dict(mse_pred=pred, mse_target=tgt, mse_loss=mse_out)
+    for k in (10, 200):
+        ce = lf.CrossEntropyLossFn(k).normalized
+        logits = rng.standard_normal((256, k)).astype(np.float32) * 3
+        labels = rng.integers(0, k, 256).astype(np.int32)
+        out[f"ce{k}_logits"] = logits
+        out[f"ce{k}_labels"] = labels
+        out[f"ce{k}_loss"] = np.asarray(ce(logits, labels, (256,)))
+    save("loss.npz", **out)
+
+
+# --------------------------------------------------------------------------- lidar
+def _lidar_module():
+    refload.load_core()
+    return refload.load("envs.lidar_localization2d")
+
+
+def make_lidar_scan():
+    lmod = _lidar_module()
+    fm = refload.load("envs.floor_map")
+    Env = lmod.LIDARLocalization2DEnv
+    rng = np.random.default_rng(11)
+    maps, segs, dist = [], [], []
+    ds = fm.FloorMapDatasetRooms(32, 32)
+    env = Env(dataset=ds, static_map=True, lidar_beam_count=8, prefetch=False)
+    scan = env._LIDARLocalization2DEnv__lidar_scan
+    set_map = env._LIDARLocalization2DEnv__set_map
+    map_sources = [fm.FloorMapDatasetRooms(32, 32).get_data_point(i) for i in (0, 1, 2)]
+    # a hand-made map with pinch points (diagonal touches), a 1-cell hole and isolated cells
+    hand = np.zeros((32, 32), bool)
+    hand[0, :] = hand[-1, :] = hand[:, 0] = hand[:, -1] = True
+    hand[10, 10] = hand[11, 11] = hand[12, 10] = True
+    hand[20:23, 20:23] = True
+    hand[21, 21] = False
+    hand[5, 5] = hand[6, 7] = hand[5, 9] = hand[15:17, 3:5] = True
+    map_sources.append(hand)
+    for mi, m in enumerate(map_sources):
+        set_map(m, mi)
+        free = np.argwhere(~m)
+        for k in range(700):
+            cy, cx = free[rng.integers(len(free))]
+            mode = k % 7
+            if mode == 0:  # cell centre, beam directions like the env (incl. exact diagonals)
+                p = np.array([cx, cy], np.float32) + 0.5
+                ang = np.linspace(-np.pi, np.pi, 8, dtype=np.float32, endpoint=False)
+                d = np.stack([np.cos(ang), np.sin(ang)], -1) * 5
+                q = p + d[k % 8]
+            elif mode == 1:  # lattice / half-lattice start, axis or diagonal direction
+                p = (np.array([cx, cy], np.float32) + rng.integers(0, 3, 2).astype(np.float32) * 0.5)
+                d = np.array([[1, 0], [0, 1], [-1, 0], [0, -1], [1, 1], [-1, 1], [1, -1], [-1, -1],
+                              [2, 1], [1, -2]], np.float32)[rng.integers(10)]
+                q = p + d * np.float32(rng.integers(1, 6))
+            elif mode == 2:  # short moves (<= 1) from generic positions
+                p = np.array([cx, cy], np.float32) + rng.uniform(0, 1, 2).astype(np.float32)
+                q = p + rng.uniform(-1, 1, 2).astype(np.float32)
+            elif mode == 3:  # start exactly on a wall boundary line
+                p = np.array([cx + rng.integers(0, 2), cy + rng.uniform(0, 1)], np.float32)
+                q = p + rng.uniform(-5, 5, 2).astype(np.float32)
+            elif mode == 4:  # integer endpoints (corner-to-corner)
+                p = np.array([cx, cy], np.float32) + rng.integers(0, 2, 2).astype(np.float32)
+                q = p + rng.integers(-5, 6, 2).astype(np.float32)
+            else:  # generic beams of length 5
+                p = np.array([cx, cy], np.float32) + rng.uniform(0, 1, 2).astype(np.float32)
+                a = rng.uniform(-np.pi, np.pi)
+                q = p + (np.array([np.cos(a), np.sin(a)]) * 5).astype(np.float32)
+            p = p.astype(np.float32)
+            q = q.astype(np.float32)
+            if np.array_equal(p, q):
+                continue
+            dd, _ = scan(p, q[None])
+            maps.append(mi)
+            segs.append(np.concatenate([p, q]))
+            dist.append(dd[0])
+    save("lidar_scan.npz", maps=np.packbits(np.stack(map_sources), axis=-1), map_hw=np.array([32, 32]),
+         map_index=np.array(maps, np.int32), segments=np.stack(segs).astype(np.float32),
+         distance=np.array(dist, np.float32))
+
+
+def run_lidar_env(name, dataset, static, beams, n_envs, steps, seed, action_mode):
+    lmod = _lidar_module()
+    gym = sys.modules["gymnasium"]
+    ap = sys.modules["ap_gym"]
+
+    def mk():
+        env = lmod.LIDARLocalization2DEnv(dataset=dataset, static_map=static, lidar_beam_count=beams,
+                                          prefetch=False)
+        env = ap.TimeLimit(env, max_episode_steps=100, issue_termination=True)
+        return ap.ActiveRegressionLogWrapper(env)
+
+    venv = gym.vector.SyncVectorEnv([mk for _ in range(n_envs)])
+    obs, info = venv.reset(seed=seed)
+    arng = np.random.default_rng(1)
+    if action_mode == "uniform":
+        actions = arng.uniform(-1, 1, (steps, n_envs, 2)).astype(np.float32)
+    elif action_mode == "wide":
+        actions = arng.uniform(-2.5, 2.5, (steps, n_envs, 2)).astype(np.float32)
+    else:  # "grid": axis/diagonal half-steps keep positions on lattice and half-lattice lines
+        choices = np.array([[0.5, 0], [-0.5, 0], [0, 0.5], [0, -0.5], [0.5, 0.5], [-0.5, 0.5], [0.5, -0.5],
+                            [-0.5, -0.5], [1, 0], [0, -1], [0, 0]], np.float32)
+        actions = choices[arng.integers(0, len(choices), (steps, n_envs))]
+    preds = arng.uniform(-1, 1, (steps, n_envs, 2)).astype(np.float32)
+    rec = {k: [] for k in ("lidar", "odometry", "time_step", "map", "reward", "terminated", "truncated",
+                           "base_reward", "target", "loss", "info_mask")}
+    reset_obs = obs
+    reset_map_idx = np.asarray(info["map_idx"], dtype=np.int64)
+    for t in range(steps):
+        obs, rew, term, trunc, info = venv.step({"action": actions[t], "prediction": preds[t]})
+        rec["lidar"].append(obs["lidar"])
+        rec["odometry"].append(obs["odometry"])
+        rec["time_step"].append(obs["time_step"])
+        if "map" in obs:
+            rec["map"].append(np.packbits(obs["map"][..., 0] > 0, axis=-1))
+        rec["reward"].append(rew)
+        rec["terminated"].append(term)
+        rec["truncated"].append(trunc)
+        mask = info.get("_base_reward", np.zeros(n_envs, bool))
+        rec["info_mask"].append(mask)
+        rec["base_reward"].append(np.where(mask, info.get("base_reward", np.zeros(n_envs, np.float32)), 0))
+        rec["target"].append(np.where(mask[:, None], info["prediction"]["target"] if "prediction" in info
+                                      else np.zeros((n_envs, 2), np.float32), 0).astype(np.float32))
+        rec["loss"].append(np.where(mask, info["prediction"]["loss"] if "prediction" in info
+                                    else np.zeros(n_envs, np.float32), 0).astype(np.float32))
+    arrays = {k: np.stack(v) for k, v in rec.items() if v}
+    arrays["reward_dtype"] = np.array(str(rew.dtype))
+    arrays["base_reward_dtype"] = np.array(str(np.asarray(info.get("base_reward", np.zeros(1, np.float32))).dtype))
+    arrays["lidar_dtype"] = np.array(str(obs["lidar"].dtype))
+    save(f"lidar_env_{name}.npz", actions=actions, predictions=preds, seed=np.array(seed),
+         reset_lidar=reset_obs["lidar"], reset_odometry=reset_obs["odometry"],
+         reset_time_step=reset_obs["time_step"], reset_map_idx=reset_map_idx,
+         reset_map=(np.packbits(reset_obs["map"][..., 0] > 0, axis=-1) if "map" in reset_obs
+                    else np.zeros(0, np.uint8)), **arrays)
+
+
+def make_lidar_env():
+    fm = refload.load("envs.floor_map")
+    run_lidar_env("rooms_static_b16", fm.FloorMapDatasetRooms(), True, 16, 16, 210, 0, "uniform")
+    run_lidar_env("rooms_static_b8_grid", fm.FloorMapDatasetRooms(), True, 8, 16, 120, 3, "grid")
+    run_lidar_env("rooms64_b32", fm.FloorMapDatasetRooms(64, 64), False, 32, 6, 110, 0, "wide")
+    run_lidar_env("maze21_b8", fm.FloorMapDatasetMaze(), False, 8, 8, 110, 7, "uniform")
+    run_lidar_env("maze21_b8_grid", fm.FloorMapDatasetMaze(), False, 8, 8, 60, 9, "grid")
+    run_lidar_env("maze127_b64", fm.FloorMapDatasetMaze(127, 127), False, 64, 2, 25, 0, "uniform")
+
+
+SECTIONS = {"rng": make_rng, "maps": make_maps, "loss": make_loss, "scan": make_lidar_scan,
+            "lidar": make_lidar_env}
+
+
+def main(argv):
+    sys.setrecursionlimit(200000)
+    threading.stack_size(1024 * 1024 * 1024)
+    names = argv or list(SECTIONS)
+    err = []
+
+    def run():
+        try:
+            for n in names:
+                SECTIONS[n]()
+        except BaseException as e:  # noqa: BLE001
+            err.append(e)
+            raise
+
+    th = threading.Thread(target=run)
+    th.start()
+    th.join()
+    if err:
+        raise SystemExit(1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
