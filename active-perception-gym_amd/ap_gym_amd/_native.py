@@ -1,0 +1,120 @@
+"""ctypes binding of the gfx950 C ABI (include/apgym_capi.h) in _lib/libapgym_hip.so.
+
+The library is the ONLY compute path of this package: there is no CPU fallback.  `lib()` raises
+NativeLibraryError when the shared object is missing or cannot be loaded, and every op calls it.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_HERE, "_lib")
+LIB_PATH = os.path.join(LIB_DIR, "libapgym_hip.so")
+
+APG_OK = 0
+APG_ERR_NAN_ACTION = 1
+APG_ERR_NAN_PREDICTION = 2
+APG_ERR_MAPGEN = 4
+APG_MAP_ROOMS = 0
+APG_MAP_MAZE = 1
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class ApgError(RuntimeError):
+    pass
+
+
+_vp = ctypes.c_void_p
+
+
+class Pcg64(ctypes.Structure):
+    _fields_ = [("state_hi", ctypes.c_uint64), ("state_lo", ctypes.c_uint64), ("inc_hi", ctypes.c_uint64),
+                ("inc_lo", ctypes.c_uint64), ("has_uint32", ctypes.c_uint32), ("uinteger", ctypes.c_uint32)]
+
+
+class LidarConfig(ctypes.Structure):
+    _fields_ = [("num_envs", ctypes.c_int32), ("height", ctypes.c_int32), ("width", ctypes.c_int32),
+                ("map_kind", ctypes.c_int32), ("is_static", ctypes.c_int32), ("static_map_index", ctypes.c_int32),
+                ("beams", ctypes.c_int32), ("step_limit", ctypes.c_int32), ("max_rooms", ctypes.c_int32),
+                ("door_width", ctypes.c_int32), ("lidar_range", ctypes.c_float), ("loss_scale", ctypes.c_float),
+                ("loss_offset", ctypes.c_float), ("branching_prob", ctypes.c_double)]
+
+
+class LidarState(ctypes.Structure):
+    _fields_ = [(n, _vp) for n in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng", "occ", "scratch", "stack",
+                                   "map_idx", "beam_dirs")]
+
+
+class LidarOutputs(ctypes.Structure):
+    _fields_ = [(n, _vp) for n in ("lidar", "odometry", "time_step", "map_obs", "reward", "terminated", "truncated",
+                                   "base_reward", "target", "loss", "info_mask", "map_idx", "err")]
+
+
+class LidarSizes(ctypes.Structure):
+    _fields_ = [("occ_bytes", ctypes.c_size_t), ("scratch_bytes", ctypes.c_size_t),
+                ("stack_bytes", ctypes.c_size_t), ("wpr", ctypes.c_int32), ("maze_frames", ctypes.c_int32)]
+
+
+# (name, restype, argtypes) for every symbol declared in include/apgym_capi.h
+SYMBOLS = [
+    ("apg_version", ctypes.c_char_p, []),
+    ("apg_last_error", ctypes.c_char_p, []),
+    ("apg_lidar_query_sizes", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(LidarSizes)]),
+    ("apg_lidar_init", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(LidarState), _vp]),
+    ("apg_lidar_reset", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(LidarState), ctypes.c_uint64,
+                                       ctypes.c_int, ctypes.POINTER(LidarOutputs), _vp]),
+    ("apg_lidar_step", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(LidarState), _vp, _vp,
+                                      ctypes.POINTER(LidarOutputs), _vp]),
+    ("apg_map_generate", ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp]),
+    ("apg_lidar_scan_batch", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp,
+                                            _vp]),
+    ("apg_rng_draws", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                     _vp, _vp]),
+]
+
+_lib = None
+
+
+def lib():
+    """Load the native library (raises NativeLibraryError if it is absent: no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryError(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(hipcc --offload-arch=gfx950). ap_gym_amd has no CPU fallback.")
+        try:
+            L = ctypes.CDLL(LIB_PATH)
+        except OSError as e:  # pragma: no cover - depends on the ROCm runtime
+            raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        for name, res, args in SYMBOLS:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "apg call") -> None:
+    if rc != APG_OK:
+        msg = lib().apg_last_error().decode(errors="replace")
+        if rc == -1:
+            raise ValueError(f"{what}: {msg}")
+        raise ApgError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,336 @@
+"""LIDARLocalization2DVectorEnv — the LIDARLoc* env ids as one batched GPU environment.
+
+Reference behaviour reproduced (ap_gym 0.5.0): `make_vec("LIDARLoc*-v0", N)` builds gymnasium's
+SyncVectorEnv over N copies of TimeLimit(100, issue_termination=True) ∘ LIDARLocalization2DEnv
+(ap_gym/envs/registration.py:319-356, :753-767).  This class is that whole composition as state in
+HBM plus three kernels per step (include/apgym_capi.h):
+
+  reset(seed=s)   sub-env i seeded with s+i (SyncVectorEnv.reset), map + start cell drawn on device
+  step(action)    NEXT_STEP autoreset: envs done at the previous step return their reset obs with
+                  reward 0 / terminated False / truncated False and no base_reward/prediction info
+  obs             {"lidar": f32[N,B], "odometry": f32[N,2], "map": f32[N,H,W,1] (dynamic maps),
+                   "time_step": f32[N]}
+  reward          float64 (SyncVectorEnv's reward array), base_reward - normalized MSE loss
+  info            {"base_reward", "prediction": {"target", "loss"}, "map_idx"} with `_key` masks
+
+Two I/O modes (constructor `array_backend`), inputs of either type are accepted:
+  "numpy" (default) -> numpy out, host copies and host-side NaN checks, like the reference
+  "torch"           -> torch out on the env's device, no host synchronisation.  Returned tensors
+                       are persistent buffers overwritten by the next step (gymnasium's copy=False
+                       contract); pass copy=True to get fresh tensors.  NaN errors are raised
+                       lazily (at a later step) unless strict_errors=True.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Any
+
+import numpy as np
+
+from . import _native as N
+from .floor_map import FloorMapDataset, FloorMapDatasetMaze, FloorMapDatasetRooms
+from .loss_fn import affine_f32, regression_loss
+from .spaces import ActivePerceptionActionSpace, Box, Dict, ImageSpace, batch_space
+
+NAN_ACTION_MSG = "NaN values detected in action."
+NAN_PREDICTION_MSG = "NaN values detected in prediction."
+
+
+def lidar_beam_directions(beams: int, lidar_range: float) -> np.ndarray:
+    """lidar_localization2d.py:181-187 evaluated with numpy exactly as the reference does."""
+    ang = np.linspace(-np.pi, np.pi, beams, dtype=np.float32, endpoint=False)
+    unscaled = np.stack([np.cos(ang), np.sin(ang)], axis=-1)
+    return np.ascontiguousarray(unscaled * lidar_range, dtype=np.float32)
+
+
+class LIDARLocalization2DVectorEnv:
+    metadata = {"render_modes": ["rgb_array"], "render_fps": 4, "autoreset_mode": "NextStep"}
+
+    def __init__(self, num_envs: int = 1, dataset: FloorMapDataset | None = None, render_mode: str = "rgb_array",
+                 static_map: bool = False, lidar_beam_count: int = 8, lidar_range: float = 5,
+                 static_map_index: int = 0, prefetch: bool = True, prefetch_buffer_size: int = 128,
+                 max_episode_steps: int = 100, device=None, env_offset: int = 0, copy: bool = False,
+                 strict_errors: bool = False, array_backend: str = "numpy"):
+        import torch
+
+        if render_mode not in self.metadata["render_modes"]:
+            raise ValueError(f"Invalid render mode: {render_mode}")
+        if dataset is None:
+            dataset = FloorMapDatasetRooms()
+        self.num_envs = int(num_envs)
+        self.dataset = dataset
+        self.render_mode = render_mode
+        self.static_map = bool(static_map)
+        self.lidar_beam_count = int(lidar_beam_count)
+        self.lidar_range = lidar_range
+        self.max_episode_steps = int(max_episode_steps)
+        self.env_offset = int(env_offset)
+        self.copy = copy
+        self.strict_errors = strict_errors
+        if array_backend not in ("numpy", "torch"):
+            raise ValueError("array_backend must be 'numpy' or 'torch'")
+        self.array_backend = array_backend
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise ValueError("LIDARLocalization2DVectorEnv runs on a GPU device (no CPU fallback)")
+        h, w = dataset.map_height, dataset.map_width
+
+        # ---- spaces (lidar_localization2d.py:144-227, time_limit.py:64-70, active_regression_env.py:55-76)
+        obs = {"lidar": Box(0, 1, (self.lidar_beam_count,), np.float32),
+               "odometry": Box(-1, 1, (2,), np.float32)}
+        if not self.static_map:
+            obs["map"] = ImageSpace(width=w, height=h, channels=1)
+        obs["time_step"] = Box(-1.0, 1.0, (), np.float32)
+        self.single_observation_space = Dict(obs)
+        self.observation_space = batch_space(self.single_observation_space, self.num_envs)
+        self.single_action_space = ActivePerceptionActionSpace(Box(-1, 1, (2,), np.float32),
+                                                               Box(-1, 1, (2,), np.float32))
+        self.action_space = batch_space(self.single_action_space, self.num_envs)
+        self.single_prediction_target_space = Box(-1, 1, (2,), np.float32)
+        self.prediction_target_space = batch_space(self.single_prediction_target_space, self.num_envs)
+        self.loss_fn = regression_loss(2, -1, 1)
+
+        # ---- native configuration
+        p = dataset.native_params()
+        scale, offset = affine_f32(self.loss_fn)
+        self._cfg = N.LidarConfig(num_envs=self.num_envs, height=h, width=w, map_kind=dataset.map_kind,
+                                  is_static=int(self.static_map), static_map_index=int(static_map_index),
+                                  beams=self.lidar_beam_count, step_limit=self.max_episode_steps,
+                                  max_rooms=p["max_rooms"], door_width=p["door_width"],
+                                  lidar_range=float(np.float32(lidar_range)), loss_scale=scale, loss_offset=offset,
+                                  branching_prob=p["branching_prob"])
+        L = N.lib()
+        sizes = N.LidarSizes()
+        N.check(L.apg_lidar_query_sizes(ctypes.byref(self._cfg), ctypes.byref(sizes)), "apg_lidar_query_sizes")
+
+        dev, n, B = self.device, self.num_envs, self.lidar_beam_count
+        t = torch
+        self._t = dict(
+            pos=t.zeros((n, 2), dtype=t.float32, device=dev),
+            init_pos=t.zeros((n, 2), dtype=t.float32, device=dev),
+            elapsed=t.zeros(n, dtype=t.int32, device=dev),
+            flags=t.zeros(n, dtype=t.uint8, device=dev),
+            rng=t.zeros((n, 5), dtype=t.int64, device=dev),
+            it_rng=t.zeros((n, 5), dtype=t.int64, device=dev),
+            occ=t.zeros(max(1, sizes.occ_bytes // 8), dtype=t.int64, device=dev),
+            scratch=t.zeros(sizes.scratch_bytes // 8, dtype=t.int64, device=dev) if sizes.scratch_bytes else None,
+            stack=t.zeros(sizes.stack_bytes // 2, dtype=t.int16, device=dev) if sizes.stack_bytes else None,
+            map_idx=t.full((n,), int(static_map_index) if self.static_map else 0, dtype=t.int64, device=dev),
+            beam_dirs=t.as_tensor(lidar_beam_directions(B, lidar_range), device=dev),
+            lidar=t.zeros((n, B), dtype=t.float32, device=dev),
+            odometry=t.zeros((n, 2), dtype=t.float32, device=dev),
+            time_step=t.zeros(n, dtype=t.float32, device=dev),
+            map_obs=None if self.static_map else t.zeros((n, h, w, 1), dtype=t.float32, device=dev),
+            reward=t.zeros(n, dtype=t.float64, device=dev),
+            terminated=t.zeros(n, dtype=t.bool, device=dev),
+            truncated=t.zeros(n, dtype=t.bool, device=dev),
+            base_reward=t.zeros(n, dtype=t.float32, device=dev),
+            target=t.zeros((n, 2), dtype=t.float32, device=dev),
+            loss=t.zeros(n, dtype=t.float32, device=dev),
+            info_mask=t.zeros(n, dtype=t.bool, device=dev),
+            map_idx_out=t.zeros(n, dtype=t.int64, device=dev),
+            err=t.zeros(1, dtype=t.int32, device=dev),
+        )
+        T = self._t
+        self._state = N.LidarState(*[N.ptr(T[k]) for k in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng",
+                                                            "occ", "scratch", "stack", "map_idx", "beam_dirs")])
+        self._out = N.LidarOutputs(N.ptr(T["lidar"]), N.ptr(T["odometry"]), N.ptr(T["time_step"]),
+                                   N.ptr(T["map_obs"]), N.ptr(T["reward"]), N.ptr(T["terminated"]),
+                                   N.ptr(T["truncated"]), N.ptr(T["base_reward"]), N.ptr(T["target"]),
+                                   N.ptr(T["loss"]), N.ptr(T["info_mask"]), N.ptr(T["map_idx_out"]), N.ptr(T["err"]))
+        self._err_host = t.zeros(1, dtype=t.int32).pin_memory()
+        self._err_event = t.cuda.Event()
+        self._err_pending = False
+        self._autoreset_host = np.zeros(n, dtype=bool)
+        self._seeded = False
+        self._closed = False
+        N.check(L.apg_lidar_init(ctypes.byref(self._cfg), ctypes.byref(self._state), self._stream()), "apg_lidar_init")
+
+    # ------------------------------------------------------------------ helpers
+    def _stream(self):
+        return N.stream_handle(self.device)
+
+    @property
+    def unwrapped(self):
+        return self
+
+    @property
+    def prediction_space(self):
+        return self.action_space["prediction"]
+
+    @property
+    def single_prediction_space(self):
+        return self.single_action_space["prediction"]
+
+    @property
+    def inner_action_space(self):
+        return self.action_space["action"]
+
+    @property
+    def single_inner_action_space(self):
+        return self.single_action_space["action"]
+
+    def _raise_error_bits(self, bits: int):
+        if bits & N.APG_ERR_NAN_ACTION:
+            raise ValueError(NAN_ACTION_MSG)
+        if bits & N.APG_ERR_NAN_PREDICTION:
+            raise ValueError(NAN_PREDICTION_MSG)
+        if bits & N.APG_ERR_MAPGEN:
+            raise N.ApgError("map generation exceeded an internal bound")
+
+    def check_errors(self, block: bool = True):
+        """Raise the reference's exception for any error flagged by the kernels so far."""
+        if block:
+            import torch
+
+            torch.cuda.synchronize(self.device)
+            bits = int(self._t["err"].item())
+        elif self._err_pending and self._err_event.query():
+            bits = int(self._err_host.item())
+            self._err_pending = False
+        else:
+            return
+        if bits:
+            self._t["err"].zero_()
+            self._raise_error_bits(bits)
+
+    def _post_launch_error_copy(self):
+        if self.strict_errors:
+            self.check_errors(block=True)
+            return
+        self._err_host.copy_(self._t["err"], non_blocking=True)
+        self._err_event.record()
+        self._err_pending = True
+
+    # ------------------------------------------------------------------ API
+    def reset(self, *, seed: int | None = None, options: dict[str, Any] | None = None):
+        if self._closed:
+            raise RuntimeError("environment is closed")
+        if seed is None and not self._seeded:
+            seed = int(np.random.SeedSequence().entropy) & ((1 << 62) - 1)
+        use_seed = seed is not None
+        if use_seed and not isinstance(seed, (int, np.integer)):
+            raise TypeError("seed must be an int (sub-env i is seeded with seed + i) or None")
+        s = (int(seed) + self.env_offset) if use_seed else 0
+        if s < 0 or s + self.num_envs > 2**64:
+            raise ValueError("seed must be a non-negative int")
+        N.check(N.lib().apg_lidar_reset(ctypes.byref(self._cfg), ctypes.byref(self._state), s, int(use_seed),
+                                        ctypes.byref(self._out), self._stream()), "apg_lidar_reset")
+        self._seeded = True
+        self._autoreset_host[:] = False
+        T = self._t
+        if self.array_backend == "numpy":
+            self.check_errors(block=True)
+            return self._to_numpy_obs(), {"map_idx": T["map_idx_out"].cpu().numpy().astype(np.int64),
+                                          "_map_idx": np.ones(self.num_envs, dtype=bool)}
+        self._post_launch_error_copy()
+        return self._obs_out(), {"map_idx": T["map_idx_out"], "_map_idx": torch_ones_like_mask(T["info_mask"])}
+
+    def step(self, action):
+        import torch
+
+        if self._closed:
+            raise RuntimeError("environment is closed")
+        a, p = action["action"], action["prediction"]
+        numpy_mode = self.array_backend == "numpy"
+        if numpy_mode:
+            if isinstance(a, torch.Tensor):
+                a = a.detach().cpu().numpy()
+            if isinstance(p, torch.Tensor):
+                p = p.detach().cpu().numpy()
+            a_np = np.ascontiguousarray(a, dtype=np.float32).reshape(self.num_envs, 2)
+            p_np = np.ascontiguousarray(p, dtype=np.float32).reshape(self.num_envs, 2)
+            active = ~self._autoreset_host
+            bad_a = np.isnan(a_np).any(axis=1) & active
+            bad_p = np.isnan(p_np).any(axis=1) & active
+            if bad_a.any() or bad_p.any():  # first offending sub-env decides, action checked first
+                i = int(np.argmax(bad_a | bad_p))
+                raise ValueError(NAN_ACTION_MSG if bad_a[i] else NAN_PREDICTION_MSG)
+            a_t = torch.from_numpy(a_np).to(self.device, non_blocking=True)
+            p_t = torch.from_numpy(p_np).to(self.device, non_blocking=True)
+        else:
+            self.check_errors(block=False)
+            a_t = torch.as_tensor(a, dtype=torch.float32, device=self.device).contiguous()
+            p_t = torch.as_tensor(p, dtype=torch.float32, device=self.device).contiguous()
+        N.check(N.lib().apg_lidar_step(ctypes.byref(self._cfg), ctypes.byref(self._state), N.ptr(a_t), N.ptr(p_t),
+                                       ctypes.byref(self._out), self._stream()), "apg_lidar_step")
+        if numpy_mode:
+            return self._numpy_step_result()
+        self._post_launch_error_copy()
+        T = self._t
+        mask = T["info_mask"]
+        c = (lambda x: x.clone()) if self.copy else (lambda x: x)
+        info = {"base_reward": c(T["base_reward"]), "_base_reward": c(mask),
+                "prediction": {"target": c(T["target"]), "_target": c(mask), "loss": c(T["loss"]),
+                               "_loss": c(mask)},
+                "_prediction": c(mask),
+                "map_idx": c(T["map_idx_out"]), "_map_idx": ~mask}
+        return self._obs_out(), c(T["reward"]), c(T["terminated"]), c(T["truncated"]), info
+
+    # ------------------------------------------------------------------ output assembly
+    def _obs_out(self):
+        T = self._t
+        c = (lambda x: x.clone()) if self.copy else (lambda x: x)
+        obs = {"lidar": c(T["lidar"]), "odometry": c(T["odometry"])}
+        if not self.static_map:
+            obs["map"] = c(T["map_obs"])
+        obs["time_step"] = c(T["time_step"])
+        return obs
+
+    def _to_numpy_obs(self):
+        T = self._t
+        obs = {"lidar": T["lidar"].cpu().numpy(), "odometry": T["odometry"].cpu().numpy()}
+        if not self.static_map:
+            obs["map"] = T["map_obs"].cpu().numpy()
+        obs["time_step"] = T["time_step"].cpu().numpy()
+        return obs
+
+    def _numpy_step_result(self):
+        import torch
+
+        torch.cuda.synchronize(self.device)
+        T = self._t
+        bits = int(T["err"].item())
+        if bits:
+            T["err"].zero_()
+            self._raise_error_bits(bits)
+        obs = self._to_numpy_obs()
+        reward = T["reward"].cpu().numpy()
+        term = T["terminated"].cpu().numpy()
+        trunc = T["truncated"].cpu().numpy()
+        mask = T["info_mask"].cpu().numpy()
+        info: dict[str, Any] = {}
+        if mask.any():
+            info["base_reward"] = np.where(mask, T["base_reward"].cpu().numpy(), np.float32(0))
+            info["_base_reward"] = mask.copy()
+            tgt = np.where(mask[:, None], T["target"].cpu().numpy(), np.float32(0))
+            loss = np.where(mask, T["loss"].cpu().numpy(), np.float32(0))
+            info["prediction"] = {"target": tgt, "_target": mask.copy(), "loss": loss, "_loss": mask.copy()}
+            info["_prediction"] = mask.copy()
+        reset_mask = ~mask
+        if reset_mask.any():
+            info["map_idx"] = np.where(reset_mask, T["map_idx_out"].cpu().numpy(), 0).astype(np.int64)
+            info["_map_idx"] = reset_mask
+        self._autoreset_host = term | trunc
+        return obs, reward, term, trunc, info
+
+    def render(self):
+        raise NotImplementedError("rendering is not part of the MI355X hot path (SURVEY §8(f) item 2)")
+
+    def close(self, **kwargs):
+        if not self._closed:
+            self._closed = True
+            self._t = {}
+
+    def __repr__(self):
+        kind = "maze" if isinstance(self.dataset, FloorMapDatasetMaze) else "rooms"
+        return (f"LIDARLocalization2DVectorEnv(num_envs={self.num_envs}, {kind} "
+                f"{self.dataset.map_width}x{self.dataset.map_height}, static={self.static_map}, "
+                f"beams={self.lidar_beam_count}, device={self.device})")
+
+
+def torch_ones_like_mask(m):
+    import torch
+
+    return torch.ones_like(m, dtype=torch.bool)

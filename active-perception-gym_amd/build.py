@@ -1,0 +1,60 @@
+"""Build the gfx950 shared library (no GPU needed: hipcc cross-compiles).
+
+    python active-perception-gym_amd/build.py [--force] [--verbose]
+
+Output: active-perception-gym_amd/ap_gym_amd/_lib/libapgym_hip.so (git-ignored; travels to the
+GPU box with the gpurun snapshot).
+"""
+
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT_DIR = os.path.join(HERE, "ap_gym_amd", "_lib")
+OUT = os.path.join(OUT_DIR, "libapgym_hip.so")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+SOURCES = ["apg_lidar.hip"]
+HEADERS = ["apg_device.hpp", "apg_maps.hpp", "apg_scan.hpp"]
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = [
+    "--offload-arch=gfx950",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-shared",
+    # exactness: the kernels restate numpy/GEOS float arithmetic operation by operation
+    "-ffp-contract=off",
+    "-fno-fast-math",
+    "-fno-gpu-flush-denormals-to-zero",
+]
+
+
+def _stale() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(INCLUDE, "apgym_capi.h"),
+                                                                  os.path.abspath(__file__)]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(OUT_DIR, exist_ok=True)
+    if not force and not _stale():
+        return OUT
+    cmd = [HIPCC, *FLAGS, "-I", INCLUDE, "-o", OUT + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
+    if verbose:
+        cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose="--verbose" in sys.argv))

@@ -1,0 +1,567 @@
+// apg_lidar.hip — gfx950 kernels + C ABI for the LIDAR localization hot path.
+//
+//   k_lidar_reset   one thread per env: reseed (reset(seed)), next map index from the
+//                   DatasetIterator stream, rooms/maze generation, start-cell draw
+//                   (lidar_localization2d.py:293-315, :547-557; dataset_iterator.py:26-32)
+//   k_map_obs       one wave per env that reset: bit-packed map -> float32 map obs (walls 1/255, :299)
+//   k_lidar_step    64 envs per 256-thread workgroup.  Phase 1 (lane = env): autoreset bookkeeping,
+//                   NaN check, reward, move + collide + slide, termination, target, normalized MSE,
+//                   TimeLimit (lidar_localization2d.py:317-389, time_limit.py:118-139,
+//                   active_perception_env.py:101-121).  Phase 2 (lane = beam): each env's 32-column
+//                   occupancy window is staged in LDS, then every beam runs the exact scan
+//                   (:238-277, :496-536).
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (see build.py).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/apgym_capi.h"
+#include "apg_maps.hpp"
+#include "apg_scan.hpp"
+
+using namespace apg;
+
+namespace {
+
+constexpr uint8_t F_AUTORESET = 1, F_JUST_RESET = 2, F_FIRST = 4;
+constexpr int EPB = 64;        // envs per step workgroup
+constexpr int STEP_THREADS = 256;
+constexpr int MAX_WIN_ROWS = 32;
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char *msg) {
+  snprintf(g_err, sizeof(g_err), "%s", msg);
+  return code;
+}
+
+int check_launch(const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    return APG_E_LAUNCH;
+  }
+  return APG_OK;
+}
+
+BinomTable make_binom_table() {
+  BinomTable t;
+  t.p = 0.3;
+  t.q = 1.0 - t.p;
+  for (int n = 0; n < 16; n++) {
+    // random_binomial_inversion's cached constants, evaluated with the host libm like numpy
+    double np_ = n * t.p;
+    t.qn[n] = std::exp(n * std::log(t.q));
+    double b = np_ + 10.0 * std::sqrt(np_ * t.q + 1);
+    t.bound[n] = (int32_t)(n < b ? n : b);
+  }
+  return t;
+}
+
+struct Geo {
+  int n, h, w, wpr, is_static, kind, max_rooms, door_width, frames;
+  double bp;
+};
+
+Geo make_geo(const apg_lidar_config *c) {
+  Geo g;
+  g.n = c->num_envs;
+  g.h = c->height;
+  g.w = c->width;
+  g.wpr = (c->width + 63) / 64;
+  g.is_static = c->is_static;
+  g.kind = c->map_kind;
+  g.max_rooms = c->max_rooms;
+  g.door_width = c->door_width;
+  g.frames = ((c->height + 1) / 2) * ((c->width + 1) / 2) + 4;
+  g.bp = c->branching_prob;
+  return g;
+}
+
+int validate(const apg_lidar_config *c) {
+  if (!c) return fail(APG_E_INVALID, "null config");
+  if (c->num_envs <= 0) return fail(APG_E_INVALID, "num_envs must be positive");
+  if (c->height < 3 || c->width < 3 || c->height > 128 || c->width > 128)
+    return fail(APG_E_INVALID, "map size must be within [3, 128]");
+  if (c->map_kind == APG_MAP_ROOMS) {
+    if (c->height != c->width) return fail(APG_E_INVALID, "rooms maps must be square");
+    if (c->max_rooms < 1 || c->max_rooms > 17) return fail(APG_E_INVALID, "max_rooms must be in [1, 17]");
+    if (c->door_width < 1) return fail(APG_E_INVALID, "door_width must be positive");
+  } else if (c->map_kind == APG_MAP_MAZE) {
+    if ((c->height % 2) == 0 || (c->width % 2) == 0)
+      return fail(APG_E_INVALID, "Width and height must be odd.");
+  } else {
+    return fail(APG_E_INVALID, "unknown map kind");
+  }
+  if (c->beams <= 0 || c->beams > 4096) return fail(APG_E_INVALID, "beams must be in [1, 4096]");
+  if (!(c->lidar_range > 0.0f) || c->lidar_range > 1000.0f) return fail(APG_E_INVALID, "bad lidar_range");
+  if (c->step_limit <= 0) return fail(APG_E_INVALID, "step_limit must be positive");
+  return APG_OK;
+}
+
+// ------------------------------------------------------------------ map helpers
+APG_DEV int place_start(Pcg64 &rng, const uint64_t *rows, int h, int w, int wpr, float &px, float &py) {
+  int nocc = 0;
+  for (int i = 0; i < h * wpr; i++) nocc += __popcll(rows[i]);
+  const int64_t nfree = (int64_t)h * w - nocc;
+  if (nfree <= 0) return -1;
+  int64_t pick = integers(rng, 0, nfree);
+  for (int y = 0; y < h; y++) {
+    int occ_row = 0;
+    for (int k = 0; k < wpr; k++) occ_row += __popcll(rows[y * wpr + k]);
+    const int free_row = w - occ_row;
+    if (pick >= free_row) {
+      pick -= free_row;
+      continue;
+    }
+    for (int x = 0; x < w; x++) {
+      if (!((rows[y * wpr + (x >> 6)] >> (x & 63)) & 1ULL)) {
+        if (pick == 0) {
+          px = __fadd_rn((float)x, 0.5f);
+          py = __fadd_rn((float)y, 0.5f);
+          return 0;
+        }
+        pick--;
+      }
+    }
+  }
+  return -1;
+}
+
+APG_DEV int gen_map(const Geo &g, Pcg64 &r, uint64_t *occ, uint64_t *scratch, uint16_t *stack,
+                    size_t stride, const BinomTable &bt) {
+  Bits occb{occ, g.wpr};
+  if (g.kind == APG_MAP_ROOMS) {
+    Bits door{scratch, g.wpr};
+    return rooms_generate(r, occb, door, g.h, g.max_rooms, g.door_width, bt);
+  }
+  return maze_generate(r, occb, g.h, g.w, g.bp, stack, stride, g.frames);
+}
+
+// ------------------------------------------------------------------ kernels
+__global__ void k_map_generate(Geo g, const uint64_t *idx, int n, uint64_t *occ, uint64_t *scratch,
+                               uint16_t *stack, uint32_t *err, BinomTable bt) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Pcg64 r = seed_pcg64(idx[i]);
+  const size_t words = (size_t)g.h * g.wpr;
+  int rc = gen_map(g, r, occ + i * words, scratch ? scratch + i * words : nullptr, stack ? stack + i : nullptr,
+                   (size_t)n, bt);
+  if (rc != 0 && err) atomicOr(err, APG_ERR_MAPGEN);
+}
+
+__global__ void k_lidar_reset(Geo g, apg_lidar_state S, uint64_t seed, int use_seed, int all,
+                              uint64_t *out_map_idx, uint32_t *err, BinomTable bt) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= g.n) return;
+  uint8_t f = S.flags[e];
+  if (!all && !(f & F_AUTORESET)) return;
+  Pcg64 rng;
+  Pcg64 it;
+  if (use_seed) {
+    rng = seed_pcg64(seed + (uint64_t)e);
+    if (!g.is_static) it = seed_pcg64(bounded_u64(rng, 0x100000000ULL));  // integers(0, 2**32, endpoint=True)
+  } else {
+    rng = *reinterpret_cast<const Pcg64 *>(&S.rng[e]);
+    if (!g.is_static) it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[e]);
+  }
+  const size_t words = (size_t)g.h * g.wpr;
+  const uint64_t *rows = S.occ;
+  uint64_t midx;
+  if (!g.is_static) {
+    midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
+    uint64_t *own = S.occ + e * words;
+    Pcg64 map_rng = seed_pcg64(midx);  // FloorMapDataset*.get_data_point: default_rng(idx)
+    int rc = gen_map(g, map_rng, own, S.scratch ? S.scratch + e * words : nullptr, S.stack ? S.stack + e : nullptr,
+                     (size_t)g.n, bt);
+    if (rc != 0) atomicOr(err, APG_ERR_MAPGEN);
+    rows = own;
+    *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
+    S.map_idx[e] = midx;
+  } else {
+    midx = S.map_idx[e];
+  }
+  float px = 0.5f, py = 0.5f;
+  if (place_start(rng, rows, g.h, g.w, g.wpr, px, py) != 0) atomicOr(err, APG_ERR_MAPGEN);
+  S.pos[2 * e] = px;
+  S.pos[2 * e + 1] = py;
+  S.init_pos[2 * e] = px;
+  S.init_pos[2 * e + 1] = py;
+  S.elapsed[e] = 0;
+  S.flags[e] = (uint8_t)((f & F_AUTORESET) | F_JUST_RESET | F_FIRST);
+  *reinterpret_cast<Pcg64 *>(&S.rng[e]) = rng;
+  if (out_map_idx) out_map_idx[e] = midx;
+}
+
+__global__ void k_map_obs(int n, int h, int w, int wpr, const uint8_t *flags, const uint64_t *occ,
+                          float *map_obs, int all) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const float wall = 1.0f / 255.0f;
+  const int cells = h * w;
+  for (int e = wave; e < n; e += nwaves) {
+    if (!all && !(flags[e] & F_JUST_RESET)) continue;
+    const uint64_t *rows = occ + (size_t)e * h * wpr;
+    float *dst = map_obs + (size_t)e * cells;
+    for (int k = lane; k < cells; k += 64) {
+      const int y = k / w, x = k - y * w;
+      dst[k] = ((rows[y * wpr + (x >> 6)] >> (x & 63)) & 1ULL) ? wall : 0.0f;
+    }
+  }
+}
+
+struct StepParams {
+  int n, h, w, wpr, beams, step_limit, is_static, R, wrows;
+  float range, loss_scale, loss_offset;
+};
+
+template <bool WINDOW>
+__global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_lidar_state S,
+                                                             const float *__restrict__ act,
+                                                             const float *__restrict__ pred,
+                                                             apg_lidar_outputs O) {
+  __shared__ float s_pos[EPB][2];
+  __shared__ int s_x0[EPB], s_y0[EPB];
+  __shared__ uint32_t s_win[EPB * MAX_WIN_ROWS];
+  const int tid = threadIdx.x;
+  const int base = blockIdx.x * EPB;
+  const size_t words = (size_t)P.h * P.wpr;
+
+  // ---------------- phase 1: one lane per env
+  if (tid < EPB) {
+    const int e = base + tid;
+    uint32_t errbits = 0;
+    if (e < P.n) {
+      uint8_t f = S.flags[e];
+      float pos0 = S.pos[2 * e], pos1 = S.pos[2 * e + 1];
+      const uint64_t *rows = S.occ + (P.is_static ? 0 : e * words);
+      const OccGlobal og{rows, P.h, P.w, P.wpr};
+      const float mapw = (float)P.w, maph = (float)P.h;
+      if (f & F_JUST_RESET) {  // NEXT_STEP autoreset: this env returned reset obs, reward 0
+        O.reward[e] = 0.0;
+        O.terminated[e] = 0;
+        O.truncated[e] = 0;
+        O.base_reward[e] = 0.0f;
+        O.target[2 * e] = 0.0f;
+        O.target[2 * e + 1] = 0.0f;
+        O.loss[e] = 0.0f;
+        O.info_mask[e] = 0;
+        f &= (uint8_t)~(F_JUST_RESET | F_AUTORESET);
+      } else {
+        float ax = act[2 * e], ay = act[2 * e + 1];
+        const float prx = pred[2 * e], pry = pred[2 * e + 1];
+        if (isnan(ax) || isnan(ay)) errbits |= APG_ERR_NAN_ACTION;
+        if (isnan(prx) || isnan(pry)) errbits |= APG_ERR_NAN_PREDICTION;
+        if (errbits) {  // the reference raises ValueError before touching this env's state
+          O.reward[e] = 0.0;
+          O.terminated[e] = 0;
+          O.truncated[e] = 0;
+          O.base_reward[e] = 0.0f;
+          O.target[2 * e] = 0.0f;
+          O.target[2 * e + 1] = 0.0f;
+          O.loss[e] = 0.0f;
+          O.info_mask[e] = 0;
+        } else {
+          const float lpx = pos0, lpy = pos1;
+          const float br = __fsub_rn(0.1f, __fmul_rn(0.001f, __fadd_rn(__fmul_rn(ax, ax), __fmul_rn(ay, ay))));
+          const float mag = norm_f32(ax, ay);
+          if (mag > 1.0f) {
+            ax = f32_div(ax, mag);
+            ay = f32_div(ay, mag);
+          }
+          const float tx = __fadd_rn(pos0, ax), ty = __fadd_rn(pos1, ay);
+          float dirx = __fsub_rn(tx, pos0), diry = __fsub_rn(ty, pos1);
+          const float total = norm_f32(dirx, diry);
+          if (total > 0.0f) {
+            dirx = f32_div(dirx, total);
+            diry = f32_div(diry, total);
+            const float d = lidar_scan(og, pos0, pos1, tx, ty).dist;
+            pos0 = __fadd_rn(pos0, __fmul_rn(dirx, d));
+            pos1 = __fadd_rn(pos1, __fmul_rn(diry, d));
+            const float rem = __fsub_rn(total, d);
+            if (rem > 1e-5f) {  // slide along the wall (:345-364)
+              const float rvx = __fmul_rn(dirx, rem), rvy = __fmul_rn(diry, rem);
+              const bool kx = rvx > 1e-5f, ky = rvy > 1e-5f;
+              if (kx || ky) {
+                const float c0x = kx ? rvx : rvy, c1y = ky ? rvy : rvx;  // eye(2) * kept
+                const float d0 = lidar_scan(og, pos0, pos1, __fadd_rn(pos0, c0x), __fadd_rn(pos1, 0.0f)).dist;
+                const float d1 = lidar_scan(og, pos0, pos1, __fadd_rn(pos0, 0.0f), __fadd_rn(pos1, c1y)).dist;
+                float cx, cy, dd;
+                if (d0 > 0.0f) {
+                  cx = c0x;
+                  cy = 0.0f;
+                  dd = d0;
+                } else {
+                  cx = 0.0f;
+                  cy = c1y;
+                  dd = d1;
+                }
+                const float nrm = norm_f32(cx, cy);
+                pos0 = __fadd_rn(pos0, __fmul_rn(f32_div(cx, nrm), dd));
+                pos1 = __fadd_rn(pos1, __fmul_rn(f32_div(cy, nrm), dd));
+              }
+            }
+          }
+          if (f & F_FIRST) {  // initial_pos aliases pos until np.clip rebinds it (:305, :371)
+            S.init_pos[2 * e] = pos0;
+            S.init_pos[2 * e + 1] = pos1;
+            f &= (uint8_t)~F_FIRST;
+          }
+          bool term = pos0 < 0.0f || pos1 < 0.0f || pos0 >= mapw || pos1 >= maph;
+          pos0 = fminf(fmaxf(pos0, 0.0f), mapw);
+          pos1 = fminf(fmaxf(pos1, 0.0f), maph);
+          const float tgx = __fsub_rn(__fmul_rn(f32_div(lpx, mapw), 2.0f), 1.0f);
+          const float tgy = __fsub_rn(__fmul_rn(f32_div(lpy, maph), 2.0f), 1.0f);
+          const int el = S.elapsed[e] + 1;
+          S.elapsed[e] = el;
+          if (el >= P.step_limit) term = true;  // TimeLimit(issue_termination=True)
+          const float ex = __fsub_rn(prx, tgx), ey = __fsub_rn(pry, tgy);
+          const float mse = f32_div(__fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey)), 2.0f);
+          const float loss = __fadd_rn(__fmul_rn(mse, P.loss_scale), P.loss_offset);
+          O.base_reward[e] = br;
+          O.target[2 * e] = tgx;
+          O.target[2 * e + 1] = tgy;
+          O.loss[e] = loss;
+          O.reward[e] = (double)__fsub_rn(br, loss);
+          O.terminated[e] = term;
+          O.truncated[e] = 0;
+          O.info_mask[e] = 1;
+          if (term) f |= F_AUTORESET;
+          S.pos[2 * e] = pos0;
+          S.pos[2 * e + 1] = pos1;
+        }
+      }
+      S.flags[e] = f;
+      // odometry (:263-270) and TimeLimit time_step (time_limit.py:113-116)
+      const float ox = __fsub_rn(pos0, S.init_pos[2 * e]), oy = __fsub_rn(pos1, S.init_pos[2 * e + 1]);
+      O.odometry[2 * e] = __fsub_rn(__fmul_rn(f32_div(__fadd_rn(ox, mapw), __fadd_rn(mapw, mapw)), 2.0f), 1.0f);
+      O.odometry[2 * e + 1] = __fsub_rn(__fmul_rn(f32_div(__fadd_rn(oy, maph), __fadd_rn(maph, maph)), 2.0f), 1.0f);
+      O.time_step[e] = (float)(2.0 * (double)S.elapsed[e] / (double)P.step_limit - 1.0);
+      s_pos[tid][0] = pos0;
+      s_pos[tid][1] = pos1;
+      if (WINDOW) {
+        s_x0[tid] = (int)floorf(pos0) - P.R - 2;
+        s_y0[tid] = (int)floorf(pos1) - P.R - 2;
+      }
+    }
+    // one atomic per wave for the error word
+    const unsigned long long any = __ballot(errbits != 0);
+    if (any) {
+      uint32_t bits = errbits;
+      for (int off = 32; off > 0; off >>= 1) bits |= __shfl_xor(bits, off);
+      if ((tid & 63) == 0) atomicOr(O.err, bits);
+    }
+  }
+  __syncthreads();
+
+  // ---------------- phase 2: stage occupancy windows, then one lane per beam
+  if (WINDOW) {
+    for (int r = tid; r < EPB * P.wrows; r += STEP_THREADS) {
+      const int el = r / P.wrows, row = r - el * P.wrows;
+      const int e = base + el;
+      uint32_t v = 0;
+      if (e < P.n) {
+        const int y = s_y0[el] + row;
+        if ((unsigned)y < (unsigned)P.h) {
+          const uint64_t *rows = S.occ + (P.is_static ? 0 : e * words) + (size_t)y * P.wpr;
+          v = extract_window_row(rows, P.wpr, s_x0[el]);
+        }
+      }
+      s_win[el * MAX_WIN_ROWS + row] = v;
+    }
+    __syncthreads();
+  }
+  const float inv_range_num = P.range;
+  for (int r = tid; r < EPB * P.beams; r += STEP_THREADS) {
+    const int el = r / P.beams, beam = r - el * P.beams;
+    const int e = base + el;
+    if (e >= P.n) break;
+    const float px = s_pos[el][0], py = s_pos[el][1];
+    const float qx = __fadd_rn(px, S.beam_dirs[2 * beam]), qy = __fadd_rn(py, S.beam_dirs[2 * beam + 1]);
+    float d;
+    if (WINDOW) {
+      const OccWindow ow{&s_win[el * MAX_WIN_ROWS], s_x0[el], s_y0[el], P.wrows};
+      d = lidar_scan(ow, px, py, qx, qy).dist;
+    } else {
+      const OccGlobal og{S.occ + (P.is_static ? 0 : e * words), P.h, P.w, P.wpr};
+      d = lidar_scan(og, px, py, qx, qy).dist;
+    }
+    const float v = f32_div(d, inv_range_num);
+    O.lidar[(size_t)e * P.beams + beam] = fminf(fmaxf(v, -1.0f), 1.0f);
+  }
+}
+
+__global__ void k_scan_batch(const uint64_t *occ, const int32_t *map_index, int h, int w, int wpr,
+                             const float *seg, int n, float *dist, int32_t *kind) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const OccGlobal og{occ + (size_t)map_index[i] * h * wpr, h, w, wpr};
+  ScanOut o = lidar_scan(og, seg[4 * i], seg[4 * i + 1], seg[4 * i + 2], seg[4 * i + 3]);
+  dist[i] = o.dist;
+  if (kind) kind[i] = o.kind;
+}
+
+__global__ void k_rng_draws(const uint64_t *seeds, int m, int kind, int64_t a, int64_t b, int n,
+                            double *out, BinomTable bt) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  Pcg64 r = seed_pcg64(seeds[i]);
+  for (int k = 0; k < n; k++) {
+    double v = 0;
+    switch (kind) {
+      case 0: v = (double)next64(r); break;
+      case 1: v = (double)next32(r); break;
+      case 2: v = next_double(r); break;
+      case 3: v = (double)integers(r, a, b); break;
+      case 4: v = (double)bounded_u64(r, 0x100000000ULL); break;
+      case 5: v = (double)binomial_inv(r, a, bt); break;
+      default: break;
+    }
+    out[(size_t)i * n + k] = v;
+  }
+}
+
+int grid_for(int n, int threads) { return (n + threads - 1) / threads; }
+
+int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *act,
+                       const float *pred, const apg_lidar_outputs *out, hipStream_t s) {
+  StepParams P;
+  P.n = cfg->num_envs;
+  P.h = cfg->height;
+  P.w = cfg->width;
+  P.wpr = (cfg->width + 63) / 64;
+  P.beams = cfg->beams;
+  P.step_limit = cfg->step_limit;
+  P.is_static = cfg->is_static;
+  P.R = (int)ceilf(cfg->lidar_range);
+  P.wrows = 2 * P.R + 4;
+  P.range = cfg->lidar_range;
+  P.loss_scale = cfg->loss_scale;
+  P.loss_offset = cfg->loss_offset;
+  const bool window = P.wrows <= MAX_WIN_ROWS && (2 * P.R + 4) <= 32;
+  const int grid = grid_for(P.n, EPB);
+  if (window)
+    hipLaunchKernelGGL(k_lidar_step<true>, dim3(grid), dim3(STEP_THREADS), 0, s, P, *st, act, pred, *out);
+  else
+    hipLaunchKernelGGL(k_lidar_step<false>, dim3(grid), dim3(STEP_THREADS), 0, s, P, *st, act, pred, *out);
+  return check_launch("k_lidar_step");
+}
+
+int launch_map_obs(const apg_lidar_config *cfg, const apg_lidar_state *st, const apg_lidar_outputs *out,
+                   int all, hipStream_t s) {
+  if (cfg->is_static || !out->map_obs) return APG_OK;
+  const int wpr = (cfg->width + 63) / 64;
+  int waves = cfg->num_envs < 4096 ? cfg->num_envs : 4096;
+  hipLaunchKernelGGL(k_map_obs, dim3(grid_for(waves * 64, 256)), dim3(256), 0, s, cfg->num_envs, cfg->height,
+                     cfg->width, wpr, st->flags, st->occ, out->map_obs, all);
+  return check_launch("k_map_obs");
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *apg_version(void) { return "apgym-mi355x 0.1.0 (gfx950)"; }
+const char *apg_last_error(void) { return g_err; }
+
+int apg_lidar_query_sizes(const apg_lidar_config *cfg, apg_lidar_state_sizes *o) {
+  int rc = validate(cfg);
+  if (rc) return rc;
+  if (!o) return fail(APG_E_INVALID, "null output");
+  Geo g = make_geo(cfg);
+  const size_t words = (size_t)g.h * g.wpr;
+  o->wpr = g.wpr;
+  o->maze_frames = g.frames;
+  o->occ_bytes = (g.is_static ? 1 : (size_t)g.n) * words * sizeof(uint64_t);
+  o->scratch_bytes = (!g.is_static && g.kind == APG_MAP_ROOMS) ? (size_t)g.n * words * sizeof(uint64_t)
+                     : (g.is_static && g.kind == APG_MAP_ROOMS) ? words * sizeof(uint64_t) : 0;
+  o->stack_bytes = g.kind == APG_MAP_MAZE ? (size_t)g.frames * (g.is_static ? 1 : (size_t)g.n) * sizeof(uint16_t) : 0;
+  return APG_OK;
+}
+
+int apg_lidar_init(const apg_lidar_config *cfg, const apg_lidar_state *st, apg_stream_t stream) {
+  int rc = validate(cfg);
+  if (rc) return rc;
+  if (!cfg->is_static) return APG_OK;
+  // One map for every env: generate dataset[static_map_index] once.
+  Geo g = make_geo(cfg);
+  hipStream_t s = (hipStream_t)stream;
+  // map_idx[0] already holds static_map_index (the host fills the state before init)
+  hipLaunchKernelGGL(k_map_generate, dim3(1), dim3(64), 0, s, g, (const uint64_t *)st->map_idx, 1, st->occ,
+                     st->scratch, st->stack, (uint32_t *)nullptr, make_binom_table());
+  return check_launch("k_map_generate(static)");
+}
+
+int apg_lidar_reset(const apg_lidar_config *cfg, const apg_lidar_state *st, uint64_t seed, int use_seed,
+                    const apg_lidar_outputs *out, apg_stream_t stream) {
+  int rc = validate(cfg);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  Geo g = make_geo(cfg);
+  hipLaunchKernelGGL(k_lidar_reset, dim3(grid_for(g.n, 64)), dim3(64), 0, s, g, *st, seed, use_seed, 1,
+                     out->map_idx, out->err, make_binom_table());
+  if ((rc = check_launch("k_lidar_reset"))) return rc;
+  if ((rc = launch_map_obs(cfg, st, out, 1, s))) return rc;
+  return launch_step_kernel(cfg, st, nullptr, nullptr, out, s);
+}
+
+int apg_lidar_step(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
+                   const float *prediction, const apg_lidar_outputs *out, apg_stream_t stream) {
+  int rc = validate(cfg);
+  if (rc) return rc;
+  if (!action || !prediction) return fail(APG_E_INVALID, "null action/prediction");
+  hipStream_t s = (hipStream_t)stream;
+  Geo g = make_geo(cfg);
+  hipLaunchKernelGGL(k_lidar_reset, dim3(grid_for(g.n, 64)), dim3(64), 0, s, g, *st, (uint64_t)0, 0, 0,
+                     out->map_idx, out->err, make_binom_table());
+  if ((rc = check_launch("k_lidar_reset"))) return rc;
+  if ((rc = launch_map_obs(cfg, st, out, 0, s))) return rc;
+  return launch_step_kernel(cfg, st, action, prediction, out, s);
+}
+
+int apg_map_generate(int map_kind, const uint64_t *idx, int n, int h, int w, int max_rooms, int door_width,
+                     double branching_prob, uint64_t *occ, uint64_t *scratch, uint16_t *stack, uint32_t *err,
+                     apg_stream_t stream) {
+  apg_lidar_config c;
+  memset(&c, 0, sizeof(c));
+  c.num_envs = n;
+  c.height = h;
+  c.width = w;
+  c.map_kind = map_kind;
+  c.beams = 1;
+  c.step_limit = 1;
+  c.lidar_range = 1.0f;
+  c.max_rooms = max_rooms;
+  c.door_width = door_width;
+  c.branching_prob = branching_prob;
+  int rc = validate(&c);
+  if (rc) return rc;
+  if (map_kind == APG_MAP_ROOMS && !scratch) return fail(APG_E_INVALID, "rooms maps need scratch");
+  if (map_kind == APG_MAP_MAZE && !stack) return fail(APG_E_INVALID, "maze maps need stack");
+  Geo g = make_geo(&c);
+  hipLaunchKernelGGL(k_map_generate, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, g, idx, n, occ,
+                     scratch, stack, err, make_binom_table());
+  return check_launch("k_map_generate");
+}
+
+int apg_lidar_scan_batch(const uint64_t *occ, const int32_t *map_index, int h, int w, const float *seg, int n,
+                         float *dist, int32_t *kind, apg_stream_t stream) {
+  if (n <= 0 || h <= 0 || w <= 0 || w > 128) return fail(APG_E_INVALID, "bad scan batch arguments");
+  hipLaunchKernelGGL(k_scan_batch, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, occ, map_index, h,
+                     w, (w + 63) / 64, seg, n, dist, kind);
+  return check_launch("k_scan_batch");
+}
+
+int apg_rng_draws(const uint64_t *seeds, int m, int kind, int64_t a, int64_t b, int n, double *out,
+                  apg_stream_t stream) {
+  if (m <= 0 || n <= 0 || kind < 0 || kind > 5) return fail(APG_E_INVALID, "bad rng draw arguments");
+  if (kind == 5 && (a < 0 || a > 15)) return fail(APG_E_INVALID, "binomial n must be in [0, 15]");
+  hipLaunchKernelGGL(k_rng_draws, dim3(grid_for(m, 64)), dim3(64), 0, (hipStream_t)stream, seeds, m, kind, a, b,
+                     n, out, make_binom_table());
+  return check_launch("k_rng_draws");
+}
+
+}  // extern "C"

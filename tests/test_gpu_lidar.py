@@ -1,0 +1,271 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the golden fixtures and the oracle.
+
+Bar: bit-exact for integer work (RNG, maps, flags, indices) and for every float output (the kernels
+restate numpy/GEOS arithmetic operation by operation; the north_star tolerance of 1e-6 is not used
+because nothing needs it).
+"""
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+ENV_CASES = {
+    "rooms_static_b16": ("rooms", 32, True, 16),
+    "rooms_static_b8_grid": ("rooms", 32, True, 8),
+    "rooms64_b32": ("rooms", 64, False, 32),
+    "maze21_b8": ("maze", 21, False, 8),
+    "maze21_b8_grid": ("maze", 21, False, 8),
+    "maze127_b64": ("maze", 127, False, 64),
+}
+
+
+def _ds(ap, kind, size):
+    return ap.FloorMapDatasetRooms(size, size) if kind == "rooms" else ap.FloorMapDatasetMaze(size, size)
+
+
+def test_device_rng_matches_numpy(gpu):
+    import torch
+
+    from ap_gym_amd import _native as N
+
+    g = golden("rng.npz")
+    seeds = torch.as_tensor(g["seeds"].view(np.int64), device=gpu)
+    m = len(g["seeds"])
+
+    def draws(kind, a=0, b=0, n=8):
+        out = torch.zeros((m, n), dtype=torch.float64, device=gpu)
+        N.check(N.lib().apg_rng_draws(N.ptr(seeds), m, kind, a, b, n, N.ptr(out), N.stream_handle(gpu)))
+        return out.cpu().numpy()
+
+    assert np.array_equal(draws(0, n=16), g["raw"].astype(np.float64))
+    assert np.array_equal(draws(4, n=1), g["u32_endpoint"].astype(np.float64))
+    assert np.array_equal(draws(2), g["random"])
+    for j, hi in enumerate(g["his"]):
+        assert np.array_equal(draws(3, 0, int(hi)), g["ints"][:, j].astype(np.float64)), hi
+    for n in range(9):
+        assert np.array_equal(draws(5, n), g["binom"][:, n].astype(np.float64)), n
+
+
+@pytest.mark.parametrize("kind,size", [("rooms", 32), ("rooms", 64), ("rooms", 16), ("maze", 21), ("maze", 63),
+                                       ("maze", 127)])
+def test_device_maps_match_reference(gpu, kind, size):
+    import ap_gym_amd as ap
+
+    g = golden("maps.npz")
+    ref = np.unpackbits(g[f"{kind}{size}_bits"], axis=-1)[..., :size].astype(bool)
+    got = _ds(ap, kind, size).get_data_point_batch(g[f"{kind}{size}_idx"], device=gpu)
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("kind,size,count", [("rooms", 64, 4096), ("rooms", 32, 2048), ("maze", 127, 256),
+                                             ("maze", 21, 2048)])
+def test_device_maps_match_oracle_random_idx(gpu, oracle_mod, kind, size, count):
+    import ap_gym_amd as ap
+
+    idx = np.random.default_rng(size).integers(0, 2**32, count).astype(np.uint64)
+    got = _ds(ap, kind, size).get_data_point_batch(idx, device=gpu)
+    for i in range(0, count, max(1, count // 256)):
+        m = oracle_mod.rooms_map(int(idx[i]), size) if kind == "rooms" else oracle_mod.maze_map(int(idx[i]), size)
+        assert np.array_equal(got[i], m.astype(bool)), (kind, size, int(idx[i]))
+
+
+def _scan_gpu(gpu, maps_bool, map_index, segs):
+    import torch
+
+    from ap_gym_amd import _native as N
+
+    nm, h, w = maps_bool.shape
+    wpr = (w + 63) // 64
+    padded = np.zeros((nm, h, wpr * 64), np.uint8)
+    padded[..., :w] = maps_bool
+    words = np.packbits(padded, axis=-1, bitorder="little").view("<u8").astype(np.uint64)
+    occ = torch.as_tensor(words.view(np.int64).copy(), device=gpu)
+    mi = torch.as_tensor(np.asarray(map_index, np.int32), device=gpu)
+    sg = torch.as_tensor(np.ascontiguousarray(segs, np.float32), device=gpu)
+    n = len(segs)
+    dist = torch.zeros(n, dtype=torch.float32, device=gpu)
+    kind = torch.zeros(n, dtype=torch.int32, device=gpu)
+    N.check(N.lib().apg_lidar_scan_batch(N.ptr(occ), N.ptr(mi), h, w, N.ptr(sg), n, N.ptr(dist), N.ptr(kind),
+                                         N.stream_handle(gpu)))
+    return dist.cpu().numpy(), kind.cpu().numpy()
+
+
+def test_device_scan_matches_reference_model(gpu):
+    g = golden("lidar_scan.npz")
+    h, w = (int(x) for x in g["map_hw"])
+    maps = np.unpackbits(g["maps"], axis=-1)[..., :w].astype(bool)
+    dist, kinds = _scan_gpu(gpu, maps, g["map_index"], g["segments"])
+    assert np.array_equal(dist, g["distance"])
+    assert set(np.unique(kinds)) == set(range(6))
+
+
+def test_device_scan_matches_oracle_degenerate_sweep(gpu, oracle_mod):
+    """Random + lattice-aligned segments (corner touches, collinear runs) on 64x64 rooms and 127 mazes."""
+    rng = np.random.default_rng(3)
+    for kind, size in (("rooms", 64), ("maze", 127)):
+        maps = np.stack([(oracle_mod.rooms_map(i, size) if kind == "rooms" else oracle_mod.maze_map(i, size))
+                         for i in range(4)]).astype(bool)
+        n = 40000
+        mi = rng.integers(0, 4, n).astype(np.int32)
+        p = rng.integers(0, size, (n, 2)).astype(np.float32) + rng.choice(
+            np.array([0.0, 0.5, 0.25], np.float32), (n, 2))
+        gen = rng.uniform(0, size, (n, 2)).astype(np.float32)
+        p = np.where((np.arange(n) % 3 == 0)[:, None], gen, p)
+        d = rng.choice(np.array([[5, 0], [0, 5], [-5, 0], [0, -5], [5, 5], [-5, 5], [3, -3], [1, 2], [-2, 1],
+                                 [0.5, 0.5], [1, 0], [0, -1]], np.float32), n)
+        d = np.where((np.arange(n) % 5 == 0)[:, None], rng.uniform(-5, 5, (n, 2)).astype(np.float32), d)
+        q = (p + d).astype(np.float32)
+        segs = np.concatenate([p, q], axis=1)
+        dist, kinds = _scan_gpu(gpu, maps, mi, segs)
+        for i in range(n):
+            od, ok = oracle_mod.lidar_scan(maps[mi[i]], segs[i, :2], segs[i, 2:])
+            assert od == dist[i] and ok == kinds[i], (kind, i, segs[i], od, dist[i], ok, kinds[i])
+
+
+@pytest.mark.parametrize("name", sorted(ENV_CASES))
+def test_vector_env_matches_reference_trace(gpu, name):
+    import ap_gym_amd as ap
+
+    kind, size, static, beams = ENV_CASES[name]
+    d = golden(f"lidar_env_{name}.npz")
+    n = d["actions"].shape[1]
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_ds(ap, kind, size), static_map=static,
+                                          lidar_beam_count=beams, device=gpu)
+    obs, info = env.reset(seed=int(d["seed"]))
+    assert np.array_equal(obs["lidar"], d["reset_lidar"])
+    assert np.array_equal(obs["odometry"], d["reset_odometry"])
+    assert np.array_equal(obs["time_step"], d["reset_time_step"])
+    assert np.array_equal(info["map_idx"], d["reset_map_idx"])
+    if not static:
+        assert np.array_equal(np.packbits(obs["map"][..., 0] > 0, axis=-1), d["reset_map"])
+    for t in range(d["actions"].shape[0]):
+        obs, rew, term, trunc, info = env.step({"action": d["actions"][t], "prediction": d["predictions"][t]})
+        assert rew.dtype == np.float64 and obs["lidar"].dtype == np.float32
+        assert np.array_equal(obs["lidar"], d["lidar"][t]), (name, t)
+        assert np.array_equal(obs["odometry"], d["odometry"][t]), (name, t)
+        assert np.array_equal(obs["time_step"], d["time_step"][t]), (name, t)
+        assert np.array_equal(rew, d["reward"][t]), (name, t)
+        assert np.array_equal(term, d["terminated"][t]) and np.array_equal(trunc, d["truncated"][t]), (name, t)
+        mask = d["info_mask"][t]
+        if mask.any():
+            assert np.array_equal(info["_base_reward"], mask)
+            assert np.array_equal(info["base_reward"], d["base_reward"][t]), (name, t)
+            assert np.array_equal(info["prediction"]["target"], d["target"][t]), (name, t)
+            assert np.array_equal(info["prediction"]["loss"], d["loss"][t]), (name, t)
+        else:
+            assert "base_reward" not in info
+        if not static:
+            assert np.array_equal(np.packbits(obs["map"][..., 0] > 0, axis=-1), d["map"][t]), (name, t)
+            assert set(np.unique(obs["map"])) <= {np.float32(0), np.float32(1) / np.float32(255)}
+    env.close()
+
+
+@pytest.mark.parametrize("kind,size,beams,n,steps", [("rooms", 64, 32, 1024, 230), ("maze", 21, 8, 1024, 120),
+                                                     ("maze", 127, 64, 64, 40), ("rooms", 32, 16, 512, 120)])
+def test_vector_env_matches_oracle(gpu, oracle_mod, kind, size, beams, n, steps):
+    import ap_gym_amd as ap
+
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_ds(ap, kind, size), lidar_beam_count=beams,
+                                          device=gpu)
+    ref = oracle_mod.OracleLidarVectorEnv(n, kind, size, False, 0, beams)
+    obs, _ = env.reset(seed=123)
+    ref.reset(123)
+    assert np.array_equal(obs["lidar"], ref.lidar)
+    rng = np.random.default_rng(9)
+    for t in range(steps):
+        a = rng.uniform(-1.5, 1.5, (n, 2)).astype(np.float32)
+        p = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        ref.step(a, p)
+        assert np.array_equal(obs["lidar"], ref.lidar), t
+        assert np.array_equal(obs["odometry"], ref.odometry), t
+        assert np.array_equal(obs["time_step"], ref.time_step), t
+        assert np.array_equal(rew, ref.reward), t
+        assert np.array_equal(term, ref.terminated.astype(bool)), t
+        assert np.array_equal(obs["map"][..., 0], ref.map), t
+    env.close()
+
+
+def test_torch_backend_matches_numpy_backend(gpu):
+    import torch
+
+    import ap_gym_amd as ap
+
+    kw = dict(num_envs=256, lidar_beam_count=32, dataset=ap.FloorMapDatasetRooms(64, 64), device=gpu)
+    e_np = ap.make_vec("LIDARLocRooms-v0", **kw)
+    e_t = ap.make_vec("LIDARLocRooms-v0", array_backend="torch", **kw)
+    e_np.reset(seed=5)
+    e_t.reset(seed=5)
+    rng = np.random.default_rng(2)
+    for t in range(105):
+        a = rng.uniform(-1, 1, (256, 2)).astype(np.float32)
+        p = rng.uniform(-1, 1, (256, 2)).astype(np.float32)
+        o1, r1, te1, tr1, i1 = e_np.step({"action": a, "prediction": p})
+        o2, r2, te2, tr2, i2 = e_t.step({"action": torch.from_numpy(a).to(gpu), "prediction": torch.from_numpy(p).to(gpu)})
+        assert isinstance(r2, torch.Tensor) and r2.device.type == "cuda"
+        assert np.array_equal(o1["lidar"], o2["lidar"].cpu().numpy())
+        assert np.array_equal(r1, r2.cpu().numpy())
+        assert np.array_equal(te1, te2.cpu().numpy())
+        assert np.array_equal(o1["map"], o2["map"].cpu().numpy())
+    e_t.check_errors()
+
+
+def test_nan_action_raises(gpu):
+    import torch
+
+    import ap_gym_amd as ap
+
+    env = ap.make_vec("LIDARLocRoomsStatic-v0", num_envs=4, device=gpu)
+    env.reset(seed=0)
+    a = np.zeros((4, 2), np.float32)
+    p = np.zeros((4, 2), np.float32)
+    a[2, 0] = np.nan
+    with pytest.raises(ValueError, match="NaN values detected in action."):
+        env.step({"action": a, "prediction": p})
+    a[2, 0] = 0
+    p[1, 1] = np.nan
+    with pytest.raises(ValueError, match="NaN values detected in prediction."):
+        env.step({"action": a, "prediction": p})
+    et = ap.make_vec("LIDARLocRoomsStatic-v0", num_envs=4, device=gpu, array_backend="torch", strict_errors=True)
+    et.reset(seed=0)
+    with pytest.raises(ValueError, match="prediction"):
+        et.step({"action": torch.zeros((4, 2), device=gpu), "prediction": torch.from_numpy(p).to(gpu)})
+
+
+def test_full_size_properties(gpu, oracle_mod):
+    """BASELINE cfg 2 size (N=65536, 32 beams, 64x64): size-independent invariants + sampled oracle checks."""
+    import torch
+
+    import ap_gym_amd as ap
+
+    n = 65536
+    env = ap.make_vec("LIDARLocRooms-v0", num_envs=n, lidar_beam_count=32, dataset=ap.FloorMapDatasetRooms(64, 64),
+                      device=gpu, array_backend="torch")
+    obs, info = env.reset(seed=0)
+    g = torch.Generator(device=gpu).manual_seed(0)
+    sample = np.random.default_rng(0).choice(n, 24, replace=False)
+    idx0 = info["map_idx"].cpu().numpy().astype(np.uint64)
+    maps = obs["map"][sample, ..., 0].cpu().numpy()
+    for j, e in enumerate(sample):
+        assert np.array_equal(maps[j] > 0, oracle_mod.rooms_map(int(idx0[e]), 64).astype(bool))
+    resets = 0
+    for t in range(1, 203):
+        a = torch.rand((n, 2), device=gpu, generator=g) * 2 - 1
+        p = torch.rand((n, 2), device=gpu, generator=g) * 2 - 1
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        lid = obs["lidar"]
+        assert bool(((lid >= 0) & (lid <= 1)).all())
+        assert not bool(trunc.any())
+        if t % 101 == 100:  # TimeLimit(100) terminates every env still in its first episode
+            assert int(term.sum()) >= 0.99 * n
+        if t % 101 == 0:
+            resets += 1
+            reset_now = ~info["_base_reward"]
+            assert int(reset_now.sum()) >= 0.99 * n and bool((rew[reset_now] == 0).all())
+    env.check_errors()
+    assert resets == 2

@@ -1,0 +1,117 @@
+"""Host-side logic that needs no GPU: C-ABI symbol export, loss functions, spaces, registry."""
+
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden
+
+
+def _header_functions():
+    src = open(os.path.join(ROOT, "include", "apgym_capi.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(apg_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_capi_library_exports_every_declared_symbol():
+    import ctypes
+
+    from ap_gym_amd import _native
+
+    names = _header_functions()
+    assert len(names) >= 9
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    for n in names:
+        assert hasattr(lib, n), n
+    assert {s[0] for s in _native.SYMBOLS} == set(names)
+    assert _native.lib().apg_version().startswith(b"apgym-mi355x")
+
+
+def test_capi_validation_without_gpu():
+    import ctypes
+
+    from ap_gym_amd import _native as N
+
+    cfg = N.LidarConfig(num_envs=4, height=64, width=64, map_kind=N.APG_MAP_ROOMS, is_static=0, beams=32,
+                        step_limit=100, max_rooms=10, door_width=3, lidar_range=5.0, loss_scale=3.0,
+                        branching_prob=1.0)
+    sz = N.LidarSizes()
+    assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0
+    assert sz.wpr == 1 and sz.occ_bytes == 4 * 64 * 8 and sz.scratch_bytes == 4 * 64 * 8 and sz.stack_bytes == 0
+    cfg.map_kind = N.APG_MAP_MAZE
+    cfg.height = cfg.width = 127
+    assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0
+    assert sz.wpr == 2 and sz.stack_bytes == sz.maze_frames * 4 * 2
+    cfg.height = cfg.width = 128  # even maze sizes are rejected like FloorMapDatasetMaze
+    assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == -1
+    assert b"odd" in N.lib().apg_last_error()
+
+
+def test_mse_loss_matches_reference_golden():
+    from ap_gym_amd.loss_fn import affine_f32, regression_loss
+
+    g = golden("loss.npz")
+    fn = regression_loss(2, -1, 1)
+    got = np.stack([fn(p, t, ()) for p, t in zip(g["mse_pred"], g["mse_target"])])
+    assert got.dtype == np.float32
+    assert np.array_equal(got, g["mse_loss"])
+    assert affine_f32(fn) == (3.0, -0.0)
+
+
+@pytest.mark.parametrize("k", [10, 200])
+def test_ce_loss_matches_reference_golden(k):
+    from ap_gym_amd.loss_fn import CrossEntropyLossFn
+
+    g = golden("loss.npz")
+    fn = CrossEntropyLossFn(k).normalized
+    got = fn(g[f"ce{k}_logits"], g[f"ce{k}_labels"], (256,))
+    assert got.dtype == g[f"ce{k}_loss"].dtype == np.float64
+    assert np.array_equal(got, g[f"ce{k}_loss"])
+
+
+def test_ce_loss_numpy_vs_torch():
+    """The reference's only unit test (test/test_active_classification_env.py:17-50), restated."""
+    import torch
+
+    from ap_gym_amd.loss_fn import CrossEntropyLossFn
+
+    fn = CrossEntropyLossFn()
+    rng = np.random.default_rng(0)
+    blen = rng.integers(0, 5, size=20)
+    plen = blen + rng.integers(1, 5, size=blen.shape)
+    shapes = [tuple(rng.integers(1, 10, size=d)) for d in plen]
+    for bl, shape in zip(blen, shapes):
+        pred = rng.standard_normal(shape)
+        tgt = rng.integers(0, shape[-1], size=shape[:-1])
+        exp = fn.numpy(pred, tgt, shape[:bl])
+        got = fn.torch(torch.from_numpy(pred), torch.from_numpy(tgt), shape[:bl]).numpy()
+        np.testing.assert_allclose(got, exp, rtol=1e-4)
+
+
+def test_registry_and_spaces():
+    import ap_gym_amd as ap
+    from ap_gym_amd.spaces import ActivePerceptionActionSpace, batch_space
+
+    assert {"LIDARLocRooms-v0", "LIDARLocRoomsStatic-v0", "LIDARLocMaze-v0", "LIDARLocMazeStatic-v0"} <= set(
+        ap.registry)
+    with pytest.raises(KeyError):
+        ap.make_vec("NoSuchEnv-v0", 2)
+    sp = ActivePerceptionActionSpace(ap.spaces.Box(-1, 1, (2,)), ap.spaces.Box(-1, 1, (2,)))
+    b = batch_space(sp, 7)
+    assert b["action"].shape == (7, 2) and b["prediction"].shape == (7, 2)
+    im = ap.ImageSpace(64, 48, 1)
+    assert im.shape == (48, 64, 1) and batch_space(im, 3).shape == (3, 48, 64, 1)
+    with pytest.raises(ValueError):
+        ap.FloorMapDatasetMaze(128, 128)
+
+
+def test_beam_directions_match_reference_formula():
+    from ap_gym_amd import lidar_beam_directions
+
+    for b in (8, 16, 32, 64):
+        ang = np.linspace(-np.pi, np.pi, b, dtype=np.float32, endpoint=False)
+        ref = np.stack([np.cos(ang), np.sin(ang)], axis=-1) * 5
+        d = lidar_beam_directions(b, 5)
+        assert d.dtype == np.float32 and np.array_equal(d, ref)

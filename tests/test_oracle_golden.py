@@ -1,0 +1,94 @@
+"""The oracle (oracle/liboracle.so) against the golden fixtures made from the reference.
+
+CPU only.  These pin the restatement before it is trusted as the checker of the HIP kernels:
+  rng.npz        numpy 2.2.6 itself
+  maps.npz       reference FloorMapDatasetRooms/Maze
+  lidar_scan.npz reference __lidar_scan + exact-rational GEOS model
+  lidar_env_*    reference LIDARLocalization2DEnv + TimeLimit + SyncVectorEnv composition
+"""
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+ENV_CASES = {
+    "rooms_static_b16": ("rooms", 32, True, 16),
+    "rooms_static_b8_grid": ("rooms", 32, True, 8),
+    "rooms64_b32": ("rooms", 64, False, 32),
+    "maze21_b8": ("maze", 21, False, 8),
+    "maze21_b8_grid": ("maze", 21, False, 8),
+    "maze127_b64": ("maze", 127, False, 64),
+}
+
+
+def _draws(O, seed, kind, a=0, b=0, p=0.0, n=8):
+    out = np.zeros(n)
+    O.lib().orc_test_draws(int(seed), kind, a, b, p, n, out.ctypes.data)
+    return out
+
+
+def test_rng_matches_numpy(oracle_mod):
+    g = golden("rng.npz")
+    for i, s in enumerate(g["seeds"]):
+        assert np.array_equal(_draws(oracle_mod, s, 0, n=16), g["raw"][i].astype(np.float64))
+        assert _draws(oracle_mod, s, 4, n=1)[0] == g["u32_endpoint"][i][0]
+        for j, hi in enumerate(g["his"]):
+            assert np.array_equal(_draws(oracle_mod, s, 3, 0, int(hi)), g["ints"][i, j].astype(np.float64))
+        for n in range(9):
+            assert np.array_equal(_draws(oracle_mod, s, 5, n, 0, 0.3), g["binom"][i, n].astype(np.float64))
+        assert np.array_equal(_draws(oracle_mod, s, 6, -1, 1), g["uniform"][i])
+        assert np.array_equal(_draws(oracle_mod, s, 2), g["random"][i])
+
+
+@pytest.mark.parametrize("kind,size", [("rooms", 32), ("rooms", 64), ("rooms", 16), ("maze", 21), ("maze", 63),
+                                       ("maze", 127)])
+def test_maps_match_reference(oracle_mod, kind, size):
+    g = golden("maps.npz")
+    idx = g[f"{kind}{size}_idx"]
+    ref = np.unpackbits(g[f"{kind}{size}_bits"], axis=-1)[..., :size].astype(bool)
+    for i, k in enumerate(idx):
+        m = oracle_mod.rooms_map(int(k), size) if kind == "rooms" else oracle_mod.maze_map(int(k), size)
+        assert np.array_equal(m.astype(bool), ref[i]), f"{kind}{size} idx={k}"
+
+
+def test_maze_even_size_raises(oracle_mod):
+    with pytest.raises(ValueError):
+        oracle_mod.maze_map(0, 128)
+
+
+def test_scan_matches_reference_model(oracle_mod):
+    g = golden("lidar_scan.npz")
+    h, w = (int(x) for x in g["map_hw"])
+    maps = np.unpackbits(g["maps"], axis=-1)[..., :w].astype(np.uint8)
+    kinds = np.zeros(6, int)
+    got = np.zeros(len(g["distance"]), np.float32)
+    for i, (mi, seg) in enumerate(zip(g["map_index"], g["segments"])):
+        got[i], k = oracle_mod.lidar_scan(maps[mi], seg[:2], seg[2:])
+        kinds[k] += 1
+    assert np.array_equal(got, g["distance"])
+    # the fixture exercises every GEOS result type the reference branches on
+    assert (kinds > 0).all(), kinds
+
+
+@pytest.mark.parametrize("name", sorted(ENV_CASES))
+def test_vector_env_trace(oracle_mod, name):
+    kind, size, static, beams = ENV_CASES[name]
+    d = golden(f"lidar_env_{name}.npz")
+    n = d["actions"].shape[1]
+    env = oracle_mod.OracleLidarVectorEnv(n, kind, size, static, 0, beams)
+    env.reset(int(d["seed"]))
+    assert np.array_equal(env.lidar, d["reset_lidar"])
+    assert np.array_equal(env.odometry, d["reset_odometry"])
+    assert np.array_equal(env.time_step, d["reset_time_step"])
+    assert np.array_equal(env.map_idx.astype(np.int64), d["reset_map_idx"])
+    for t in range(d["actions"].shape[0]):
+        env.step(d["actions"][t], d["predictions"][t])
+        for key, got in (("lidar", env.lidar), ("odometry", env.odometry), ("time_step", env.time_step),
+                         ("reward", env.reward), ("terminated", env.terminated.astype(bool)),
+                         ("truncated", env.truncated.astype(bool)), ("base_reward", env.base_reward),
+                         ("target", env.target), ("loss", env.loss), ("info_mask", env.info_mask.astype(bool))):
+            assert np.array_equal(got, d[key][t]), f"{name} step {t} {key}"
+        if not static:
+            assert np.array_equal(np.packbits(env.map > 0, axis=-1), d["map"][t]), f"{name} step {t} map"
+    assert str(d["reward_dtype"]) == "float64" and str(d["base_reward_dtype"]) == "float32"
