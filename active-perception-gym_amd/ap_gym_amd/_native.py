@@ -70,6 +70,8 @@ SYMBOLS = [
                                        ctypes.c_int, ctypes.POINTER(LidarOutputs), _vp]),
     ("apg_lidar_step", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(LidarState), _vp, _vp,
                                       ctypes.POINTER(LidarOutputs), _vp]),
+    ("apg_lidar_step_profiled", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(LidarState), _vp, _vp,
+                                               ctypes.POINTER(LidarOutputs), _vp, _vp, _vp]),
     ("apg_map_generate", ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp]),
     ("apg_lidar_scan_batch", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp,

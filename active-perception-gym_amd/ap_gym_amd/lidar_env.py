@@ -145,6 +145,7 @@ class LIDARLocalization2DVectorEnv:
         self._autoreset_host = np.zeros(n, dtype=bool)
         self._seeded = False
         self._closed = False
+        self._kernel_events = None
         N.check(L.apg_lidar_init(ctypes.byref(self._cfg), ctypes.byref(self._state), self._stream()), "apg_lidar_init")
 
     # ------------------------------------------------------------------ helpers
@@ -170,6 +171,11 @@ class LIDARLocalization2DVectorEnv:
     @property
     def single_inner_action_space(self):
         return self.single_action_space["action"]
+
+    def set_kernel_timing_events(self, begin=None, end=None):
+        """Record hipEvent_t handles `begin`/`end` around the fused step kernel of the next step
+        (bench.py's live per-launch timing).  None disables."""
+        self._kernel_events = None if begin is None else (begin, end)
 
     def _raise_error_bits(self, bits: int):
         if bits & N.APG_ERR_NAN_ACTION:
@@ -253,8 +259,14 @@ class LIDARLocalization2DVectorEnv:
             self.check_errors(block=False)
             a_t = torch.as_tensor(a, dtype=torch.float32, device=self.device).contiguous()
             p_t = torch.as_tensor(p, dtype=torch.float32, device=self.device).contiguous()
-        N.check(N.lib().apg_lidar_step(ctypes.byref(self._cfg), ctypes.byref(self._state), N.ptr(a_t), N.ptr(p_t),
-                                       ctypes.byref(self._out), self._stream()), "apg_lidar_step")
+        if self._kernel_events is None:
+            rc = N.lib().apg_lidar_step(ctypes.byref(self._cfg), ctypes.byref(self._state), N.ptr(a_t), N.ptr(p_t),
+                                        ctypes.byref(self._out), self._stream())
+        else:
+            ev_b, ev_e = self._kernel_events
+            rc = N.lib().apg_lidar_step_profiled(ctypes.byref(self._cfg), ctypes.byref(self._state), N.ptr(a_t),
+                                                 N.ptr(p_t), ctypes.byref(self._out), self._stream(), ev_b, ev_e)
+        N.check(rc, "apg_lidar_step")
         if numpy_mode:
             return self._numpy_step_result()
         self._post_launch_error_copy()

@@ -508,8 +508,9 @@ int apg_lidar_reset(const apg_lidar_config *cfg, const apg_lidar_state *st, uint
   return launch_step_kernel(cfg, st, nullptr, nullptr, out, s);
 }
 
-int apg_lidar_step(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
-                   const float *prediction, const apg_lidar_outputs *out, apg_stream_t stream) {
+int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
+                            const float *prediction, const apg_lidar_outputs *out, apg_stream_t stream,
+                            void *ev_begin, void *ev_end) {
   int rc = validate(cfg);
   if (rc) return rc;
   if (!action || !prediction) return fail(APG_E_INVALID, "null action/prediction");
@@ -519,7 +520,16 @@ int apg_lidar_step(const apg_lidar_config *cfg, const apg_lidar_state *st, const
                      out->map_idx, out->err, make_binom_table());
   if ((rc = check_launch("k_lidar_reset"))) return rc;
   if ((rc = launch_map_obs(cfg, st, out, 0, s))) return rc;
-  return launch_step_kernel(cfg, st, action, prediction, out, s);
+  if (ev_begin && hipEventRecord((hipEvent_t)ev_begin, s) != hipSuccess) return fail(APG_E_LAUNCH, "hipEventRecord");
+  rc = launch_step_kernel(cfg, st, action, prediction, out, s);
+  if (rc == APG_OK && ev_end && hipEventRecord((hipEvent_t)ev_end, s) != hipSuccess)
+    return fail(APG_E_LAUNCH, "hipEventRecord");
+  return rc;
+}
+
+int apg_lidar_step(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
+                   const float *prediction, const apg_lidar_outputs *out, apg_stream_t stream) {
+  return apg_lidar_step_profiled(cfg, st, action, prediction, out, stream, nullptr, nullptr);
 }
 
 int apg_map_generate(int map_kind, const uint64_t *idx, int n, int h, int w, int max_rooms, int door_width,

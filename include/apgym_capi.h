@@ -121,6 +121,13 @@ int apg_lidar_reset(const apg_lidar_config *cfg, const apg_lidar_state *st, uint
 int apg_lidar_step(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
                    const float *prediction, const apg_lidar_outputs *out, apg_stream_t stream);
 
+/* apg_lidar_step, additionally recording hipEvent_t `ev_begin` / `ev_end` (may be NULL) on `stream`
+ * immediately before and after the fused step kernel (k_lidar_step) — used by bench.py to time the
+ * dominant kernel live. */
+int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
+                            const float *prediction, const apg_lidar_outputs *out, apg_stream_t stream,
+                            void *ev_begin, void *ev_end);
+
 /* n maps from dataset indices idx[n] into occ[n][h][wpr]; scratch/stack as in apg_lidar_state. */
 int apg_map_generate(int map_kind, const uint64_t *idx, int n, int h, int w, int max_rooms,
                      int door_width, double branching_prob, uint64_t *occ, uint64_t *scratch,
