@@ -52,7 +52,7 @@ class LidarState(ctypes.Structure):
 
 class LidarOutputs(ctypes.Structure):
     _fields_ = [(n, _vp) for n in ("lidar", "odometry", "time_step", "map_obs", "reward", "terminated", "truncated",
-                                   "base_reward", "target", "loss", "info_mask", "map_idx", "err")]
+                                   "base_reward", "target", "loss", "info_mask", "map_idx", "reset_mask", "err")]
 
 
 class LidarSizes(ctypes.Structure):

@@ -46,6 +46,7 @@ def lidar_beam_directions(beams: int, lidar_range: float) -> np.ndarray:
 
 class LIDARLocalization2DVectorEnv:
     metadata = {"render_modes": ["rgb_array"], "render_fps": 4, "autoreset_mode": "NextStep"}
+    ERROR_POLL_INTERVAL = 32
 
     def __init__(self, num_envs: int = 1, dataset: FloorMapDataset | None = None, render_mode: str = "rgb_array",
                  static_map: bool = False, lidar_beam_count: int = 8, lidar_range: float = 5,
@@ -130,6 +131,7 @@ class LIDARLocalization2DVectorEnv:
             loss=t.zeros(n, dtype=t.float32, device=dev),
             info_mask=t.zeros(n, dtype=t.bool, device=dev),
             map_idx_out=t.zeros(n, dtype=t.int64, device=dev),
+            reset_mask=t.zeros(n, dtype=t.bool, device=dev),
             err=t.zeros(1, dtype=t.int32, device=dev),
         )
         T = self._t
@@ -138,7 +140,8 @@ class LIDARLocalization2DVectorEnv:
         self._out = N.LidarOutputs(N.ptr(T["lidar"]), N.ptr(T["odometry"]), N.ptr(T["time_step"]),
                                    N.ptr(T["map_obs"]), N.ptr(T["reward"]), N.ptr(T["terminated"]),
                                    N.ptr(T["truncated"]), N.ptr(T["base_reward"]), N.ptr(T["target"]),
-                                   N.ptr(T["loss"]), N.ptr(T["info_mask"]), N.ptr(T["map_idx_out"]), N.ptr(T["err"]))
+                                   N.ptr(T["loss"]), N.ptr(T["info_mask"]), N.ptr(T["map_idx_out"]),
+                                   N.ptr(T["reset_mask"]), N.ptr(T["err"]))
         self._err_host = t.zeros(1, dtype=t.int32).pin_memory()
         self._err_event = t.cuda.Event()
         self._err_pending = False
@@ -146,6 +149,7 @@ class LIDARLocalization2DVectorEnv:
         self._seeded = False
         self._closed = False
         self._kernel_events = None
+        self._steps_since_poll = 0
         N.check(L.apg_lidar_init(ctypes.byref(self._cfg), ctypes.byref(self._state), self._stream()), "apg_lidar_init")
 
     # ------------------------------------------------------------------ helpers
@@ -202,9 +206,15 @@ class LIDARLocalization2DVectorEnv:
             self._raise_error_bits(bits)
 
     def _post_launch_error_copy(self):
+        """Lazy error reporting: every ERROR_POLL_INTERVAL steps copy the device error word to pinned
+        host memory (async) and raise once that copy has landed; strict mode checks every step."""
         if self.strict_errors:
             self.check_errors(block=True)
             return
+        self._steps_since_poll += 1
+        if self._err_pending or self._steps_since_poll < self.ERROR_POLL_INTERVAL:
+            return
+        self._steps_since_poll = 0
         self._err_host.copy_(self._t["err"], non_blocking=True)
         self._err_event.record()
         self._err_pending = True
@@ -231,7 +241,7 @@ class LIDARLocalization2DVectorEnv:
             return self._to_numpy_obs(), {"map_idx": T["map_idx_out"].cpu().numpy().astype(np.int64),
                                           "_map_idx": np.ones(self.num_envs, dtype=bool)}
         self._post_launch_error_copy()
-        return self._obs_out(), {"map_idx": T["map_idx_out"], "_map_idx": torch_ones_like_mask(T["info_mask"])}
+        return self._obs_out(), {"map_idx": T["map_idx_out"], "_map_idx": T["reset_mask"]}
 
     def step(self, action):
         import torch
@@ -277,7 +287,7 @@ class LIDARLocalization2DVectorEnv:
                 "prediction": {"target": c(T["target"]), "_target": c(mask), "loss": c(T["loss"]),
                                "_loss": c(mask)},
                 "_prediction": c(mask),
-                "map_idx": c(T["map_idx_out"]), "_map_idx": ~mask}
+                "map_idx": c(T["map_idx_out"]), "_map_idx": c(T["reset_mask"])}
         return self._obs_out(), c(T["reward"]), c(T["terminated"]), c(T["truncated"]), info
 
     # ------------------------------------------------------------------ output assembly
@@ -320,7 +330,7 @@ class LIDARLocalization2DVectorEnv:
             loss = np.where(mask, T["loss"].cpu().numpy(), np.float32(0))
             info["prediction"] = {"target": tgt, "_target": mask.copy(), "loss": loss, "_loss": mask.copy()}
             info["_prediction"] = mask.copy()
-        reset_mask = ~mask
+        reset_mask = T["reset_mask"].cpu().numpy()
         if reset_mask.any():
             info["map_idx"] = np.where(reset_mask, T["map_idx_out"].cpu().numpy(), 0).astype(np.int64)
             info["_map_idx"] = reset_mask
@@ -340,9 +350,3 @@ class LIDARLocalization2DVectorEnv:
         return (f"LIDARLocalization2DVectorEnv(num_envs={self.num_envs}, {kind} "
                 f"{self.dataset.map_width}x{self.dataset.map_height}, static={self.static_map}, "
                 f"beams={self.lidar_beam_count}, device={self.device})")
-
-
-def torch_ones_like_mask(m):
-    import torch
-
-    return torch.ones_like(m, dtype=torch.bool)

@@ -96,7 +96,8 @@ int validate(const apg_lidar_config *c) {
     return fail(APG_E_INVALID, "unknown map kind");
   }
   if (c->beams <= 0 || c->beams > 4096) return fail(APG_E_INVALID, "beams must be in [1, 4096]");
-  if (!(c->lidar_range > 0.0f) || c->lidar_range > 1000.0f) return fail(APG_E_INVALID, "bad lidar_range");
+  if (!(c->lidar_range > 0.0f) || c->lidar_range > 10.0f)
+    return fail(APG_E_INVALID, "lidar_range must be in (0, 10] (occupancy window of the fused step kernel)");
   if (c->step_limit <= 0) return fail(APG_E_INVALID, "step_limit must be positive");
   return APG_OK;
 }
@@ -218,7 +219,11 @@ struct StepParams {
   float range, loss_scale, loss_offset;
 };
 
-template <bool WINDOW>
+// Occupancy window per env, staged in LDS from the PRE-move position p0: columns/rows
+// [floor(p0) - R - 6, +32) x [.., + 2R + 12).  A step moves the agent by at most ~2 cells
+// (clamped move <= 1, slide <= 1), and every cell a scan of length <= R from the new position can
+// touch lies within [floor(p) - R - 2, floor(p) + R + 1], so both the move scans and all beams
+// read only this window (R <= 10 => 2R + 12 <= 32 rows).
 __global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_lidar_state S,
                                                              const float *__restrict__ act,
                                                              const float *__restrict__ pred,
@@ -230,17 +235,39 @@ __global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_l
   const int base = blockIdx.x * EPB;
   const size_t words = (size_t)P.h * P.wpr;
 
+  // ---------------- phase 0: window origins from the pre-move positions
+  if (tid < EPB) {
+    const int e = base + tid;
+    if (e < P.n) {
+      s_x0[tid] = (int)floorf(S.pos[2 * e]) - P.R - 6;
+      s_y0[tid] = (int)floorf(S.pos[2 * e + 1]) - P.R - 6;
+    }
+  }
+  __syncthreads();
+  for (int r = tid; r < EPB * P.wrows; r += STEP_THREADS) {
+    const int el = r / P.wrows, row = r - el * P.wrows;
+    const int e = base + el;
+    uint32_t v = 0;
+    if (e < P.n) {
+      const int y = s_y0[el] + row;
+      if ((unsigned)y < (unsigned)P.h)
+        v = extract_window_row(S.occ + (P.is_static ? 0 : e * words) + (size_t)y * P.wpr, P.wpr, s_x0[el]);
+    }
+    s_win[el * MAX_WIN_ROWS + row] = v;
+  }
+  __syncthreads();
+
   // ---------------- phase 1: one lane per env
   if (tid < EPB) {
     const int e = base + tid;
     uint32_t errbits = 0;
     if (e < P.n) {
+      const RowsWindow rw{&s_win[tid * MAX_WIN_ROWS], s_x0[tid], s_y0[tid], P.wrows};
       uint8_t f = S.flags[e];
+      const bool was_reset = f & F_JUST_RESET;
       float pos0 = S.pos[2 * e], pos1 = S.pos[2 * e + 1];
-      const uint64_t *rows = S.occ + (P.is_static ? 0 : e * words);
-      const OccGlobal og{rows, P.h, P.w, P.wpr};
       const float mapw = (float)P.w, maph = (float)P.h;
-      if (f & F_JUST_RESET) {  // NEXT_STEP autoreset: this env returned reset obs, reward 0
+      if (was_reset) {  // NEXT_STEP autoreset: this env returned reset obs, reward 0
         O.reward[e] = 0.0;
         O.terminated[e] = 0;
         O.truncated[e] = 0;
@@ -278,7 +305,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_l
           if (total > 0.0f) {
             dirx = f32_div(dirx, total);
             diry = f32_div(diry, total);
-            const float d = lidar_scan(og, pos0, pos1, tx, ty).dist;
+            const float d = lidar_scan(rw, pos0, pos1, tx, ty).dist;
             pos0 = __fadd_rn(pos0, __fmul_rn(dirx, d));
             pos1 = __fadd_rn(pos1, __fmul_rn(diry, d));
             const float rem = __fsub_rn(total, d);
@@ -287,8 +314,8 @@ __global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_l
               const bool kx = rvx > 1e-5f, ky = rvy > 1e-5f;
               if (kx || ky) {
                 const float c0x = kx ? rvx : rvy, c1y = ky ? rvy : rvx;  // eye(2) * kept
-                const float d0 = lidar_scan(og, pos0, pos1, __fadd_rn(pos0, c0x), __fadd_rn(pos1, 0.0f)).dist;
-                const float d1 = lidar_scan(og, pos0, pos1, __fadd_rn(pos0, 0.0f), __fadd_rn(pos1, c1y)).dist;
+                const float d0 = lidar_scan(rw, pos0, pos1, __fadd_rn(pos0, c0x), __fadd_rn(pos1, 0.0f)).dist;
+                const float d1 = lidar_scan(rw, pos0, pos1, __fadd_rn(pos0, 0.0f), __fadd_rn(pos1, c1y)).dist;
                 float cx, cy, dd;
                 if (d0 > 0.0f) {
                   cx = c0x;
@@ -335,6 +362,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_l
         }
       }
       S.flags[e] = f;
+      if (O.reset_mask) O.reset_mask[e] = was_reset;
       // odometry (:263-270) and TimeLimit time_step (time_limit.py:113-116)
       const float ox = __fsub_rn(pos0, S.init_pos[2 * e]), oy = __fsub_rn(pos1, S.init_pos[2 * e + 1]);
       O.odometry[2 * e] = __fsub_rn(__fmul_rn(f32_div(__fadd_rn(ox, mapw), __fadd_rn(mapw, mapw)), 2.0f), 1.0f);
@@ -342,10 +370,6 @@ __global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_l
       O.time_step[e] = (float)(2.0 * (double)S.elapsed[e] / (double)P.step_limit - 1.0);
       s_pos[tid][0] = pos0;
       s_pos[tid][1] = pos1;
-      if (WINDOW) {
-        s_x0[tid] = (int)floorf(pos0) - P.R - 2;
-        s_y0[tid] = (int)floorf(pos1) - P.R - 2;
-      }
     }
     // one atomic per wave for the error word
     const unsigned long long any = __ballot(errbits != 0);
@@ -357,39 +381,16 @@ __global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_l
   }
   __syncthreads();
 
-  // ---------------- phase 2: stage occupancy windows, then one lane per beam
-  if (WINDOW) {
-    for (int r = tid; r < EPB * P.wrows; r += STEP_THREADS) {
-      const int el = r / P.wrows, row = r - el * P.wrows;
-      const int e = base + el;
-      uint32_t v = 0;
-      if (e < P.n) {
-        const int y = s_y0[el] + row;
-        if ((unsigned)y < (unsigned)P.h) {
-          const uint64_t *rows = S.occ + (P.is_static ? 0 : e * words) + (size_t)y * P.wpr;
-          v = extract_window_row(rows, P.wpr, s_x0[el]);
-        }
-      }
-      s_win[el * MAX_WIN_ROWS + row] = v;
-    }
-    __syncthreads();
-  }
-  const float inv_range_num = P.range;
+  // ---------------- phase 2: one lane per beam
   for (int r = tid; r < EPB * P.beams; r += STEP_THREADS) {
     const int el = r / P.beams, beam = r - el * P.beams;
     const int e = base + el;
     if (e >= P.n) break;
     const float px = s_pos[el][0], py = s_pos[el][1];
     const float qx = __fadd_rn(px, S.beam_dirs[2 * beam]), qy = __fadd_rn(py, S.beam_dirs[2 * beam + 1]);
-    float d;
-    if (WINDOW) {
-      const OccWindow ow{&s_win[el * MAX_WIN_ROWS], s_x0[el], s_y0[el], P.wrows};
-      d = lidar_scan(ow, px, py, qx, qy).dist;
-    } else {
-      const OccGlobal og{S.occ + (P.is_static ? 0 : e * words), P.h, P.w, P.wpr};
-      d = lidar_scan(og, px, py, qx, qy).dist;
-    }
-    const float v = f32_div(d, inv_range_num);
+    const RowsWindow rw{&s_win[el * MAX_WIN_ROWS], s_x0[el], s_y0[el], P.wrows};
+    const float d = lidar_scan(rw, px, py, qx, qy).dist;
+    const float v = f32_div(d, P.range);
     O.lidar[(size_t)e * P.beams + beam] = fminf(fmaxf(v, -1.0f), 1.0f);
   }
 }
@@ -398,8 +399,9 @@ __global__ void k_scan_batch(const uint64_t *occ, const int32_t *map_index, int 
                              const float *seg, int n, float *dist, int32_t *kind) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const OccGlobal og{occ + (size_t)map_index[i] * h * wpr, h, w, wpr};
-  ScanOut o = lidar_scan(og, seg[4 * i], seg[4 * i + 1], seg[4 * i + 2], seg[4 * i + 3]);
+  const float px = seg[4 * i], py = seg[4 * i + 1], qx = seg[4 * i + 2], qy = seg[4 * i + 3];
+  const RowsGlobal rg{occ + (size_t)map_index[i] * h * wpr, h, wpr, (int)floorf(fminf(px, qx)) - 1};
+  ScanOut o = lidar_scan(rg, px, py, qx, qy);
   dist[i] = o.dist;
   if (kind) kind[i] = o.kind;
 }
@@ -437,16 +439,11 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   P.step_limit = cfg->step_limit;
   P.is_static = cfg->is_static;
   P.R = (int)ceilf(cfg->lidar_range);
-  P.wrows = 2 * P.R + 4;
+  P.wrows = 2 * P.R + 12;
   P.range = cfg->lidar_range;
   P.loss_scale = cfg->loss_scale;
   P.loss_offset = cfg->loss_offset;
-  const bool window = P.wrows <= MAX_WIN_ROWS && (2 * P.R + 4) <= 32;
-  const int grid = grid_for(P.n, EPB);
-  if (window)
-    hipLaunchKernelGGL(k_lidar_step<true>, dim3(grid), dim3(STEP_THREADS), 0, s, P, *st, act, pred, *out);
-  else
-    hipLaunchKernelGGL(k_lidar_step<false>, dim3(grid), dim3(STEP_THREADS), 0, s, P, *st, act, pred, *out);
+  hipLaunchKernelGGL(k_lidar_step, dim3(grid_for(P.n, EPB)), dim3(STEP_THREADS), 0, s, P, *st, act, pred, *out);
   return check_launch("k_lidar_step");
 }
 
@@ -560,6 +557,7 @@ int apg_map_generate(int map_kind, const uint64_t *idx, int n, int h, int w, int
 int apg_lidar_scan_batch(const uint64_t *occ, const int32_t *map_index, int h, int w, const float *seg, int n,
                          float *dist, int32_t *kind, apg_stream_t stream) {
   if (n <= 0 || h <= 0 || w <= 0 || w > 128) return fail(APG_E_INVALID, "bad scan batch arguments");
+  // segments must span <= 28 columns (32-column row window); callers check this on the host
   hipLaunchKernelGGL(k_scan_batch, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, occ, map_index, h,
                      w, (w + 63) / 64, seg, n, dist, kind);
   return check_launch("k_scan_batch");

@@ -95,6 +95,7 @@ typedef struct apg_lidar_outputs {
   float *loss;         /* [N] info["prediction"]["loss"] */
   uint8_t *info_mask;  /* [N] 1 where the step info carries base_reward/prediction (0 on autoreset) */
   uint64_t *map_idx;   /* [N] info["map_idx"] of envs that reset this step (others untouched) or NULL */
+  uint8_t *reset_mask; /* [N] 1 where the env auto-reset this step (info["_map_idx"]) or NULL */
   uint32_t *err;       /* [1] OR-ed APG_ERR_* bits (never cleared by the library) */
 } apg_lidar_outputs;
 
