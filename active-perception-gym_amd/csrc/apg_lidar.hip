@@ -3,7 +3,7 @@
 //   k_lidar_reset   one thread per env: reseed (reset(seed)), next map index from the
 //                   DatasetIterator stream, rooms/maze generation, start-cell draw
 //                   (lidar_localization2d.py:293-315, :547-557; dataset_iterator.py:26-32)
-//   k_map_obs       one wave per env that reset: bit-packed map -> float32 map obs (walls 1/255, :299)
+//                   The same wave then rewrites the float32 map obs of each env that reset (:299).
 //   k_lidar_step    64 envs per 256-thread workgroup.  Phase 1 (lane = env): autoreset bookkeeping,
 //                   NaN check, reward, move + collide + slide, termination, target, normalized MSE,
 //                   TimeLimit (lidar_localization2d.py:317-389, time_limit.py:118-139,
@@ -131,14 +131,9 @@ APG_DEV int place_start(Pcg64 &rng, const uint64_t *rows, int h, int w, int wpr,
   return -1;
 }
 
-APG_DEV int gen_map(const Geo &g, Pcg64 &r, uint64_t *occ, uint64_t *scratch, uint16_t *stack,
-                    size_t stride, const BinomTable &bt) {
-  Bits occb{occ, g.wpr};
-  if (g.kind == APG_MAP_ROOMS) {
-    Bits door{scratch, g.wpr};
-    return rooms_generate(r, occb, door, g.h, g.max_rooms, g.door_width, bt);
-  }
-  return maze_generate(r, occb, g.h, g.w, g.bp, stack, stride, g.frames);
+APG_DEV int gen_map(const Geo &g, Pcg64 &r, uint64_t *occ, uint16_t *stack, size_t stride, const BinomTable &bt) {
+  if (g.kind == APG_MAP_ROOMS) return rooms_generate(r, occ, g.wpr, g.h, g.max_rooms, g.door_width, bt);
+  return maze_generate(r, Bits{occ, g.wpr}, g.h, g.w, g.bp, stack, stride, g.frames);
 }
 
 // ------------------------------------------------------------------ kernels
@@ -148,68 +143,85 @@ __global__ void k_map_generate(Geo g, const uint64_t *idx, int n, uint64_t *occ,
   if (i >= n) return;
   Pcg64 r = seed_pcg64(idx[i]);
   const size_t words = (size_t)g.h * g.wpr;
-  int rc = gen_map(g, r, occ + i * words, scratch ? scratch + i * words : nullptr, stack ? stack + i : nullptr,
-                   (size_t)n, bt);
+  int rc = gen_map(g, r, occ + i * words, stack ? stack + i : nullptr, (size_t)n, bt);
   if (rc != 0 && err) atomicOr(err, APG_ERR_MAPGEN);
 }
 
-__global__ void k_lidar_reset(Geo g, apg_lidar_state S, uint64_t seed, int use_seed, int all,
-                              uint64_t *out_map_idx, uint32_t *err, BinomTable bt) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= g.n) return;
-  uint8_t f = S.flags[e];
-  if (!all && !(f & F_AUTORESET)) return;
-  Pcg64 rng;
-  Pcg64 it;
-  if (use_seed) {
-    rng = seed_pcg64(seed + (uint64_t)e);
-    if (!g.is_static) it = seed_pcg64(bounded_u64(rng, 0x100000000ULL));  // integers(0, 2**32, endpoint=True)
-  } else {
-    rng = *reinterpret_cast<const Pcg64 *>(&S.rng[e]);
-    if (!g.is_static) it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[e]);
-  }
+// One wave per 64 envs.  Envs pending autoreset (or all, for reset(seed)) draw their next map
+// index, generate the map, draw the start cell; then the wave cooperatively rewrites the float32
+// map observation of each env that reset (coalesced float4 stores).  Waves with nothing to reset
+// exit after one flag load.
+__global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, uint64_t seed, int use_seed,
+                                                    int all, uint64_t *out_map_idx, float *map_obs, uint32_t *err,
+                                                    BinomTable bt) {
+  const int base = blockIdx.x * 64, lane = threadIdx.x;
+  const int e = base + lane;
+  const uint8_t f = e < g.n ? S.flags[e] : 0;
+  const bool active = e < g.n && (all || (f & F_AUTORESET));
+  const unsigned long long todo = __ballot(active);
+  if (todo == 0ULL) return;
   const size_t words = (size_t)g.h * g.wpr;
-  const uint64_t *rows = S.occ;
-  uint64_t midx;
-  if (!g.is_static) {
-    midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
-    uint64_t *own = S.occ + e * words;
-    Pcg64 map_rng = seed_pcg64(midx);  // FloorMapDataset*.get_data_point: default_rng(idx)
-    int rc = gen_map(g, map_rng, own, S.scratch ? S.scratch + e * words : nullptr, S.stack ? S.stack + e : nullptr,
-                     (size_t)g.n, bt);
-    if (rc != 0) atomicOr(err, APG_ERR_MAPGEN);
-    rows = own;
-    *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
-    S.map_idx[e] = midx;
-  } else {
-    midx = S.map_idx[e];
+  if (active) {
+    Pcg64 rng;
+    Pcg64 it;
+    if (use_seed) {
+      rng = seed_pcg64(seed + (uint64_t)e);
+      if (!g.is_static) it = seed_pcg64(bounded_u64(rng, 0x100000000ULL));  // integers(0, 2**32, endpoint=True)
+    } else {
+      rng = *reinterpret_cast<const Pcg64 *>(&S.rng[e]);
+      if (!g.is_static) it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[e]);
+    }
+    const uint64_t *rows = S.occ;
+    uint64_t midx;
+    if (!g.is_static) {
+      midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
+      uint64_t *own = S.occ + e * words;
+      Pcg64 map_rng = seed_pcg64(midx);  // FloorMapDataset*.get_data_point: default_rng(idx)
+      if (gen_map(g, map_rng, own, S.stack ? S.stack + e : nullptr, (size_t)g.n, bt) != 0)
+        atomicOr(err, APG_ERR_MAPGEN);
+      rows = own;
+      *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
+      S.map_idx[e] = midx;
+    } else {
+      midx = S.map_idx[e];
+    }
+    float px = 0.5f, py = 0.5f;
+    if (place_start(rng, rows, g.h, g.w, g.wpr, px, py) != 0) atomicOr(err, APG_ERR_MAPGEN);
+    S.pos[2 * e] = px;
+    S.pos[2 * e + 1] = py;
+    S.init_pos[2 * e] = px;
+    S.init_pos[2 * e + 1] = py;
+    S.elapsed[e] = 0;
+    S.flags[e] = (uint8_t)((f & F_AUTORESET) | F_JUST_RESET | F_FIRST);
+    *reinterpret_cast<Pcg64 *>(&S.rng[e]) = rng;
+    if (out_map_idx) out_map_idx[e] = midx;
   }
-  float px = 0.5f, py = 0.5f;
-  if (place_start(rng, rows, g.h, g.w, g.wpr, px, py) != 0) atomicOr(err, APG_ERR_MAPGEN);
-  S.pos[2 * e] = px;
-  S.pos[2 * e + 1] = py;
-  S.init_pos[2 * e] = px;
-  S.init_pos[2 * e + 1] = py;
-  S.elapsed[e] = 0;
-  S.flags[e] = (uint8_t)((f & F_AUTORESET) | F_JUST_RESET | F_FIRST);
-  *reinterpret_cast<Pcg64 *>(&S.rng[e]) = rng;
-  if (out_map_idx) out_map_idx[e] = midx;
-}
-
-__global__ void k_map_obs(int n, int h, int w, int wpr, const uint8_t *flags, const uint64_t *occ,
-                          float *map_obs, int all) {
-  const int lane = threadIdx.x & 63;
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int nwaves = (gridDim.x * blockDim.x) >> 6;
-  const float wall = 1.0f / 255.0f;
-  const int cells = h * w;
-  for (int e = wave; e < n; e += nwaves) {
-    if (!all && !(flags[e] & F_JUST_RESET)) continue;
-    const uint64_t *rows = occ + (size_t)e * h * wpr;
-    float *dst = map_obs + (size_t)e * cells;
-    for (int k = lane; k < cells; k += 64) {
-      const int y = k / w, x = k - y * w;
-      dst[k] = ((rows[y * wpr + (x >> 6)] >> (x & 63)) & 1ULL) ? wall : 0.0f;
+  if (g.is_static || !map_obs) return;
+  __syncthreads();  // workgroup = this wave: the maps written above are visible to every lane
+  const float wall = 1.0f / 255.0f;  // bool map / 255 (lidar_localization2d.py:299)
+  const int cells = g.h * g.w;
+  unsigned long long m = todo;
+  while (m) {
+    const int j = __ffsll((long long)m) - 1;
+    m &= m - 1ULL;
+    const uint64_t *rows = S.occ + (size_t)(base + j) * words;
+    float *dst = map_obs + (size_t)(base + j) * cells;
+    if ((cells & 3) == 0) {
+      for (int k4 = lane; k4 < cells / 4; k4 += 64) {
+        float4 v;
+        float *pv = reinterpret_cast<float *>(&v);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int k = 4 * k4 + u, y = k / g.w, x = k - y * g.w;
+          pv[u] = ((rows[y * g.wpr + (x >> 6)] >> (x & 63)) & 1ULL) ? wall : 0.0f;
+        }
+        reinterpret_cast<float4 *>(dst)[k4] = v;
+      }
+    } else {
+      for (int k = lane; k < cells; k += 64) {
+        const int y = k / g.w, x = k - y * g.w;
+        dst[k] = ((rows[y * g.wpr + (x >> 6)] >> (x & 63)) & 1ULL) ? wall : 0.0f;
+      }
     }
   }
 }
@@ -447,16 +459,6 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   return check_launch("k_lidar_step");
 }
 
-int launch_map_obs(const apg_lidar_config *cfg, const apg_lidar_state *st, const apg_lidar_outputs *out,
-                   int all, hipStream_t s) {
-  if (cfg->is_static || !out->map_obs) return APG_OK;
-  const int wpr = (cfg->width + 63) / 64;
-  int waves = cfg->num_envs < 4096 ? cfg->num_envs : 4096;
-  hipLaunchKernelGGL(k_map_obs, dim3(grid_for(waves * 64, 256)), dim3(256), 0, s, cfg->num_envs, cfg->height,
-                     cfg->width, wpr, st->flags, st->occ, out->map_obs, all);
-  return check_launch("k_map_obs");
-}
-
 }  // namespace
 
 extern "C" {
@@ -473,8 +475,7 @@ int apg_lidar_query_sizes(const apg_lidar_config *cfg, apg_lidar_state_sizes *o)
   o->wpr = g.wpr;
   o->maze_frames = g.frames;
   o->occ_bytes = (g.is_static ? 1 : (size_t)g.n) * words * sizeof(uint64_t);
-  o->scratch_bytes = (!g.is_static && g.kind == APG_MAP_ROOMS) ? (size_t)g.n * words * sizeof(uint64_t)
-                     : (g.is_static && g.kind == APG_MAP_ROOMS) ? words * sizeof(uint64_t) : 0;
+  o->scratch_bytes = 0;  // reserved (rooms maps are painted from primitives, no scratch plane)
   o->stack_bytes = g.kind == APG_MAP_MAZE ? (size_t)g.frames * (g.is_static ? 1 : (size_t)g.n) * sizeof(uint16_t) : 0;
   return APG_OK;
 }
@@ -499,9 +500,8 @@ int apg_lidar_reset(const apg_lidar_config *cfg, const apg_lidar_state *st, uint
   hipStream_t s = (hipStream_t)stream;
   Geo g = make_geo(cfg);
   hipLaunchKernelGGL(k_lidar_reset, dim3(grid_for(g.n, 64)), dim3(64), 0, s, g, *st, seed, use_seed, 1,
-                     out->map_idx, out->err, make_binom_table());
+                     out->map_idx, out->map_obs, out->err, make_binom_table());
   if ((rc = check_launch("k_lidar_reset"))) return rc;
-  if ((rc = launch_map_obs(cfg, st, out, 1, s))) return rc;
   return launch_step_kernel(cfg, st, nullptr, nullptr, out, s);
 }
 
@@ -514,9 +514,8 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
   hipStream_t s = (hipStream_t)stream;
   Geo g = make_geo(cfg);
   hipLaunchKernelGGL(k_lidar_reset, dim3(grid_for(g.n, 64)), dim3(64), 0, s, g, *st, (uint64_t)0, 0, 0,
-                     out->map_idx, out->err, make_binom_table());
+                     out->map_idx, out->map_obs, out->err, make_binom_table());
   if ((rc = check_launch("k_lidar_reset"))) return rc;
-  if ((rc = launch_map_obs(cfg, st, out, 0, s))) return rc;
   if (ev_begin && hipEventRecord((hipEvent_t)ev_begin, s) != hipSuccess) return fail(APG_E_LAUNCH, "hipEventRecord");
   rc = launch_step_kernel(cfg, st, action, prediction, out, s);
   if (rc == APG_OK && ev_end && hipEventRecord((hipEvent_t)ev_end, s) != hipSuccess)
@@ -546,7 +545,6 @@ int apg_map_generate(int map_kind, const uint64_t *idx, int n, int h, int w, int
   c.branching_prob = branching_prob;
   int rc = validate(&c);
   if (rc) return rc;
-  if (map_kind == APG_MAP_ROOMS && !scratch) return fail(APG_E_INVALID, "rooms maps need scratch");
   if (map_kind == APG_MAP_MAZE && !stack) return fail(APG_E_INVALID, "maze maps need stack");
   Geo g = make_geo(&c);
   hipLaunchKernelGGL(k_map_generate, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, g, idx, n, occ,

@@ -95,23 +95,21 @@ APG_DEV uint64_t pack_task(int y0, int x0, int t, int n0, int n1, int mr) {
          ((uint64_t)n1 << 25) | ((uint64_t)mr << 33);
 }
 
-// Returns 0 on success. wall/door: [h][wpr] words, caller-zeroed not required.
-APG_DEV int rooms_generate(Pcg64 &r, Bits wall, Bits door, int m, int max_rooms, int door_width,
-                           const BinomTable &bt) {
+// The reference paints walls (`room[wp] = where(room[wp] != -1, 1, -1)`) and doors (`= -1`) into an
+// int8 map in task order, then maps -1 to free.  A cell ends up a wall iff it is on the border or
+// covered by some wall segment, and covered by no door block: paint order never matters.  So the
+// generator only records the segments and blocks (in map coordinates) and paints rows at the end,
+// with the final 50% transpose applied to the primitives instead of the bitmap.
+struct RoomsPrims {
+  int nw, nd;
+  uint32_t wall[16];  // vertical << 31 | fixed << 16 | start << 8 | len   (len <= 255)
+  uint32_t door[16];  // r0 << 24 | c0 << 16 | h << 8 | w
+};
+
+APG_DEV int rooms_primitives(Pcg64 &r, int m, int max_rooms, int door_width, const BinomTable &bt,
+                             RoomsPrims &P) {
   const int min_size = door_width + 2;
-  for (int y = 0; y < m; y++)
-    for (int k = 0; k < wall.wpr; k++) {
-      wall.w[y * wall.wpr + k] = 0;
-      door.w[y * door.wpr + k] = 0;
-    }
-  for (int x = 0; x < m; x++) {
-    wall.set(0, x);
-    wall.set(m - 1, x);
-  }
-  for (int y = 0; y < m; y++) {
-    wall.set(y, 0);
-    wall.set(y, m - 1);
-  }
+  P.nw = P.nd = 0;
   uint64_t stack[64];
   int sp = 0;
   stack[sp++] = pack_task(1, 1, 0, m - 2, m - 2, max_rooms);
@@ -124,7 +122,7 @@ APG_DEV int rooms_generate(Pcg64 &r, Bits wall, Bits door, int m, int max_rooms,
     if (mrl <= 1) continue;
     if (mrl > 16) return -2;
     const int k = (int)binomial_inv(r, mrl - 2, bt) + 2;
-    int64_t cap[16], sizes[16], starts[16], ends[16], doors[16];
+    int64_t cap[16], sizes[16], starts[16], ends[16];
     distribute_integers(r, mrl, k, cap);
     distribute_integers(r, n0 - (int64_t)k * (1 + min_size) + 1, k, sizes);
     int64_t acc = 0;
@@ -135,28 +133,22 @@ APG_DEV int rooms_generate(Pcg64 &r, Bits wall, Bits door, int m, int max_rooms,
     }
     starts[0] = 0;
     for (int i = 1; i < k; i++) starts[i] = ends[i - 1] + 2;
-    for (int i = 0; i < k - 1; i++) doors[i] = integers(r, 0, n1 - door_width);
-    // walls: room[wall_positions] = where(room != -1, 1, -1)
+    if (P.nw + k - 1 > 16) return -4;
     for (int i = 1; i < k; i++) {
       const int wp = (int)(starts[i] - 1);
-      if (wp < 0 || wp >= n0) return -3;
-      for (int j = 0; j < n1; j++) {
-        const int y = t ? y0 + j : y0 + wp, x = t ? x0 + wp : x0 + j;
-        if (!door.get(y, x)) wall.set(y, x);
+      const int dp = (int)integers(r, 0, n1 - door_width);
+      if (wp - (door_width - 1) < 0 || wp + (door_width - 1) >= n0 || dp + door_width > n1) return -3;
+      // wall: the whole view row wp; door: view rows wp-dw+1 .. wp+dw-1, columns dp .. dp+dw-1
+      const int lo = wp - (door_width - 1), span = 2 * door_width - 1;
+      if (t == 0) {
+        P.wall[P.nw++] = ((uint32_t)(y0 + wp) << 16) | ((uint32_t)x0 << 8) | (uint32_t)n1;
+        P.door[P.nd++] = ((uint32_t)(y0 + lo) << 24) | ((uint32_t)(x0 + dp) << 16) | ((uint32_t)span << 8) |
+                         (uint32_t)door_width;
+      } else {
+        P.wall[P.nw++] = (1u << 31) | ((uint32_t)(x0 + wp) << 16) | ((uint32_t)y0 << 8) | (uint32_t)n1;
+        P.door[P.nd++] = ((uint32_t)(y0 + dp) << 24) | ((uint32_t)(x0 + lo) << 16) | ((uint32_t)door_width << 8) |
+                         (uint32_t)span;
       }
-    }
-    // doors: cells (wp +- a, dp + b) become -1
-    for (int i = 1; i < k; i++) {
-      const int wp = (int)(starts[i] - 1), dp = (int)doors[i - 1];
-      for (int a = 0; a < door_width; a++)
-        for (int b = 0; b < door_width; b++)
-          for (int s = 0; s < 2; s++) {
-            const int vi = s ? wp - a : wp + a, vj = dp + b;
-            if (vi < 0 || vi >= n0 || vj >= n1) return -3;
-            const int y = t ? y0 + vj : y0 + vi, x = t ? x0 + vi : x0 + vj;
-            door.set(y, x);
-            wall.clr(y, x);
-          }
     }
     // children room[s:e+1].T, depth-first in order => push in reverse
     if (sp + k > 64) return -4;
@@ -168,14 +160,52 @@ APG_DEV int rooms_generate(Pcg64 &r, Bits wall, Bits door, int m, int max_rooms,
       stack[sp++] = pack_task(cy0, cx0, 1 - t, n1, (int)(e - s), (int)cap[i]);
     }
   }
-  if (integers(r, 0, 2) == 0) {  // map_int = map_int.T  (square maps only)
-    for (int y = 0; y < m; y++)
-      for (int x = 0; x < m; x++)
-        if (wall.get(x, y)) door.set(y, x); else door.clr(y, x);
-    for (int y = 0; y < m; y++)
-      for (int kk = 0; kk < wall.wpr; kk++) wall.w[y * wall.wpr + kk] = door.w[y * door.wpr + kk];
+  if (integers(r, 0, 2) == 0) {  // map_int = map_int.T: transpose the primitives
+    for (int i = 0; i < P.nw; i++) P.wall[i] ^= 1u << 31;
+    for (int i = 0; i < P.nd; i++) {
+      const uint32_t d = P.door[i];
+      P.door[i] = (((d >> 16) & 255u) << 24) | (((d >> 24) & 255u) << 16) | ((d & 255u) << 8) | ((d >> 8) & 255u);
+    }
   }
   return 0;
+}
+
+// bits [s, s+l) of the 64-bit word covering columns [64k, 64k+64)
+APG_DEV uint64_t span_mask(int s, int l, int k) {
+  const int lo = s > 64 * k ? s : 64 * k, hi = (s + l) < 64 * k + 64 ? s + l : 64 * k + 64;
+  if (hi <= lo) return 0ULL;
+  const int n = hi - lo;
+  return (n >= 64 ? ~0ULL : ((1ULL << n) - 1ULL)) << (lo - 64 * k);
+}
+
+// word k of map row y: border | walls & ~doors
+APG_DEV uint64_t rooms_row_word(const RoomsPrims &P, int m, int y, int k) {
+  uint64_t v = (y == 0 || y == m - 1) ? span_mask(0, m, k) : (span_mask(0, 1, k) | span_mask(m - 1, 1, k));
+  for (int i = 0; i < P.nw; i++) {
+    const uint32_t wl = P.wall[i];
+    const int fixed = (int)((wl >> 16) & 255u), st = (int)((wl >> 8) & 255u), len = (int)(wl & 255u);
+    if (wl >> 31) {
+      if (y >= st && y < st + len) v |= span_mask(fixed, 1, k);
+    } else if (y == fixed) {
+      v |= span_mask(st, len, k);
+    }
+  }
+  for (int i = 0; i < P.nd; i++) {
+    const uint32_t d = P.door[i];
+    const int r0 = (int)(d >> 24), c0 = (int)((d >> 16) & 255u), hh = (int)((d >> 8) & 255u), ww = (int)(d & 255u);
+    if (y >= r0 && y < r0 + hh) v &= ~span_mask(c0, ww, k);
+  }
+  return v;
+}
+
+// generate + paint: occ rows [m][wpr]
+APG_DEV int rooms_generate(Pcg64 &r, uint64_t *occ, int wpr, int m, int max_rooms, int door_width,
+                           const BinomTable &bt) {
+  RoomsPrims P;
+  const int rc = rooms_primitives(r, m, max_rooms, door_width, bt, P);
+  for (int y = 0; y < m; y++)
+    for (int k = 0; k < wpr; k++) occ[y * wpr + k] = rooms_row_word(P, m, y, k);
+  return rc;
 }
 
 // Maze: recursive carve() as an explicit DFS. Frame (u16): perm 4x2 bits | k << 8 | first << 11 |

@@ -39,7 +39,7 @@ def test_capi_validation_without_gpu():
                         branching_prob=1.0)
     sz = N.LidarSizes()
     assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0
-    assert sz.wpr == 1 and sz.occ_bytes == 4 * 64 * 8 and sz.scratch_bytes == 4 * 64 * 8 and sz.stack_bytes == 0
+    assert sz.wpr == 1 and sz.occ_bytes == 4 * 64 * 8 and sz.scratch_bytes == 0 and sz.stack_bytes == 0
     cfg.map_kind = N.APG_MAP_MAZE
     cfg.height = cfg.width = 127
     assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0
