@@ -206,6 +206,19 @@ APG_DEV int orient(double px, double py, double qx, double qy, double vx, double
   return orient_exact6(px, py, qx, qy, vx, vy);
 }
 
+// Same predicate for f32 p, q and integer lattice point (a, b): Shewchuk's filter evaluated in
+// float32 first (error bound (3 + 16 eps) eps * (|dl| + |dr|), eps = 2^-24), then the f64 path.
+APG_DEV int orient_lattice(float fpx, float fpy, float fqx, float fqy, int a, int b) {
+  const float fa = (float)a, fb = (float)b;
+  const float dl = __fmul_rn(__fsub_rn(fpx, fa), __fsub_rn(fqy, fb));
+  const float dr = __fmul_rn(__fsub_rn(fpy, fb), __fsub_rn(fqx, fa));
+  const float det = __fsub_rn(dl, dr);
+  const float bound = 1.7881398e-7f * __fadd_rn(fabsf(dl), fabsf(dr));
+  if (det > bound) return 1;
+  if (-det > bound) return -1;
+  return orient(fpx, fpy, fqx, fqy, (double)a, (double)b);
+}
+
 // GEOS algorithm::Intersection::intersection (midpoint-conditioned homogeneous formula).
 APG_DEV void geos_intersection(double p1x_, double p1y_, double p2x_, double p2y_, double q1x_,
                                double q1y_, double q2x_, double q2y_, double &ox, double &oy) {

@@ -69,20 +69,26 @@ APG_DEV ScanOut lidar_scan(const Rows &rows, float fpx, float fpy, float fqx, fl
   int cy = (sy < 0 && pyi) ? ipy - 1 : ipy;
   const int ivdi = colv ? 1 : 0, ivdj = colh ? 1 : 0;  // interval cells [cx - ivdi, cx] x [cy - ivdj, cy]
 
-  // previous node: type 0 = p, 1 = lattice (a, b), 2 = x-crossing on edge (a, b)-(a, b+1),
-  // 3 = y-crossing on edge (a, b)-(a+1, b)
+  // node descriptors: type 0 = p, 1 = lattice (a, b), 2 = x-crossing on edge (a, b)-(a, b+1),
+  // 3 = y-crossing on edge (a, b)-(a+1, b), 4 = q
   int pv_t = 0, pv_a = 0, pv_b = 0;
   bool pv_onb = quad_status(rows, pxi ? ipx - 1 : ipx, pxi ? 1 : 0, pyi ? ipy - 1 : ipy, pyi ? 1 : 0) == 1u;
   bool pv_left_in = false;
   bool cur_in = quad_status(rows, cx - ivdi, ivdi, cy - ivdj, ivdj) & 1u;
+  // The first line start and the first point are resolved after the loop (their coordinates are
+  // the only ones the LineString/Point branches need); later ones (Multi* only) are rare and
+  // folded into running f32 minima on the spot.
   int n_lines = 0, n_points = 0;
-  double l0x = 0.0, l0y = 0.0;
-  float best_line = __builtin_inff(), best_point = __builtin_inff();
+  int l0_t = 0, l0_a = 0, l0_b = 0, p0_t = 0, p0_a = 0, p0_b = 0;
+  float later_line = __builtin_inff(), later_point = __builtin_inff();
 
   auto node_coord = [&](int t, int a, int b, double &x, double &y) {
     if (t == 0) {
       x = px;
       y = py;
+    } else if (t == 4) {
+      x = qx;
+      y = qy;
     } else if (t == 1) {
       x = (double)a;
       y = (double)b;
@@ -97,84 +103,110 @@ APG_DEV ScanOut lidar_scan(const Rows &rows, float fpx, float fpy, float fqx, fl
   };
   // close the piece [previous node, new node] (status cur_in)
   auto close_piece = [&]() {
-    if (cur_in || (pv_onb && !pv_left_in)) {
-      double x, y;
-      node_coord(pv_t, pv_a, pv_b, x, y);
-      const float d = dist_f32(x, y);
-      if (cur_in) {
-        if (n_lines == 0) {
-          l0x = x;
-          l0y = y;
-        }
-        n_lines++;
-        best_line = fminf(best_line, d);
+    if (cur_in) {
+      if (n_lines == 0) {
+        l0_t = pv_t;
+        l0_a = pv_a;
+        l0_b = pv_b;
       } else {
-        n_points++;
-        best_point = fminf(best_point, d);
+        double x, y;
+        node_coord(pv_t, pv_a, pv_b, x, y);
+        later_line = fminf(later_line, dist_f32(x, y));
       }
+      n_lines++;
+    } else if (pv_onb && !pv_left_in) {
+      if (n_points == 0) {
+        p0_t = pv_t;
+        p0_a = pv_a;
+        p0_b = pv_b;
+      } else {
+        double x, y;
+        node_coord(pv_t, pv_a, pv_b, x, y);
+        later_point = fminf(later_point, dist_f32(x, y));
+      }
+      n_points++;
     }
     pv_left_in = cur_in;
   };
 
   const int ntot = nxl + nyl;
   int xi = 0, yi = 0;
-  for (int it = 0; xi + yi < ntot; it++) {
+  while (xi + yi < ntot) {
     const int a = ax + sx * xi, b = by + sy * yi;
     const bool hx = xi < nxl, hy = yi < nyl;
     int c = hx ? -1 : 1;  // c < 0: x-crossing first, c > 0: y-crossing first, 0: both (lattice)
-    if (hx && hy) c = -orient(px, py, qx, qy, (double)a, (double)b) * sx * sy;
+    if (hx && hy) c = -orient_lattice(fpx, fpy, fqx, fqy, a, b) * sx * sy;
     const bool takex = c <= 0, takey = c >= 0;
-    const bool lattice = (takex && takey) || (takex && colh) || (takey && colv);
-    // closure quad of the crossing
+    // closure quad of the crossing: cells [i0, i0+di] x [j0, j0+dj]
     const int i0 = takex ? a - 1 : (colv ? ipx - 1 : cx);
     const int j0 = takey ? b - 1 : (colh ? ipy - 1 : cy);
-    const int di = (takex || colv) ? 1 : 0, dj = (takey || colh) ? 1 : 0;
-    const unsigned st = quad_status(rows, i0, di, j0, dj);
-    cx += takex ? sx : 0;
-    cy += takey ? sy : 0;
-    xi += takex ? 1 : 0;
-    yi += takey ? 1 : 0;
-    if (st == 1u) {  // on the boundary of U => node of the noded line
+    const bool di = takex || colv, dj = takey || colh;
+    const int sh = i0 - rows.x0;
+    const uint32_t r0 = rows.row(j0);
+    const uint32_t r1 = dj ? rows.row(j0 + 1) : r0;
+    const unsigned q0 = (r0 >> sh) & 3u, q1 = (r1 >> sh) & 3u, m = di ? 3u : 1u;
+    const bool onb = ((q0 | q1) & m) != 0u && ((q0 & q1 & m) != m);
+    const int ncx = cx + (takex ? sx : 0), ncy = cy + (takey ? sy : 0);
+    // status of the next open interval from the same quad: cell (ncx, ncy) (+ its collinear twin)
+    const unsigned u = (unsigned)(ncx - i0), v = (unsigned)(ncy - j0);
+    const unsigned rowv = v ? q1 : q0;
+    const bool in_after = colv ? (rowv & 3u) != 0u : (colh ? (((q0 | q1) >> u) & 1u) != 0u : ((rowv >> u) & 1u) != 0u);
+    if (onb) {  // boundary point => node of the noded line
       close_piece();
+      const bool lattice = (takex && takey) || (takex && colh) || (takey && colv);
       pv_t = lattice ? 1 : (takex ? 2 : 3);
       pv_a = takex ? a : (colv ? ipx : cx);
       pv_b = takey ? b : (colh ? ipy : cy);
       pv_onb = true;
     }
-    cur_in = quad_status(rows, cx - ivdi, ivdi, cy - ivdj, ivdj) & 1u;
+    cx = ncx;
+    cy = ncy;
+    xi += takex ? 1 : 0;
+    yi += takey ? 1 : 0;
+    cur_in = in_after;
   }
-  // q
+  // q: always a node
   const unsigned qst = quad_status(rows, qxi ? iqx - 1 : iqx, qxi ? 1 : 0, qyi ? iqy - 1 : iqy, qyi ? 1 : 0);
   close_piece();
-  if (qst == 1u && !pv_left_in) {
+  pv_t = 4;
+  pv_onb = qst == 1u;
+  if (pv_onb && !pv_left_in) {
+    if (n_points == 0) {
+      p0_t = 4;
+    } else {
+      later_point = fminf(later_point, dist_f32(qx, qy));
+    }
     n_points++;
-    best_point = fminf(best_point, dist_f32(qx, qy));
   }
 
   ScanOut o;
   const float full = norm_f32(__fsub_rn(fqx, fpx), __fsub_rn(fqy, fpy));
+  o.kind = SCAN_EMPTY;
+  o.dist = full;
   if (n_lines > 0 && n_points > 0) {
-    o.kind = SCAN_COLLECTION;
-    o.dist = full;
-  } else if (n_lines == 1) {
-    o.kind = SCAN_LINE;
-    const double dx = __dsub_rn(l0x, px), dy = __dsub_rn(l0y, py);
-    const double d = __dsub_rn(__dsqrt_rn(__fma_rn(dy, dy, __dmul_rn(dx, dx))), 1e-3);
-    o.dist = (float)(d > 0.0 ? d : 0.0);
-  } else if (n_lines > 1) {
-    o.kind = SCAN_MULTILINE;
-    const float d = __fsub_rn(best_line, 0.001f);
-    o.dist = d > 0.0f ? d : 0.0f;
+    o.kind = SCAN_COLLECTION;  // mixed points and lines: the reference's `else` branch (no hit)
+  } else if (n_lines > 0) {
+    double x, y;
+    node_coord(l0_t, l0_a, l0_b, x, y);
+    if (n_lines == 1) {
+      o.kind = SCAN_LINE;
+      const double dx = __dsub_rn(x, px), dy = __dsub_rn(y, py);
+      const double d = __dsub_rn(__dsqrt_rn(__fma_rn(dy, dy, __dmul_rn(dx, dx))), 1e-3);
+      o.dist = (float)(d > 0.0 ? d : 0.0);
+    } else {
+      o.kind = SCAN_MULTILINE;
+      const float d = __fsub_rn(fminf(dist_f32(x, y), later_line), 0.001f);
+      o.dist = d > 0.0f ? d : 0.0f;
+    }
   } else if (n_points == 1) {
     o.kind = SCAN_POINT;
     o.dist = 0.0f;
   } else if (n_points > 1) {
+    double x, y;
+    node_coord(p0_t, p0_a, p0_b, x, y);
     o.kind = SCAN_MULTIPOINT;
-    const float d = __fsub_rn(best_point, 0.001f);
+    const float d = __fsub_rn(fminf(dist_f32(x, y), later_point), 0.001f);
     o.dist = d > 0.0f ? d : 0.0f;
-  } else {
-    o.kind = SCAN_EMPTY;
-    o.dist = full;
   }
   return o;
 }
