@@ -214,9 +214,9 @@ APG_DEV int orient_lattice(float fpx, float fpy, float fqx, float fqy, int a, in
   const float dr = __fmul_rn(__fsub_rn(fpy, fb), __fsub_rn(fqx, fa));
   const float det = __fsub_rn(dl, dr);
   const float bound = 1.7881398e-7f * __fadd_rn(fabsf(dl), fabsf(dr));
-  if (det > bound) return 1;
-  if (-det > bound) return -1;
-  return orient(fpx, fpy, fqx, fqy, (double)a, (double)b);
+  int r = det > bound ? 1 : (-det > bound ? -1 : 0);
+  if (r == 0) r = orient(fpx, fpy, fqx, fqy, (double)a, (double)b);  // near-tie: f64 filter, then exact
+  return r;
 }
 
 // GEOS algorithm::Intersection::intersection (midpoint-conditioned homogeneous formula).

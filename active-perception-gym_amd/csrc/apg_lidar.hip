@@ -29,6 +29,8 @@ constexpr uint8_t F_AUTORESET = 1, F_JUST_RESET = 2, F_FIRST = 4;
 constexpr int EPB = 64;        // envs per step workgroup
 constexpr int STEP_THREADS = 256;
 constexpr int MAX_WIN_ROWS = 32;
+constexpr int WIN_STRIDE = MAX_WIN_ROWS + 1;  // LDS words per env window (+1: lanes = envs hit distinct banks)
+constexpr int MAX_STAGED_BEAMS = 64;          // lidar rows staged in LDS for coalesced stores
 
 thread_local char g_err[512] = "";
 
@@ -231,18 +233,19 @@ struct StepParams {
   float range, loss_scale, loss_offset;
 };
 
-// Occupancy window per env, staged in LDS from the PRE-move position p0: columns/rows
-// [floor(p0) - R - 6, +32) x [.., + 2R + 12).  A step moves the agent by at most ~2 cells
-// (clamped move <= 1, slide <= 1), and every cell a scan of length <= R from the new position can
-// touch lies within [floor(p) - R - 2, floor(p) + R + 1], so both the move scans and all beams
-// read only this window (R <= 10 => 2R + 12 <= 32 rows).
+// Occupancy window per env, staged in LDS from the PRE-move position p0: the 32 x 32 cells
+// [floor(p0) - 15, floor(p0) + 17)^2 (zero outside the map).  A step moves the agent by at most
+// ~2 cells (clamped move <= 1, slide <= 1), and every cell a scan of length <= R from the new
+// position p can touch lies within [floor(p) - R - 2, floor(p) + R + 1] (+1 column for the 2-bit
+// quad reads), i.e. within [floor(p0) - R - 5, floor(p0) + R + 5]: inside the window for R <= 10.
 __global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_lidar_state S,
                                                              const float *__restrict__ act,
                                                              const float *__restrict__ pred,
                                                              apg_lidar_outputs O) {
   __shared__ float s_pos[EPB][2];
   __shared__ int s_x0[EPB], s_y0[EPB];
-  __shared__ uint32_t s_win[EPB * MAX_WIN_ROWS];
+  __shared__ uint32_t s_win[EPB * WIN_STRIDE];
+  __shared__ float s_lid[EPB * (MAX_STAGED_BEAMS + 1)];
   const int tid = threadIdx.x;
   const int base = blockIdx.x * EPB;
   const size_t words = (size_t)P.h * P.wpr;
@@ -251,8 +254,8 @@ __global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_l
   if (tid < EPB) {
     const int e = base + tid;
     if (e < P.n) {
-      s_x0[tid] = (int)floorf(S.pos[2 * e]) - P.R - 6;
-      s_y0[tid] = (int)floorf(S.pos[2 * e + 1]) - P.R - 6;
+      s_x0[tid] = (int)floorf(S.pos[2 * e]) - 15;
+      s_y0[tid] = (int)floorf(S.pos[2 * e + 1]) - 15;
     }
   }
   __syncthreads();
@@ -265,7 +268,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_l
       if ((unsigned)y < (unsigned)P.h)
         v = extract_window_row(S.occ + (P.is_static ? 0 : e * words) + (size_t)y * P.wpr, P.wpr, s_x0[el]);
     }
-    s_win[el * MAX_WIN_ROWS + row] = v;
+    s_win[el * WIN_STRIDE + row] = v;
   }
   __syncthreads();
 
@@ -274,7 +277,7 @@ __global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_l
     const int e = base + tid;
     uint32_t errbits = 0;
     if (e < P.n) {
-      const RowsWindow rw{&s_win[tid * MAX_WIN_ROWS], s_x0[tid], s_y0[tid], P.wrows};
+      const RowsWindow rw{&s_win[tid * WIN_STRIDE], s_x0[tid], s_y0[tid], P.wrows};
       uint8_t f = S.flags[e];
       const bool was_reset = f & F_JUST_RESET;
       float pos0 = S.pos[2 * e], pos1 = S.pos[2 * e + 1];
@@ -393,17 +396,31 @@ __global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_l
   }
   __syncthreads();
 
-  // ---------------- phase 2: one lane per beam
-  for (int r = tid; r < EPB * P.beams; r += STEP_THREADS) {
-    const int el = r / P.beams, beam = r - el * P.beams;
-    const int e = base + el;
-    if (e >= P.n) break;
+  // ---------------- phase 2: lane = env, wave = beam index (all 64 lanes of a wave cast the same
+  // beam direction, so trip counts and branch paths agree across lanes); results staged in LDS and
+  // written out coalesced.
+  const int el = tid & (EPB - 1), e = base + el;
+  const bool staged = P.beams <= MAX_STAGED_BEAMS;
+  if (e < P.n) {
     const float px = s_pos[el][0], py = s_pos[el][1];
-    const float qx = __fadd_rn(px, S.beam_dirs[2 * beam]), qy = __fadd_rn(py, S.beam_dirs[2 * beam + 1]);
-    const RowsWindow rw{&s_win[el * MAX_WIN_ROWS], s_x0[el], s_y0[el], P.wrows};
-    const float d = lidar_scan(rw, px, py, qx, qy).dist;
-    const float v = f32_div(d, P.range);
-    O.lidar[(size_t)e * P.beams + beam] = fminf(fmaxf(v, -1.0f), 1.0f);
+    const RowsWindow rw{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
+    for (int beam = tid / EPB; beam < P.beams; beam += STEP_THREADS / EPB) {
+      const float qx = __fadd_rn(px, S.beam_dirs[2 * beam]), qy = __fadd_rn(py, S.beam_dirs[2 * beam + 1]);
+      const float d = lidar_scan(rw, px, py, qx, qy).dist;
+      const float v = fminf(fmaxf(f32_div(d, P.range), -1.0f), 1.0f);
+      if (staged)
+        s_lid[el * (MAX_STAGED_BEAMS + 1) + beam] = v;
+      else
+        O.lidar[(size_t)e * P.beams + beam] = v;
+    }
+  }
+  if (staged) {
+    __syncthreads();
+    const int nenv = P.n - base < EPB ? P.n - base : EPB;
+    for (int i = tid; i < nenv * P.beams; i += STEP_THREADS) {
+      const int l = i / P.beams, beam = i - l * P.beams;
+      O.lidar[(size_t)base * P.beams + i] = s_lid[l * (MAX_STAGED_BEAMS + 1) + beam];
+    }
   }
 }
 
@@ -451,7 +468,7 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   P.step_limit = cfg->step_limit;
   P.is_static = cfg->is_static;
   P.R = (int)ceilf(cfg->lidar_range);
-  P.wrows = 2 * P.R + 12;
+  P.wrows = MAX_WIN_ROWS;
   P.range = cfg->lidar_range;
   P.loss_scale = cfg->loss_scale;
   P.loss_offset = cfg->loss_offset;

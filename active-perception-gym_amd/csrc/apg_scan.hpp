@@ -134,8 +134,9 @@ APG_DEV ScanOut lidar_scan(const Rows &rows, float fpx, float fpy, float fqx, fl
   while (xi + yi < ntot) {
     const int a = ax + sx * xi, b = by + sy * yi;
     const bool hx = xi < nxl, hy = yi < nyl;
-    int c = hx ? -1 : 1;  // c < 0: x-crossing first, c > 0: y-crossing first, 0: both (lattice)
-    if (hx && hy) c = -orient_lattice(fpx, fpy, fqx, fqy, a, b) * sx * sy;
+    // c < 0: x-crossing first, c > 0: y-crossing first, 0: both (lattice point)
+    const int o = orient_lattice(fpx, fpy, fqx, fqy, a, b);
+    const int c = (hx && hy) ? -o * sx * sy : (hx ? -1 : 1);
     const bool takex = c <= 0, takey = c >= 0;
     // closure quad of the crossing: cells [i0, i0+di] x [j0, j0+dj]
     const int i0 = takex ? a - 1 : (colv ? ipx - 1 : cx);
@@ -143,7 +144,7 @@ APG_DEV ScanOut lidar_scan(const Rows &rows, float fpx, float fpy, float fqx, fl
     const bool di = takex || colv, dj = takey || colh;
     const int sh = i0 - rows.x0;
     const uint32_t r0 = rows.row(j0);
-    const uint32_t r1 = dj ? rows.row(j0 + 1) : r0;
+    const uint32_t r1 = rows.row(dj ? j0 + 1 : j0);
     const unsigned q0 = (r0 >> sh) & 3u, q1 = (r1 >> sh) & 3u, m = di ? 3u : 1u;
     const bool onb = ((q0 | q1) & m) != 0u && ((q0 & q1 & m) != m);
     const int ncx = cx + (takex ? sx : 0), ncy = cy + (takey ? sy : 0);
@@ -151,14 +152,31 @@ APG_DEV ScanOut lidar_scan(const Rows &rows, float fpx, float fpy, float fqx, fl
     const unsigned u = (unsigned)(ncx - i0), v = (unsigned)(ncy - j0);
     const unsigned rowv = v ? q1 : q0;
     const bool in_after = colv ? (rowv & 3u) != 0u : (colh ? (((q0 | q1) >> u) & 1u) != 0u : ((rowv >> u) & 1u) != 0u);
-    if (onb) {  // boundary point => node of the noded line
-      close_piece();
-      const bool lattice = (takex && takey) || (takex && colh) || (takey && colv);
-      pv_t = lattice ? 1 : (takex ? 2 : 3);
-      pv_a = takex ? a : (colv ? ipx : cx);
-      pv_b = takey ? b : (colh ? ipy : cy);
-      pv_onb = true;
+    // node bookkeeping, predicated (close the piece [previous node, this node])
+    const bool is_line = onb && cur_in;
+    const bool is_point = onb && !cur_in && pv_onb && !pv_left_in;
+    const bool first_line = is_line && n_lines == 0, first_point = is_point && n_points == 0;
+    if ((is_line && n_lines > 0) || (is_point && n_points > 0)) {  // Multi* only: rare
+      double x, y;
+      node_coord(pv_t, pv_a, pv_b, x, y);
+      const float d = dist_f32(x, y);
+      if (is_line) later_line = fminf(later_line, d);
+      else later_point = fminf(later_point, d);
     }
+    l0_t = first_line ? pv_t : l0_t;
+    l0_a = first_line ? pv_a : l0_a;
+    l0_b = first_line ? pv_b : l0_b;
+    p0_t = first_point ? pv_t : p0_t;
+    p0_a = first_point ? pv_a : p0_a;
+    p0_b = first_point ? pv_b : p0_b;
+    n_lines += is_line ? 1 : 0;
+    n_points += is_point ? 1 : 0;
+    pv_left_in = onb ? cur_in : pv_left_in;
+    const bool lattice = (takex && takey) || (takex && colh) || (takey && colv);
+    pv_t = onb ? (lattice ? 1 : (takex ? 2 : 3)) : pv_t;
+    pv_a = onb ? (takex ? a : (colv ? ipx : cx)) : pv_a;
+    pv_b = onb ? (takey ? b : (colh ? ipy : cy)) : pv_b;
+    pv_onb = pv_onb || onb;
     cx = ncx;
     cy = ncy;
     xi += takex ? 1 : 0;
@@ -224,13 +242,10 @@ APG_DEV uint32_t extract_window_row(const uint64_t *row, int wpr, int x0) {
   return res;
 }
 
-struct RowsWindow {  // 32-column window rows staged in LDS: rows [y0, y0+nrows)
-  const uint32_t *win;
+struct RowsWindow {  // 32-row x 32-column window staged in LDS (rows [y0, y0+32)); callers keep
+  const uint32_t *win;  // every access inside the window (see k_lidar_step), so no bounds test
   int x0, y0, nrows;
-  APG_DEV uint32_t row(int y) const {
-    const unsigned r = (unsigned)(y - y0);
-    return r < (unsigned)nrows ? win[r] : 0u;
-  }
+  APG_DEV uint32_t row(int y) const { return win[(unsigned)(y - y0) & 31u]; }
 };
 
 struct RowsGlobal {  // bit rows in global memory, read through a 32-column window at x0
