@@ -11,7 +11,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "_lib")
-LIB_PATH = os.path.join(LIB_DIR, "libapgym_hip.so")
+LIB_PATH = os.environ.get("APG_LIBRARY") or os.path.join(LIB_DIR, "libapgym_hip.so")  # override: tuning builds
 
 APG_OK = 0
 APG_ERR_NAN_ACTION = 1

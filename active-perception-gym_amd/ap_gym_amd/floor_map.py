@@ -95,7 +95,7 @@ def generate_maps(ds: FloorMapDataset, idx: np.ndarray, device="cuda") -> np.nda
     occ = torch.zeros((n, h, wpr), dtype=torch.int64, device=dev)
     scratch = torch.zeros_like(occ) if ds.map_kind == N.APG_MAP_ROOMS else None
     frames = ((h + 1) // 2) * ((w + 1) // 2) + 4
-    stack = torch.zeros((frames, n), dtype=torch.int16, device=dev) if ds.map_kind == N.APG_MAP_MAZE else None
+    stack = torch.zeros((n, frames), dtype=torch.int16, device=dev) if ds.map_kind == N.APG_MAP_MAZE else None
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     rc = N.lib().apg_map_generate(ds.map_kind, N.ptr(idx_t), n, h, w, p["max_rooms"], p["door_width"],
                                   p["branching_prob"], N.ptr(occ), N.ptr(scratch), N.ptr(stack), N.ptr(err),

@@ -133,62 +133,69 @@ APG_DEV int place_start(Pcg64 &rng, const uint64_t *rows, int h, int w, int wpr,
   return -1;
 }
 
-APG_DEV int gen_map(const Geo &g, Pcg64 &r, uint64_t *occ, uint16_t *stack, size_t stride, const BinomTable &bt) {
-  if (g.kind == APG_MAP_ROOMS) return rooms_generate(r, occ, g.wpr, g.h, g.max_rooms, g.door_width, bt);
-  return maze_generate(r, Bits{occ, g.wpr}, g.h, g.w, g.bp, stack, stride, g.frames);
+// ------------------------------------------------------------------ kernels
+// Map generator of a kernel instance (template parameter GEN): static maps are generated once by
+// apg_lidar_init, so the reset kernel for them only draws start cells.
+enum : int { GEN_NONE = 0, GEN_ROOMS = 1, GEN_MAZE = 2 };
+
+template <int GEN>
+APG_DEV int generate_one(const Geo &g, Pcg64 &r, uint64_t *occ, uint16_t *stack, const BinomTable &bt) {
+  if constexpr (GEN == GEN_MAZE) return maze_generate(r, Bits{occ, g.wpr}, g.h, g.w, g.bp, stack, 1, g.frames);
+  else return rooms_generate(r, occ, g.wpr, g.h, g.max_rooms, g.door_width, bt);
 }
 
-// ------------------------------------------------------------------ kernels
-__global__ void k_map_generate(Geo g, const uint64_t *idx, int n, uint64_t *occ, uint64_t *scratch,
-                               uint16_t *stack, uint32_t *err, BinomTable bt) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+template <int GEN>
+__global__ __launch_bounds__(64) void k_map_generate(Geo g, const uint64_t *idx, int n, uint64_t *occ,
+                                                     uint16_t *stack, uint32_t *err, BinomTable bt, int lanes) {
+  const int i = blockIdx.x * lanes + threadIdx.x;
+  if ((int)threadIdx.x >= lanes || i >= n) return;
   Pcg64 r = seed_pcg64(idx[i]);
-  const size_t words = (size_t)g.h * g.wpr;
-  int rc = gen_map(g, r, occ + i * words, stack ? stack + i : nullptr, (size_t)n, bt);
+  const int rc = generate_one<GEN>(g, r, occ + (size_t)i * g.h * g.wpr,
+                                   stack ? stack + (size_t)i * g.frames : nullptr, bt);
   if (rc != 0 && err) atomicOr(err, APG_ERR_MAPGEN);
 }
 
-// One wave per 64 envs.  Envs pending autoreset (or all, for reset(seed)) draw their next map
-// index, generate the map, draw the start cell; then the wave cooperatively rewrites the float32
-// map observation of each env that reset (coalesced float4 stores).  Waves with nothing to reset
-// exit after one flag load.
+// One wave per `lanes` (<= 64) envs.  Envs pending autoreset (or all, for reset(seed)) draw their
+// next map index, generate the map and draw the start cell (the float32 map observation is expanded
+// by the following k_lidar_step, whose workgroups have the bandwidth for it).  Map generation is a
+// long serial, divergent chain per env whose speed is set by instruction latency, not by lanes, so
+// the host spreads the envs over as many waves as fit on the chip at once (pick_lanes).  Waves with
+// nothing to reset exit after one flag load.
+template <int GEN>
 __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, uint64_t seed, int use_seed,
-                                                    int all, uint64_t *out_map_idx, float *map_obs, uint32_t *err,
-                                                    BinomTable bt) {
-  const int base = blockIdx.x * 64, lane = threadIdx.x;
-  const int e = base + lane;
-  const uint8_t f = e < g.n ? S.flags[e] : 0;
-  const bool active = e < g.n && (all || (f & F_AUTORESET));
-  const unsigned long long todo = __ballot(active);
-  if (todo == 0ULL) return;
-  const size_t words = (size_t)g.h * g.wpr;
-  if (active) {
+                                                    int all, uint64_t *out_map_idx, uint32_t *err, BinomTable bt,
+                                                    int lanes) {
+  const int lane = threadIdx.x;
+  const int e = blockIdx.x * lanes + lane;
+  const bool mine = lane < lanes && e < g.n;
+  const uint8_t f = mine ? S.flags[e] : 0;
+  const bool active = mine && (all || (f & F_AUTORESET));
+  if (!active) return;
+  {
     Pcg64 rng;
     Pcg64 it;
     if (use_seed) {
       rng = seed_pcg64(seed + (uint64_t)e);
-      if (!g.is_static) it = seed_pcg64(bounded_u64(rng, 0x100000000ULL));  // integers(0, 2**32, endpoint=True)
+      if constexpr (GEN != GEN_NONE) it = seed_pcg64(bounded_u64(rng, 0x100000000ULL));  // integers(0, 2**32, endpoint=True)
     } else {
       rng = *reinterpret_cast<const Pcg64 *>(&S.rng[e]);
-      if (!g.is_static) it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[e]);
+      if constexpr (GEN != GEN_NONE) it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[e]);
     }
-    const uint64_t *rows = S.occ;
     uint64_t midx;
-    if (!g.is_static) {
+    float px = 0.5f, py = 0.5f;
+    if constexpr (GEN != GEN_NONE) {
       midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
-      uint64_t *own = S.occ + e * words;
       Pcg64 map_rng = seed_pcg64(midx);  // FloorMapDataset*.get_data_point: default_rng(idx)
-      if (gen_map(g, map_rng, own, S.stack ? S.stack + e : nullptr, (size_t)g.n, bt) != 0)
-        atomicOr(err, APG_ERR_MAPGEN);
-      rows = own;
+      uint64_t *own = S.occ + (size_t)e * g.h * g.wpr;
+      int rc = generate_one<GEN>(g, map_rng, own, S.stack + (size_t)e * g.frames, bt);
+      if (place_start(rng, own, g.h, g.w, g.wpr, px, py) != 0) rc = -6;
+      if (rc != 0) atomicOr(err, APG_ERR_MAPGEN);
       *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
       S.map_idx[e] = midx;
     } else {
       midx = S.map_idx[e];
+      if (place_start(rng, S.occ, g.h, g.w, g.wpr, px, py) != 0) atomicOr(err, APG_ERR_MAPGEN);
     }
-    float px = 0.5f, py = 0.5f;
-    if (place_start(rng, rows, g.h, g.w, g.wpr, px, py) != 0) atomicOr(err, APG_ERR_MAPGEN);
     S.pos[2 * e] = px;
     S.pos[2 * e + 1] = py;
     S.init_pos[2 * e] = px;
@@ -197,34 +204,6 @@ __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, ui
     S.flags[e] = (uint8_t)((f & F_AUTORESET) | F_JUST_RESET | F_FIRST);
     *reinterpret_cast<Pcg64 *>(&S.rng[e]) = rng;
     if (out_map_idx) out_map_idx[e] = midx;
-  }
-  if (g.is_static || !map_obs) return;
-  __syncthreads();  // workgroup = this wave: the maps written above are visible to every lane
-  const float wall = 1.0f / 255.0f;  // bool map / 255 (lidar_localization2d.py:299)
-  const int cells = g.h * g.w;
-  unsigned long long m = todo;
-  while (m) {
-    const int j = __ffsll((long long)m) - 1;
-    m &= m - 1ULL;
-    const uint64_t *rows = S.occ + (size_t)(base + j) * words;
-    float *dst = map_obs + (size_t)(base + j) * cells;
-    if ((cells & 3) == 0) {
-      for (int k4 = lane; k4 < cells / 4; k4 += 64) {
-        float4 v;
-        float *pv = reinterpret_cast<float *>(&v);
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const int k = 4 * k4 + u, y = k / g.w, x = k - y * g.w;
-          pv[u] = ((rows[y * g.wpr + (x >> 6)] >> (x & 63)) & 1ULL) ? wall : 0.0f;
-        }
-        reinterpret_cast<float4 *>(dst)[k4] = v;
-      }
-    } else {
-      for (int k = lane; k < cells; k += 64) {
-        const int y = k / g.w, x = k - y * g.w;
-        dst[k] = ((rows[y * g.wpr + (x >> 6)] >> (x & 63)) & 1ULL) ? wall : 0.0f;
-      }
-    }
   }
 }
 
@@ -238,7 +217,10 @@ struct StepParams {
 // ~2 cells (clamped move <= 1, slide <= 1), and every cell a scan of length <= R from the new
 // position p can touch lies within [floor(p) - R - 2, floor(p) + R + 1] (+1 column for the 2-bit
 // quad reads), i.e. within [floor(p0) - R - 5, floor(p0) + R + 5]: inside the window for R <= 10.
-__global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_lidar_state S,
+#ifndef APG_STEP_MIN_WAVES
+#define APG_STEP_MIN_WAVES 1
+#endif
+__global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step(StepParams P, apg_lidar_state S,
                                                              const float *__restrict__ act,
                                                              const float *__restrict__ pred,
                                                              apg_lidar_outputs O) {
@@ -250,15 +232,50 @@ __global__ __launch_bounds__(STEP_THREADS) void k_lidar_step(StepParams P, apg_l
   const int base = blockIdx.x * EPB;
   const size_t words = (size_t)P.h * P.wpr;
 
-  // ---------------- phase 0: window origins from the pre-move positions
+  // ---------------- phase 0: window origins from the pre-move positions; which envs reset
+  __shared__ unsigned long long s_reset;
   if (tid < EPB) {
     const int e = base + tid;
+    bool rs = false;
     if (e < P.n) {
       s_x0[tid] = (int)floorf(S.pos[2 * e]) - 15;
       s_y0[tid] = (int)floorf(S.pos[2 * e + 1]) - 15;
+      rs = (S.flags[e] & F_JUST_RESET) != 0;
     }
+    const unsigned long long m = __ballot(rs);
+    if (tid == 0) s_reset = m;
   }
   __syncthreads();
+  // map obs of the envs that reset this step: bool map / 255 (lidar_localization2d.py:299), written by
+  // the whole workgroup with float4 stores (only in reset steps; the maps came from k_lidar_reset)
+  if (s_reset != 0ULL && O.map_obs && !P.is_static) {
+    const float wall = 1.0f / 255.0f;
+    const int cells = P.h * P.w;
+    unsigned long long m = s_reset;
+    while (m) {
+      const int j = __ffsll((long long)m) - 1;
+      m &= m - 1ULL;
+      const uint64_t *rows = S.occ + (size_t)(base + j) * words;
+      float *dst = O.map_obs + (size_t)(base + j) * cells;
+      if ((cells & 3) == 0) {
+        for (int k4 = tid; k4 < cells / 4; k4 += STEP_THREADS) {
+          float4 v;
+          float *pv = reinterpret_cast<float *>(&v);
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            const int k = 4 * k4 + u, y = k / P.w, x = k - y * P.w;
+            pv[u] = ((rows[y * P.wpr + (x >> 6)] >> (x & 63)) & 1ULL) ? wall : 0.0f;
+          }
+          reinterpret_cast<float4 *>(dst)[k4] = v;
+        }
+      } else {
+        for (int k = tid; k < cells; k += STEP_THREADS) {
+          const int y = k / P.w, x = k - y * P.w;
+          dst[k] = ((rows[y * P.wpr + (x >> 6)] >> (x & 63)) & 1ULL) ? wall : 0.0f;
+        }
+      }
+    }
+  }
   for (int r = tid; r < EPB * P.wrows; r += STEP_THREADS) {
     const int el = r / P.wrows, row = r - el * P.wrows;
     const int e = base + el;
@@ -457,6 +474,58 @@ __global__ void k_rng_draws(const uint64_t *seeds, int m, int kind, int64_t a, i
 
 int grid_for(int n, int threads) { return (n + threads - 1) / threads; }
 
+// Envs per 64-lane workgroup (one wave) for the serial map-generation kernels.  Each env's map is a
+// long divergent chain: with one wave per SIMD its instruction latency is exposed, with many waves of
+// few lanes the SIMD issues the same divergent instruction stream for little work.  Measured best
+// (maze 127 x 127 and rooms 64 x 64 on MI355X): about APG_GEN_WAVES_PER_SIMD waves per SIMD.
+#ifndef APG_GEN_WAVES_PER_SIMD
+#define APG_GEN_WAVES_PER_SIMD 2
+#endif
+int gen_lanes(int n) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const int64_t waves = (int64_t)cus * 4 * APG_GEN_WAVES_PER_SIMD;
+  int lanes = 1;
+  while (lanes < 64 && (int64_t)grid_for(n, lanes) > waves) lanes *= 2;
+  return lanes;
+}
+
+template <int GEN>
+int launch_reset_gen(const Geo &g, const apg_lidar_state *st, uint64_t seed, int use_seed, int all,
+                     const apg_lidar_outputs *out, hipStream_t s) {
+  const int lanes = GEN == GEN_NONE ? 64 : gen_lanes(g.n);
+  hipLaunchKernelGGL(k_lidar_reset<GEN>, dim3(grid_for(g.n, lanes)), dim3(64), 0, s, g, *st, seed, use_seed, all,
+                     out->map_idx, out->err, make_binom_table(), lanes);
+  return check_launch("k_lidar_reset");
+}
+
+int launch_reset(const Geo &g, const apg_lidar_state *st, uint64_t seed, int use_seed, int all,
+                 const apg_lidar_outputs *out, hipStream_t s) {
+  if (g.is_static) return launch_reset_gen<GEN_NONE>(g, st, seed, use_seed, all, out, s);
+  if (g.kind == APG_MAP_MAZE) return launch_reset_gen<GEN_MAZE>(g, st, seed, use_seed, all, out, s);
+  return launch_reset_gen<GEN_ROOMS>(g, st, seed, use_seed, all, out, s);
+}
+
+template <int GEN>
+int launch_map_generate(const Geo &g, const uint64_t *idx, int n, uint64_t *occ, uint16_t *stack, uint32_t *err,
+                        hipStream_t s) {
+  const int lanes = gen_lanes(n);
+  hipLaunchKernelGGL(k_map_generate<GEN>, dim3(grid_for(n, lanes)), dim3(64), 0, s, g, idx, n, occ, stack, err,
+                     make_binom_table(), lanes);
+  return check_launch("k_map_generate");
+}
+
+int launch_map_generate_any(const Geo &g, const uint64_t *idx, int n, uint64_t *occ, uint16_t *stack,
+                            uint32_t *err, hipStream_t s) {
+  if (g.kind == APG_MAP_MAZE) return launch_map_generate<GEN_MAZE>(g, idx, n, occ, stack, err, s);
+  return launch_map_generate<GEN_ROOMS>(g, idx, n, occ, stack, err, s);
+}
+
 int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *act,
                        const float *pred, const apg_lidar_outputs *out, hipStream_t s) {
   StepParams P;
@@ -505,9 +574,7 @@ int apg_lidar_init(const apg_lidar_config *cfg, const apg_lidar_state *st, apg_s
   Geo g = make_geo(cfg);
   hipStream_t s = (hipStream_t)stream;
   // map_idx[0] already holds static_map_index (the host fills the state before init)
-  hipLaunchKernelGGL(k_map_generate, dim3(1), dim3(64), 0, s, g, (const uint64_t *)st->map_idx, 1, st->occ,
-                     st->scratch, st->stack, (uint32_t *)nullptr, make_binom_table());
-  return check_launch("k_map_generate(static)");
+  return launch_map_generate_any(g, (const uint64_t *)st->map_idx, 1, st->occ, st->stack, nullptr, s);
 }
 
 int apg_lidar_reset(const apg_lidar_config *cfg, const apg_lidar_state *st, uint64_t seed, int use_seed,
@@ -516,9 +583,7 @@ int apg_lidar_reset(const apg_lidar_config *cfg, const apg_lidar_state *st, uint
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   Geo g = make_geo(cfg);
-  hipLaunchKernelGGL(k_lidar_reset, dim3(grid_for(g.n, 64)), dim3(64), 0, s, g, *st, seed, use_seed, 1,
-                     out->map_idx, out->map_obs, out->err, make_binom_table());
-  if ((rc = check_launch("k_lidar_reset"))) return rc;
+  if ((rc = launch_reset(g, st, seed, use_seed, 1, out, s))) return rc;
   return launch_step_kernel(cfg, st, nullptr, nullptr, out, s);
 }
 
@@ -530,9 +595,7 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
   if (!action || !prediction) return fail(APG_E_INVALID, "null action/prediction");
   hipStream_t s = (hipStream_t)stream;
   Geo g = make_geo(cfg);
-  hipLaunchKernelGGL(k_lidar_reset, dim3(grid_for(g.n, 64)), dim3(64), 0, s, g, *st, (uint64_t)0, 0, 0,
-                     out->map_idx, out->map_obs, out->err, make_binom_table());
-  if ((rc = check_launch("k_lidar_reset"))) return rc;
+  if ((rc = launch_reset(g, st, 0, 0, 0, out, s))) return rc;
   if (ev_begin && hipEventRecord((hipEvent_t)ev_begin, s) != hipSuccess) return fail(APG_E_LAUNCH, "hipEventRecord");
   rc = launch_step_kernel(cfg, st, action, prediction, out, s);
   if (rc == APG_OK && ev_end && hipEventRecord((hipEvent_t)ev_end, s) != hipSuccess)
@@ -564,9 +627,8 @@ int apg_map_generate(int map_kind, const uint64_t *idx, int n, int h, int w, int
   if (rc) return rc;
   if (map_kind == APG_MAP_MAZE && !stack) return fail(APG_E_INVALID, "maze maps need stack");
   Geo g = make_geo(&c);
-  hipLaunchKernelGGL(k_map_generate, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, g, idx, n, occ,
-                     scratch, stack, err, make_binom_table());
-  return check_launch("k_map_generate");
+  (void)scratch;  // unused since rooms maps are painted from primitives; kept for ABI stability
+  return launch_map_generate_any(g, idx, n, occ, stack, err, (hipStream_t)stream);
 }
 
 int apg_lidar_scan_batch(const uint64_t *occ, const int32_t *map_index, int h, int w, const float *seg, int n,

@@ -209,7 +209,7 @@ APG_DEV int rooms_generate(Pcg64 &r, uint64_t *occ, int wpr, int m, int max_room
 }
 
 // Maze: recursive carve() as an explicit DFS. Frame (u16): perm 4x2 bits | k << 8 | first << 11 |
-// from << 12. `stack` is frame-major: frame f of this map lives at stack[f * stride].
+// from << 12; frame f of this map lives at stack[f * stride].
 APG_DEV uint32_t draw_perm4(Pcg64 &r) {
   uint32_t p = 0 | (1u << 2) | (2u << 4) | (3u << 6);
 #pragma unroll
@@ -232,7 +232,10 @@ APG_DEV int maze_generate(Pcg64 &r, Bits occ, int h, int w, double branching_pro
       occ.w[y * occ.wpr + k] = v;
     }
   occ.clr(1, 1);
-  const int dxs[4] = {2, -2, 0, 0}, dys[4] = {0, 0, 2, -2};
+  // directions [[2, 0], [-2, 0], [0, 2], [0, -2]] (maze.py:76) computed, not indexed: a runtime-indexed
+  // local array would live in scratch memory
+  auto dxs = [](uint32_t d) { return d == 0u ? 2 : (d == 1u ? -2 : 0); };
+  auto dys = [](uint32_t d) { return d == 2u ? 2 : (d == 3u ? -2 : 0); };
   int x = 1, y = 1, sp = 1;
   uint32_t top = draw_perm4(r) | (1u << 11);  // k = 0, first = 1
   while (true) {
@@ -240,18 +243,18 @@ APG_DEV int maze_generate(Pcg64 &r, Bits occ, int h, int w, double branching_pro
     if (k >= 4) {  // pop
       if (--sp == 0) break;
       const uint32_t from = (top >> 12) & 3u;
-      x -= dxs[from];
-      y -= dys[from];
+      x -= dxs(from);
+      y -= dys(from);
       top = stack[(size_t)(sp - 1) * stride];
       continue;
     }
     const uint32_t d = (top >> (2 * k)) & 3u;
     top = (top & ~(7u << 8)) | ((k + 1) << 8);
-    const int nx = x + dxs[d], ny = y + dys[d];
+    const int nx = x + dxs(d), ny = y + dys(d);
     if (0 < nx && 0 < ny && nx < w - 1 && ny < h - 1 && occ.get(ny, nx)) {
       const bool first = (top >> 11) & 1u;
       if (first || next_double(r) < branching_prob) {
-        occ.clr(y + dys[d] / 2, x + dxs[d] / 2);
+        occ.clr(y + dys(d) / 2, x + dxs(d) / 2);
         occ.clr(ny, nx);
         top &= ~(1u << 11);
         if (sp >= cap) return -5;

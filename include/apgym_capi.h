@@ -77,7 +77,7 @@ typedef struct apg_lidar_state {
   apg_pcg64 *it_rng;   /* [N]   DatasetIterator rng (dynamic maps) */
   uint64_t *occ;       /* [N or 1][H][wpr] bit-packed occupancy, wpr = ceil(W/64) */
   uint64_t *scratch;   /* [N][H][wpr] rooms door plane (dynamic rooms only) */
-  uint16_t *stack;     /* [maze_frames][N] DFS frames (dynamic maze only) */
+  uint16_t *stack;     /* [N][maze_frames] DFS frames, contiguous per env (dynamic maze only) */
   uint64_t *map_idx;   /* [N]   dataset index of the current map */
   const float *beam_dirs; /* [beams][2] lidar_directions (f32, computed by the host like the reference) */
 } apg_lidar_state;
