@@ -29,6 +29,8 @@ sys.path.insert(0, os.path.join(ROOT, "active-perception-gym_amd"))
 sys.path.insert(0, ROOT)
 
 BYTES_PER_ENV_STEP = lambda beams: 228 + 4 * beams  # noqa: E731  SURVEY §8(d): compulsory bytes per env-step
+MAP_OBS_BYTES = lambda m: 4 * m * m  # noqa: E731  f32 map observation written on an env's autoreset step
+EPISODE_PERIOD = 101  # TimeLimit(100) + the NEXT_STEP autoreset step: every env resets on steps 101, 202, ...
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -159,7 +161,12 @@ def main():
 
     if rank == 0:
         value = n_total * args.steps / elapsed
-        bytes_per_launch = BYTES_PER_ENV_STEP(args.beams) * n_local
+        # algorithmic bytes of the timed k_lidar_step launches: the per-env-step bytes every step, plus
+        # the map observation on the autoreset steps (all envs reset together: synchronized episodes)
+        reset_steps = sum(1 for t in range(args.steps) if (args.warmup + t + 1) % EPISODE_PERIOD == 0)
+        bytes_total = (BYTES_PER_ENV_STEP(args.beams) * n_local * args.steps
+                       + MAP_OBS_BYTES(args.map_size) * n_local * reset_steps)
+        bytes_per_launch = bytes_total / args.steps
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
         traffic = None
         tpath = os.path.join(ROOT, "profiles", "traffic_lidar_step.json")
@@ -188,7 +195,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_lidar_step", "kernel_ms": kernel_ms,
-                         "bytes_per_launch": bytes_per_launch},
+                         "bytes_per_launch": bytes_per_launch, "reset_steps_timed": reset_steps},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.beams, args.map_size, args.cpu_envs, args.cpu_steps)
