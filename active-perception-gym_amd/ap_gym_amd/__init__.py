@@ -12,6 +12,13 @@ no CPU fallback.
 
 from . import _native  # noqa: F401
 from .floor_map import FloorMapDataset, FloorMapDatasetMaze, FloorMapDatasetRooms  # noqa: F401
+from .image_dataset import (  # noqa: F401
+    ArrayImageClassificationDataset,
+    HuggingfaceImageClassificationDataset,
+    ImageClassificationDataset,
+    SyntheticImageClassificationDataset,
+)
+from .image_env import ImageClassificationVectorEnv, ImageLocalizationVectorEnv, ImagePerceptionConfig  # noqa: F401
 from .lidar_env import LIDARLocalization2DVectorEnv, lidar_beam_directions  # noqa: F401
 from .loss_fn import (  # noqa: F401
     CrossEntropyLossFn,
@@ -23,6 +30,6 @@ from .loss_fn import (  # noqa: F401
     ZeroLossFn,
 )
 from .registration import make_vec, register, registry  # noqa: F401
-from .spaces import ActivePerceptionActionSpace, ImageSpace  # noqa: F401
+from .spaces import ActivePerceptionActionSpace, ImageSpace, LogitSpace  # noqa: F401
 
 __version__ = "0.1.0"

@@ -17,8 +17,16 @@ APG_OK = 0
 APG_ERR_NAN_ACTION = 1
 APG_ERR_NAN_PREDICTION = 2
 APG_ERR_MAPGEN = 4
+APG_ERR_OOB_Y = 8
+APG_ERR_OOB_X = 16
 APG_MAP_ROOMS = 0
 APG_MAP_MAZE = 1
+APG_DRAW_UNIFORM = 0
+APG_DRAW_INTEGERS = 1
+APG_IMAGE_CLASSIFY = 0
+APG_IMAGE_LOCALIZE = 1
+APG_POOL_U8 = 0
+APG_POOL_F32 = 1
 
 
 class NativeLibraryError(RuntimeError):
@@ -60,6 +68,25 @@ class LidarSizes(ctypes.Structure):
                 ("stack_bytes", ctypes.c_size_t), ("wpr", ctypes.c_int32), ("maze_frames", ctypes.c_int32)]
 
 
+class ImageConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("num_envs", "kind", "height", "width", "pool_channels", "channels",
+                                              "pool_dtype", "sensor_h", "sensor_w", "step_limit", "num_classes",
+                                              "invert_labels", "top_k", "unique_points")] + [
+        ("pool_len", ctypes.c_int64), ("sensor_scale", ctypes.c_double), ("max_step", ctypes.c_double * 2),
+        ("cell", ctypes.c_double * 2), ("ce_scale", ctypes.c_double), ("ce_offset", ctypes.c_double),
+        ("mse_scale", ctypes.c_float), ("mse_offset", ctypes.c_float)]
+
+
+class ImageState(ctypes.Structure):
+    _fields_ = [(n, _vp) for n in ("pool", "pool_labels", "unique_grid", "index", "label", "inverted", "pos",
+                                   "target", "rng", "scratch_i64", "scratch_f64", "top_k")]
+
+
+class ImageOutputs(ctypes.Structure):
+    _fields_ = [(n, _vp) for n in ("glimpse", "glimpse_pos", "time_step", "target_glimpse", "reward", "base_reward",
+                                   "target", "label_target", "loss_f64", "loss_f32", "err")]
+
+
 # (name, restype, argtypes) for every symbol declared in include/apgym_capi.h
 SYMBOLS = [
     ("apg_version", ctypes.c_char_p, []),
@@ -78,6 +105,22 @@ SYMBOLS = [
                                             _vp]),
     ("apg_rng_draws", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                      _vp, _vp]),
+    ("apg_rng_fill", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, _vp, _vp, ctypes.c_int64,
+                                    ctypes.c_uint64, _vp, _vp]),
+    ("apg_image_seed", ctypes.c_int, [ctypes.POINTER(ImageConfig), ctypes.POINTER(ImageState), ctypes.c_uint64,
+                                      _vp]),
+    ("apg_image_reset", ctypes.c_int, [ctypes.POINTER(ImageConfig), ctypes.POINTER(ImageState),
+                                       ctypes.POINTER(ImageOutputs), _vp]),
+    ("apg_image_step", ctypes.c_int, [ctypes.POINTER(ImageConfig), ctypes.POINTER(ImageState), _vp, _vp,
+                                      ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ImageOutputs), _vp]),
+    ("apg_image_glimpse", ctypes.c_int, [ctypes.POINTER(ImageConfig), _vp, _vp, _vp, ctypes.c_int, ctypes.c_int32,
+                                         _vp, _vp, _vp]),
+    ("apg_image_unique_top_k", ctypes.c_int, [ctypes.POINTER(ImageConfig), _vp, _vp, _vp, ctypes.c_int32,
+                                              ctypes.c_int32, _vp, _vp, _vp]),
+    ("apg_loss_ce", ctypes.c_int, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double, _vp,
+                                   _vp]),
+    ("apg_loss_mse", ctypes.c_int, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_float, ctypes.c_float, _vp,
+                                    _vp]),
 ]
 
 _lib = None

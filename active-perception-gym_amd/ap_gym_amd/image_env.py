@@ -1,0 +1,416 @@
+"""Image glimpse envs on the GPU: ImageClassificationVectorEnv and ImageLocalizationVectorEnv.
+
+Reference (ap_gym 0.5.0): ap_gym/envs/image_classification.py:22-167,
+ap_gym/envs/image_localization.py:24-256 over ImagePerceptionModule
+(ap_gym/envs/image/image_perception_module.py:20-477), built by `make_vec("MNIST-v0", N)` and the
+other image ids (registration.py:145-192, 516-627).  Same constructor
+(num_envs, image_perception_config, render_mode), spaces, reset/step semantics and dtypes; the
+dataset is held in HBM as one pool and every per-step array op (glimpse gather, losses, move,
+rewards) and every vector-level numpy draw (DatasetBatchIterator, the module's and the env's
+generators) runs on the device through the C ABI (include/apgym_capi.h: apg_image_*).
+
+  obs     {"glimpse": f32[N,G0,G1,C], "glimpse_pos": f32[N,2], "time_step": f32[N],
+           ("inverted_label": i32/i64[N]), ("target_glimpse": f32[N,G0,G1,C] localization)}
+  reward  base_reward - normalized loss (CE: float64; MSE: float32, float64 on autoreset steps)
+  info    {"index": i64[N], "base_reward", "prediction": {"target", "loss"}}
+  episode all envs terminate together after step_limit steps; the next step resets the batch
+          (NEXT_STEP autoreset inside the module, base_reward = zeros(N) float64)
+
+array_backend="numpy" (default) returns numpy exactly like the reference; "torch" returns
+persistent device tensors without host synchronisation (errors raised lazily, like the LIDAR env).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Any, Sequence
+
+import numpy as np
+
+from . import _native as N
+from .image_dataset import ImageClassificationDataset
+from .loss_fn import CrossEntropyLossFn, affine_f32, regression_loss
+from .spaces import ActivePerceptionActionSpace, Box, Dict, Discrete, ImageSpace, LogitSpace, MultiDiscrete, batch_space
+
+NAN_ACTION_MSG = "NaN values detected in action."
+NAN_PREDICTION_MSG = "NaN values detected in prediction."
+OOB_MSG = "One of the requested xi is out of bounds in dimension %d"
+
+
+@dataclass(frozen=True)
+class ImagePerceptionConfig:
+    """image_perception_module.py:20-34 (same fields and defaults)."""
+
+    dataset: ImageClassificationDataset
+    sensor_size: tuple[int, int] = (5, 5)
+    sensor_scale: float = 1.0
+    max_step_length: float | Sequence[float] = 0.2
+    step_limit: int = 16
+    display_visitation: bool = True
+    render_unvisited_opacity: float = 0.0
+    render_visited_opacity: float = 0.3
+    prefetch_buffer_size: int = 128
+    prefetch: bool = True
+    unique_sampling_max_grid_cell_size_rel = 0.2  # class attribute in the reference too
+    unique_sampling_top_k: int = 10
+    randomly_invert_labels: bool = False
+
+
+def sensor_pos_lim_pixels(image_hw, sensor_size, sensor_scale) -> np.ndarray:
+    """image_perception_module.py:419-423, evaluated with numpy like the reference."""
+    eff = np.array(sensor_size) * sensor_scale
+    return (np.flip(np.array(image_hw)) - 1) / 2 - (eff - 1) / 2
+
+
+def unique_sampling_grid(image_hw, sensor_size, sensor_scale, rel=0.2):
+    """Sampling positions and cell size of sample_unique_glimpse_positions (:254-267)."""
+    eff = np.array(sensor_size) * sensor_scale
+    cell = (eff / sensor_pos_lim_pixels(image_hw, sensor_size, sensor_scale)) * rel
+    cnt = np.ceil(2 / cell)
+    grid = np.stack(np.meshgrid(np.linspace(-1, 1, int(cnt[0])), np.linspace(-1, 1, int(cnt[1])), indexing="ij"),
+                    axis=-1).reshape(-1, 2)
+    return np.ascontiguousarray(grid), cell
+
+
+def softmax_nan_rows(logits: np.ndarray) -> np.ndarray:
+    """Rows where scipy.special.softmax(row)[label] is NaN: a NaN or +inf logit, or all -inf."""
+    return np.isnan(logits).any(-1) | np.isposinf(logits).any(-1) | np.isneginf(logits).all(-1)
+
+
+class _ImageVectorEnv:
+    metadata = {"render_modes": ["rgb_array"], "render_fps": 2, "autoreset_mode": "NextStep"}
+    ERROR_POLL_INTERVAL = 32
+    kind: int
+
+    def __init__(self, num_envs: int, image_perception_config: ImagePerceptionConfig,
+                 render_mode: str = "rgb_array", device=None, copy: bool = False, strict_errors: bool = False,
+                 array_backend: str = "numpy"):
+        import torch
+
+        if render_mode not in self.metadata["render_modes"]:
+            raise ValueError(f"Unsupported render mode: {render_mode}")
+        if array_backend not in ("numpy", "torch"):
+            raise ValueError("array_backend must be 'numpy' or 'torch'")
+        cfg = image_perception_config
+        self.config = cfg
+        self.num_envs = n = int(num_envs)
+        self.render_mode = render_mode
+        self.copy, self.strict_errors, self.array_backend = copy, strict_errors, array_backend
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise ValueError("the image envs run on a GPU device (no CPU fallback)")
+        ds = cfg.dataset
+        ds.load()
+        pool, labels = ds.device_pool()
+        m, h, w, pc = pool.shape
+        c = int(ds.num_channels)
+        if c not in (1, 3):
+            raise ValueError(f"Target channels must be either 1 or 3 but is {c}.")
+        if pc != c and not (pc == 1 and c == 3):
+            raise ValueError(f"Invalid image format. Expected {c} channels but got {pc}")
+        s0, s1 = (int(v) for v in cfg.sensor_size)
+        eff = np.array(cfg.sensor_size) * cfg.sensor_scale
+        if np.any(np.array([h, w]) < eff):
+            raise ValueError(f"Image size {(h, w)} cannot be smaller than effective sensor size {tuple(eff)}.")
+        self.image_size = (h, w)
+        k = int(ds.num_classes)
+        self._k = k
+
+        # ---- spaces (image_perception_module.py:51-91, image_classification.py:86-103,
+        #      image_localization.py:86-118, active_{classification,regression}_env.py)
+        obs = {"glimpse": ImageSpace(s1, s0, c), "glimpse_pos": Box(-1, 1, (2,), np.float32),
+               "time_step": Box(-1, 1, (), np.float32)}
+        if cfg.randomly_invert_labels:
+            obs["inverted_label"] = Discrete(3)
+        if self.kind == N.APG_IMAGE_LOCALIZE:
+            obs["target_glimpse"] = ImageSpace(s1, s0, c)
+            pred_space = Box(-1, 1, (2,), np.float32)
+            self.single_prediction_target_space = Box(-1, 1, (2,), np.float32)
+            self.prediction_target_space = batch_space(self.single_prediction_target_space, n)
+            self.loss_fn = regression_loss(2, -1, 1)
+        else:
+            pred_space = LogitSpace(-np.inf, np.inf, (k,), np.float32)
+            self.single_prediction_target_space = Discrete(k)
+            self.prediction_target_space = MultiDiscrete([k] * n)
+            self.loss_fn = CrossEntropyLossFn(num_classes=k).normalized
+        self.single_observation_space = Dict(obs)
+        self.observation_space = batch_space(self.single_observation_space, n)
+        self.single_action_space = ActivePerceptionActionSpace(Box(-1, 1, (2,), np.float32), pred_space)
+        self.action_space = batch_space(self.single_action_space, n)
+
+        # ---- native configuration
+        grid, cell = unique_sampling_grid((h, w), cfg.sensor_size, cfg.sensor_scale,
+                                          cfg.unique_sampling_max_grid_cell_size_rel)
+        msl = np.ones(2) * np.array(cfg.max_step_length)
+        if self.kind == N.APG_IMAGE_CLASSIFY:
+            ce = self.loss_fn
+            ce_scale, ce_offset = float(ce.scale), float(ce.offset)
+            mse_scale, mse_offset = 1.0, 0.0
+        else:
+            ce_scale, ce_offset = 1.0, 0.0
+            mse_scale, mse_offset = affine_f32(self.loss_fn)
+        self._cfg = N.ImageConfig(
+            num_envs=n, kind=self.kind, height=h, width=w, pool_channels=pc, channels=c,
+            pool_dtype=N.APG_POOL_U8 if pool.dtype == np.uint8 else N.APG_POOL_F32, sensor_h=s0, sensor_w=s1,
+            step_limit=int(cfg.step_limit), num_classes=k, invert_labels=int(bool(cfg.randomly_invert_labels)),
+            top_k=int(cfg.unique_sampling_top_k), unique_points=int(grid.shape[0]), pool_len=m,
+            sensor_scale=float(cfg.sensor_scale), max_step=(ctypes.c_double * 2)(*msl.tolist()),
+            cell=(ctypes.c_double * 2)(*cell.tolist()), ce_scale=ce_scale, ce_offset=ce_offset,
+            mse_scale=mse_scale, mse_offset=mse_offset)
+
+        t, dev = torch, self.device
+        gshape = (n, s0, s1, c)
+        self._t = T = dict(
+            pool=t.from_numpy(pool).to(dev), pool_labels=t.from_numpy(labels).to(dev),
+            unique_grid=t.from_numpy(grid).to(dev),
+            index=t.zeros(n, dtype=t.int64, device=dev), label=t.zeros(n, dtype=t.int32, device=dev),
+            inverted=t.zeros(n, dtype=t.int32, device=dev), pos=t.zeros((n, 2), dtype=t.float64, device=dev),
+            target=t.zeros((n, 2), dtype=t.float32, device=dev), rng=t.zeros((3, 5), dtype=t.int64, device=dev),
+            scratch_i64=t.zeros(n, dtype=t.int64, device=dev), scratch_f64=t.zeros(2 * n, dtype=t.float64, device=dev),
+            top_k=t.zeros((n, int(cfg.unique_sampling_top_k)), dtype=t.int32, device=dev),
+            glimpse=t.zeros(gshape, dtype=t.float32, device=dev),
+            glimpse_pos=t.zeros((n, 2), dtype=t.float32, device=dev),
+            time_step=t.zeros(n, dtype=t.float32, device=dev),
+            target_glimpse=t.zeros(gshape, dtype=t.float32, device=dev) if self.kind == N.APG_IMAGE_LOCALIZE else None,
+            reward=t.zeros(n, dtype=t.float64, device=dev), base_reward=t.zeros(n, dtype=t.float32, device=dev),
+            target_out=t.zeros((n, 2), dtype=t.float32, device=dev),
+            label_target=t.zeros(n, dtype=t.int32, device=dev),
+            loss_f64=t.zeros(n, dtype=t.float64, device=dev), loss_f32=t.zeros(n, dtype=t.float32, device=dev),
+            err=t.zeros(1, dtype=t.int32, device=dev))
+        self._state = N.ImageState(*[N.ptr(T[k_]) for k_ in ("pool", "pool_labels", "unique_grid", "index", "label",
+                                                              "inverted", "pos", "target", "rng", "scratch_i64",
+                                                              "scratch_f64", "top_k")])
+        self._out = N.ImageOutputs(*[N.ptr(T[k_]) for k_ in ("glimpse", "glimpse_pos", "time_step", "target_glimpse",
+                                                              "reward", "base_reward", "target_out", "label_target",
+                                                              "loss_f64", "loss_f32", "err")])
+        self._err_host = t.zeros(1, dtype=t.int32).pin_memory()
+        self._err_event = t.cuda.Event()
+        self._err_pending = False
+        self._steps_since_poll = 0
+        self._seeded = False
+        self._closed = False
+        self._t_step = 0
+        self._prev_done = False
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def unwrapped(self):
+        return self
+
+    @property
+    def prediction_space(self):
+        return self.action_space["prediction"]
+
+    @property
+    def single_prediction_space(self):
+        return self.single_action_space["prediction"]
+
+    @property
+    def inner_action_space(self):
+        return self.action_space["action"]
+
+    @property
+    def single_inner_action_space(self):
+        return self.single_action_space["action"]
+
+    @property
+    def current_labels(self):
+        return self._t["label"]
+
+    def _stream(self):
+        return N.stream_handle(self.device)
+
+    # ------------------------------------------------------------------ errors
+    @staticmethod
+    def _raise_error_bits(bits: int):
+        if bits & N.APG_ERR_NAN_PREDICTION:
+            raise ValueError(NAN_PREDICTION_MSG)
+        if bits & N.APG_ERR_NAN_ACTION:
+            raise ValueError(NAN_ACTION_MSG)
+        if bits & N.APG_ERR_OOB_Y:
+            raise ValueError(OOB_MSG % 0)
+        if bits & N.APG_ERR_OOB_X:
+            raise ValueError(OOB_MSG % 1)
+
+    def check_errors(self, block: bool = True):
+        if block:
+            import torch
+
+            torch.cuda.synchronize(self.device)
+            bits = int(self._t["err"].item())
+        elif self._err_pending and self._err_event.query():
+            bits = int(self._err_host.item())
+            self._err_pending = False
+        else:
+            return
+        if bits:
+            self._t["err"].zero_()
+            self._raise_error_bits(bits)
+
+    def _post_launch_error_copy(self):
+        if self.strict_errors:
+            self.check_errors(block=True)
+            return
+        self._steps_since_poll += 1
+        if self._err_pending or self._steps_since_poll < self.ERROR_POLL_INTERVAL:
+            return
+        self._steps_since_poll = 0
+        self._err_host.copy_(self._t["err"], non_blocking=True)
+        self._err_event.record()
+        self._err_pending = True
+
+    # ------------------------------------------------------------------ API
+    def reset(self, *, seed: int | None = None, options: dict[str, Any] | None = None):
+        if self._closed:
+            raise RuntimeError("environment is closed")
+        L = N.lib()
+        if seed is None and not self._seeded:
+            seed = int(np.random.SeedSequence().entropy) & ((1 << 63) - 1)
+        if seed is not None:
+            if not isinstance(seed, (int, np.integer)) or int(seed) < 0 or int(seed) >= 2**64:
+                raise ValueError("seed must be a non-negative int below 2**64")
+            N.check(L.apg_image_seed(ctypes.byref(self._cfg), ctypes.byref(self._state), int(seed), self._stream()),
+                    "apg_image_seed")
+            self._seeded = True
+        N.check(L.apg_image_reset(ctypes.byref(self._cfg), ctypes.byref(self._state), ctypes.byref(self._out),
+                                  self._stream()), "apg_image_reset")
+        self._t_step = 0
+        self._prev_done = False
+        if self.array_backend == "numpy":
+            self.check_errors(block=True)
+            return self._numpy_obs(), {"index": self._t["index"].cpu().numpy()}
+        self._post_launch_error_copy()
+        return self._torch_obs(), {"index": self._c(self._t["index"])}
+
+    def step(self, action):
+        import torch
+
+        if self._closed:
+            raise RuntimeError("environment is closed")
+        a, p = action["action"], action["prediction"]
+        n = self.num_envs
+        numpy_mode = self.array_backend == "numpy"
+        pdim = self._k if self.kind == N.APG_IMAGE_CLASSIFY else 2
+        if numpy_mode:
+            if isinstance(a, torch.Tensor):
+                a = a.detach().cpu().numpy()
+            if isinstance(p, torch.Tensor):
+                p = p.detach().cpu().numpy()
+            a_np = np.ascontiguousarray(a, dtype=np.float32).reshape(n, 2)
+            p_np = np.ascontiguousarray(p, dtype=np.float32).reshape(n, pdim)
+            # the module checks the prediction quality first, then (if it does not reset) the action
+            bad_p = softmax_nan_rows(p_np) if self.kind == N.APG_IMAGE_CLASSIFY else np.isnan(p_np).any(-1)
+            if bad_p.any():
+                raise ValueError(NAN_PREDICTION_MSG)
+            if not self._prev_done and np.isnan(a_np).any():
+                raise ValueError(NAN_ACTION_MSG)
+            a_t = torch.from_numpy(a_np).to(self.device, non_blocking=True)
+            p_t = torch.from_numpy(p_np).to(self.device, non_blocking=True)
+        else:
+            self.check_errors(block=False)
+            a_t = torch.as_tensor(a, dtype=torch.float32, device=self.device).reshape(n, 2).contiguous()
+            p_t = torch.as_tensor(p, dtype=torch.float32, device=self.device).reshape(n, pdim).contiguous()
+        resetting = self._prev_done
+        N.check(N.lib().apg_image_step(ctypes.byref(self._cfg), ctypes.byref(self._state), N.ptr(a_t), N.ptr(p_t),
+                                       int(self._t_step), int(resetting), ctypes.byref(self._out), self._stream()),
+                "apg_image_step")
+        if resetting:
+            self._t_step = 0
+            terminated = False
+        else:
+            self._t_step += 1
+            terminated = self._t_step >= self.config.step_limit
+        self._prev_done = terminated
+        if numpy_mode:
+            return self._numpy_step(resetting, terminated)
+        self._post_launch_error_copy()
+        return self._torch_step(resetting, terminated)
+
+    # ------------------------------------------------------------------ outputs
+    def _c(self, x):
+        return x.clone() if self.copy else x
+
+    def _numpy_obs(self):
+        T = self._t
+        obs = {"glimpse": T["glimpse"].cpu().numpy(), "glimpse_pos": T["glimpse_pos"].cpu().numpy(),
+               "time_step": T["time_step"].cpu().numpy()}
+        if self.config.randomly_invert_labels:
+            obs["inverted_label"] = (np.full(self.num_envs, 2) if self._t_step > 0
+                                     else T["inverted"].cpu().numpy().astype(np.int32))
+        if self.kind == N.APG_IMAGE_LOCALIZE:
+            obs["target_glimpse"] = T["target_glimpse"].cpu().numpy()
+        return obs
+
+    def _torch_obs(self):
+        import torch
+
+        T = self._t
+        obs = {"glimpse": self._c(T["glimpse"]), "glimpse_pos": self._c(T["glimpse_pos"]),
+               "time_step": self._c(T["time_step"])}
+        if self.config.randomly_invert_labels:
+            obs["inverted_label"] = (torch.full((self.num_envs,), 2, dtype=torch.int64, device=self.device)
+                                     if self._t_step > 0 else self._c(T["inverted"]))
+        if self.kind == N.APG_IMAGE_LOCALIZE:
+            obs["target_glimpse"] = self._c(T["target_glimpse"])
+        return obs
+
+    def _numpy_step(self, resetting, terminated):
+        import torch
+
+        torch.cuda.synchronize(self.device)
+        T = self._t
+        bits = int(T["err"].item())
+        if bits:
+            T["err"].zero_()
+            self._raise_error_bits(bits)
+        n = self.num_envs
+        obs = self._numpy_obs()
+        reward = T["reward"].cpu().numpy()
+        if self.kind == N.APG_IMAGE_LOCALIZE:
+            target = T["target_out"].cpu().numpy()
+            loss = T["loss_f32"].cpu().numpy()
+            if not resetting:
+                reward = reward.astype(np.float32)  # every value is a float32 (base - loss in f32)
+        else:
+            target = T["label_target"].cpu().numpy()
+            loss = T["loss_f64"].cpu().numpy()
+        base = np.zeros(n) if resetting else T["base_reward"].cpu().numpy()
+        info = {"index": T["index"].cpu().numpy(), "base_reward": base,
+                "prediction": {"target": target, "loss": loss}}
+        return obs, reward, np.full(n, terminated), np.zeros(n, dtype=np.bool_), info
+
+    def _torch_step(self, resetting, terminated):
+        import torch
+
+        T = self._t
+        n = self.num_envs
+        if self.kind == N.APG_IMAGE_LOCALIZE:
+            target, loss = T["target_out"], T["loss_f32"]
+        else:
+            target, loss = T["label_target"], T["loss_f64"]
+        info = {"index": self._c(T["index"]), "base_reward": self._c(T["base_reward"]),
+                "prediction": {"target": self._c(target), "loss": self._c(loss)}}
+        term = torch.full((n,), bool(terminated), dtype=torch.bool, device=self.device)
+        trunc = torch.zeros(n, dtype=torch.bool, device=self.device)
+        return self._torch_obs(), self._c(T["reward"]), term, trunc, info
+
+    def render(self):
+        raise NotImplementedError("rendering is not part of the MI355X hot path (SURVEY §8(f) item 2)")
+
+    def close(self, **kwargs):
+        if not self._closed:
+            self._closed = True
+            self._t = {}
+
+
+class ImageClassificationVectorEnv(_ImageVectorEnv):
+    """image_classification.py:22-167 (target = current labels after the module step)."""
+
+    kind = N.APG_IMAGE_CLASSIFY
+
+
+class ImageLocalizationVectorEnv(_ImageVectorEnv):
+    """image_localization.py:24-256 (unique-glimpse targets at reset, uniform targets after autoreset)."""
+
+    kind = N.APG_IMAGE_LOCALIZE

@@ -1,9 +1,13 @@
-"""Env ids of the hot path and make_vec (ap_gym/envs/registration.py:319-356, 640-690, 753-767).
+"""Env ids of the hot path and make_vec (ap_gym/envs/registration.py:145-192, 319-356, 516-690, 753-767).
 
 Only the ids whose step is accelerated by this backend are registered.  `make_vec(id, num_envs,
 **kwargs)` accepts the same keyword overrides as the reference (dataset, lidar_beam_count,
-lidar_range, static_map_index, ...) plus backend options (device, array_backend, copy,
-strict_errors, env_offset).
+lidar_range, static_map_index, image_perception_config, ...) plus backend options (device,
+array_backend, copy, strict_errors, env_offset).
+
+Image ids: the reference loads MNIST / CIFAR10 / Tiny ImageNet from the HuggingFace hub, which is
+not reachable here; pass `dataset=` (e.g. ArrayImageClassificationDataset) to use local data.  The
+registered sensor size / step limit / render options are kept.
 """
 
 from __future__ import annotations
@@ -35,6 +39,40 @@ def _lidar(num_envs: int = 1, **kwargs):
     return LIDARLocalization2DVectorEnv(num_envs=num_envs, **kwargs)
 
 
+def _image(kind: str):
+    def entry(num_envs: int = 1, image_perception_config=None, dataset=None, dataset_factory=None,
+              config_kwargs=None, **kwargs):
+        from .image_env import ImageClassificationVectorEnv, ImageLocalizationVectorEnv, ImagePerceptionConfig
+
+        if image_perception_config is None:
+            if dataset is None:
+                dataset = dataset_factory()
+            image_perception_config = ImagePerceptionConfig(dataset=dataset, **(config_kwargs or {}))
+        cls = ImageClassificationVectorEnv if kind == "cls" else ImageLocalizationVectorEnv
+        return cls(num_envs, image_perception_config, **kwargs)
+
+    return entry
+
+
+def _hf(name: str, split: str, **kw):
+    def factory():
+        from .image_dataset import HuggingfaceImageClassificationDataset
+
+        return HuggingfaceImageClassificationDataset(name, split=split, **kw)
+
+    return factory
+
+
+CIFAR10_CLASSES = ["airplane", "automobile", "bird", "cat", "deer", "dog", "frog", "horse", "ship", "truck"]
+
+
+def _register_image_ids(kind, name, factory, config_kwargs):
+    # register_img_envs (registration.py:224-260): <name>-v0 and <name>-train-v0 use the train split
+    for suffix, split in (("", "train"), ("-train", "train"), ("-test", "test")):
+        register(f"{name}{suffix}-v0", _image(kind),
+                 kwargs=dict(dataset_factory=factory(split), config_kwargs=dict(config_kwargs)))
+
+
 def register_envs():
     # registration.py:640-690: maze maps default to 21x21, rooms maps to 32x32; TimeLimit(100)
     for name, ds, static in (("LIDARLocMazeStatic-v0", FloorMapDatasetMaze, True),
@@ -42,6 +80,22 @@ def register_envs():
                              ("LIDARLocRoomsStatic-v0", FloorMapDatasetRooms, True),
                              ("LIDARLocRooms-v0", FloorMapDatasetRooms, False)):
         register(name, _lidar, kwargs=dict(dataset_factory=ds, static_map=static), max_episode_steps=100)
+    render_kw = dict(render_unvisited_opacity=0.5, render_visited_opacity=0.25)
+    _register_image_ids("cls", "MNIST", lambda split: _hf("mnist", split, channels=1), dict(step_limit=16))
+    _register_image_ids("cls", "CIFAR10", lambda split: _hf("cifar10", split, image_feature_name="img"),
+                        dict(step_limit=16, **render_kw))
+    for i in range(2, 11):
+        _register_image_ids("cls", f"CIFAR10-c{i}",
+                            lambda split, i=i: _hf("cifar10", split, image_feature_name="img",
+                                                   filter_labels=CIFAR10_CLASSES[:i]),
+                            dict(step_limit=16, **render_kw))
+    tin = lambda split: _hf("zh-plus/tiny-imagenet", split if split == "train" else "valid")  # noqa: E731
+    _register_image_ids("cls", "TinyImageNet", tin, dict(step_limit=16, sensor_size=(10, 10), **render_kw))
+    _register_image_ids("loc", "MNISTLoc", lambda split: _hf("mnist", split, channels=1),
+                        dict(step_limit=16, **render_kw))
+    _register_image_ids("loc", "CIFAR10Loc", lambda split: _hf("cifar10", split, image_feature_name="img"),
+                        dict(step_limit=16, **render_kw))
+    _register_image_ids("loc", "TinyImageNetLoc", tin, dict(step_limit=16, sensor_size=(10, 10), **render_kw))
 
 
 def make_vec(id: str | EnvSpec, num_envs: int = 1, vectorization_mode: str | None = None,
@@ -54,9 +108,12 @@ def make_vec(id: str | EnvSpec, num_envs: int = 1, vectorization_mode: str | Non
     if wrappers:
         raise NotImplementedError("per-sub-env wrappers are not supported by the batched backend")
     kw = dict(spec.kwargs)
-    factory = kw.pop("dataset_factory", None)
-    if "dataset" not in kwargs and factory is not None:
-        kwargs["dataset"] = factory()
+    if "config_kwargs" in kw:  # image ids: the entry point builds the ImagePerceptionConfig
+        kw["config_kwargs"] = dict(kw["config_kwargs"], **kwargs.pop("config_kwargs", {}))
+    else:
+        factory = kw.pop("dataset_factory", None)
+        if "dataset" not in kwargs and factory is not None:
+            kwargs["dataset"] = factory()
     if spec.max_episode_steps is not None:
         kw.setdefault("max_episode_steps", spec.max_episode_steps)
     kw.update(kwargs)

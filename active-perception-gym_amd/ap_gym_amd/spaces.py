@@ -17,6 +17,7 @@ try:  # pragma: no cover - gymnasium is absent in the build image
     Box = _gym.spaces.Box
     Dict = _gym.spaces.Dict
     Discrete = _gym.spaces.Discrete
+    MultiDiscrete = _gym.spaces.MultiDiscrete
     HAVE_GYMNASIUM = True
 except ImportError:
     HAVE_GYMNASIUM = False
@@ -51,6 +52,12 @@ except ImportError:
             self.n = int(n)
             self.start = int(start)
 
+    class MultiDiscrete(Space):  # type: ignore[no-redef]
+        def __init__(self, nvec, dtype=np.int64):
+            nvec = np.asarray(nvec, dtype=np.int64)
+            super().__init__(nvec.shape, dtype)
+            self.nvec = nvec
+
     class Dict(Space):  # type: ignore[no-redef]
         def __init__(self, spaces=None, **kw):
             super().__init__(None, None)
@@ -67,6 +74,13 @@ except ImportError:
 
         def __repr__(self):
             return "Dict(" + ", ".join(f"{k!r}: {v}" for k, v in self.spaces.items()) + ")"
+
+
+class LogitSpace(Box):
+    """Unbounded logits of a classifier (ap_gym/logit_space.py)."""
+
+    def __repr__(self):
+        return f"LogitSpace({self.shape}, {self.dtype})"
 
 
 class ImageSpace(Box):
@@ -119,6 +133,11 @@ def batch_space(space, n: int):
         return ActivePerceptionActionSpace(batch_space(space["action"], n), batch_space(space["prediction"], n))
     if isinstance(space, Dict):
         return Dict({k: batch_space(v, n) for k, v in space.spaces.items()})
+    if isinstance(space, LogitSpace):
+        b = batch_box(space, n)
+        return LogitSpace(b.low, b.high, b.shape, b.dtype)
     if isinstance(space, Box):
         return batch_box(space, n)
+    if isinstance(space, Discrete):
+        return MultiDiscrete(np.full(n, space.n))
     raise TypeError(f"cannot batch {type(space).__name__}")

@@ -1,0 +1,813 @@
+// apg_image.hip — gfx950 kernels + C ABI for the image glimpse envs (ImageClassificationVectorEnv,
+// ImageLocalizationVectorEnv over ImagePerceptionModule; ap_gym/envs/image_*.py, image/*.py).
+//
+//   k_rng_fill       one workgroup draws a whole batch from ONE numpy stream (apg_rng.hpp).
+//   k_image_gather   labels of the newly drawn data points, optional label inversion (:130-139).
+//   k_image_env      one thread per env: prediction/action NaN checks, normalized CE (f64) or MSE
+//                    (f32) loss, project_sphere move + clip (f64), base reward, reward (:191-217,
+//                    image_classification.py:113-127, image_localization.py:151-181).
+//   k_glimpse        one thread per glimpse pixel: scipy RGI "linear" bilinear in f64 in
+//                    _evaluate_linear's term order, clip(0, 1), float32 (:294-331).  Images stay in
+//                    the resident uint8 pool; the u8 -> f32/255 conversion is a 256-entry table.
+//   k_unique         one workgroup per env: glimpses of the P sampling-grid points are staged in LDS
+//                    tile by tile, every unordered pair's mean squared difference is summed in
+//                    numpy's pairwise order, min-reduced per point (LDS atomics), then one wave
+//                    ranks the top k (:253-277).
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (see build.py).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+
+#include "../../include/apgym_capi.h"
+#include "apg_host.hpp"
+#include "apg_rng.hpp"
+
+using namespace apg;
+
+namespace {
+
+// ------------------------------------------------------------------ numpy pairwise summation
+// numpy loops_utils.h.src pairwise_sum (PW_BLOCKSIZE 128) over n values x(i), f32 accumulators.
+// The leaf is kept out of line: the recursion below expands into one call per leaf.
+template <class F>
+__device__ __noinline__ float pw_leaf(const F &x, int off, int n) {
+  if (n < 8) {
+    float r = 0.0f;
+    for (int i = 0; i < n; i++) r = __fadd_rn(r, x(off + i));
+    return r;
+  }
+  float r0 = x(off), r1 = x(off + 1), r2 = x(off + 2), r3 = x(off + 3);
+  float r4 = x(off + 4), r5 = x(off + 5), r6 = x(off + 6), r7 = x(off + 7);
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+    r0 = __fadd_rn(r0, x(off + i));
+    r1 = __fadd_rn(r1, x(off + i + 1));
+    r2 = __fadd_rn(r2, x(off + i + 2));
+    r3 = __fadd_rn(r3, x(off + i + 3));
+    r4 = __fadd_rn(r4, x(off + i + 4));
+    r5 = __fadd_rn(r5, x(off + i + 5));
+    r6 = __fadd_rn(r6, x(off + i + 6));
+    r7 = __fadd_rn(r7, x(off + i + 7));
+  }
+  float res = __fadd_rn(__fadd_rn(__fadd_rn(r0, r1), __fadd_rn(r2, r3)), __fadd_rn(__fadd_rn(r4, r5), __fadd_rn(r6, r7)));
+  for (; i < n; i++) res = __fadd_rn(res, x(off + i));
+  return res;
+}
+
+template <int DEPTH, class F>
+APG_DEV float pw_sum(const F &x, int off, int n) {
+  if constexpr (DEPTH == 0) {
+    return pw_leaf(x, off, n);  // callers keep n <= 128 << MAX_PW_DEPTH
+  } else {
+    if (n <= 128) return pw_leaf(x, off, n);
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return __fadd_rn(pw_sum<DEPTH - 1>(x, off, n2), pw_sum<DEPTH - 1>(x, off + n2, n - n2));
+  }
+}
+constexpr int MAX_PW_DEPTH = 7;  // n <= 128 * 2^7 = 16384 summands
+constexpr int MAX_PW_N = 128 << MAX_PW_DEPTH;
+
+// ------------------------------------------------------------------ geometry of a glimpse
+struct GlimpseGeo {
+  int h, w, pc, c, s0, s1;
+  double lim_x, lim_y;  // sensor_pos_lim_pixels (x first, like the reference)
+  double scale, cy, cx;  // grid centres (h - 1) / 2, (w - 1) / 2
+  int pool_f32;
+  int64_t img_elems;     // h * w * pc
+};
+
+GlimpseGeo make_geo(const apg_image_config *c) {
+  GlimpseGeo g;
+  g.h = c->height;
+  g.w = c->width;
+  g.pc = c->pool_channels;
+  g.c = c->channels;
+  g.s0 = c->sensor_h;
+  g.s1 = c->sensor_w;
+  g.scale = c->sensor_scale;
+  // (flip(image_shape[1:3]) - 1) / 2 - (sensor_size * sensor_scale - 1) / 2   (:419-423)
+  g.lim_x = ((double)c->width - 1.0) / 2.0 - ((double)c->sensor_h * c->sensor_scale - 1.0) / 2.0;
+  g.lim_y = ((double)c->height - 1.0) / 2.0 - ((double)c->sensor_w * c->sensor_scale - 1.0) / 2.0;
+  g.cy = ((double)c->height - 1.0) / 2.0;
+  g.cx = ((double)c->width - 1.0) / 2.0;
+  g.pool_f32 = c->pool_dtype == APG_POOL_F32;
+  g.img_elems = (int64_t)c->height * c->width * c->pool_channels;
+  return g;
+}
+
+// float32(v) / 255 for v = 0..255, correctly rounded (f64 division, then one rounding)
+__constant__ float c_u8_to_f32[256];
+
+APG_DEV float pool_value(const GlimpseGeo &g, const void *pool, int64_t base, int y, int x, int ch) {
+  const int64_t i = base + ((int64_t)y * g.w + x) * g.pc + (g.pc == 1 ? 0 : ch);
+  return g.pool_f32 ? static_cast<const float *>(pool)[i] : c_u8_to_f32[static_cast<const uint8_t *>(pool)[i]];
+}
+
+// grid interval of v on the unit grid k - c (k = 0..n-1): g[i] <= v < g[i+1], clipped to [0, n-2]
+// (scipy _rgi_cython.find_indices / find_interval_ascending); returns i and v - g[i]
+APG_DEV int grid_interval(double v, double c, int n, double &frac) {
+  double f = floor(__dadd_rn(v, c));
+  int i = (int)f;
+  if (i > n - 2) i = n - 2;
+  if (i < 0) i = 0;
+  if (__dsub_rn((double)i, c) > v && i > 0) i--;
+  frac = __dsub_rn(v, __dsub_rn((double)i, c));
+  return i;
+}
+
+// One glimpse pixel (i, j) of image `base` at normalized position (px, py): C channels into out.
+// Returns APG_ERR_OOB_* bits for points outside the image grid (RGI bounds_error=True).
+APG_DEV uint32_t glimpse_pixel(const GlimpseGeo &g, const void *pool, int64_t base, double px, double py, int i, int j,
+                               float *out) {
+  // flip(denormalize(pos)) + offsets: (y, x) = (pos_y * lim_y + o0[i], pos_x * lim_x + o1[j])
+  const double o0 = __dmul_rn(__dsub_rn((double)i, ((double)g.s0 - 1.0) / 2.0), g.scale);
+  const double o1 = __dmul_rn(__dsub_rn((double)j, ((double)g.s1 - 1.0) / 2.0), g.scale);
+  const double y = __dadd_rn(__dmul_rn(py, g.lim_y), o0);
+  const double x = __dadd_rn(__dmul_rn(px, g.lim_x), o1);
+  uint32_t err = 0;
+  if (!(y >= -g.cy && y <= g.cy)) err |= APG_ERR_OOB_Y;
+  if (!(x >= -g.cx && x <= g.cx)) err |= APG_ERR_OOB_X;
+  double wy, wx;
+  const int iy = grid_interval(y, g.cy, g.h, wy);
+  const int ix = grid_interval(x, g.cx, g.w, wx);
+  const double ny = __dsub_rn(1.0, wy), nx = __dsub_rn(1.0, wx);
+  // hypercube order of _evaluate_linear: (i0, j0), (i0, j0+1), (i0+1, j0), (i0+1, j0+1); w = (1*wy)*wx
+  const double w00 = __dmul_rn(ny, nx), w01 = __dmul_rn(ny, wx), w10 = __dmul_rn(wy, nx), w11 = __dmul_rn(wy, wx);
+  for (int ch = 0; ch < g.c; ch++) {
+    double v = __dadd_rn(0.0, __dmul_rn((double)pool_value(g, pool, base, iy, ix, ch), w00));
+    v = __dadd_rn(v, __dmul_rn((double)pool_value(g, pool, base, iy, ix + 1, ch), w01));
+    v = __dadd_rn(v, __dmul_rn((double)pool_value(g, pool, base, iy + 1, ix, ch), w10));
+    v = __dadd_rn(v, __dmul_rn((double)pool_value(g, pool, base, iy + 1, ix + 1, ch), w11));
+    v = v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);  // np.clip(0, 1)
+    out[ch] = (float)v;
+  }
+  return err;
+}
+
+// ------------------------------------------------------------------ k_rng_fill
+constexpr int FILL_THREADS = 1024;
+
+struct FillArgs {
+  int kind;
+  int64_t n;
+  int cols;
+  double low[2], range[2];
+  int64_t lo;
+  uint64_t bound;   // exclusive range of integers(lo, lo + bound)
+  int64_t cand;     // candidate words examined in parallel (>= n)
+};
+
+// block-wide exclusive scan of per-thread counts; returns the exclusive prefix, total in *total
+__device__ int64_t block_exclusive_scan(int64_t v, int64_t *s_wave, int64_t *total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t inc = v;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) s_wave[wave] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t acc = 0;
+    for (int k = 0; k < FILL_THREADS / 64; k++) {
+      const int64_t t = s_wave[k];
+      s_wave[k] = acc;
+      acc += t;
+    }
+    s_wave[FILL_THREADS / 64] = acc;
+  }
+  __syncthreads();
+  *total = s_wave[FILL_THREADS / 64];
+  return s_wave[wave] + inc - v;
+}
+
+__global__ __launch_bounds__(FILL_THREADS) void k_rng_fill(apg_pcg64 *st, FillArgs a, void *out) {
+  __shared__ int64_t s_wave[FILL_THREADS / 64 + 1];
+  __shared__ uint64_t s_consumed;
+  const int tid = threadIdx.x;
+  const Pcg64 base = *reinterpret_cast<const Pcg64 *>(st);
+  if (a.kind == APG_DRAW_UNIFORM) {
+    // random_uniform: off + scale * next_double, one next64 per value, C order over (n, cols)
+    const int64_t m = a.n * a.cols, chunk = (m + FILL_THREADS - 1) / FILL_THREADS;
+    const int64_t k0 = tid * chunk, k1 = k0 + chunk < m ? k0 + chunk : m;
+    double *o = static_cast<double *>(out);
+    if (k0 < k1) {
+      Pcg64 r = base;
+      pcg_advance(r, (uint64_t)k0);
+      for (int64_t k = k0; k < k1; k++) {
+        const int c = (int)(k % a.cols);
+        o[k] = __dadd_rn(a.low[c], __dmul_rn(a.range[c], next_double(r)));
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      Pcg64 r = base;
+      pcg_advance(r, (uint64_t)m);
+      *reinterpret_cast<Pcg64 *>(st) = r;
+    }
+    return;
+  }
+  // integers: random_bounded_uint64_fill for rng = bound - 1 < 2^32 (Lemire on next_uint32; the
+  // full 32-bit range takes next_uint32 as is; a one-value range draws nothing)
+  int64_t *o = static_cast<int64_t *>(out);
+  const uint64_t rng = a.bound - 1;
+  if (rng == 0) {
+    for (int64_t i = tid; i < a.n; i += FILL_THREADS) o[i] = a.lo;
+    return;
+  }
+  const bool full = rng == 0xffffffffULL;
+  const uint32_t rex = (uint32_t)(rng + 1);             // unused when full
+  const uint32_t thr = full ? 0u : (uint32_t)((0xffffffffULL - rng) % rex);
+  const int64_t chunk = (a.cand + FILL_THREADS - 1) / FILL_THREADS;
+  const int64_t k0 = tid * chunk, k1 = k0 + chunk < a.cand ? k0 + chunk : a.cand;
+  // pass 1: accepted candidates per thread
+  int64_t cnt = 0;
+  if (k0 < k1) {
+    Next32Walker wk(base, (uint64_t)k0);
+    for (int64_t k = k0; k < k1; k++) {
+      const uint32_t u = wk.next();
+      if (full || (uint32_t)((uint64_t)u * rex) >= thr) cnt++;
+    }
+  }
+  int64_t total;
+  const int64_t before = block_exclusive_scan(cnt, s_wave, &total);
+  if (tid == 0) s_consumed = (uint64_t)a.cand;
+  __syncthreads();
+  // pass 2: the i-th accepted candidate is output i
+  int64_t q = before;
+  if (q < a.n && k0 < k1) {
+    Next32Walker wk(base, (uint64_t)k0);
+    for (int64_t k = k0; k < k1 && q < a.n; k++) {
+      const uint32_t u = wk.next();
+      const uint64_t mlt = (uint64_t)u * rex;
+      if (full || (uint32_t)mlt >= thr) {
+        o[q] = a.lo + (int64_t)(full ? (uint64_t)u : (mlt >> 32));
+        if (q == a.n - 1) s_consumed = (uint64_t)k + 1;
+        q++;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    Pcg64 r = after_next32_words(base, s_consumed);
+    // not enough accepted candidates (astronomically rare for the sizes used): finish sequentially
+    for (int64_t i = total; i < a.n; i++) {
+      uint64_t mlt;
+      uint32_t u;
+      do {
+        u = next32(r);
+        mlt = (uint64_t)u * rex;
+      } while (!full && (uint32_t)mlt < thr);
+      o[i] = a.lo + (int64_t)(full ? (uint64_t)u : (mlt >> 32));
+    }
+    *reinterpret_cast<Pcg64 *>(st) = r;
+  }
+}
+
+// ------------------------------------------------------------------ seeding chain
+__global__ void k_image_seed(apg_pcg64 *rng, uint64_t seed) {
+  // gymnasium VectorEnv.reset(seed): np_random = default_rng(seed); the _np_random setter seeds the
+  // module with np_random.integers(0, 2**32 - 1, endpoint=True) (a full-range next_uint32);
+  // module.seed: current_rng = default_rng(s); DatasetBatchIterator(seed=current_rng.integers(...))
+  Pcg64 env = seed_pcg64(seed);
+  const uint32_t s_module = next32(env);
+  Pcg64 cur = seed_pcg64(s_module);
+  const uint32_t s_iter = next32(cur);
+  const Pcg64 it = seed_pcg64(s_iter);
+  reinterpret_cast<Pcg64 *>(rng)[0] = env;
+  reinterpret_cast<Pcg64 *>(rng)[1] = cur;
+  reinterpret_cast<Pcg64 *>(rng)[2] = it;
+}
+
+// ------------------------------------------------------------------ k_image_gather
+__global__ void k_image_gather(int n, const int32_t *pool_labels, const int64_t *index, int invert,
+                               const int64_t *inv_draw, int num_classes, int32_t *label, int32_t *inverted) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  int32_t l = pool_labels[index[e]];
+  if (invert) {
+    const int32_t inv = inv_draw[e] == 1 ? 1 : 0;  // integers(0, 2, N) == 1
+    inverted[e] = inv;
+    if (inv) l = num_classes - l - 1;
+  }
+  label[e] = l;
+}
+
+// ------------------------------------------------------------------ k_glimpse
+template <class PosT>
+__global__ __launch_bounds__(256) void k_glimpse(GlimpseGeo g, const void *pool, const int64_t *index,
+                                                 const PosT *pos, int npos, int64_t total, float *out,
+                                                 uint32_t *err) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int j = (int)(t % g.s1);
+  const int i = (int)((t / g.s1) % g.s0);
+  const int64_t np_ = t / ((int64_t)g.s0 * g.s1);  // env * npos + p
+  const int64_t e = np_ / npos;
+  const double px = (double)pos[2 * np_], py = (double)pos[2 * np_ + 1];
+  float v[3];
+  const uint32_t bad = glimpse_pixel(g, pool, index[e] * g.img_elems, px, py, i, j, v);
+  for (int ch = 0; ch < g.c; ch++) out[t * g.c + ch] = v[ch];
+  if (bad) atomicOr(err, bad);
+}
+
+// ------------------------------------------------------------------ k_image_env
+struct EnvArgs {
+  int n, kind, k, resetting;
+  double msl[2];
+  double ce_scale, ce_offset;
+  float mse_scale, mse_offset;
+  float time_value;
+};
+
+// scipy.special.log_softmax(row)[target] in float32 (x_max zeroed when not finite); -> -value
+APG_DEV float ce_f32(const float *row, int k, int target) {
+  float m = row[0];
+  bool nan = false;
+  for (int i = 0; i < k; i++) {
+    const float v = row[i];
+    if (v != v) nan = true;
+    m = v > m ? v : m;
+  }
+  if (nan || isinf(m)) m = 0.0f;  // np.amax propagates NaN; x_max[~isfinite] = 0
+  auto ex = [&](int i) { return expf(__fsub_rn(row[i], m)); };
+  const float s = pw_sum<MAX_PW_DEPTH>(ex, 0, k);
+  const float out = __fsub_rn(__fsub_rn(row[target], m), logf(s));
+  return -out;
+}
+
+// NaN in softmax(row)[label] (the quality the reference checks, image_classification.py:114-116):
+// exactly when a logit is NaN or +inf, or all logits are -inf
+APG_DEV bool softmax_nan(const float *row, int k) {
+  bool bad = false, all_neg_inf = true;
+  for (int i = 0; i < k; i++) {
+    const float v = row[i];
+    if (v != v || v == INFINITY) bad = true;
+    if (v != -INFINITY) all_neg_inf = false;
+  }
+  return bad || all_neg_inf;
+}
+
+__global__ __launch_bounds__(256) void k_image_env(EnvArgs a, const float *__restrict__ act,
+                                                   const float *__restrict__ pred, const int32_t *label,
+                                                   double *pos, apg_image_outputs out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n) return;
+  uint32_t err = 0;
+  double loss_d;
+  float loss_f = 0.0f;
+  if (a.kind == APG_IMAGE_CLASSIFY) {
+    const float *row = pred + (size_t)e * a.k;
+    if (softmax_nan(row, a.k)) err |= APG_ERR_NAN_PREDICTION;
+    const int32_t l = label[e];
+    // CrossEntropyLossFn(...).normalized: f32 CE * scale(f64) + offset(f64)
+    loss_d = __dadd_rn(__dmul_rn((double)ce_f32(row, a.k, l), a.ce_scale), a.ce_offset);
+    out.loss_f64[e] = loss_d;
+    out.label_target[e] = l;
+  } else {
+    const float p0 = pred[2 * e], p1 = pred[2 * e + 1];
+    if (p0 != p0 || p1 != p1) err |= APG_ERR_NAN_PREDICTION;  // 1 - |pred - target| / 2 is NaN
+    // the loss compares against the target before the autoreset update (out.target: pre-update copy)
+    const float t0 = out.target[2 * e], t1 = out.target[2 * e + 1];
+    const float d0 = __fsub_rn(p0, t0), d1 = __fsub_rn(p1, t1);
+    // np.mean(f32 [2]): (0 + d0^2 + d1^2) / 2, then * scale + offset in f32
+    const float mse = f32_div(__fadd_rn(__fadd_rn(0.0f, __fmul_rn(d0, d0)), __fmul_rn(d1, d1)), 2.0f);
+    loss_f = __fadd_rn(__fmul_rn(mse, a.mse_scale), a.mse_offset);
+    out.loss_f32[e] = loss_f;
+    loss_d = (double)loss_f;
+  }
+  double px = pos[2 * e], py = pos[2 * e + 1];
+  if (a.resetting) {
+    // module.reset() replaced the batch; base_reward = np.zeros(N) (float64)
+    out.base_reward[e] = 0.0f;
+    out.reward[e] = __dsub_rn(0.0, loss_d);
+  } else {
+    const float a0 = act[2 * e], a1 = act[2 * e + 1];
+    if (a0 != a0 || a1 != a1) err |= APG_ERR_NAN_ACTION;
+    // project_sphere (util.py:94-97) in f32, then max_step_length (f64) * step, clip(-1, 1)
+    const float mag = norm_f32(a0, a1);
+    float s0 = a0, s1 = a1;
+    if (mag > 1.0f) {
+      const float den = mag > 1.0f ? mag : 1.0f;
+      s0 = __fmul_rn(f32_div(a0, den), 1.0f);
+      s1 = __fmul_rn(f32_div(a1, den), 1.0f);
+    }
+    px = __dadd_rn(px, __dmul_rn(a.msl[0], (double)s0));
+    py = __dadd_rn(py, __dmul_rn(a.msl[1], (double)s1));
+    px = px < -1.0 ? -1.0 : (px > 1.0 ? 1.0 : px);
+    py = py < -1.0 ? -1.0 : (py > 1.0 ? 1.0 : py);
+    pos[2 * e] = px;
+    pos[2 * e + 1] = py;
+    const float base = __fmul_rn(-mag, 1e-3f);  // -norm(action) * 1e-3 (f32, weak Python scalar)
+    out.base_reward[e] = base;
+    out.reward[e] = a.kind == APG_IMAGE_CLASSIFY ? __dsub_rn((double)base, loss_d)
+                                                 : (double)__fsub_rn(base, loss_f);
+  }
+  out.glimpse_pos[2 * e] = (float)px;
+  out.glimpse_pos[2 * e + 1] = (float)py;
+  out.time_step[e] = a.time_value;
+  if (err) atomicOr(out.err, err);
+}
+
+// ------------------------------------------------------------------ k_unique
+constexpr int UNIQ_THREADS = 256;
+constexpr int UNIQ_LDS_FLOATS = 24 * 1024;  // 96 KiB of glimpse tiles (two tiles)
+constexpr int UNIQ_MAX_POINTS = 4096;
+
+// tile of T glimpses (rows p0 .. p0+T-1 of the sampling grid) into LDS rows of stride L + 1
+APG_DEV void unique_tile(const GlimpseGeo &g, const void *pool, int64_t base, const double *grid, int p0, int T,
+                         int P, int L, float *tile) {
+  const int per = g.s0 * g.s1;
+  for (int q = threadIdx.x; q < T * per; q += UNIQ_THREADS) {
+    const int r = q / per, pix = q % per, p = p0 + r;
+    if (p >= P) continue;
+    float v[3];
+    glimpse_pixel(g, pool, base, grid[2 * p], grid[2 * p + 1], pix / g.s1, pix % g.s1, v);
+    for (int ch = 0; ch < g.c; ch++) tile[r * (L + 1) + pix * g.c + ch] = v[ch];
+  }
+}
+
+__global__ __launch_bounds__(UNIQ_THREADS) void k_unique(GlimpseGeo g, const void *pool, const int64_t *index,
+                                                         const double *grid, int P, int T, int k, int32_t *top_k,
+                                                         float *uniq) {
+  extern __shared__ float s_dyn[];
+  __shared__ uint32_t s_min[UNIQ_MAX_POINTS];
+  const int e = blockIdx.x;
+  const int L = g.s0 * g.s1 * g.c;
+  float *tA = s_dyn, *tB = s_dyn + T * (L + 1);
+  const int64_t base = index[e] * g.img_elems;
+  for (int p = threadIdx.x; p < P; p += UNIQ_THREADS) s_min[p] = 0x7f800000u;  // +inf
+  const int tiles = (P + T - 1) / T;
+  const float inv_l_den = (float)L;
+  for (int A = 0; A < tiles; A++) {
+    __syncthreads();
+    unique_tile(g, pool, base, grid, A * T, T, P, L, tA);
+    for (int B = A; B < tiles; B++) {
+      __syncthreads();
+      if (B != A) unique_tile(g, pool, base, grid, B * T, T, P, L, tB);
+      __syncthreads();
+      const float *sb = B == A ? tA : tB;
+      const int na = A * T + T <= P ? T : P - A * T, nb = B * T + T <= P ? T : P - B * T;
+      for (int q = threadIdx.x; q < na * nb; q += UNIQ_THREADS) {
+        const int ra = q / nb, rb = q % nb;
+        if (B == A && rb <= ra) continue;  // unordered pairs a < b (the mean is symmetric)
+        const float *xa = tA + ra * (L + 1), *xb = sb + rb * (L + 1);
+        auto sq = [&](int l) {
+          const float d = __fsub_rn(xb[l], xa[l]);
+          return __fmul_rn(d, d);
+        };
+        // np.mean over the (G, G, C) block: (0 + pairwise_sum) / L in f32
+        const float m = f32_div(__fadd_rn(0.0f, pw_sum<MAX_PW_DEPTH>(sq, 0, L)), inv_l_den);
+        const uint32_t bits = __float_as_uint(m);  // m >= 0: unsigned order == float order
+        atomicMin(&s_min[A * T + ra], bits);
+        atomicMin(&s_min[B * T + rb], bits);
+      }
+    }
+  }
+  __syncthreads();
+  if (uniq)
+    for (int p = threadIdx.x; p < P; p += UNIQ_THREADS) uniq[(size_t)e * P + p] = __uint_as_float(s_min[p]);
+  // top k by descending uniqueness, exact ties by ascending index: one wave, k selection rounds
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    for (int r = 0; r < k; r++) {
+      uint32_t best = 0;
+      int bi = 0x7fffffff;
+      for (int p = lane; p < P; p += 64) {
+        const uint32_t v = s_min[p];
+        if (v != 0xffffffffu && (bi == 0x7fffffff || v > best)) {
+          best = v;
+          bi = p;
+        }
+      }
+      for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t ob = __shfl_xor(best, d, 64);
+        const int oi = __shfl_xor(bi, d, 64);
+        if (oi != 0x7fffffff && (bi == 0x7fffffff || ob > best || (ob == best && oi < bi))) {
+          best = ob;
+          bi = oi;
+        }
+      }
+      if (lane == 0) {
+        top_k[(size_t)e * k + r] = bi;
+        s_min[bi] = 0xffffffffu;  // taken
+      }
+      __builtin_amdgcn_wave_barrier();
+      __threadfence_block();
+    }
+  }
+}
+
+// target = clip(grid[top_k[sel]] + jitter, -1, 1).astype(float32)  (:281-292, image_localization.py:139-143)
+__global__ void k_unique_finish(int n, int k, const int32_t *top_k, const int64_t *sel, const double *grid,
+                                const double *jitter, float *target) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int p = top_k[(size_t)e * k + sel[e]];
+  for (int c = 0; c < 2; c++) {
+    double v = __dadd_rn(grid[2 * p + c], jitter[2 * e + c]);
+    v = v < -1.0 ? -1.0 : (v > 1.0 ? 1.0 : v);
+    target[2 * e + c] = (float)v;
+  }
+}
+
+// target[prev_done] = np_random.uniform(-1, 1, (k, 2)).astype(float32); out_prev = pre-update copy
+__global__ void k_loc_target(int n, int refresh, const double *draw, float *target, float *out_prev) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  for (int c = 0; c < 2; c++) {
+    out_prev[2 * e + c] = target[2 * e + c];
+    if (refresh) target[2 * e + c] = (float)draw[2 * e + c];
+  }
+}
+
+// glimpse_pos = pos.astype(float32); time_step = full(N, value)
+__global__ void k_obs_pos(int n, const double *pos, float *glimpse_pos, float *time_step, float value) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  glimpse_pos[2 * e] = (float)pos[2 * e];
+  glimpse_pos[2 * e + 1] = (float)pos[2 * e + 1];
+  time_step[e] = value;
+}
+
+// ------------------------------------------------------------------ standalone losses
+__global__ void k_loss_ce(const float *logits, const int32_t *target, int n, int k, double scale, double offset,
+                          double *out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  out[e] = __dadd_rn(__dmul_rn((double)ce_f32(logits + (size_t)e * k, k, target[e]), scale), offset);
+}
+
+__global__ void k_loss_mse(const float *pred, const float *target, int n, int d, float scale, float offset,
+                           float *out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const float *p = pred + (size_t)e * d, *t = target + (size_t)e * d;
+  auto sq = [&](int i) {
+    const float x = __fsub_rn(p[i], t[i]);
+    return __fmul_rn(x, x);
+  };
+  const float m = f32_div(__fadd_rn(0.0f, pw_sum<MAX_PW_DEPTH>(sq, 0, d)), (float)d);
+  out[e] = __fadd_rn(__fmul_rn(m, scale), offset);
+}
+
+// ------------------------------------------------------------------ host side
+int grid_for(int64_t n, int threads) { return (int)((n + threads - 1) / threads); }
+
+int ensure_u8_table() {
+  static bool done = false;
+  if (done) return APG_OK;
+  float t[256];
+  for (int v = 0; v < 256; v++) t[v] = (float)((double)(float)v / 255.0);  // f32(v) / 255, correctly rounded
+  if (hipMemcpyToSymbol(HIP_SYMBOL(c_u8_to_f32), t, sizeof(t)) != hipSuccess)
+    return fail(APG_E_LAUNCH, "hipMemcpyToSymbol(u8 table) failed");
+  done = true;
+  return APG_OK;
+}
+
+int validate(const apg_image_config *c) {
+  if (c->num_envs <= 0) return fail(APG_E_INVALID, "num_envs must be positive");
+  if (c->height < 2 || c->width < 2) return fail(APG_E_INVALID, "images must be at least 2 x 2");
+  if (c->pool_channels != 1 && c->pool_channels != 3) return fail(APG_E_INVALID, "pool channels must be 1 or 3");
+  if (c->channels != 1 && c->channels != 3) return fail(APG_E_INVALID, "Target channels must be either 1 or 3");
+  if (c->pool_channels == 3 && c->channels == 1)
+    return fail(APG_E_INVALID, "Invalid image format. Expected 1 channels but got 3");
+  if (c->sensor_h <= 0 || c->sensor_w <= 0) return fail(APG_E_INVALID, "sensor size must be positive");
+  if ((int64_t)c->sensor_h * c->sensor_w * c->channels > MAX_PW_N)
+    return fail(APG_E_INVALID, "glimpse too large");
+  if (c->pool_len <= 0 || c->pool_len > 0xffffffffLL) return fail(APG_E_INVALID, "pool_len must be in [1, 2**32]");
+  if (c->step_limit <= 0) return fail(APG_E_INVALID, "step_limit must be positive");
+  if (c->kind == APG_IMAGE_CLASSIFY && (c->num_classes <= 0 || c->num_classes > MAX_PW_N))
+    return fail(APG_E_INVALID, "num_classes out of range");
+  if (c->kind != APG_IMAGE_CLASSIFY && c->kind != APG_IMAGE_LOCALIZE) return fail(APG_E_INVALID, "unknown image env kind");
+  return APG_OK;
+}
+
+int launch_fill(apg_pcg64 *state, const FillArgs &a0, void *out, hipStream_t s) {
+  FillArgs a = a0;
+  if (a.kind == APG_DRAW_INTEGERS) {
+    // enough candidates that the n-th acceptance falls inside them with overwhelming probability
+    const uint64_t rng = a.bound - 1;
+    double p_rej = 0.0;
+    if (rng != 0xffffffffULL && rng != 0) p_rej = (double)((0xffffffffULL - rng) % (rng + 1)) / 4294967296.0;
+    const double expect = (double)a.n / (1.0 - p_rej);
+    a.cand = (int64_t)(expect + 8.0 * std::sqrt(expect * p_rej + 1.0) + 64.0);
+    if (a.cand < a.n) a.cand = a.n;
+  }
+  hipLaunchKernelGGL(k_rng_fill, dim3(1), dim3(FILL_THREADS), 0, s, state, a, out);
+  return check_launch("k_rng_fill");
+}
+
+int launch_integers(apg_pcg64 *state, int64_t n, int64_t lo, uint64_t bound, int64_t *out, hipStream_t s) {
+  FillArgs a{};
+  a.kind = APG_DRAW_INTEGERS;
+  a.n = n;
+  a.cols = 1;
+  a.lo = lo;
+  a.bound = bound;
+  return launch_fill(state, a, out, s);
+}
+
+int launch_uniform(apg_pcg64 *state, int64_t n, int cols, const double *low, const double *range, double *out,
+                   hipStream_t s) {
+  FillArgs a{};
+  a.kind = APG_DRAW_UNIFORM;
+  a.n = n;
+  a.cols = cols;
+  for (int c = 0; c < cols; c++) {
+    a.low[c] = low[c];
+    a.range[c] = range[c];
+  }
+  return launch_fill(state, a, out, s);
+}
+
+template <class PosT>
+int launch_glimpse(const GlimpseGeo &g, const void *pool, const int64_t *index, const PosT *pos, int n, int npos,
+                   float *out, uint32_t *err, hipStream_t s) {
+  const int64_t total = (int64_t)n * npos * g.s0 * g.s1;
+  hipLaunchKernelGGL(k_glimpse<PosT>, dim3(grid_for(total, 256)), dim3(256), 0, s, g, pool, index, pos, npos, total,
+                     out, err);
+  return check_launch("k_glimpse");
+}
+
+int unique_tile_rows(int L) {
+  int T = UNIQ_LDS_FLOATS / (2 * (L + 1));
+  if (T > 32) T = 32;
+  return T;
+}
+
+int launch_unique(const GlimpseGeo &g, const void *pool, const int64_t *index, const double *grid, int n, int P,
+                  int k, int32_t *top_k, float *uniq, hipStream_t s) {
+  const int L = g.s0 * g.s1 * g.c;
+  const int T = unique_tile_rows(L);
+  if (T < 1) return fail(APG_E_INVALID, "glimpse too large for the uniqueness tiles");
+  if (P > UNIQ_MAX_POINTS) return fail(APG_E_INVALID, "too many unique-sampling grid points");
+  if (k < 1 || k > P) return fail(APG_E_INVALID, "top_k must be in [1, P]");
+  const size_t dyn = (size_t)2 * T * (L + 1) * sizeof(float);
+  static bool big = false;
+  if (!big) {
+    if (hipFuncSetAttribute((const void *)k_unique, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) !=
+        hipSuccess)
+      return fail(APG_E_LAUNCH, "hipFuncSetAttribute(k_unique) failed");
+    big = true;
+  }
+  hipLaunchKernelGGL(k_unique, dim3(n), dim3(UNIQ_THREADS), dyn, s, g, pool, index, grid, P, T, k, top_k, uniq);
+  return check_launch("k_unique");
+}
+
+}  // namespace
+
+extern "C" {
+
+int apg_rng_fill(apg_pcg64 *state, int kind, int64_t n, int cols, const double *low, const double *range, int64_t lo,
+                 uint64_t bound, void *out, apg_stream_t stream) {
+  if (!state || !out || n < 0) return fail(APG_E_INVALID, "bad apg_rng_fill arguments");
+  if (n == 0) return APG_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (kind == APG_DRAW_UNIFORM) {
+    if (cols < 1 || cols > 2 || !low || !range) return fail(APG_E_INVALID, "uniform draws need 1 or 2 columns");
+    return launch_uniform(state, n, cols, low, range, static_cast<double *>(out), s);
+  }
+  if (kind == APG_DRAW_INTEGERS) {
+    if (bound < 1 || bound > 0x100000000ULL) return fail(APG_E_INVALID, "integers range must be in [1, 2**32]");
+    return launch_integers(state, n, lo, bound, static_cast<int64_t *>(out), s);
+  }
+  return fail(APG_E_INVALID, "unknown draw kind");
+}
+
+int apg_image_seed(const apg_image_config *cfg, const apg_image_state *st, uint64_t seed, apg_stream_t stream) {
+  if (int rc = validate(cfg)) return rc;
+  hipLaunchKernelGGL(k_image_seed, dim3(1), dim3(1), 0, (hipStream_t)stream, st->rng, seed);
+  return check_launch("k_image_seed");
+}
+
+static int module_reset(const apg_image_config *c, const apg_image_state *st, const apg_image_outputs *out,
+                        hipStream_t s) {
+  const int n = c->num_envs;
+  int rc;
+  // next(DatasetBatchIterator): integers(0, len(dataset), N)
+  if ((rc = launch_integers(st->rng + 2, n, 0, (uint64_t)c->pool_len, st->index, s))) return rc;
+  // randomly_invert_labels: current_rng.integers(0, 2, size=N) == 1
+  if (c->invert_labels && (rc = launch_integers(st->rng + 1, n, 0, 2, st->scratch_i64, s))) return rc;
+  hipLaunchKernelGGL(k_image_gather, dim3(grid_for(n, 256)), dim3(256), 0, s, n, st->pool_labels, st->index,
+                     c->invert_labels, st->scratch_i64, c->num_classes, st->label, st->inverted);
+  if ((rc = check_launch("k_image_gather"))) return rc;
+  // current_rng.uniform(-1, 1, size=(N, 2))
+  const double low[2] = {-1.0, -1.0}, range[2] = {2.0, 2.0};
+  return launch_uniform(st->rng + 1, n, 2, low, range, st->pos, s);
+}
+
+static int observe(const apg_image_config *c, const apg_image_state *st, const apg_image_outputs *out, hipStream_t s) {
+  const GlimpseGeo g = make_geo(c);
+  int rc = launch_glimpse<double>(g, st->pool, st->index, st->pos, c->num_envs, 1, out->glimpse, out->err, s);
+  if (rc || c->kind != APG_IMAGE_LOCALIZE) return rc;
+  return launch_glimpse<float>(g, st->pool, st->index, st->target, c->num_envs, 1, out->target_glimpse, out->err, s);
+}
+
+int apg_image_reset(const apg_image_config *c, const apg_image_state *st, const apg_image_outputs *out,
+                    apg_stream_t stream) {
+  if (int rc = validate(c)) return rc;
+  if (int rc = ensure_u8_table()) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const int n = c->num_envs;
+  int rc;
+  if ((rc = module_reset(c, st, out, s))) return rc;
+  if (c->kind == APG_IMAGE_LOCALIZE) {
+    // sample_unique_glimpse_positions: rank, then current_rng.integers(0, k, N) and
+    // current_rng.uniform(-cell, cell, (N, 2)); ImageLocalizationVectorEnv keeps it as float32
+    const GlimpseGeo g = make_geo(c);
+    if ((rc = launch_unique(g, st->pool, st->index, st->unique_grid, n, c->unique_points, c->top_k, st->top_k,
+                            nullptr, s)))
+      return rc;
+    if ((rc = launch_integers(st->rng + 1, n, 0, (uint64_t)c->top_k, st->scratch_i64, s))) return rc;
+    const double low[2] = {-c->cell[0], -c->cell[1]};
+    const double range[2] = {c->cell[0] - -c->cell[0], c->cell[1] - -c->cell[1]};
+    if ((rc = launch_uniform(st->rng + 1, n, 2, low, range, st->scratch_f64, s))) return rc;
+    hipLaunchKernelGGL(k_unique_finish, dim3(grid_for(n, 256)), dim3(256), 0, s, n, c->top_k, st->top_k,
+                       st->scratch_i64, st->unique_grid, st->scratch_f64, st->target);
+    if ((rc = check_launch("k_unique_finish"))) return rc;
+  }
+  // obs: glimpse, glimpse_pos, time_step (= (0 / limit) * 2 - 1 = -1)
+  hipLaunchKernelGGL(k_obs_pos, dim3(grid_for(n, 256)), dim3(256), 0, s, n, st->pos, out->glimpse_pos,
+                     out->time_step, -1.0f);
+  if ((rc = check_launch("k_obs_pos"))) return rc;
+  return observe(c, st, out, s);
+}
+
+int apg_image_step(const apg_image_config *c, const apg_image_state *st, const float *action,
+                   const float *prediction, int32_t t, int32_t prev_done, const apg_image_outputs *out,
+                   apg_stream_t stream) {
+  if (int rc = validate(c)) return rc;
+  if (int rc = ensure_u8_table()) return rc;
+  if (!action || !prediction) return fail(APG_E_INVALID, "null action/prediction");
+  hipStream_t s = (hipStream_t)stream;
+  const int n = c->num_envs;
+  int rc;
+  if (c->kind == APG_IMAGE_LOCALIZE) {
+    // prediction_target = target.copy(); target[prev_done] = np_random.uniform(-1, 1, (k, 2)) as f32
+    if (prev_done) {
+      const double low[2] = {-1.0, -1.0}, range[2] = {2.0, 2.0};
+      if ((rc = launch_uniform(st->rng + 0, n, 2, low, range, st->scratch_f64, s))) return rc;
+    }
+    hipLaunchKernelGGL(k_loc_target, dim3(grid_for(n, 256)), dim3(256), 0, s, n, prev_done, st->scratch_f64,
+                       st->target, out->target);
+    if ((rc = check_launch("k_loc_target"))) return rc;
+  }
+  if (prev_done && (rc = module_reset(c, st, out, s))) return rc;
+  EnvArgs a;
+  a.n = n;
+  a.kind = c->kind;
+  a.k = c->num_classes;
+  a.resetting = prev_done ? 1 : 0;
+  a.msl[0] = c->max_step[0];
+  a.msl[1] = c->max_step[1];
+  a.ce_scale = c->ce_scale;
+  a.ce_offset = c->ce_offset;
+  a.mse_scale = c->mse_scale;
+  a.mse_offset = c->mse_offset;
+  const int32_t t_new = prev_done ? 0 : t + 1;
+  a.time_value = (float)(((double)t_new / (double)c->step_limit) * 2.0 - 1.0);
+  hipLaunchKernelGGL(k_image_env, dim3(grid_for(n, 256)), dim3(256), 0, s, a, action, prediction, st->label,
+                     st->pos, *out);
+  if ((rc = check_launch("k_image_env"))) return rc;
+  return observe(c, st, out, s);
+}
+
+int apg_image_glimpse(const apg_image_config *c, const void *pool, const int64_t *index, const void *pos,
+                      int pos_is_f32, int32_t npos, float *out, uint32_t *err, apg_stream_t stream) {
+  if (int rc = validate(c)) return rc;
+  if (int rc = ensure_u8_table()) return rc;
+  if (npos <= 0) return fail(APG_E_INVALID, "npos must be positive");
+  const GlimpseGeo g = make_geo(c);
+  hipStream_t s = (hipStream_t)stream;
+  if (pos_is_f32)
+    return launch_glimpse<float>(g, pool, index, static_cast<const float *>(pos), c->num_envs, npos, out, err, s);
+  return launch_glimpse<double>(g, pool, index, static_cast<const double *>(pos), c->num_envs, npos, out, err, s);
+}
+
+int apg_image_unique_top_k(const apg_image_config *c, const void *pool, const int64_t *index, const double *grid,
+                           int32_t npoints, int32_t k, int32_t *top_k, float *uniq, apg_stream_t stream) {
+  if (int rc = validate(c)) return rc;
+  if (int rc = ensure_u8_table()) return rc;
+  return launch_unique(make_geo(c), pool, index, grid, c->num_envs, npoints, k, top_k, uniq, (hipStream_t)stream);
+}
+
+int apg_loss_ce(const float *logits, const int32_t *target, int32_t n, int32_t k, double scale, double offset,
+                double *out, apg_stream_t stream) {
+  if (n <= 0 || k <= 0 || k > MAX_PW_N) return fail(APG_E_INVALID, "bad apg_loss_ce shape");
+  hipLaunchKernelGGL(k_loss_ce, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, logits, target, n, k,
+                     scale, offset, out);
+  return check_launch("k_loss_ce");
+}
+
+int apg_loss_mse(const float *pred, const float *target, int32_t n, int32_t d, float scale, float offset, float *out,
+                 apg_stream_t stream) {
+  if (n <= 0 || d <= 0 || d > MAX_PW_N) return fail(APG_E_INVALID, "bad apg_loss_mse shape");
+  hipLaunchKernelGGL(k_loss_mse, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, pred, target, n, d,
+                     scale, offset, out);
+  return check_launch("k_loss_mse");
+}
+
+}  // extern "C"

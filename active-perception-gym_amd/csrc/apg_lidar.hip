@@ -18,21 +18,16 @@
 #include <cstring>
 
 #include "../../include/apgym_capi.h"
+#include "apg_host.hpp"
 #include "apg_maps.hpp"
 #include "apg_scan.hpp"
 
 using namespace apg;
 
+namespace apg {
 namespace {
-
-constexpr uint8_t F_AUTORESET = 1, F_JUST_RESET = 2, F_FIRST = 4;
-constexpr int EPB = 64;        // envs per step workgroup
-constexpr int STEP_THREADS = 256;
-constexpr int MAX_WIN_ROWS = 32;
-constexpr int WIN_STRIDE = MAX_WIN_ROWS + 1;  // LDS words per env window (+1: lanes = envs hit distinct banks)
-constexpr int MAX_STAGED_BEAMS = 64;          // lidar rows staged in LDS for coalesced stores
-
 thread_local char g_err[512] = "";
+}
 
 int fail(int code, const char *msg) {
   snprintf(g_err, sizeof(g_err), "%s", msg);
@@ -47,6 +42,16 @@ int check_launch(const char *what) {
   }
   return APG_OK;
 }
+}  // namespace apg
+
+namespace {
+
+constexpr uint8_t F_AUTORESET = 1, F_JUST_RESET = 2, F_FIRST = 4;
+constexpr int EPB = 64;        // envs per step workgroup
+constexpr int STEP_THREADS = 256;
+constexpr int MAX_WIN_ROWS = 32;
+constexpr int WIN_STRIDE = MAX_WIN_ROWS + 1;  // LDS words per env window (+1: lanes = envs hit distinct banks)
+constexpr int MAX_STAGED_BEAMS = 64;          // lidar rows staged in LDS for coalesced stores
 
 BinomTable make_binom_table() {
   BinomTable t;

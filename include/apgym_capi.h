@@ -23,6 +23,26 @@
  *       LIDARLocalization2DEnv.__lidar_scan  ap_gym/envs/lidar_localization2d.py:496-536
  *   apg_rng_draws
  *       numpy Generator(PCG64(SeedSequence(seed))) draws as used by the above (test entry point).
+ *   apg_rng_fill
+ *       one vector-level numpy Generator drawing a whole batch: Generator.integers(lo, hi, n)
+ *       (numpy distributions.c random_bounded_uint64_fill, Lemire on next_uint32) and
+ *       Generator.uniform(low, high, (n, cols)) (random_uniform) as used by
+ *       DatasetBatchIterator.__next__ ap_gym/envs/dataset/dataset_iterator.py:52-57 and
+ *       ImagePerceptionModule ap_gym/envs/image/image_perception_module.py:105-118, 130-161, 278-291.
+ *   apg_image_seed / apg_image_reset / apg_image_step
+ *       ImageClassificationVectorEnv  ap_gym/envs/image_classification.py:107-151 (reset, _step,
+ *       _np_random setter) and ImageLocalizationVectorEnv ap_gym/envs/image_localization.py:131-181,
+ *       237-246 over ImagePerceptionModule ap_gym/envs/image/image_perception_module.py:105-251
+ *       (seed, reset, step, _get_obs), with ActivePerceptionVectorEnv.step
+ *       ap_gym/active_perception_vector_env.py:84-111 and the normalized CE / MSE losses
+ *       ap_gym/loss_fn.py:69-83, 207-267.
+ *   apg_image_glimpse
+ *       ImagePerceptionModule.get_glimpse  image_perception_module.py:294-331 (scipy
+ *       RegularGridInterpolator "linear", bounds_error=True; clip(0, 1); float32).
+ *   apg_image_unique_top_k
+ *       ImagePerceptionModule.sample_unique_glimpse_positions  image_perception_module.py:253-277.
+ *   apg_loss_ce / apg_loss_mse
+ *       CrossEntropyLossFn.numpy / MSELossFn.numpy + LossFnAffineTransformation (loss_fn.py).
  */
 #ifndef APGYM_CAPI_H
 #define APGYM_CAPI_H
@@ -41,6 +61,8 @@ extern "C" {
 #define APG_ERR_NAN_ACTION 1u     /* "NaN values detected in action." */
 #define APG_ERR_NAN_PREDICTION 2u /* "NaN values detected in prediction." */
 #define APG_ERR_MAPGEN 4u         /* internal map-generation bound exceeded */
+#define APG_ERR_OOB_Y 8u          /* "One of the requested xi is out of bounds in dimension 0" */
+#define APG_ERR_OOB_X 16u         /* "One of the requested xi is out of bounds in dimension 1" */
 
 #define APG_MAP_ROOMS 0
 #define APG_MAP_MAZE 1
@@ -142,6 +164,103 @@ int apg_lidar_scan_batch(const uint64_t *occ, const int32_t *map_index, int h, i
  * 5 binomial(a, 0.3)) from default_rng(seed[i]) for each of m seeds; out[m][n] as float64. */
 int apg_rng_draws(const uint64_t *seeds, int m, int kind, int64_t a, int64_t b, int n, double *out,
                   apg_stream_t stream);
+
+/* ---------------------------------------------------------------- vector-level numpy streams */
+#define APG_DRAW_UNIFORM 0 /* out f64[n][cols] = low[c] + range[c] * next_double   (Generator.uniform) */
+#define APG_DRAW_INTEGERS 1 /* out i64[n] = lo + bounded(hi - lo - 1)               (Generator.integers) */
+
+/* n draws (n x cols for uniform, cols <= 2) from the ONE stream *state (device), advancing it
+ * exactly as numpy would.  integers: bound = hi - lo (exclusive range, 1 <= bound <= 2**32). */
+int apg_rng_fill(apg_pcg64 *state, int kind, int64_t n, int cols, const double *low, const double *range,
+                 int64_t lo, uint64_t bound, void *out, apg_stream_t stream);
+
+/* ---------------------------------------------------------------- image glimpse envs */
+#define APG_IMAGE_CLASSIFY 0 /* ImageClassificationVectorEnv */
+#define APG_IMAGE_LOCALIZE 1 /* ImageLocalizationVectorEnv */
+#define APG_POOL_U8 0        /* pool values v -> float32(v) / 255 (_process_imgs_np) */
+#define APG_POOL_F32 1
+
+typedef struct apg_image_config {
+  int32_t num_envs;
+  int32_t kind;               /* APG_IMAGE_CLASSIFY | APG_IMAGE_LOCALIZE */
+  int32_t height, width;      /* image size of the dataset */
+  int32_t pool_channels;      /* channels stored in the pool (1 or 3) */
+  int32_t channels;           /* observation channels (1 or 3; 1 -> 3 repeats the grey channel) */
+  int32_t pool_dtype;         /* APG_POOL_U8 | APG_POOL_F32 */
+  int32_t sensor_h, sensor_w; /* sensor_size[0], sensor_size[1] */
+  int32_t step_limit;
+  int32_t num_classes;
+  int32_t invert_labels;      /* randomly_invert_labels */
+  int32_t top_k;              /* unique_sampling_top_k */
+  int32_t unique_points;      /* P: sampling grid points of sample_unique_glimpse_positions */
+  int64_t pool_len;           /* len(dataset) */
+  double sensor_scale;
+  double max_step[2];         /* max_step_length broadcast to (2,) */
+  double cell[2];             /* unique sampling max_grid_cell_size_norm */
+  double ce_scale, ce_offset; /* normalized CrossEntropyLossFn affine (float64) */
+  float mse_scale, mse_offset;/* normalized MSELossFn affine (float32, NEP 50) */
+} apg_image_config;
+
+typedef struct apg_image_state {
+  const void *pool;           /* [pool_len][H][W][pool_channels] u8 or f32 */
+  const int32_t *pool_labels; /* [pool_len] */
+  const double *unique_grid;  /* [P][2] sampling positions (localize) */
+  int64_t *index;             /* [N] data point index of each env (info["index"]) */
+  int32_t *label;             /* [N] current label (after inversion) */
+  int32_t *inverted;          /* [N] 0/1 label inverted this episode */
+  double *pos;                /* [N][2] sensor position, normalized (float64 like the reference) */
+  float *target;              /* [N][2] localization target */
+  apg_pcg64 *rng;             /* [3] env np_random, module current_rng, DatasetBatchIterator rng */
+  int64_t *scratch_i64;       /* [N] */
+  double *scratch_f64;        /* [2N] */
+  int32_t *top_k;             /* [N][top_k] unique-sampling ranking (localize) */
+} apg_image_state;
+
+typedef struct apg_image_outputs {
+  float *glimpse;             /* [N][sensor_h][sensor_w][C] */
+  float *glimpse_pos;         /* [N][2] */
+  float *time_step;           /* [N] */
+  float *target_glimpse;      /* [N][sensor_h][sensor_w][C] (localize) */
+  double *reward;             /* [N] base_reward - loss; a float32 value whenever the reference's is */
+  float *base_reward;         /* [N] (the reference's are float64 zeros on the autoreset step) */
+  float *target;              /* [N][2] localize: info["prediction"]["target"] (pre-update copy) */
+  int32_t *label_target;      /* [N] classify: info["prediction"]["target"] */
+  double *loss_f64;           /* [N] classify: normalized cross entropy (float64) */
+  float *loss_f32;            /* [N] localize: normalized MSE (float32) */
+  uint32_t *err;              /* [1] OR-ed APG_ERR_* bits */
+} apg_image_outputs;
+
+/* reset(seed=seed) seeding chain: np_random = default_rng(seed); module.seed(np_random.integers(0,
+ * 2**32-1, endpoint=True)); iterator seed = current_rng.integers(0, 2**32-1, endpoint=True). */
+int apg_image_seed(const apg_image_config *cfg, const apg_image_state *st, uint64_t seed, apg_stream_t stream);
+
+/* ImagePerceptionModule.reset (+ ImageLocalizationVectorEnv unique targets): draws the batch,
+ * positions and labels; writes glimpse / glimpse_pos / time_step (and target_glimpse). */
+int apg_image_reset(const apg_image_config *cfg, const apg_image_state *st, const apg_image_outputs *out,
+                    apg_stream_t stream);
+
+/* One vector step.  t = time step before the step, prev_done = the previous step terminated all
+ * envs (the module then resets instead of moving; the host tracks both, they are batch-global). */
+int apg_image_step(const apg_image_config *cfg, const apg_image_state *st, const float *action,
+                   const float *prediction, int32_t t, int32_t prev_done, const apg_image_outputs *out,
+                   apg_stream_t stream);
+
+/* Glimpses of npos positions per env: pos (f64 or f32, pos_is_f32) [N][npos][2] -> out
+ * [N][npos][sensor_h][sensor_w][C]; index[N] selects the pool image of each env. */
+int apg_image_glimpse(const apg_image_config *cfg, const void *pool, const int64_t *index, const void *pos,
+                      int pos_is_f32, int32_t npos, float *out, uint32_t *err, apg_stream_t stream);
+
+/* Uniqueness ranking of sample_unique_glimpse_positions: top_k[N][k] grid indices by descending
+ * min_{b != a} mean((g_b - g_a)^2) (exact ties: ascending index); uniq[N][P] (float, may be NULL). */
+int apg_image_unique_top_k(const apg_image_config *cfg, const void *pool, const int64_t *index,
+                           const double *grid, int32_t npoints, int32_t k, int32_t *top_k, float *uniq,
+                           apg_stream_t stream);
+
+/* Normalized losses over n rows: CE on logits [n][k] vs int32 targets -> f64; MSE on [n][d] -> f32. */
+int apg_loss_ce(const float *logits, const int32_t *target, int32_t n, int32_t k, double scale, double offset,
+                double *out, apg_stream_t stream);
+int apg_loss_mse(const float *pred, const float *target, int32_t n, int32_t d, float scale, float offset,
+                 float *out, apg_stream_t stream);
 
 #ifdef __cplusplus
 }

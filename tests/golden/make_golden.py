@@ -12,6 +12,10 @@ Sources of truth, per fixture:
   lidar_env_*.npz  the reference's LIDARLocalization2DEnv wrapped exactly as registration.py:319-356
                    composes it (TimeLimit(100, issue_termination=True) + ActiveRegressionLogWrapper),
                    vectorised by the gymnasium SyncVectorEnv restatement in tests/golden/_stubs.
+  image_*.npz      the reference's ImageClassificationVectorEnv / ImageLocalizationVectorEnv
+                   (ImagePerceptionModule, scipy RegularGridInterpolator, CE/MSE losses) run as-is on
+                   small synthetic uint8 pools (HF datasets are not available offline), seeded through
+                   the gymnasium VectorEnv.reset restatement in tests/golden/_stubs.
 The fixtures hold data only (inputs and expected outputs).  See DESIGN.md §Oracle for what each pins.
 """
 
@@ -227,8 +231,83 @@ def make_lidar_env():
     run_lidar_env("maze127_b64", fm.FloorMapDatasetMaze(127, 127), False, 64, 2, 25, 0, "uniform")
 
 
+# --------------------------------------------------------------------------- image envs
+def _image_modules():
+    pkg = refload.load_core()
+    v2s = refload.load("vector_to_single_wrapper")
+    for k, v in vars(v2s).items():
+        if not k.startswith("_"):
+            setattr(pkg, k, v)
+    return (refload.load("envs.image.image_perception_module"), refload.load("envs.image.image_classification_dataset"),
+            refload.load("envs.image_classification"), refload.load("envs.image_localization"))
+
+
+def run_image_env(name, kind, pool_shape, channels, num_classes, sensor, scale, step_limit, invert, n_envs,
+                  steps, seed, pool_len, pool_seed):
+    ipm, icd, ic, il = _image_modules()
+    prng = np.random.default_rng(pool_seed)
+    pool = prng.integers(0, 256, (pool_len, *pool_shape), dtype=np.uint8)
+    # smooth a little so glimpses differ in structured ways (ties in uniqueness are rare either way)
+    labels = prng.integers(0, num_classes, pool_len).astype(np.int64)
+
+    class PoolDataset(icd.ImageClassificationDataset):
+        def _get_length(self):
+            return pool_len
+
+        def _get_num_classes(self):
+            return num_classes
+
+        def _get_num_channels(self):
+            return channels
+
+        def _get_data_point_batch(self, idx):
+            return pool[np.asarray(idx)], labels[np.asarray(idx)]
+
+    cfg = ipm.ImagePerceptionConfig(dataset=PoolDataset(), sensor_size=sensor, sensor_scale=scale,
+                                    step_limit=step_limit, prefetch=False, randomly_invert_labels=invert)
+    env = (ic.ImageClassificationVectorEnv if kind == "cls" else il.ImageLocalizationVectorEnv)(n_envs, cfg)
+    obs, info = env.reset(seed=seed)
+    arng = np.random.default_rng(11)
+    actions = arng.uniform(-1.5, 1.5, (steps, n_envs, 2)).astype(np.float32)
+    if kind == "cls":
+        preds = arng.standard_normal((steps, n_envs, num_classes)).astype(np.float32)
+    else:
+        preds = arng.uniform(-1, 1, (steps, n_envs, 2)).astype(np.float32)
+    out = {"pool": pool, "labels": labels, "actions": actions, "predictions": preds, "seed": np.array(seed),
+           "config": np.array([pool_shape[0], pool_shape[1], channels, num_classes, sensor[0], sensor[1],
+                               step_limit, int(invert), n_envs, steps], np.int64),
+           "sensor_scale": np.array(scale, np.float64), "kind": np.array(kind)}
+    for k, v in obs.items():
+        out[f"reset_{k}"] = np.asarray(v)
+    out["reset_index"] = np.asarray(info["index"], np.int64)
+    rec = {}
+    for t in range(steps):
+        obs, rew, term, trunc, info = env.step({"action": actions[t], "prediction": preds[t]})
+        fields = dict(obs)
+        fields.update(reward=rew, terminated=term, truncated=trunc, index=np.asarray(info["index"], np.int64),
+                      base_reward=np.asarray(info["base_reward"]), target=np.asarray(info["prediction"]["target"]),
+                      loss=np.asarray(info["prediction"]["loss"]))
+        for k, v in fields.items():
+            v = np.asarray(v)
+            rec.setdefault(k, []).append(v)
+            rec.setdefault(k + "_dtype", []).append(str(v.dtype))
+    for k, v in rec.items():
+        out["step_" + k] = np.array(v) if k.endswith("_dtype") else np.stack(v)
+    env.close()
+    save(f"image_{name}.npz", **out)
+
+
+def make_image_env():
+    run_image_env("cls_mnist", "cls", (28, 28), 1, 10, (5, 5), 1.0, 16, False, 8, 40, 0, 40, 100)
+    run_image_env("cls_tin", "cls", (64, 64, 3), 3, 200, (10, 10), 1.0, 16, False, 4, 20, 3, 12, 101)
+    run_image_env("cls_gray3_rect", "cls", (20, 24), 3, 4, (5, 5), 1.5, 8, True, 6, 30, 5, 16, 102)
+    run_image_env("loc_mnist", "loc", (28, 28), 1, 10, (5, 5), 1.0, 16, False, 6, 40, 1, 30, 103)
+    run_image_env("loc_tin12", "loc", (64, 64, 3), 3, 200, (12, 12), 1.0, 16, False, 2, 20, 4, 6, 104)
+    run_image_env("loc_rect", "loc", (24, 20, 3), 3, 5, (4, 4), 1.25, 6, False, 4, 16, 9, 10, 105)
+
+
 SECTIONS = {"rng": make_rng, "maps": make_maps, "loss": make_loss, "scan": make_lidar_scan,
-            "lidar": make_lidar_env}
+            "lidar": make_lidar_env, "image": make_image_env}
 
 
 def main(argv):

@@ -1,0 +1,380 @@
+"""GPU parity of the image glimpse path: HIP kernels (through the C ABI) against numpy itself (the
+vector-level streams), the reference-generated goldens (tests/golden/image_*.npz) and the numpy
+oracle (oracle/image_oracle.py) at larger sizes.
+
+Bar: bit-exact for every integer and float output (glimpses, positions, targets, MSE losses,
+rewards, RNG streams), except the cross-entropy loss (and the rewards derived from it), whose
+float32 exp/log are the device libm's rather than numpy's SIMD ones: those are compared within the
+north_star tolerance (|got - want| <= 1e-6 + 1e-6 |want|), and everything else in the same step is
+still compared bit for bit.
+"""
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+CE_RTOL = 1e-6
+CE_ATOL = 1e-6
+GOLDEN_CASES = ["cls_mnist", "cls_tin", "cls_gray3_rect", "loc_mnist", "loc_tin12", "loc_rect"]
+
+
+def _state_from_numpy(gen: np.random.Generator):
+    st = gen.bit_generator.state
+    s, inc = st["state"]["state"], st["state"]["inc"]
+    words = [s >> 64, s & (2**64 - 1), inc >> 64, inc & (2**64 - 1),
+             (st["has_uint32"] & 0xFFFFFFFF) | ((st["uinteger"] & 0xFFFFFFFF) << 32)]
+    return np.array(words, dtype=np.uint64).view(np.int64)
+
+
+def _state_equal(dev_words: np.ndarray, gen: np.random.Generator) -> bool:
+    want = _state_from_numpy(gen)
+    got = dev_words.copy()
+    if (want[4] & 0xFFFFFFFF) == 0:  # buffered word is irrelevant when nothing is buffered
+        got[4] &= 0xFFFFFFFF
+        want = want.copy()
+        want[4] &= 0xFFFFFFFF
+    return np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("bound", [1, 2, 10, 60000, 100000, 2**31 + 5, 3 * 2**30, 2**32 - 1, 2**32])
+@pytest.mark.parametrize("n", [1, 7, 1000, 70001])
+@pytest.mark.parametrize("pre", [0, 1])
+def test_rng_fill_integers_matches_numpy(gpu, bound, n, pre):
+    import torch
+
+    from ap_gym_amd import _native as N
+
+    gen = np.random.default_rng(1234 + n + bound % 1000)
+    if pre:  # leave a buffered half word in the generator (next_uint32)
+        gen.integers(0, 5)
+    st = torch.as_tensor(_state_from_numpy(gen), device=gpu)
+    out = torch.zeros(n, dtype=torch.int64, device=gpu)
+    N.check(N.lib().apg_rng_fill(N.ptr(st), N.APG_DRAW_INTEGERS, n, 1, None, None, 3, bound, N.ptr(out),
+                                 N.stream_handle(gpu)))
+    want = gen.integers(3, 3 + bound, n)
+    assert np.array_equal(out.cpu().numpy(), want)
+    assert _state_equal(st.cpu().numpy(), gen)
+
+
+@pytest.mark.parametrize("n,cols", [(1, 2), (513, 2), (65536, 2), (1000, 1)])
+def test_rng_fill_uniform_matches_numpy(gpu, n, cols):
+    import torch
+
+    from ap_gym_amd import _native as N
+
+    gen = np.random.default_rng(77 + n)
+    gen.integers(0, 3)  # buffered half word must survive next64 draws untouched
+    st = torch.as_tensor(_state_from_numpy(gen), device=gpu)
+    low = np.array([-1.0, -0.3][:cols])
+    high = np.array([1.0, 0.3][:cols])
+    out = torch.zeros((n, cols), dtype=torch.float64, device=gpu)
+    lo_c = (ctypes.c_double * cols)(*low.tolist())
+    rg_c = (ctypes.c_double * cols)(*(high - low).tolist())
+    N.check(N.lib().apg_rng_fill(N.ptr(st), N.APG_DRAW_UNIFORM, n, cols, lo_c, rg_c, 0, 0, N.ptr(out),
+                                 N.stream_handle(gpu)))
+    want = gen.uniform(low, high, (n, cols))
+    assert np.array_equal(out.cpu().numpy(), want)
+    assert _state_equal(st.cpu().numpy(), gen)
+
+
+# ---------------------------------------------------------------------------------------- glimpse
+GLIMPSE_CASES = [  # (H, W, pool C, obs C, sensor, scale, dtype)
+    (28, 28, 1, 1, (5, 5), 1.0, np.uint8),
+    (64, 64, 3, 3, (12, 12), 1.0, np.uint8),
+    (64, 64, 3, 3, (10, 10), 1.0, np.uint8),
+    (20, 24, 1, 3, (5, 5), 1.5, np.uint8),
+    (24, 20, 3, 3, (4, 4), 1.25, np.float32),
+    (17, 31, 1, 1, (3, 3), 2.0, np.uint8),
+]
+
+
+def _cfg(N, n, kind, h, w, pc, c, sensor, scale, dtype, pool_len, k=10, top_k=10, points=0, cell=(0.0, 0.0)):
+    return N.ImageConfig(num_envs=n, kind=kind, height=h, width=w, pool_channels=pc, channels=c,
+                         pool_dtype=N.APG_POOL_U8 if dtype == np.uint8 else N.APG_POOL_F32, sensor_h=sensor[0],
+                         sensor_w=sensor[1], step_limit=16, num_classes=k, invert_labels=0, top_k=top_k,
+                         unique_points=points, pool_len=pool_len, sensor_scale=scale,
+                         max_step=(ctypes.c_double * 2)(0.2, 0.2), cell=(ctypes.c_double * 2)(*cell), ce_scale=1.0,
+                         ce_offset=0.0, mse_scale=1.0, mse_offset=0.0)
+
+
+def _pool(rng, m, h, w, pc, dtype):
+    if dtype == np.uint8:
+        return rng.integers(0, 256, (m, h, w, pc), dtype=np.uint8)
+    return rng.uniform(-0.2, 1.2, (m, h, w, pc)).astype(np.float32)
+
+
+@pytest.mark.parametrize("case", range(len(GLIMPSE_CASES)))
+def test_glimpse_matches_oracle(gpu, case):
+    import torch
+
+    from ap_gym_amd import _native as N
+    from oracle import image_oracle as io
+
+    h, w, pc, c, sensor, scale, dtype = GLIMPSE_CASES[case]
+    rng = np.random.default_rng(case)
+    n, npos, m = 37, 64, 9
+    pool = _pool(rng, m, h, w, pc, dtype)
+    index = rng.integers(0, m, n)
+    pos = rng.uniform(-1, 1, (n, npos, 2))
+    pos[:, :8] = np.array([[-1, -1], [1, 1], [-1, 1], [1, -1], [0, 0], [0.5, -0.5], [1, 0], [0, -1]])
+    lim = io.sensor_pos_lim((h, w), sensor, scale)
+    pos[:, 8, 0] = 3 / lim[0]  # grid-exact sensing points
+    pos[:, 8, 1] = -2 / lim[1]
+    cfg = _cfg(N, n, N.APG_IMAGE_CLASSIFY, h, w, pc, c, sensor, scale, dtype, m)
+    out = torch.zeros((n, npos, sensor[0], sensor[1], c), dtype=torch.float32, device=gpu)
+    err = torch.zeros(1, dtype=torch.int32, device=gpu)
+    pool_t, idx_t, pos_t = (torch.as_tensor(x, device=gpu) for x in (pool, index, pos))
+    N.check(N.lib().apg_image_glimpse(ctypes.byref(cfg), N.ptr(pool_t), N.ptr(idx_t), N.ptr(pos_t), 0, npos,
+                                      N.ptr(out), N.ptr(err), N.stream_handle(gpu)))
+    imgs = io.images_f32(pool, c)[index]
+    want = io.glimpse(imgs, pos, sensor, scale)
+    assert int(err.item()) == 0
+    assert np.array_equal(out.cpu().numpy(), want)
+    # float32 positions (the target glimpse path)
+    pos32 = pos.astype(np.float32)
+    pos32_t = torch.as_tensor(pos32, device=gpu)
+    N.check(N.lib().apg_image_glimpse(ctypes.byref(cfg), N.ptr(pool_t), N.ptr(idx_t), N.ptr(pos32_t), 1, npos,
+                                      N.ptr(out), N.ptr(err), N.stream_handle(gpu)))
+    assert np.array_equal(out.cpu().numpy(), io.glimpse(imgs, pos32, sensor, scale))
+
+
+def test_glimpse_out_of_bounds_flags_like_scipy(gpu):
+    import torch
+
+    from ap_gym_amd import _native as N
+    from oracle import image_oracle as io
+
+    rng = np.random.default_rng(5)
+    h = w = 16
+    pool = _pool(rng, 2, h, w, 1, np.uint8)
+    sensor, scale = (5, 5), 0.5  # scale < 1 lets the sensing points leave the image at |pos| = 1
+    for pos, dim in (([[0.0, 1.0]], 0), ([[1.0, 0.0]], 1), ([[1.0, 1.0]], 0)):
+        pos = np.array([pos])
+        with pytest.raises(ValueError, match=f"dimension {dim}"):
+            io.glimpse(io.images_f32(pool, 1)[:1], pos, sensor, scale)
+        cfg = _cfg(N, 1, N.APG_IMAGE_CLASSIFY, h, w, 1, 1, sensor, scale, np.uint8, 2)
+        out = torch.zeros((1, 1, 5, 5, 1), dtype=torch.float32, device=gpu)
+        err = torch.zeros(1, dtype=torch.int32, device=gpu)
+        keep = [torch.as_tensor(pool, device=gpu), torch.zeros(1, dtype=torch.int64, device=gpu),
+                torch.as_tensor(pos, device=gpu)]  # device buffers must outlive the async launch
+        N.check(N.lib().apg_image_glimpse(ctypes.byref(cfg), *[N.ptr(x) for x in keep], 0, 1, N.ptr(out), N.ptr(err),
+                                          N.stream_handle(gpu)))
+        bits = int(err.item())
+        assert bits & (N.APG_ERR_OOB_Y if dim == 0 else N.APG_ERR_OOB_X)
+        if dim == 1:
+            assert not bits & N.APG_ERR_OOB_Y
+
+
+@pytest.mark.parametrize("h,w,c,sensor,n", [(28, 28, 1, (5, 5), 24), (32, 32, 3, (6, 6), 6), (64, 64, 3, (12, 12), 2)])
+def test_unique_top_k_matches_oracle(gpu, h, w, c, sensor, n):
+    import torch
+
+    from ap_gym_amd import _native as N
+    from ap_gym_amd.image_env import unique_sampling_grid
+    from oracle import image_oracle as io
+
+    rng = np.random.default_rng(h + n)
+    pool = _pool(rng, n, h, w, c, np.uint8)
+    index = np.arange(n)
+    grid, cell = unique_sampling_grid((h, w), sensor, 1.0)
+    top, g_grid, g_cell, u = io.unique_top_k(io.images_f32(pool, c), sensor, 1.0, 10)
+    assert np.array_equal(grid, g_grid) and np.array_equal(cell, g_cell)
+    p = grid.shape[0]
+    cfg = _cfg(N, n, N.APG_IMAGE_LOCALIZE, h, w, c, c, sensor, 1.0, np.uint8, n, top_k=10, points=p)
+    top_d = torch.zeros((n, 10), dtype=torch.int32, device=gpu)
+    uniq = torch.zeros((n, p), dtype=torch.float32, device=gpu)
+    keep = [torch.as_tensor(x, device=gpu) for x in (pool, index, grid)]
+    N.check(N.lib().apg_image_unique_top_k(ctypes.byref(cfg), *[N.ptr(x) for x in keep], p, 10, N.ptr(top_d),
+                                           N.ptr(uniq), N.stream_handle(gpu)))
+    assert np.array_equal(uniq.cpu().numpy().astype(np.float64), u)
+    assert np.array_equal(top_d.cpu().numpy(), top)
+
+
+# ---------------------------------------------------------------------------------------- losses
+@pytest.mark.parametrize("k", [2, 10, 200, 1000])
+def test_ce_loss_kernel_within_tolerance(gpu, k):
+    import scipy.special
+    import torch
+
+    from ap_gym_amd import _native as N
+
+    rng = np.random.default_rng(k)
+    n = 4099
+    logits = (rng.standard_normal((n, k)) * 4).astype(np.float32)
+    logits[0, 0] = -np.inf
+    target = rng.integers(0, k, n).astype(np.int32)
+    scale = 1 / np.log(k)
+    out = torch.zeros(n, dtype=torch.float64, device=gpu)
+    keep = [torch.as_tensor(x, device=gpu) for x in (logits, target)]
+    N.check(N.lib().apg_loss_ce(*[N.ptr(x) for x in keep], n, k, float(scale), -0.0, N.ptr(out),
+                                N.stream_handle(gpu)))
+    want = -np.take_along_axis(scipy.special.log_softmax(logits, axis=-1), target[:, None], -1)[:, 0] * scale + -0.0
+    np.testing.assert_allclose(out.cpu().numpy(), want, rtol=CE_RTOL, atol=CE_ATOL)
+
+
+@pytest.mark.parametrize("d", [1, 2, 7, 130])
+def test_mse_loss_kernel_bit_exact(gpu, d):
+    import torch
+
+    from ap_gym_amd import _native as N
+
+    rng = np.random.default_rng(d)
+    n = 1000
+    p, t = rng.standard_normal((2, n, d)).astype(np.float32)
+    out = torch.zeros(n, dtype=torch.float32, device=gpu)
+    keep = [torch.as_tensor(x, device=gpu) for x in (p, t)]
+    N.check(N.lib().apg_loss_mse(*[N.ptr(x) for x in keep], n, d, 3.0, -0.0, N.ptr(out), N.stream_handle(gpu)))
+    assert np.array_equal(out.cpu().numpy(), np.mean((p - t) ** 2, axis=-1) * 3.0 + -0.0)
+
+
+# ---------------------------------------------------------------------------------------- envs
+def _make_env(ap, g, backend="numpy", n=None, copy=False):
+    h, w, c, k, s0, s1, lim, inv, n_g, _ = (int(v) for v in g["config"])
+    ds = ap.ArrayImageClassificationDataset(g["pool"], g["labels"], k, c)
+    cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=(s0, s1), sensor_scale=float(g["sensor_scale"]),
+                                   step_limit=lim, randomly_invert_labels=bool(inv))
+    cls = ap.ImageClassificationVectorEnv if str(g["kind"]) == "cls" else ap.ImageLocalizationVectorEnv
+    return cls(n or n_g, cfg, array_backend=backend, copy=copy)
+
+
+def _assert_field(name, got, want, want_dtype, ce, key=None):
+    got = np.asarray(got)
+    assert str(got.dtype) == str(want_dtype), (name, got.dtype, want_dtype)
+    if ce and (key or name) in ("loss", "reward"):
+        np.testing.assert_allclose(got, want, rtol=CE_RTOL, atol=CE_ATOL, err_msg=name)
+    else:
+        assert np.array_equal(got, want), name
+
+
+@pytest.mark.parametrize("name", GOLDEN_CASES)
+def test_image_env_matches_reference_trace(gpu, name):
+    import ap_gym_amd as ap
+
+    g = golden(f"image_{name}.npz")
+    env = _make_env(ap, g)
+    ce = str(g["kind"]) == "cls"
+    obs, info = env.reset(seed=int(g["seed"]))
+    for k, v in obs.items():
+        _assert_field("reset_" + k, v, g["reset_" + k], g["reset_" + k].dtype, False)
+    assert np.array_equal(info["index"], g["reset_index"])
+    steps = int(g["config"][-1])
+    for t in range(steps):
+        obs, rew, term, trunc, info = env.step({"action": g["actions"][t], "prediction": g["predictions"][t]})
+        fields = dict(obs, reward=rew, terminated=term, truncated=trunc, index=info["index"],
+                      base_reward=info["base_reward"], target=info["prediction"]["target"],
+                      loss=info["prediction"]["loss"])
+        assert set(fields) == {k[5:] for k in g.files if k.startswith("step_") and not k.endswith("_dtype")}
+        for k, v in fields.items():
+            _assert_field(f"step{t}_{k}", v, g["step_" + k][t], g["step_" + k + "_dtype"][t], ce, key=k)
+    env.close()
+
+
+@pytest.mark.parametrize("kind,n,shape,sensor,k,steps", [("cls", 2048, (28, 28), (5, 5), 10, 40),
+                                                         ("cls", 256, (64, 64, 3), (10, 10), 200, 20),
+                                                         ("loc", 48, (28, 28), (5, 5), 10, 36)])
+def test_image_env_matches_oracle_at_scale(gpu, kind, n, shape, sensor, k, steps):
+    import ap_gym_amd as ap
+    from oracle import image_oracle as io
+
+    rng = np.random.default_rng(n)
+    pool = rng.integers(0, 256, (300, *shape), dtype=np.uint8)
+    labels = rng.integers(0, k, 300)
+    c = 1 if len(shape) == 2 else shape[-1]
+    ds = ap.ArrayImageClassificationDataset(pool, labels, k, c)
+    cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=sensor, step_limit=16)
+    env = (ap.ImageClassificationVectorEnv if kind == "cls" else ap.ImageLocalizationVectorEnv)(n, cfg)
+    ref = io.ImageVectorEnvOracle(kind, pool, labels, k, c, n, sensor, 1.0, 16)
+    obs, info = env.reset(seed=11)
+    robs, rinfo = ref.reset(11)
+    for key in robs:
+        assert np.array_equal(obs[key], robs[key]), key
+    arng = np.random.default_rng(3)
+    for t in range(steps):
+        a = arng.uniform(-1.5, 1.5, (n, 2)).astype(np.float32)
+        p = (arng.standard_normal((n, k)) if kind == "cls" else arng.uniform(-1, 1, (n, 2))).astype(np.float32)
+        got = env.step({"action": a, "prediction": p})
+        want = ref.step(a, p)
+        for key in want[0]:
+            assert np.array_equal(got[0][key], want[0][key]), (t, key)
+        for i, name in ((1, "reward"), (2, "terminated"), (3, "truncated")):
+            _assert_field(name, got[i], want[i], want[i].dtype, kind == "cls")
+        gi, wi = got[4], want[4]
+        assert np.array_equal(gi["index"], wi["index"])
+        _assert_field("base_reward", gi["base_reward"], wi["base_reward"], wi["base_reward"].dtype, False)
+        _assert_field("target", gi["prediction"]["target"], wi["prediction"]["target"],
+                      np.asarray(wi["prediction"]["target"]).dtype, False)
+        _assert_field("loss", gi["prediction"]["loss"], wi["prediction"]["loss"], wi["prediction"]["loss"].dtype,
+                      kind == "cls")
+    env.close()
+
+
+@pytest.mark.parametrize("kind", ["cls", "loc"])
+def test_image_env_torch_backend_matches_numpy(gpu, kind):
+    import ap_gym_amd as ap
+
+    g = golden("image_cls_mnist.npz" if kind == "cls" else "image_loc_mnist.npz")
+    e_np, e_t = _make_env(ap, g), _make_env(ap, g, backend="torch", copy=True)
+    o1, _ = e_np.reset(seed=5)
+    o2, _ = e_t.reset(seed=5)
+    for k in o1:
+        assert np.array_equal(o1[k], o2[k].cpu().numpy()), k
+    for t in range(int(g["config"][-1])):
+        act = {"action": g["actions"][t], "prediction": g["predictions"][t]}
+        r1 = e_np.step(act)
+        r2 = e_t.step(act)
+        for k in r1[0]:
+            assert np.array_equal(r1[0][k], r2[0][k].cpu().numpy()), (t, k)
+        assert np.array_equal(r1[1].astype(np.float64), r2[1].cpu().numpy())
+        assert np.array_equal(r1[2], r2[2].cpu().numpy())
+        assert np.array_equal(r1[4]["prediction"]["loss"], r2[4]["prediction"]["loss"].cpu().numpy())
+    e_t.check_errors()
+
+
+def test_image_env_nan_errors(gpu):
+    import ap_gym_amd as ap
+
+    g = golden("image_cls_mnist.npz")
+    for backend in ("numpy", "torch"):
+        env = _make_env(ap, g, backend=backend)
+        env.reset(seed=0)
+        a = g["actions"][0].copy()
+        p = g["predictions"][0].copy()
+        a[3, 1] = np.nan
+        with pytest.raises(ValueError, match="action"):
+            env.step({"action": a, "prediction": p})
+            env.check_errors()
+        env.reset(seed=0)
+        p[2, :] = -np.inf
+        with pytest.raises(ValueError, match="prediction"):
+            env.step({"action": g["actions"][0], "prediction": p})
+            env.check_errors()
+        env.close()
+
+
+def test_image_env_full_size_properties(gpu):
+    """MNIST-shaped classification at N = 65536 (BASELINE config 4) and localization at N = 4096:
+    bounded glimpses, clipped positions, reset cadence, label targets from the pool."""
+    import torch
+
+    import ap_gym_amd as ap
+
+    ds = ap.SyntheticImageClassificationDataset(60000, (28, 28), 10, seed=0)
+    env = ap.ImageClassificationVectorEnv(65536, ap.ImagePerceptionConfig(dataset=ds), array_backend="torch")
+    obs, info = env.reset(seed=0)
+    pool_labels = torch.as_tensor(ds.device_pool()[1], device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(0)
+    for t in range(40):
+        a = torch.rand((65536, 2), generator=g, device=gpu) * 3 - 1.5
+        p = torch.randn((65536, 10), generator=g, device=gpu)
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        assert bool(((obs["glimpse"] >= 0) & (obs["glimpse"] <= 1)).all())
+        assert bool((obs["glimpse_pos"].abs() <= 1).all())
+        assert bool((info["prediction"]["target"] == pool_labels[info["index"]]).all())
+        assert bool(term.all()) == (t % 17 == 15)
+    env.check_errors()
+    env.close()

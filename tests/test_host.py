@@ -115,3 +115,35 @@ def test_beam_directions_match_reference_formula():
         ref = np.stack([np.cos(ang), np.sin(ang)], axis=-1) * 5
         d = lidar_beam_directions(b, 5)
         assert d.dtype == np.float32 and np.array_equal(d, ref)
+
+
+def test_image_host_helpers_match_reference_formulas():
+    import scipy.special
+
+    from ap_gym_amd.image_env import sensor_pos_lim_pixels, softmax_nan_rows, unique_sampling_grid
+    from oracle import image_oracle as io
+
+    for hw, sensor, scale in (((28, 28), (5, 5), 1.0), ((64, 64), (10, 10), 1.0), ((64, 64), (12, 12), 1.0),
+                              ((20, 24), (5, 5), 1.5)):
+        assert np.array_equal(sensor_pos_lim_pixels(hw, sensor, scale), io.sensor_pos_lim(hw, sensor, scale))
+        g1, c1 = unique_sampling_grid(hw, sensor, scale)
+        g2, c2 = io.unique_grid(hw, sensor, scale)
+        assert np.array_equal(g1, g2) and np.array_equal(c1, c2)
+    rows = np.array([[0, 1, 2], [np.nan, 0, 0], [np.inf, 0, 0], [-np.inf, -np.inf, -np.inf], [-np.inf, 0, 1],
+                     [1e30, -1e30, 0]], np.float32)
+    with np.errstate(invalid="ignore"):
+        want = np.isnan(scipy.special.softmax(rows, axis=-1)).any(-1)
+    assert np.array_equal(softmax_nan_rows(rows), want)
+
+
+def test_image_registry_and_spaces():
+    import ap_gym_amd as ap
+
+    for i in ("MNIST-v0", "MNIST-test-v0", "CIFAR10-c3-v0", "TinyImageNet-v0", "MNISTLoc-v0", "TinyImageNetLoc-v0"):
+        assert i in ap.registry
+    ds = ap.SyntheticImageClassificationDataset(20, (28, 28), 10, seed=1)
+    imgs, labels = ds.get_data_point_batch([0, 3])
+    assert imgs.shape == (2, 28, 28, 1) and imgs.dtype == np.float32 and labels.dtype == np.int32
+    pool, lab = ds.device_pool()
+    assert pool.dtype == np.uint8 and pool.shape == (20, 28, 28, 1)
+    assert np.array_equal(imgs, pool[[0, 3]].astype(np.float32) / 255)

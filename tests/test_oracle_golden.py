@@ -92,3 +92,43 @@ def test_vector_env_trace(oracle_mod, name):
         if not static:
             assert np.array_equal(np.packbits(env.map > 0, axis=-1), d["map"][t]), f"{name} step {t} map"
     assert str(d["reward_dtype"]) == "float64" and str(d["base_reward_dtype"]) == "float32"
+
+
+IMAGE_CASES = ["cls_mnist", "cls_tin", "cls_gray3_rect", "loc_mnist", "loc_tin12", "loc_rect"]
+
+
+@pytest.mark.parametrize("name", IMAGE_CASES)
+def test_image_oracle_matches_reference_trace(name):
+    """oracle/image_oracle.py against the reference's own image envs (tests/golden/image_*.npz)."""
+    from oracle import image_oracle as io
+
+    g = golden(f"image_{name}.npz")
+    h, w, c, k, s0, s1, lim, inv, n, steps = (int(v) for v in g["config"])
+    env = io.ImageVectorEnvOracle(str(g["kind"]), g["pool"], g["labels"], k, c, n, (s0, s1),
+                                  float(g["sensor_scale"]), lim, invert=bool(inv))
+    obs, info = env.reset(int(g["seed"]))
+    for key, v in obs.items():
+        assert np.array_equal(v, g["reset_" + key]) and v.dtype == g["reset_" + key].dtype, key
+    assert np.array_equal(info["index"], g["reset_index"])
+    for t in range(steps):
+        obs, rew, term, trunc, info = env.step(g["actions"][t], g["predictions"][t])
+        fields = dict(obs, reward=rew, terminated=term, truncated=trunc, index=info["index"],
+                      base_reward=info["base_reward"], target=info["prediction"]["target"],
+                      loss=info["prediction"]["loss"])
+        for key, v in fields.items():
+            v = np.asarray(v)
+            assert np.array_equal(v, g["step_" + key][t]), (t, key)
+            assert str(v.dtype) == g["step_" + key + "_dtype"][t], (t, key)
+
+
+def test_pairwise_sum_matches_numpy_mean():
+    """The restated pairwise order is the one np.mean uses over a contiguous float32 block."""
+    from oracle import image_oracle as io
+
+    rng = np.random.default_rng(0)
+    for shape in ((5, 5, 1), (12, 12, 3), (10, 10, 3), (3, 3, 1), (129,), (1000,), (4, 4, 3)):
+        x = rng.random((64, *shape)).astype(np.float32) ** 2
+        want = np.mean(x, axis=tuple(range(1, x.ndim)))
+        n = int(np.prod(shape))
+        got = (np.float32(0) + io.pairwise_sum_f32(x.reshape(64, n))) / np.float32(n)
+        assert np.array_equal(got, want), shape
