@@ -79,7 +79,7 @@ class ImageConfig(ctypes.Structure):
 
 class ImageState(ctypes.Structure):
     _fields_ = [(n, _vp) for n in ("pool", "pool_labels", "unique_grid", "index", "label", "inverted", "pos",
-                                   "target", "rng", "scratch_i64", "scratch_f64", "top_k")]
+                                   "target", "rng", "scratch_i64", "scratch_f64", "top_k", "rng_work")]
 
 
 class ImageOutputs(ctypes.Structure):
@@ -105,8 +105,9 @@ SYMBOLS = [
                                             _vp]),
     ("apg_rng_draws", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                      _vp, _vp]),
+    ("apg_rng_fill_work_elems", ctypes.c_int64, [ctypes.c_int64, ctypes.c_uint64]),
     ("apg_rng_fill", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, _vp, _vp, ctypes.c_int64,
-                                    ctypes.c_uint64, _vp, _vp]),
+                                    ctypes.c_uint64, _vp, _vp, _vp]),
     ("apg_image_seed", ctypes.c_int, [ctypes.POINTER(ImageConfig), ctypes.POINTER(ImageState), ctypes.c_uint64,
                                       _vp]),
     ("apg_image_reset", ctypes.c_int, [ctypes.POINTER(ImageConfig), ctypes.POINTER(ImageState),

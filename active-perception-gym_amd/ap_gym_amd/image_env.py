@@ -161,6 +161,7 @@ class _ImageVectorEnv:
 
         t, dev = torch, self.device
         gshape = (n, s0, s1, c)
+        work = max(N.lib().apg_rng_fill_work_elems(n, b) for b in (m, int(cfg.unique_sampling_top_k), 2))
         self._t = T = dict(
             pool=t.from_numpy(pool).to(dev), pool_labels=t.from_numpy(labels).to(dev),
             unique_grid=t.from_numpy(grid).to(dev),
@@ -169,6 +170,7 @@ class _ImageVectorEnv:
             target=t.zeros((n, 2), dtype=t.float32, device=dev), rng=t.zeros((3, 5), dtype=t.int64, device=dev),
             scratch_i64=t.zeros(n, dtype=t.int64, device=dev), scratch_f64=t.zeros(2 * n, dtype=t.float64, device=dev),
             top_k=t.zeros((n, int(cfg.unique_sampling_top_k)), dtype=t.int32, device=dev),
+            rng_work=t.zeros(work, dtype=t.int64, device=dev),
             glimpse=t.zeros(gshape, dtype=t.float32, device=dev),
             glimpse_pos=t.zeros((n, 2), dtype=t.float32, device=dev),
             time_step=t.zeros(n, dtype=t.float32, device=dev),
@@ -180,7 +182,7 @@ class _ImageVectorEnv:
             err=t.zeros(1, dtype=t.int32, device=dev))
         self._state = N.ImageState(*[N.ptr(T[k_]) for k_ in ("pool", "pool_labels", "unique_grid", "index", "label",
                                                               "inverted", "pos", "target", "rng", "scratch_i64",
-                                                              "scratch_f64", "top_k")])
+                                                              "scratch_f64", "top_k", "rng_work")])
         self._out = N.ImageOutputs(*[N.ptr(T[k_]) for k_ in ("glimpse", "glimpse_pos", "time_step", "target_glimpse",
                                                               "reward", "base_reward", "target_out", "label_target",
                                                               "loss_f64", "loss_f32", "err")])
@@ -192,6 +194,7 @@ class _ImageVectorEnv:
         self._closed = False
         self._t_step = 0
         self._prev_done = False
+        self._done_consts = None
 
     # ------------------------------------------------------------------ properties
     @property
@@ -391,8 +394,12 @@ class _ImageVectorEnv:
             target, loss = T["label_target"], T["loss_f64"]
         info = {"index": self._c(T["index"]), "base_reward": self._c(T["base_reward"]),
                 "prediction": {"target": self._c(target), "loss": self._c(loss)}}
-        term = torch.full((n,), bool(terminated), dtype=torch.bool, device=self.device)
-        trunc = torch.zeros(n, dtype=torch.bool, device=self.device)
+        # episodes end for the whole batch at once: terminated is all-True or all-False, never truncated
+        if self._done_consts is None:
+            self._done_consts = (torch.zeros(n, dtype=torch.bool, device=self.device),
+                                 torch.ones(n, dtype=torch.bool, device=self.device))
+        term = self._c(self._done_consts[1 if terminated else 0])
+        trunc = self._c(self._done_consts[0])
         return self._torch_obs(), self._c(T["reward"]), term, trunc, info
 
     def render(self):

@@ -1,7 +1,8 @@
 // apg_image.hip — gfx950 kernels + C ABI for the image glimpse envs (ImageClassificationVectorEnv,
 // ImageLocalizationVectorEnv over ImagePerceptionModule; ap_gym/envs/image_*.py, image/*.py).
 //
-//   k_rng_fill       one workgroup draws a whole batch from ONE numpy stream (apg_rng.hpp).
+//   k_fill_*         a whole batch drawn from ONE numpy stream across the chip (apg_rng.hpp):
+//                    PCG64 jump-ahead per thread, Lemire rejections as a stream compaction.
 //   k_image_gather   labels of the newly drawn data points, optional label inversion (:130-139).
 //   k_image_env      one thread per env: prediction/action NaN checks, normalized CE (f64) or MSE
 //                    (f32) loss, project_sphere move + clip (f64), base reward, reward (:191-217,
@@ -97,12 +98,17 @@ GlimpseGeo make_geo(const apg_image_config *c) {
   return g;
 }
 
-// float32(v) / 255 for v = 0..255, correctly rounded (f64 division, then one rounding)
-__constant__ float c_u8_to_f32[256];
+// float32(v) / 255 for v = 0..255 (_process_imgs_np), staged in LDS by every glimpse workgroup:
+// the f64 quotient rounded once more to f32 equals numpy's correctly rounded f32 division for all
+// 256 values (checked bit for bit by the glimpse parity tests, which cover every u8 value)
+APG_DEV void load_u8_table(float *lut) {
+  for (int v = threadIdx.x; v < 256; v += blockDim.x) lut[v] = (float)__ddiv_rn((double)v, 255.0);
+  __syncthreads();
+}
 
-APG_DEV float pool_value(const GlimpseGeo &g, const void *pool, int64_t base, int y, int x, int ch) {
-  const int64_t i = base + ((int64_t)y * g.w + x) * g.pc + (g.pc == 1 ? 0 : ch);
-  return g.pool_f32 ? static_cast<const float *>(pool)[i] : c_u8_to_f32[static_cast<const uint8_t *>(pool)[i]];
+APG_DEV float pool_value(const GlimpseGeo &g, const void *pool, const float *lut, int64_t base, int y, int x, int ch) {
+  const int64_t i = base + (int64_t)((y * g.w + x) * g.pc + (g.pc == 1 ? 0 : ch));
+  return g.pool_f32 ? static_cast<const float *>(pool)[i] : lut[static_cast<const uint8_t *>(pool)[i]];
 }
 
 // grid interval of v on the unit grid k - c (k = 0..n-1): g[i] <= v < g[i+1], clipped to [0, n-2]
@@ -119,8 +125,8 @@ APG_DEV int grid_interval(double v, double c, int n, double &frac) {
 
 // One glimpse pixel (i, j) of image `base` at normalized position (px, py): C channels into out.
 // Returns APG_ERR_OOB_* bits for points outside the image grid (RGI bounds_error=True).
-APG_DEV uint32_t glimpse_pixel(const GlimpseGeo &g, const void *pool, int64_t base, double px, double py, int i, int j,
-                               float *out) {
+APG_DEV uint32_t glimpse_pixel(const GlimpseGeo &g, const void *pool, const float *lut, int64_t base, double px,
+                               double py, int i, int j, float *out) {
   // flip(denormalize(pos)) + offsets: (y, x) = (pos_y * lim_y + o0[i], pos_x * lim_x + o1[j])
   const double o0 = __dmul_rn(__dsub_rn((double)i, ((double)g.s0 - 1.0) / 2.0), g.scale);
   const double o1 = __dmul_rn(__dsub_rn((double)j, ((double)g.s1 - 1.0) / 2.0), g.scale);
@@ -136,18 +142,26 @@ APG_DEV uint32_t glimpse_pixel(const GlimpseGeo &g, const void *pool, int64_t ba
   // hypercube order of _evaluate_linear: (i0, j0), (i0, j0+1), (i0+1, j0), (i0+1, j0+1); w = (1*wy)*wx
   const double w00 = __dmul_rn(ny, nx), w01 = __dmul_rn(ny, wx), w10 = __dmul_rn(wy, nx), w11 = __dmul_rn(wy, wx);
   for (int ch = 0; ch < g.c; ch++) {
-    double v = __dadd_rn(0.0, __dmul_rn((double)pool_value(g, pool, base, iy, ix, ch), w00));
-    v = __dadd_rn(v, __dmul_rn((double)pool_value(g, pool, base, iy, ix + 1, ch), w01));
-    v = __dadd_rn(v, __dmul_rn((double)pool_value(g, pool, base, iy + 1, ix, ch), w10));
-    v = __dadd_rn(v, __dmul_rn((double)pool_value(g, pool, base, iy + 1, ix + 1, ch), w11));
+    double v = __dadd_rn(0.0, __dmul_rn((double)pool_value(g, pool, lut, base, iy, ix, ch), w00));
+    v = __dadd_rn(v, __dmul_rn((double)pool_value(g, pool, lut, base, iy, ix + 1, ch), w01));
+    v = __dadd_rn(v, __dmul_rn((double)pool_value(g, pool, lut, base, iy + 1, ix, ch), w10));
+    v = __dadd_rn(v, __dmul_rn((double)pool_value(g, pool, lut, base, iy + 1, ix + 1, ch), w11));
     v = v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);  // np.clip(0, 1)
     out[ch] = (float)v;
   }
   return err;
 }
 
-// ------------------------------------------------------------------ k_rng_fill
-constexpr int FILL_THREADS = 1024;
+// ------------------------------------------------------------------ stream draws (k_fill_*)
+// A batch of n draws from ONE numpy stream, spread over the chip: every thread jumps to its own
+// stretch of FILL_PER_THREAD words of the stream (pcg_advance) and walks it.  integers() rejects
+// candidates (Lemire), so output i is the i-th accepted candidate: k_fill_count counts per thread,
+// k_fill_write places each thread's accepted draws at its prefix, k_fill_finish advances the
+// generator state past the consumed words (and, if the candidates ran out, which is astronomically
+// rare for the sizes used, finishes sequentially).
+constexpr int FILL_THREADS = 256;
+constexpr int FILL_PER_THREAD = 32;
+constexpr int FILL_PER_BLOCK = FILL_THREADS * FILL_PER_THREAD;
 
 struct FillArgs {
   int kind;
@@ -157,113 +171,140 @@ struct FillArgs {
   int64_t lo;
   uint64_t bound;   // exclusive range of integers(lo, lo + bound)
   int64_t cand;     // candidate words examined in parallel (>= n)
+  int nblocks;
 };
 
-// block-wide exclusive scan of per-thread counts; returns the exclusive prefix, total in *total
-__device__ int64_t block_exclusive_scan(int64_t v, int64_t *s_wave, int64_t *total) {
+// work layout (int64): [nblocks] block totals, [nblocks * FILL_THREADS] thread counts, consumed
+APG_DEV int64_t *fill_consumed(int64_t *work, int nblocks) { return work + (size_t)nblocks * (FILL_THREADS + 1); }
+
+int64_t fill_work_elems(int64_t cand) {
+  const int64_t nb = (cand + FILL_PER_BLOCK - 1) / FILL_PER_BLOCK;
+  return nb * (FILL_THREADS + 1) + 1;
+}
+
+struct LemireSpec {
+  bool full;
+  uint32_t rex, thr;
+};
+
+APG_DEV LemireSpec lemire_spec(uint64_t bound) {
+  LemireSpec l;
+  const uint64_t rng = bound - 1;
+  l.full = rng == 0xffffffffULL;
+  l.rex = (uint32_t)(rng + 1);
+  l.thr = l.full ? 0u : (uint32_t)((0xffffffffULL - rng) % l.rex);
+  return l;
+}
+
+APG_DEV bool lemire_accept(const LemireSpec &l, uint32_t u) {
+  return l.full || (uint32_t)((uint64_t)u * l.rex) >= l.thr;
+}
+
+APG_DEV int64_t lemire_value(const LemireSpec &l, uint32_t u) {
+  return (int64_t)(l.full ? (uint64_t)u : (((uint64_t)u * l.rex) >> 32));
+}
+
+__global__ __launch_bounds__(FILL_THREADS) void k_fill_uniform(const apg_pcg64 *st, FillArgs a, double *out) {
+  // random_uniform: off + scale * next_double, one next64 per value, C order over (n, cols)
+  const int64_t m = a.n * a.cols;
+  const int64_t k0 = ((int64_t)blockIdx.x * FILL_THREADS + threadIdx.x) * FILL_PER_THREAD;
+  if (k0 >= m) return;
+  const int64_t k1 = k0 + FILL_PER_THREAD < m ? k0 + FILL_PER_THREAD : m;
+  Pcg64 r = *reinterpret_cast<const Pcg64 *>(st);
+  pcg_advance(r, (uint64_t)k0);
+  for (int64_t k = k0; k < k1; k++) {
+    const int c = a.cols == 1 ? 0 : (int)(k & 1);
+    out[k] = __dadd_rn(a.low[c], __dmul_rn(a.range[c], next_double(r)));
+  }
+}
+
+__global__ void k_fill_uniform_finish(apg_pcg64 *st, int64_t m) {
+  Pcg64 r = *reinterpret_cast<const Pcg64 *>(st);
+  pcg_advance(r, (uint64_t)m);
+  *reinterpret_cast<Pcg64 *>(st) = r;
+}
+
+__global__ __launch_bounds__(FILL_THREADS) void k_fill_count(const apg_pcg64 *st, FillArgs a, int64_t *work) {
+  __shared__ int s_sum[FILL_THREADS / 64];
+  const LemireSpec l = lemire_spec(a.bound);
+  const int64_t k0 = ((int64_t)blockIdx.x * FILL_THREADS + threadIdx.x) * FILL_PER_THREAD;
+  int cnt = 0;
+  if (k0 < a.cand) {
+    const int64_t k1 = k0 + FILL_PER_THREAD < a.cand ? k0 + FILL_PER_THREAD : a.cand;
+    Next32Walker wk(*reinterpret_cast<const Pcg64 *>(st), (uint64_t)k0);
+    for (int64_t k = k0; k < k1; k++) cnt += lemire_accept(l, wk.next()) ? 1 : 0;
+  }
+  work[a.nblocks + (size_t)blockIdx.x * FILL_THREADS + threadIdx.x] = cnt;
+  int v = cnt;
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < FILL_THREADS / 64; w++) t += s_sum[w];
+    work[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(FILL_THREADS) void k_fill_write(const apg_pcg64 *st, FillArgs a, int64_t *out,
+                                                             int64_t *work) {
+  __shared__ int64_t s_wave[FILL_THREADS / 64];
+  __shared__ int64_t s_base;
+  const LemireSpec l = lemire_spec(a.bound);
+  if (threadIdx.x == 0) {
+    int64_t b = 0;
+    for (int k = 0; k < (int)blockIdx.x; k++) b += work[k];
+    s_base = b;
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int64_t inc = v;
+  const int64_t cnt = work[a.nblocks + (size_t)blockIdx.x * FILL_THREADS + threadIdx.x];
+  int64_t inc = cnt;
   for (int d = 1; d < 64; d <<= 1) {
     const int64_t o = __shfl_up(inc, d, 64);
     if (lane >= d) inc += o;
   }
   if (lane == 63) s_wave[wave] = inc;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int64_t acc = 0;
-    for (int k = 0; k < FILL_THREADS / 64; k++) {
-      const int64_t t = s_wave[k];
-      s_wave[k] = acc;
-      acc += t;
+  int64_t q = s_base + inc - cnt;
+  for (int w = 0; w < wave; w++) q += s_wave[w];
+  const int64_t k0 = ((int64_t)blockIdx.x * FILL_THREADS + threadIdx.x) * FILL_PER_THREAD;
+  if (cnt == 0 || q >= a.n) return;
+  const int64_t k1 = k0 + FILL_PER_THREAD < a.cand ? k0 + FILL_PER_THREAD : a.cand;
+  Next32Walker wk(*reinterpret_cast<const Pcg64 *>(st), (uint64_t)k0);
+  for (int64_t k = k0; k < k1 && q < a.n; k++) {
+    const uint32_t u = wk.next();
+    if (lemire_accept(l, u)) {
+      out[q] = a.lo + lemire_value(l, u);
+      if (q == a.n - 1) *fill_consumed(work, a.nblocks) = k + 1;
+      q++;
     }
-    s_wave[FILL_THREADS / 64] = acc;
   }
-  __syncthreads();
-  *total = s_wave[FILL_THREADS / 64];
-  return s_wave[wave] + inc - v;
 }
 
-__global__ __launch_bounds__(FILL_THREADS) void k_rng_fill(apg_pcg64 *st, FillArgs a, void *out) {
-  __shared__ int64_t s_wave[FILL_THREADS / 64 + 1];
-  __shared__ uint64_t s_consumed;
-  const int tid = threadIdx.x;
+__global__ void k_fill_finish(apg_pcg64 *st, FillArgs a, int64_t *out, int64_t *work) {
+  const LemireSpec l = lemire_spec(a.bound);
   const Pcg64 base = *reinterpret_cast<const Pcg64 *>(st);
-  if (a.kind == APG_DRAW_UNIFORM) {
-    // random_uniform: off + scale * next_double, one next64 per value, C order over (n, cols)
-    const int64_t m = a.n * a.cols, chunk = (m + FILL_THREADS - 1) / FILL_THREADS;
-    const int64_t k0 = tid * chunk, k1 = k0 + chunk < m ? k0 + chunk : m;
-    double *o = static_cast<double *>(out);
-    if (k0 < k1) {
-      Pcg64 r = base;
-      pcg_advance(r, (uint64_t)k0);
-      for (int64_t k = k0; k < k1; k++) {
-        const int c = (int)(k % a.cols);
-        o[k] = __dadd_rn(a.low[c], __dmul_rn(a.range[c], next_double(r)));
-      }
-    }
-    __syncthreads();
-    if (tid == 0) {
-      Pcg64 r = base;
-      pcg_advance(r, (uint64_t)m);
-      *reinterpret_cast<Pcg64 *>(st) = r;
-    }
-    return;
-  }
-  // integers: random_bounded_uint64_fill for rng = bound - 1 < 2^32 (Lemire on next_uint32; the
-  // full 32-bit range takes next_uint32 as is; a one-value range draws nothing)
-  int64_t *o = static_cast<int64_t *>(out);
-  const uint64_t rng = a.bound - 1;
-  if (rng == 0) {
-    for (int64_t i = tid; i < a.n; i += FILL_THREADS) o[i] = a.lo;
-    return;
-  }
-  const bool full = rng == 0xffffffffULL;
-  const uint32_t rex = (uint32_t)(rng + 1);             // unused when full
-  const uint32_t thr = full ? 0u : (uint32_t)((0xffffffffULL - rng) % rex);
-  const int64_t chunk = (a.cand + FILL_THREADS - 1) / FILL_THREADS;
-  const int64_t k0 = tid * chunk, k1 = k0 + chunk < a.cand ? k0 + chunk : a.cand;
-  // pass 1: accepted candidates per thread
-  int64_t cnt = 0;
-  if (k0 < k1) {
-    Next32Walker wk(base, (uint64_t)k0);
-    for (int64_t k = k0; k < k1; k++) {
-      const uint32_t u = wk.next();
-      if (full || (uint32_t)((uint64_t)u * rex) >= thr) cnt++;
-    }
-  }
-  int64_t total;
-  const int64_t before = block_exclusive_scan(cnt, s_wave, &total);
-  if (tid == 0) s_consumed = (uint64_t)a.cand;
-  __syncthreads();
-  // pass 2: the i-th accepted candidate is output i
-  int64_t q = before;
-  if (q < a.n && k0 < k1) {
-    Next32Walker wk(base, (uint64_t)k0);
-    for (int64_t k = k0; k < k1 && q < a.n; k++) {
-      const uint32_t u = wk.next();
-      const uint64_t mlt = (uint64_t)u * rex;
-      if (full || (uint32_t)mlt >= thr) {
-        o[q] = a.lo + (int64_t)(full ? (uint64_t)u : (mlt >> 32));
-        if (q == a.n - 1) s_consumed = (uint64_t)k + 1;
-        q++;
-      }
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    Pcg64 r = after_next32_words(base, s_consumed);
-    // not enough accepted candidates (astronomically rare for the sizes used): finish sequentially
+  int64_t total = 0;
+  for (int b = 0; b < a.nblocks; b++) total += work[b];
+  Pcg64 r;
+  if (total >= a.n) {
+    r = after_next32_words(base, (uint64_t)*fill_consumed(work, a.nblocks));
+  } else {  // not enough accepted candidates: continue sequentially after all of them
+    r = after_next32_words(base, (uint64_t)a.cand);
     for (int64_t i = total; i < a.n; i++) {
-      uint64_t mlt;
       uint32_t u;
       do {
         u = next32(r);
-        mlt = (uint64_t)u * rex;
-      } while (!full && (uint32_t)mlt < thr);
-      o[i] = a.lo + (int64_t)(full ? (uint64_t)u : (mlt >> 32));
+      } while (!lemire_accept(l, u));
+      out[i] = a.lo + lemire_value(l, u);
     }
-    *reinterpret_cast<Pcg64 *>(st) = r;
   }
+  *reinterpret_cast<Pcg64 *>(st) = r;
+}
+
+__global__ void k_fill_const(int64_t n, int64_t v, int64_t *out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = v;
 }
 
 // ------------------------------------------------------------------ seeding chain
@@ -298,18 +339,19 @@ __global__ void k_image_gather(int n, const int32_t *pool_labels, const int64_t 
 // ------------------------------------------------------------------ k_glimpse
 template <class PosT>
 __global__ __launch_bounds__(256) void k_glimpse(GlimpseGeo g, const void *pool, const int64_t *index,
-                                                 const PosT *pos, int npos, int64_t total, float *out,
-                                                 uint32_t *err) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                 const PosT *pos, int npos, int total, float *out, uint32_t *err) {
+  __shared__ float s_lut[256];
+  load_u8_table(s_lut);
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;  // total < 2^31 (checked by the host)
   if (t >= total) return;
-  const int j = (int)(t % g.s1);
-  const int i = (int)((t / g.s1) % g.s0);
-  const int64_t np_ = t / ((int64_t)g.s0 * g.s1);  // env * npos + p
-  const int64_t e = np_ / npos;
+  const int per = g.s0 * g.s1;
+  const int np_ = t / per, pix = t - np_ * per;  // np_ = env * npos + p
+  const int i = pix / g.s1, j = pix - i * g.s1;
+  const int e = np_ / npos;
   const double px = (double)pos[2 * np_], py = (double)pos[2 * np_ + 1];
   float v[3];
-  const uint32_t bad = glimpse_pixel(g, pool, index[e] * g.img_elems, px, py, i, j, v);
-  for (int ch = 0; ch < g.c; ch++) out[t * g.c + ch] = v[ch];
+  const uint32_t bad = glimpse_pixel(g, pool, s_lut, index[e] * g.img_elems, px, py, i, j, v);
+  for (int ch = 0; ch < g.c; ch++) out[(size_t)t * g.c + ch] = v[ch];
   if (bad) atomicOr(err, bad);
 }
 
@@ -338,46 +380,11 @@ APG_DEV float ce_f32(const float *row, int k, int target) {
   return -out;
 }
 
-// NaN in softmax(row)[label] (the quality the reference checks, image_classification.py:114-116):
-// exactly when a logit is NaN or +inf, or all logits are -inf
-APG_DEV bool softmax_nan(const float *row, int k) {
-  bool bad = false, all_neg_inf = true;
-  for (int i = 0; i < k; i++) {
-    const float v = row[i];
-    if (v != v || v == INFINITY) bad = true;
-    if (v != -INFINITY) all_neg_inf = false;
-  }
-  return bad || all_neg_inf;
-}
-
-__global__ __launch_bounds__(256) void k_image_env(EnvArgs a, const float *__restrict__ act,
-                                                   const float *__restrict__ pred, const int32_t *label,
-                                                   double *pos, apg_image_outputs out) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= a.n) return;
+// The per-env tail of ImagePerceptionModule.step (:197-213) + ActivePerceptionVectorEnv.step
+// (reward = base_reward - loss): move (or not, on the autoreset step), rewards, glimpse_pos, time.
+APG_DEV uint32_t env_tail(const EnvArgs &a, int e, const float *__restrict__ act, double *pos,
+                          const apg_image_outputs &out, double loss_d, float loss_f) {
   uint32_t err = 0;
-  double loss_d;
-  float loss_f = 0.0f;
-  if (a.kind == APG_IMAGE_CLASSIFY) {
-    const float *row = pred + (size_t)e * a.k;
-    if (softmax_nan(row, a.k)) err |= APG_ERR_NAN_PREDICTION;
-    const int32_t l = label[e];
-    // CrossEntropyLossFn(...).normalized: f32 CE * scale(f64) + offset(f64)
-    loss_d = __dadd_rn(__dmul_rn((double)ce_f32(row, a.k, l), a.ce_scale), a.ce_offset);
-    out.loss_f64[e] = loss_d;
-    out.label_target[e] = l;
-  } else {
-    const float p0 = pred[2 * e], p1 = pred[2 * e + 1];
-    if (p0 != p0 || p1 != p1) err |= APG_ERR_NAN_PREDICTION;  // 1 - |pred - target| / 2 is NaN
-    // the loss compares against the target before the autoreset update (out.target: pre-update copy)
-    const float t0 = out.target[2 * e], t1 = out.target[2 * e + 1];
-    const float d0 = __fsub_rn(p0, t0), d1 = __fsub_rn(p1, t1);
-    // np.mean(f32 [2]): (0 + d0^2 + d1^2) / 2, then * scale + offset in f32
-    const float mse = f32_div(__fadd_rn(__fadd_rn(0.0f, __fmul_rn(d0, d0)), __fmul_rn(d1, d1)), 2.0f);
-    loss_f = __fadd_rn(__fmul_rn(mse, a.mse_scale), a.mse_offset);
-    out.loss_f32[e] = loss_f;
-    loss_d = (double)loss_f;
-  }
   double px = pos[2 * e], py = pos[2 * e + 1];
   if (a.resetting) {
     // module.reset() replaced the batch; base_reward = np.zeros(N) (float64)
@@ -390,9 +397,8 @@ __global__ __launch_bounds__(256) void k_image_env(EnvArgs a, const float *__res
     const float mag = norm_f32(a0, a1);
     float s0 = a0, s1 = a1;
     if (mag > 1.0f) {
-      const float den = mag > 1.0f ? mag : 1.0f;
-      s0 = __fmul_rn(f32_div(a0, den), 1.0f);
-      s1 = __fmul_rn(f32_div(a1, den), 1.0f);
+      s0 = __fmul_rn(f32_div(a0, mag), 1.0f);
+      s1 = __fmul_rn(f32_div(a1, mag), 1.0f);
     }
     px = __dadd_rn(px, __dmul_rn(a.msl[0], (double)s0));
     py = __dadd_rn(py, __dmul_rn(a.msl[1], (double)s1));
@@ -408,6 +414,113 @@ __global__ __launch_bounds__(256) void k_image_env(EnvArgs a, const float *__res
   out.glimpse_pos[2 * e] = (float)px;
   out.glimpse_pos[2 * e + 1] = (float)py;
   out.time_step[e] = a.time_value;
+  return err;
+}
+
+// Localization: one thread per env; MSE against the target before the autoreset update.
+__global__ __launch_bounds__(256) void k_image_env_loc(EnvArgs a, const float *__restrict__ act,
+                                                       const float *__restrict__ pred, double *pos,
+                                                       apg_image_outputs out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n) return;
+  uint32_t err = 0;
+  const float p0 = pred[2 * e], p1 = pred[2 * e + 1];
+  if (p0 != p0 || p1 != p1) err |= APG_ERR_NAN_PREDICTION;  // 1 - |pred - target| / 2 is NaN
+  const float t0 = out.target[2 * e], t1 = out.target[2 * e + 1];
+  const float d0 = __fsub_rn(p0, t0), d1 = __fsub_rn(p1, t1);
+  // np.mean(f32 [2]): (0 + d0^2 + d1^2) / 2, then * scale + offset in f32
+  const float mse = f32_div(__fadd_rn(__fadd_rn(0.0f, __fmul_rn(d0, d0)), __fmul_rn(d1, d1)), 2.0f);
+  const float loss_f = __fadd_rn(__fmul_rn(mse, a.mse_scale), a.mse_offset);
+  out.loss_f32[e] = loss_f;
+  err |= env_tail(a, e, act, pos, out, (double)loss_f, loss_f);
+  if (err) atomicOr(out.err, err);
+}
+
+// numpy pairwise sum of x[off .. off+n) by the 8 lanes of a group (lane j owns accumulator j of
+// every <= 128 block; the combine and the < 8 tail are evaluated identically by all 8 lanes)
+APG_DEV float pw_leaf8(const float *x, int off, int n, int j) {
+  if (n < 8) {
+    float r = 0.0f;
+    for (int i = 0; i < n; i++) r = __fadd_rn(r, x[off + i]);
+    return r;
+  }
+  float r = x[off + j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) r = __fadd_rn(r, x[off + i + j]);
+  const int g0 = (int)(threadIdx.x & 63u) & ~7;
+  float q[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) q[k] = __shfl(r, g0 + k, 64);
+  float res = __fadd_rn(__fadd_rn(__fadd_rn(q[0], q[1]), __fadd_rn(q[2], q[3])),
+                        __fadd_rn(__fadd_rn(q[4], q[5]), __fadd_rn(q[6], q[7])));
+  for (; i < n; i++) res = __fadd_rn(res, x[off + i]);
+  return res;
+}
+
+template <int DEPTH>
+APG_DEV float pw_sum8(const float *x, int off, int n, int j) {
+  if constexpr (DEPTH == 0) {
+    return pw_leaf8(x, off, n, j);
+  } else {
+    if (n <= 128) return pw_leaf8(x, off, n, j);
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return __fadd_rn(pw_sum8<DEPTH - 1>(x, off, n2, j), pw_sum8<DEPTH - 1>(x, off + n2, n - n2, j));
+  }
+}
+
+// Classification: 8 lanes per env, the block's logits staged in LDS with coalesced loads.
+// Cross entropy = -(x[t] - m - log(sum(exp(x - m)))) in f32 (scipy.special.log_softmax), the exp
+// sum in numpy's pairwise order; normalized with the f64 affine (loss_fn.py:100-110).
+constexpr int CLS_LANES = 8;
+__global__ __launch_bounds__(256) void k_image_env_cls(EnvArgs a, int envs_per_block, const float *__restrict__ act,
+                                                       const float *__restrict__ pred, const int32_t *label,
+                                                       double *pos, apg_image_outputs out) {
+  extern __shared__ float s_logit[];  // [envs_per_block][k + 1]
+  const int k = a.k, stride = k + 1;
+  const int e0 = blockIdx.x * envs_per_block;
+  const int ne = a.n - e0 < envs_per_block ? a.n - e0 : envs_per_block;
+  for (int q = threadIdx.x; q < ne * k; q += blockDim.x) {
+    const int r = q / k;
+    s_logit[r * stride + (q - r * k)] = pred[(size_t)e0 * k + q];
+  }
+  __syncthreads();
+  const int grp = threadIdx.x / CLS_LANES, j = threadIdx.x % CLS_LANES;
+  const bool live = grp < ne;
+  float *row = s_logit + (live ? grp : 0) * stride;
+  // max (NaN-propagating like np.amax) and the softmax NaN condition, over the 8 lanes
+  float m = -INFINITY;
+  bool nan = false, pos_inf = false, all_neg_inf = true;
+  for (int i = j; i < k; i += CLS_LANES) {
+    const float v = row[i];
+    nan |= v != v;
+    pos_inf |= v == INFINITY;
+    all_neg_inf &= v == -INFINITY;
+    m = v > m ? v : m;
+  }
+  for (int d = 1; d < CLS_LANES; d <<= 1) {
+    const float om = __shfl_xor(m, d, 64);
+    m = om > m ? om : m;
+    nan |= __shfl_xor((int)nan, d, 64) != 0;
+    pos_inf |= __shfl_xor((int)pos_inf, d, 64) != 0;
+    all_neg_inf &= __shfl_xor((int)all_neg_inf, d, 64) != 0;
+  }
+  if (nan || isinf(m)) m = 0.0f;  // x_max[~isfinite(x_max)] = 0
+  const int32_t l = live ? label[e0 + grp] : 0;
+  const float xt = row[l < 0 ? 0 : (l >= k ? k - 1 : l)];
+  __syncthreads();
+  if (live)  // lanes of the tail groups (grp >= ne) alias row 0 and must not write it
+    for (int i = j; i < k; i += CLS_LANES) row[i] = expf(__fsub_rn(row[i], m));
+  __syncthreads();
+  const float sum = pw_sum8<MAX_PW_DEPTH>(row, 0, k, j);
+  if (!live || j != 0) return;
+  const int e = e0 + grp;
+  uint32_t err = (nan || pos_inf || all_neg_inf) ? APG_ERR_NAN_PREDICTION : 0u;
+  const float ce = -__fsub_rn(__fsub_rn(xt, m), logf(sum));
+  const double loss_d = __dadd_rn(__dmul_rn((double)ce, a.ce_scale), a.ce_offset);
+  out.loss_f64[e] = loss_d;
+  out.label_target[e] = l;
+  err |= env_tail(a, e, act, pos, out, loss_d, 0.0f);
   if (err) atomicOr(out.err, err);
 }
 
@@ -417,14 +530,14 @@ constexpr int UNIQ_LDS_FLOATS = 24 * 1024;  // 96 KiB of glimpse tiles (two tile
 constexpr int UNIQ_MAX_POINTS = 4096;
 
 // tile of T glimpses (rows p0 .. p0+T-1 of the sampling grid) into LDS rows of stride L + 1
-APG_DEV void unique_tile(const GlimpseGeo &g, const void *pool, int64_t base, const double *grid, int p0, int T,
-                         int P, int L, float *tile) {
+APG_DEV void unique_tile(const GlimpseGeo &g, const void *pool, const float *lut, int64_t base, const double *grid,
+                         int p0, int T, int P, int L, float *tile) {
   const int per = g.s0 * g.s1;
   for (int q = threadIdx.x; q < T * per; q += UNIQ_THREADS) {
     const int r = q / per, pix = q % per, p = p0 + r;
     if (p >= P) continue;
     float v[3];
-    glimpse_pixel(g, pool, base, grid[2 * p], grid[2 * p + 1], pix / g.s1, pix % g.s1, v);
+    glimpse_pixel(g, pool, lut, base, grid[2 * p], grid[2 * p + 1], pix / g.s1, pix % g.s1, v);
     for (int ch = 0; ch < g.c; ch++) tile[r * (L + 1) + pix * g.c + ch] = v[ch];
   }
 }
@@ -434,6 +547,8 @@ __global__ __launch_bounds__(UNIQ_THREADS) void k_unique(GlimpseGeo g, const voi
                                                          float *uniq) {
   extern __shared__ float s_dyn[];
   __shared__ uint32_t s_min[UNIQ_MAX_POINTS];
+  __shared__ float s_lut[256];
+  load_u8_table(s_lut);
   const int e = blockIdx.x;
   const int L = g.s0 * g.s1 * g.c;
   float *tA = s_dyn, *tB = s_dyn + T * (L + 1);
@@ -443,10 +558,10 @@ __global__ __launch_bounds__(UNIQ_THREADS) void k_unique(GlimpseGeo g, const voi
   const float inv_l_den = (float)L;
   for (int A = 0; A < tiles; A++) {
     __syncthreads();
-    unique_tile(g, pool, base, grid, A * T, T, P, L, tA);
+    unique_tile(g, pool, s_lut, base, grid, A * T, T, P, L, tA);
     for (int B = A; B < tiles; B++) {
       __syncthreads();
-      if (B != A) unique_tile(g, pool, base, grid, B * T, T, P, L, tB);
+      if (B != A) unique_tile(g, pool, s_lut, base, grid, B * T, T, P, L, tB);
       __syncthreads();
       const float *sb = B == A ? tA : tB;
       const int na = A * T + T <= P ? T : P - A * T, nb = B * T + T <= P ? T : P - B * T;
@@ -556,17 +671,6 @@ __global__ void k_loss_mse(const float *pred, const float *target, int n, int d,
 // ------------------------------------------------------------------ host side
 int grid_for(int64_t n, int threads) { return (int)((n + threads - 1) / threads); }
 
-int ensure_u8_table() {
-  static bool done = false;
-  if (done) return APG_OK;
-  float t[256];
-  for (int v = 0; v < 256; v++) t[v] = (float)((double)(float)v / 255.0);  // f32(v) / 255, correctly rounded
-  if (hipMemcpyToSymbol(HIP_SYMBOL(c_u8_to_f32), t, sizeof(t)) != hipSuccess)
-    return fail(APG_E_LAUNCH, "hipMemcpyToSymbol(u8 table) failed");
-  done = true;
-  return APG_OK;
-}
-
 int validate(const apg_image_config *c) {
   if (c->num_envs <= 0) return fail(APG_E_INVALID, "num_envs must be positive");
   if (c->height < 2 || c->width < 2) return fail(APG_E_INVALID, "images must be at least 2 x 2");
@@ -585,33 +689,40 @@ int validate(const apg_image_config *c) {
   return APG_OK;
 }
 
-int launch_fill(apg_pcg64 *state, const FillArgs &a0, void *out, hipStream_t s) {
-  FillArgs a = a0;
-  if (a.kind == APG_DRAW_INTEGERS) {
-    // enough candidates that the n-th acceptance falls inside them with overwhelming probability
-    const uint64_t rng = a.bound - 1;
-    double p_rej = 0.0;
-    if (rng != 0xffffffffULL && rng != 0) p_rej = (double)((0xffffffffULL - rng) % (rng + 1)) / 4294967296.0;
-    const double expect = (double)a.n / (1.0 - p_rej);
-    a.cand = (int64_t)(expect + 8.0 * std::sqrt(expect * p_rej + 1.0) + 64.0);
-    if (a.cand < a.n) a.cand = a.n;
-  }
-  hipLaunchKernelGGL(k_rng_fill, dim3(1), dim3(FILL_THREADS), 0, s, state, a, out);
-  return check_launch("k_rng_fill");
+// candidates examined for n integers draws: n / P(accept) plus eight standard deviations
+int64_t fill_candidates(int64_t n, uint64_t bound) {
+  const uint64_t rng = bound - 1;
+  double p_rej = 0.0;
+  if (rng != 0xffffffffULL && rng != 0) p_rej = (double)((0xffffffffULL - rng) % (rng + 1)) / 4294967296.0;
+  const double expect = (double)n / (1.0 - p_rej);
+  int64_t cand = (int64_t)(expect + 8.0 * std::sqrt(expect * p_rej + 1.0) + 64.0);
+  return cand < n ? n : cand;
 }
 
-int launch_integers(apg_pcg64 *state, int64_t n, int64_t lo, uint64_t bound, int64_t *out, hipStream_t s) {
+int launch_integers(apg_pcg64 *state, int64_t n, int64_t lo, uint64_t bound, int64_t *out, int64_t *work,
+                    hipStream_t s) {
+  if (n <= 0) return APG_OK;
+  if (bound == 1) {  // integers(lo, lo + 1): no draw at all
+    hipLaunchKernelGGL(k_fill_const, dim3(grid_for(n, 256)), dim3(256), 0, s, n, lo, out);
+    return check_launch("k_fill_const");
+  }
   FillArgs a{};
   a.kind = APG_DRAW_INTEGERS;
   a.n = n;
   a.cols = 1;
   a.lo = lo;
   a.bound = bound;
-  return launch_fill(state, a, out, s);
+  a.cand = fill_candidates(n, bound);
+  a.nblocks = grid_for(a.cand, FILL_PER_BLOCK);
+  hipLaunchKernelGGL(k_fill_count, dim3(a.nblocks), dim3(FILL_THREADS), 0, s, state, a, work);
+  hipLaunchKernelGGL(k_fill_write, dim3(a.nblocks), dim3(FILL_THREADS), 0, s, state, a, out, work);
+  hipLaunchKernelGGL(k_fill_finish, dim3(1), dim3(1), 0, s, state, a, out, work);
+  return check_launch("k_fill_*");
 }
 
 int launch_uniform(apg_pcg64 *state, int64_t n, int cols, const double *low, const double *range, double *out,
                    hipStream_t s) {
+  if (n <= 0) return APG_OK;
   FillArgs a{};
   a.kind = APG_DRAW_UNIFORM;
   a.n = n;
@@ -620,15 +731,19 @@ int launch_uniform(apg_pcg64 *state, int64_t n, int cols, const double *low, con
     a.low[c] = low[c];
     a.range[c] = range[c];
   }
-  return launch_fill(state, a, out, s);
+  const int64_t m = n * cols;
+  hipLaunchKernelGGL(k_fill_uniform, dim3(grid_for(m, FILL_PER_BLOCK)), dim3(FILL_THREADS), 0, s, state, a, out);
+  hipLaunchKernelGGL(k_fill_uniform_finish, dim3(1), dim3(1), 0, s, state, m);
+  return check_launch("k_fill_uniform");
 }
 
 template <class PosT>
 int launch_glimpse(const GlimpseGeo &g, const void *pool, const int64_t *index, const PosT *pos, int n, int npos,
                    float *out, uint32_t *err, hipStream_t s) {
   const int64_t total = (int64_t)n * npos * g.s0 * g.s1;
-  hipLaunchKernelGGL(k_glimpse<PosT>, dim3(grid_for(total, 256)), dim3(256), 0, s, g, pool, index, pos, npos, total,
-                     out, err);
+  if (total >= (int64_t)1 << 31) return fail(APG_E_INVALID, "glimpse batch too large (>= 2**31 pixels)");
+  hipLaunchKernelGGL(k_glimpse<PosT>, dim3(grid_for(total, 256)), dim3(256), 0, s, g, pool, index, pos, npos,
+                     (int)total, out, err);
   return check_launch("k_glimpse");
 }
 
@@ -661,8 +776,13 @@ int launch_unique(const GlimpseGeo &g, const void *pool, const int64_t *index, c
 
 extern "C" {
 
+int64_t apg_rng_fill_work_elems(int64_t n, uint64_t bound) {
+  if (n <= 0 || bound < 1 || bound > 0x100000000ULL) return 0;
+  return fill_work_elems(fill_candidates(n, bound));
+}
+
 int apg_rng_fill(apg_pcg64 *state, int kind, int64_t n, int cols, const double *low, const double *range, int64_t lo,
-                 uint64_t bound, void *out, apg_stream_t stream) {
+                 uint64_t bound, void *out, int64_t *work, apg_stream_t stream) {
   if (!state || !out || n < 0) return fail(APG_E_INVALID, "bad apg_rng_fill arguments");
   if (n == 0) return APG_OK;
   hipStream_t s = (hipStream_t)stream;
@@ -672,7 +792,8 @@ int apg_rng_fill(apg_pcg64 *state, int kind, int64_t n, int cols, const double *
   }
   if (kind == APG_DRAW_INTEGERS) {
     if (bound < 1 || bound > 0x100000000ULL) return fail(APG_E_INVALID, "integers range must be in [1, 2**32]");
-    return launch_integers(state, n, lo, bound, static_cast<int64_t *>(out), s);
+    if (!work && bound > 1) return fail(APG_E_INVALID, "integers draws need apg_rng_fill_work_elems() of work");
+    return launch_integers(state, n, lo, bound, static_cast<int64_t *>(out), work, s);
   }
   return fail(APG_E_INVALID, "unknown draw kind");
 }
@@ -688,9 +809,9 @@ static int module_reset(const apg_image_config *c, const apg_image_state *st, co
   const int n = c->num_envs;
   int rc;
   // next(DatasetBatchIterator): integers(0, len(dataset), N)
-  if ((rc = launch_integers(st->rng + 2, n, 0, (uint64_t)c->pool_len, st->index, s))) return rc;
+  if ((rc = launch_integers(st->rng + 2, n, 0, (uint64_t)c->pool_len, st->index, st->rng_work, s))) return rc;
   // randomly_invert_labels: current_rng.integers(0, 2, size=N) == 1
-  if (c->invert_labels && (rc = launch_integers(st->rng + 1, n, 0, 2, st->scratch_i64, s))) return rc;
+  if (c->invert_labels && (rc = launch_integers(st->rng + 1, n, 0, 2, st->scratch_i64, st->rng_work, s))) return rc;
   hipLaunchKernelGGL(k_image_gather, dim3(grid_for(n, 256)), dim3(256), 0, s, n, st->pool_labels, st->index,
                      c->invert_labels, st->scratch_i64, c->num_classes, st->label, st->inverted);
   if ((rc = check_launch("k_image_gather"))) return rc;
@@ -699,17 +820,17 @@ static int module_reset(const apg_image_config *c, const apg_image_state *st, co
   return launch_uniform(st->rng + 1, n, 2, low, range, st->pos, s);
 }
 
-static int observe(const apg_image_config *c, const apg_image_state *st, const apg_image_outputs *out, hipStream_t s) {
+static int observe(const apg_image_config *c, const apg_image_state *st, const apg_image_outputs *out, hipStream_t s,
+                   bool target_changed) {
   const GlimpseGeo g = make_geo(c);
   int rc = launch_glimpse<double>(g, st->pool, st->index, st->pos, c->num_envs, 1, out->glimpse, out->err, s);
-  if (rc || c->kind != APG_IMAGE_LOCALIZE) return rc;
+  if (rc || c->kind != APG_IMAGE_LOCALIZE || !target_changed) return rc;
   return launch_glimpse<float>(g, st->pool, st->index, st->target, c->num_envs, 1, out->target_glimpse, out->err, s);
 }
 
 int apg_image_reset(const apg_image_config *c, const apg_image_state *st, const apg_image_outputs *out,
                     apg_stream_t stream) {
   if (int rc = validate(c)) return rc;
-  if (int rc = ensure_u8_table()) return rc;
   hipStream_t s = (hipStream_t)stream;
   const int n = c->num_envs;
   int rc;
@@ -721,7 +842,7 @@ int apg_image_reset(const apg_image_config *c, const apg_image_state *st, const 
     if ((rc = launch_unique(g, st->pool, st->index, st->unique_grid, n, c->unique_points, c->top_k, st->top_k,
                             nullptr, s)))
       return rc;
-    if ((rc = launch_integers(st->rng + 1, n, 0, (uint64_t)c->top_k, st->scratch_i64, s))) return rc;
+    if ((rc = launch_integers(st->rng + 1, n, 0, (uint64_t)c->top_k, st->scratch_i64, st->rng_work, s))) return rc;
     const double low[2] = {-c->cell[0], -c->cell[1]};
     const double range[2] = {c->cell[0] - -c->cell[0], c->cell[1] - -c->cell[1]};
     if ((rc = launch_uniform(st->rng + 1, n, 2, low, range, st->scratch_f64, s))) return rc;
@@ -733,14 +854,13 @@ int apg_image_reset(const apg_image_config *c, const apg_image_state *st, const 
   hipLaunchKernelGGL(k_obs_pos, dim3(grid_for(n, 256)), dim3(256), 0, s, n, st->pos, out->glimpse_pos,
                      out->time_step, -1.0f);
   if ((rc = check_launch("k_obs_pos"))) return rc;
-  return observe(c, st, out, s);
+  return observe(c, st, out, s, true);
 }
 
 int apg_image_step(const apg_image_config *c, const apg_image_state *st, const float *action,
                    const float *prediction, int32_t t, int32_t prev_done, const apg_image_outputs *out,
                    apg_stream_t stream) {
   if (int rc = validate(c)) return rc;
-  if (int rc = ensure_u8_table()) return rc;
   if (!action || !prediction) return fail(APG_E_INVALID, "null action/prediction");
   hipStream_t s = (hipStream_t)stream;
   const int n = c->num_envs;
@@ -769,16 +889,24 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
   a.mse_offset = c->mse_offset;
   const int32_t t_new = prev_done ? 0 : t + 1;
   a.time_value = (float)(((double)t_new / (double)c->step_limit) * 2.0 - 1.0);
-  hipLaunchKernelGGL(k_image_env, dim3(grid_for(n, 256)), dim3(256), 0, s, a, action, prediction, st->label,
-                     st->pos, *out);
+  if (c->kind == APG_IMAGE_CLASSIFY) {
+    int epb = 256 / CLS_LANES;
+    while (epb > 1 && (size_t)epb * (c->num_classes + 1) * sizeof(float) > 64 * 1024) epb /= 2;
+    const size_t lds = (size_t)epb * (c->num_classes + 1) * sizeof(float);
+    hipLaunchKernelGGL(k_image_env_cls, dim3(grid_for(n, epb)), dim3(epb * CLS_LANES), lds, s, a, epb, action,
+                       prediction, st->label, st->pos, *out);
+  } else {
+    hipLaunchKernelGGL(k_image_env_loc, dim3(grid_for(n, 256)), dim3(256), 0, s, a, action, prediction, st->pos,
+                       *out);
+  }
   if ((rc = check_launch("k_image_env"))) return rc;
-  return observe(c, st, out, s);
+  // the target glimpse only changes with the target or the images, i.e. on the autoreset step
+  return observe(c, st, out, s, prev_done != 0);
 }
 
 int apg_image_glimpse(const apg_image_config *c, const void *pool, const int64_t *index, const void *pos,
                       int pos_is_f32, int32_t npos, float *out, uint32_t *err, apg_stream_t stream) {
   if (int rc = validate(c)) return rc;
-  if (int rc = ensure_u8_table()) return rc;
   if (npos <= 0) return fail(APG_E_INVALID, "npos must be positive");
   const GlimpseGeo g = make_geo(c);
   hipStream_t s = (hipStream_t)stream;
@@ -790,7 +918,6 @@ int apg_image_glimpse(const apg_image_config *c, const void *pool, const int64_t
 int apg_image_unique_top_k(const apg_image_config *c, const void *pool, const int64_t *index, const double *grid,
                            int32_t npoints, int32_t k, int32_t *top_k, float *uniq, apg_stream_t stream) {
   if (int rc = validate(c)) return rc;
-  if (int rc = ensure_u8_table()) return rc;
   return launch_unique(make_geo(c), pool, index, grid, c->num_envs, npoints, k, top_k, uniq, (hipStream_t)stream);
 }
 

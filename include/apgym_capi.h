@@ -170,9 +170,11 @@ int apg_rng_draws(const uint64_t *seeds, int m, int kind, int64_t a, int64_t b, 
 #define APG_DRAW_INTEGERS 1 /* out i64[n] = lo + bounded(hi - lo - 1)               (Generator.integers) */
 
 /* n draws (n x cols for uniform, cols <= 2) from the ONE stream *state (device), advancing it
- * exactly as numpy would.  integers: bound = hi - lo (exclusive range, 1 <= bound <= 2**32). */
+ * exactly as numpy would.  integers: bound = hi - lo (exclusive range, 1 <= bound <= 2**32) and
+ * `work` holds apg_rng_fill_work_elems(n, bound) int64 (device; unused for uniform draws). */
+int64_t apg_rng_fill_work_elems(int64_t n, uint64_t bound);
 int apg_rng_fill(apg_pcg64 *state, int kind, int64_t n, int cols, const double *low, const double *range,
-                 int64_t lo, uint64_t bound, void *out, apg_stream_t stream);
+                 int64_t lo, uint64_t bound, void *out, int64_t *work, apg_stream_t stream);
 
 /* ---------------------------------------------------------------- image glimpse envs */
 #define APG_IMAGE_CLASSIFY 0 /* ImageClassificationVectorEnv */
@@ -214,6 +216,7 @@ typedef struct apg_image_state {
   int64_t *scratch_i64;       /* [N] */
   double *scratch_f64;        /* [2N] */
   int32_t *top_k;             /* [N][top_k] unique-sampling ranking (localize) */
+  int64_t *rng_work;          /* apg_rng_fill_work_elems(N, max(pool_len, top_k, 2)) int64 */
 } apg_image_state;
 
 typedef struct apg_image_outputs {

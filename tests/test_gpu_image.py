@@ -54,8 +54,9 @@ def test_rng_fill_integers_matches_numpy(gpu, bound, n, pre):
         gen.integers(0, 5)
     st = torch.as_tensor(_state_from_numpy(gen), device=gpu)
     out = torch.zeros(n, dtype=torch.int64, device=gpu)
+    work = torch.zeros(max(1, N.lib().apg_rng_fill_work_elems(n, bound)), dtype=torch.int64, device=gpu)
     N.check(N.lib().apg_rng_fill(N.ptr(st), N.APG_DRAW_INTEGERS, n, 1, None, None, 3, bound, N.ptr(out),
-                                 N.stream_handle(gpu)))
+                                 N.ptr(work), N.stream_handle(gpu)))
     want = gen.integers(3, 3 + bound, n)
     assert np.array_equal(out.cpu().numpy(), want)
     assert _state_equal(st.cpu().numpy(), gen)
@@ -75,7 +76,7 @@ def test_rng_fill_uniform_matches_numpy(gpu, n, cols):
     out = torch.zeros((n, cols), dtype=torch.float64, device=gpu)
     lo_c = (ctypes.c_double * cols)(*low.tolist())
     rg_c = (ctypes.c_double * cols)(*(high - low).tolist())
-    N.check(N.lib().apg_rng_fill(N.ptr(st), N.APG_DRAW_UNIFORM, n, cols, lo_c, rg_c, 0, 0, N.ptr(out),
+    N.check(N.lib().apg_rng_fill(N.ptr(st), N.APG_DRAW_UNIFORM, n, cols, lo_c, rg_c, 0, 0, N.ptr(out), None,
                                  N.stream_handle(gpu)))
     want = gen.uniform(low, high, (n, cols))
     assert np.array_equal(out.cpu().numpy(), want)
