@@ -71,7 +71,8 @@ class LidarSizes(ctypes.Structure):
 class ImageConfig(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in ("num_envs", "kind", "height", "width", "pool_channels", "channels",
                                               "pool_dtype", "sensor_h", "sensor_w", "step_limit", "num_classes",
-                                              "invert_labels", "top_k", "unique_points")] + [
+                                              "invert_labels", "top_k", "unique_points", "num_envs_total",
+                                              "env_offset")] + [
         ("pool_len", ctypes.c_int64), ("sensor_scale", ctypes.c_double), ("max_step", ctypes.c_double * 2),
         ("cell", ctypes.c_double * 2), ("ce_scale", ctypes.c_double), ("ce_offset", ctypes.c_double),
         ("mse_scale", ctypes.c_float), ("mse_offset", ctypes.c_float)]

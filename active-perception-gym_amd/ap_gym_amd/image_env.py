@@ -85,7 +85,7 @@ class _ImageVectorEnv:
 
     def __init__(self, num_envs: int, image_perception_config: ImagePerceptionConfig,
                  render_mode: str = "rgb_array", device=None, copy: bool = False, strict_errors: bool = False,
-                 array_backend: str = "numpy"):
+                 array_backend: str = "numpy", num_envs_total: int | None = None, env_offset: int = 0):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -95,6 +95,12 @@ class _ImageVectorEnv:
         cfg = image_perception_config
         self.config = cfg
         self.num_envs = n = int(num_envs)
+        # sharding (ap_gym_amd.sharding): this env is envs [env_offset, env_offset + num_envs) of a batch
+        # of num_envs_total; every rank draws the whole batch from the same streams and keeps its slice
+        self.num_envs_total = nt = int(num_envs_total) if num_envs_total is not None else n
+        self.env_offset = int(env_offset)
+        if self.env_offset < 0 or self.env_offset + n > nt:
+            raise ValueError("the shard [env_offset, env_offset + num_envs) must lie inside num_envs_total")
         self.render_mode = render_mode
         self.copy, self.strict_errors, self.array_backend = copy, strict_errors, array_backend
         self.device = torch.device(device if device is not None else "cuda")
@@ -154,21 +160,23 @@ class _ImageVectorEnv:
             num_envs=n, kind=self.kind, height=h, width=w, pool_channels=pc, channels=c,
             pool_dtype=N.APG_POOL_U8 if pool.dtype == np.uint8 else N.APG_POOL_F32, sensor_h=s0, sensor_w=s1,
             step_limit=int(cfg.step_limit), num_classes=k, invert_labels=int(bool(cfg.randomly_invert_labels)),
-            top_k=int(cfg.unique_sampling_top_k), unique_points=int(grid.shape[0]), pool_len=m,
+            top_k=int(cfg.unique_sampling_top_k), unique_points=int(grid.shape[0]), num_envs_total=nt,
+            env_offset=self.env_offset, pool_len=m,
             sensor_scale=float(cfg.sensor_scale), max_step=(ctypes.c_double * 2)(*msl.tolist()),
             cell=(ctypes.c_double * 2)(*cell.tolist()), ce_scale=ce_scale, ce_offset=ce_offset,
             mse_scale=mse_scale, mse_offset=mse_offset)
 
         t, dev = torch, self.device
         gshape = (n, s0, s1, c)
-        work = max(N.lib().apg_rng_fill_work_elems(n, b) for b in (m, int(cfg.unique_sampling_top_k), 2))
+        work = max(N.lib().apg_rng_fill_work_elems(nt, b) for b in (m, int(cfg.unique_sampling_top_k), 2))
         self._t = T = dict(
             pool=t.from_numpy(pool).to(dev), pool_labels=t.from_numpy(labels).to(dev),
             unique_grid=t.from_numpy(grid).to(dev),
             index=t.zeros(n, dtype=t.int64, device=dev), label=t.zeros(n, dtype=t.int32, device=dev),
             inverted=t.zeros(n, dtype=t.int32, device=dev), pos=t.zeros((n, 2), dtype=t.float64, device=dev),
             target=t.zeros((n, 2), dtype=t.float32, device=dev), rng=t.zeros((3, 5), dtype=t.int64, device=dev),
-            scratch_i64=t.zeros(n, dtype=t.int64, device=dev), scratch_f64=t.zeros(2 * n, dtype=t.float64, device=dev),
+            scratch_i64=t.zeros(2 * nt, dtype=t.int64, device=dev),
+            scratch_f64=t.zeros(2 * nt, dtype=t.float64, device=dev),
             top_k=t.zeros((n, int(cfg.unique_sampling_top_k)), dtype=t.int32, device=dev),
             rng_work=t.zeros(work, dtype=t.int64, device=dev),
             glimpse=t.zeros(gshape, dtype=t.float32, device=dev),

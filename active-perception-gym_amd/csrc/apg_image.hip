@@ -323,17 +323,24 @@ __global__ void k_image_seed(apg_pcg64 *rng, uint64_t seed) {
 }
 
 // ------------------------------------------------------------------ k_image_gather
-__global__ void k_image_gather(int n, const int32_t *pool_labels, const int64_t *index, int invert,
-                               const int64_t *inv_draw, int num_classes, int32_t *label, int32_t *inverted) {
+// This shard's slice of the batch draws: data point index, label (+ inversion), start position.
+__global__ void k_image_gather(int n, int offset, const int32_t *pool_labels, const int64_t *idx_draw,
+                               int invert, const int64_t *inv_draw, const double *pos_draw, int num_classes,
+                               int64_t *index, int32_t *label, int32_t *inverted, double *pos) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
-  int32_t l = pool_labels[index[e]];
+  const int d = offset + e;
+  const int64_t idx = idx_draw[d];
+  index[e] = idx;
+  int32_t l = pool_labels[idx];
   if (invert) {
-    const int32_t inv = inv_draw[e] == 1 ? 1 : 0;  // integers(0, 2, N) == 1
+    const int32_t inv = inv_draw[d] == 1 ? 1 : 0;  // integers(0, 2, N) == 1
     inverted[e] = inv;
     if (inv) l = num_classes - l - 1;
   }
   label[e] = l;
+  pos[2 * e] = pos_draw[2 * d];
+  pos[2 * e + 1] = pos_draw[2 * d + 1];
 }
 
 // ------------------------------------------------------------------ k_glimpse
@@ -616,25 +623,26 @@ __global__ __launch_bounds__(UNIQ_THREADS) void k_unique(GlimpseGeo g, const voi
 }
 
 // target = clip(grid[top_k[sel]] + jitter, -1, 1).astype(float32)  (:281-292, image_localization.py:139-143)
-__global__ void k_unique_finish(int n, int k, const int32_t *top_k, const int64_t *sel, const double *grid,
-                                const double *jitter, float *target) {
+__global__ void k_unique_finish(int n, int offset, int k, const int32_t *top_k, const int64_t *sel,
+                                const double *grid, const double *jitter, float *target) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
-  const int p = top_k[(size_t)e * k + sel[e]];
+  const int d = offset + e;
+  const int p = top_k[(size_t)e * k + sel[d]];
   for (int c = 0; c < 2; c++) {
-    double v = __dadd_rn(grid[2 * p + c], jitter[2 * e + c]);
+    double v = __dadd_rn(grid[2 * p + c], jitter[2 * d + c]);
     v = v < -1.0 ? -1.0 : (v > 1.0 ? 1.0 : v);
     target[2 * e + c] = (float)v;
   }
 }
 
 // target[prev_done] = np_random.uniform(-1, 1, (k, 2)).astype(float32); out_prev = pre-update copy
-__global__ void k_loc_target(int n, int refresh, const double *draw, float *target, float *out_prev) {
+__global__ void k_loc_target(int n, int offset, int refresh, const double *draw, float *target, float *out_prev) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   for (int c = 0; c < 2; c++) {
     out_prev[2 * e + c] = target[2 * e + c];
-    if (refresh) target[2 * e + c] = (float)draw[2 * e + c];
+    if (refresh) target[2 * e + c] = (float)draw[2 * (offset + e) + c];
   }
 }
 
@@ -686,6 +694,8 @@ int validate(const apg_image_config *c) {
   if (c->kind == APG_IMAGE_CLASSIFY && (c->num_classes <= 0 || c->num_classes > MAX_PW_N))
     return fail(APG_E_INVALID, "num_classes out of range");
   if (c->kind != APG_IMAGE_CLASSIFY && c->kind != APG_IMAGE_LOCALIZE) return fail(APG_E_INVALID, "unknown image env kind");
+  if (c->env_offset < 0 || (int64_t)c->env_offset + c->num_envs > c->num_envs_total)
+    return fail(APG_E_INVALID, "shard [env_offset, env_offset + num_envs) must lie inside num_envs_total");
   return APG_OK;
 }
 
@@ -806,18 +816,20 @@ int apg_image_seed(const apg_image_config *cfg, const apg_image_state *st, uint6
 
 static int module_reset(const apg_image_config *c, const apg_image_state *st, const apg_image_outputs *out,
                         hipStream_t s) {
-  const int n = c->num_envs;
+  const int n = c->num_envs, nt = c->num_envs_total;
+  int64_t *idx_draw = st->scratch_i64, *inv_draw = st->scratch_i64 + nt;
   int rc;
   // next(DatasetBatchIterator): integers(0, len(dataset), N)
-  if ((rc = launch_integers(st->rng + 2, n, 0, (uint64_t)c->pool_len, st->index, st->rng_work, s))) return rc;
+  if ((rc = launch_integers(st->rng + 2, nt, 0, (uint64_t)c->pool_len, idx_draw, st->rng_work, s))) return rc;
   // randomly_invert_labels: current_rng.integers(0, 2, size=N) == 1
-  if (c->invert_labels && (rc = launch_integers(st->rng + 1, n, 0, 2, st->scratch_i64, st->rng_work, s))) return rc;
-  hipLaunchKernelGGL(k_image_gather, dim3(grid_for(n, 256)), dim3(256), 0, s, n, st->pool_labels, st->index,
-                     c->invert_labels, st->scratch_i64, c->num_classes, st->label, st->inverted);
-  if ((rc = check_launch("k_image_gather"))) return rc;
+  if (c->invert_labels && (rc = launch_integers(st->rng + 1, nt, 0, 2, inv_draw, st->rng_work, s))) return rc;
   // current_rng.uniform(-1, 1, size=(N, 2))
   const double low[2] = {-1.0, -1.0}, range[2] = {2.0, 2.0};
-  return launch_uniform(st->rng + 1, n, 2, low, range, st->pos, s);
+  if ((rc = launch_uniform(st->rng + 1, nt, 2, low, range, st->scratch_f64, s))) return rc;
+  hipLaunchKernelGGL(k_image_gather, dim3(grid_for(n, 256)), dim3(256), 0, s, n, c->env_offset, st->pool_labels,
+                     idx_draw, c->invert_labels, inv_draw, st->scratch_f64, c->num_classes, st->index, st->label,
+                     st->inverted, st->pos);
+  return check_launch("k_image_gather");
 }
 
 static int observe(const apg_image_config *c, const apg_image_state *st, const apg_image_outputs *out, hipStream_t s,
@@ -842,12 +854,13 @@ int apg_image_reset(const apg_image_config *c, const apg_image_state *st, const 
     if ((rc = launch_unique(g, st->pool, st->index, st->unique_grid, n, c->unique_points, c->top_k, st->top_k,
                             nullptr, s)))
       return rc;
-    if ((rc = launch_integers(st->rng + 1, n, 0, (uint64_t)c->top_k, st->scratch_i64, st->rng_work, s))) return rc;
+    const int nt = c->num_envs_total;
+    if ((rc = launch_integers(st->rng + 1, nt, 0, (uint64_t)c->top_k, st->scratch_i64, st->rng_work, s))) return rc;
     const double low[2] = {-c->cell[0], -c->cell[1]};
     const double range[2] = {c->cell[0] - -c->cell[0], c->cell[1] - -c->cell[1]};
-    if ((rc = launch_uniform(st->rng + 1, n, 2, low, range, st->scratch_f64, s))) return rc;
-    hipLaunchKernelGGL(k_unique_finish, dim3(grid_for(n, 256)), dim3(256), 0, s, n, c->top_k, st->top_k,
-                       st->scratch_i64, st->unique_grid, st->scratch_f64, st->target);
+    if ((rc = launch_uniform(st->rng + 1, nt, 2, low, range, st->scratch_f64, s))) return rc;
+    hipLaunchKernelGGL(k_unique_finish, dim3(grid_for(n, 256)), dim3(256), 0, s, n, c->env_offset, c->top_k,
+                       st->top_k, st->scratch_i64, st->unique_grid, st->scratch_f64, st->target);
     if ((rc = check_launch("k_unique_finish"))) return rc;
   }
   // obs: glimpse, glimpse_pos, time_step (= (0 / limit) * 2 - 1 = -1)
@@ -869,10 +882,10 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
     // prediction_target = target.copy(); target[prev_done] = np_random.uniform(-1, 1, (k, 2)) as f32
     if (prev_done) {
       const double low[2] = {-1.0, -1.0}, range[2] = {2.0, 2.0};
-      if ((rc = launch_uniform(st->rng + 0, n, 2, low, range, st->scratch_f64, s))) return rc;
+      if ((rc = launch_uniform(st->rng + 0, c->num_envs_total, 2, low, range, st->scratch_f64, s))) return rc;
     }
-    hipLaunchKernelGGL(k_loc_target, dim3(grid_for(n, 256)), dim3(256), 0, s, n, prev_done, st->scratch_f64,
-                       st->target, out->target);
+    hipLaunchKernelGGL(k_loc_target, dim3(grid_for(n, 256)), dim3(256), 0, s, n, c->env_offset, prev_done,
+                       st->scratch_f64, st->target, out->target);
     if ((rc = check_launch("k_loc_target"))) return rc;
   }
   if (prev_done && (rc = module_reset(c, st, out, s))) return rc;

@@ -195,6 +195,8 @@ typedef struct apg_image_config {
   int32_t invert_labels;      /* randomly_invert_labels */
   int32_t top_k;              /* unique_sampling_top_k */
   int32_t unique_points;      /* P: sampling grid points of sample_unique_glimpse_positions */
+  int32_t num_envs_total;     /* envs of the whole (sharded) batch: every vector-level draw has this size */
+  int32_t env_offset;         /* first env of this shard: the shard uses draws [offset, offset + num_envs) */
   int64_t pool_len;           /* len(dataset) */
   double sensor_scale;
   double max_step[2];         /* max_step_length broadcast to (2,) */
@@ -213,8 +215,8 @@ typedef struct apg_image_state {
   double *pos;                /* [N][2] sensor position, normalized (float64 like the reference) */
   float *target;              /* [N][2] localization target */
   apg_pcg64 *rng;             /* [3] env np_random, module current_rng, DatasetBatchIterator rng */
-  int64_t *scratch_i64;       /* [N] */
-  double *scratch_f64;        /* [2N] */
+  int64_t *scratch_i64;       /* [2][N_total] batch draws */
+  double *scratch_f64;        /* [N_total][2] batch draws */
   int32_t *top_k;             /* [N][top_k] unique-sampling ranking (localize) */
   int64_t *rng_work;          /* apg_rng_fill_work_elems(N, max(pool_len, top_k, 2)) int64 */
 } apg_image_state;

@@ -98,7 +98,7 @@ def _cfg(N, n, kind, h, w, pc, c, sensor, scale, dtype, pool_len, k=10, top_k=10
     return N.ImageConfig(num_envs=n, kind=kind, height=h, width=w, pool_channels=pc, channels=c,
                          pool_dtype=N.APG_POOL_U8 if dtype == np.uint8 else N.APG_POOL_F32, sensor_h=sensor[0],
                          sensor_w=sensor[1], step_limit=16, num_classes=k, invert_labels=0, top_k=top_k,
-                         unique_points=points, pool_len=pool_len, sensor_scale=scale,
+                         unique_points=points, num_envs_total=n, env_offset=0, pool_len=pool_len, sensor_scale=scale,
                          max_step=(ctypes.c_double * 2)(0.2, 0.2), cell=(ctypes.c_double * 2)(*cell), ce_scale=1.0,
                          ce_offset=0.0, mse_scale=1.0, mse_offset=0.0)
 
@@ -334,6 +334,37 @@ def test_image_env_torch_backend_matches_numpy(gpu, kind):
         assert np.array_equal(r1[2], r2[2].cpu().numpy())
         assert np.array_equal(r1[4]["prediction"]["loss"], r2[4]["prediction"]["loss"].cpu().numpy())
     e_t.check_errors()
+
+
+@pytest.mark.parametrize("kind", ["cls", "loc"])
+def test_image_env_shards_equal_unsharded(gpu, kind):
+    """Each shard draws the whole batch from the same streams and keeps its slice (ap_gym_amd.sharding)."""
+    import ap_gym_amd as ap
+
+    g = golden("image_cls_gray3_rect.npz" if kind == "cls" else "image_loc_mnist.npz")
+    h, w, c, k, s0, s1, lim, inv, n, steps = (int(v) for v in g["config"])
+    ds = ap.ArrayImageClassificationDataset(g["pool"], g["labels"], k, c)
+    cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=(s0, s1), sensor_scale=float(g["sensor_scale"]),
+                                   step_limit=lim, randomly_invert_labels=bool(inv))
+    cls = ap.ImageClassificationVectorEnv if kind == "cls" else ap.ImageLocalizationVectorEnv
+    full = cls(n, cfg)
+    half = n // 2
+    shards = [cls(half, cfg, num_envs_total=n, env_offset=r * half) for r in range(2)]
+    outs = [e.reset(seed=3) for e in [full] + shards]
+    for key in outs[0][0]:
+        assert np.array_equal(outs[0][0][key], np.concatenate([outs[1][0][key], outs[2][0][key]])), key
+    for t in range(steps):
+        act = {"action": g["actions"][t], "prediction": g["predictions"][t]}
+        f = full.step(act)
+        parts = [e.step({kk: v[r * half:(r + 1) * half] for kk, v in act.items()}) for r, e in enumerate(shards)]
+        for key in f[0]:
+            assert np.array_equal(f[0][key], np.concatenate([p[0][key] for p in parts])), (t, key)
+        for i in (1, 2, 3):
+            assert np.array_equal(f[i], np.concatenate([p[i] for p in parts])), (t, i)
+        for key in ("index", "base_reward"):
+            assert np.array_equal(f[4][key], np.concatenate([p[4][key] for p in parts])), (t, key)
+        for key in ("target", "loss"):
+            assert np.array_equal(f[4]["prediction"][key], np.concatenate([p[4]["prediction"][key] for p in parts]))
 
 
 def test_image_env_nan_errors(gpu):
