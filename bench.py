@@ -13,6 +13,10 @@ scaling, each rank owns an independent env shard (seed offset rank*N), no data-p
 (--gather adds the optional RCCL all-gather of the step outputs and reports its time separately).
 
 Prints ONE JSON line on rank 0 (value = env-steps/s summed over all GPUs).
+
+`--workload mnist` / `--workload tinyimagenet-loc` measure the image glimpse path on BASELINE.json
+configs 4 and 5 instead (synthetic uint8 pools of the datasets' shapes; same JSON contract, the
+timed region is the whole device step between HIP events).
 """
 
 from __future__ import annotations
@@ -23,6 +27,8 @@ import json
 import os
 import sys
 import time
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "active-perception-gym_amd"))
@@ -86,12 +92,133 @@ def cpu_baseline(beams: int, size: int, num_envs: int, steps: int) -> dict:
                       f"({dt:.1f} s)"}
 
 
+# image workloads (BASELINE.json configs 4, 5): per-GPU envs, pool, classes, sensor, kind
+IMAGE_WORKLOADS = {
+    "mnist": dict(name="MNIST-v0 ImageClassificationVectorEnv", kind="cls", envs=65536, shape=(28, 28),
+                  pool=60000, classes=10, sensor=(5, 5)),
+    "tinyimagenet-loc": dict(name="TinyImageNetLoc-v0 ImageLocalizationVectorEnv", kind="loc", envs=32768,
+                             shape=(64, 64, 3), pool=100000, classes=200, sensor=(12, 12)),
+}
+
+
+def image_bytes_per_env_step(kind: str, k: int, g: tuple, c: int) -> int:
+    """Compulsory HBM bytes of one env-step of the image path: reads pos f64,
+    action, prediction, label/target, data-point index, the (G+1)^2 C u8 bilinear taps; writes the glimpse
+    (f32), glimpse_pos, pos, reward (f64), base_reward, loss, target, time_step."""
+    taps = (g[0] + 1) * (g[1] + 1) * c
+    glimpse = 4 * g[0] * g[1] * c
+    if kind == "cls":
+        return (16 + 8 + 4 * k + 4 + 8 + taps) + (glimpse + 8 + 16 + 8 + 4 + 8 + 4 + 4)
+    return (16 + 8 + 8 + 8 + 8 + taps) + (glimpse + 8 + 16 + 8 + 4 + 4 + 8 + 4)
+
+
+def image_cpu_baseline(w: dict, pool: np.ndarray, labels: np.ndarray, c: int, num_envs: int, steps: int) -> dict:
+    from oracle import image_oracle as io
+
+    env = io.ImageVectorEnvOracle(w["kind"], pool, labels, w["classes"], c, num_envs, w["sensor"])
+    env.reset(0)
+    rng = np.random.default_rng(1)
+    acts = rng.uniform(-1, 1, (steps, num_envs, 2)).astype(np.float32)
+    preds = (rng.standard_normal((steps, num_envs, w["classes"])) if w["kind"] == "cls"
+             else rng.uniform(-1, 1, (steps, num_envs, 2))).astype(np.float32)
+    t0 = time.perf_counter()
+    for t in range(steps):
+        env.step(acts[t], preds[t])
+    dt = time.perf_counter() - t0
+    return {"value": num_envs * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/image_oracle.py numpy port (1 thread), {w['name']}, {num_envs} envs x {steps} steps "
+                      f"after reset(seed=0) (reset untimed) incl. one autoreset ({dt:.1f} s)"}
+
+
+def run_image(args, world, rank, dev):
+    import torch
+    import torch.distributed as dist
+
+    import ap_gym_amd as apg
+
+    w = IMAGE_WORKLOADS[args.workload]
+    n_local = args.num_envs or w["envs"]
+    n_total = n_local * world
+    c = 1 if len(w["shape"]) == 2 else w["shape"][-1]
+    pool_len = args.pool_len or w["pool"]
+    ds = apg.SyntheticImageClassificationDataset(pool_len, w["shape"], w["classes"], c, seed=0)
+    cfg = apg.ImagePerceptionConfig(dataset=ds, sensor_size=w["sensor"], step_limit=16)
+    cls = apg.ImageClassificationVectorEnv if w["kind"] == "cls" else apg.ImageLocalizationVectorEnv
+    env = cls(n_local, cfg, device=dev, array_backend="torch", num_envs_total=n_total, env_offset=rank * n_local)
+    ring = 17
+    g = torch.Generator(device=dev).manual_seed(1 + rank)
+    acts = torch.rand((ring, n_local, 2), generator=g, device=dev) * 2 - 1
+    if w["kind"] == "cls":
+        preds = torch.randn((ring, n_local, w["classes"]), generator=g, device=dev)
+    else:
+        preds = torch.rand((ring, n_local, 2), generator=g, device=dev) * 2 - 1
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    env.reset(seed=0)
+    torch.cuda.synchronize(dev)
+    reset_ms = (time.perf_counter() - t0) * 1e3
+    for t in range(args.warmup):
+        env.step({"action": acts[t % ring], "prediction": preds[t % ring]})
+    ev = HipEvents(args.steps)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    ev.hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for t in range(args.steps):
+        b, e = ev.pair(t)
+        k = (args.warmup + t) % ring
+        ev.hip.hipEventRecord(b, stream)
+        env.step({"action": acts[k], "prediction": preds[k]})
+        ev.hip.hipEventRecord(e, stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    env.check_errors()
+    step_ms = sum(ev.elapsed_ms(i) for i in range(args.steps)) / args.steps
+    ev.close()
+    if world > 1:
+        tt = torch.tensor([elapsed, step_ms, reset_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, step_ms, reset_ms = (float(x) for x in tt)
+    if rank == 0:
+        bpe = image_bytes_per_env_step(w["kind"], w["classes"], w["sensor"], c)
+        achieved = bpe * n_local / (step_ms * 1e-3) / 1e9
+        out = {
+            "metric": "env-steps/sec (vectorized step) at 1/2/4/8 MI355X + achieved HBM GB/s",
+            "value": n_total * args.steps / elapsed, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64 bilinear / f32 outputs",
+            "data": f"synthetic uint8 pool {pool_len}x{'x'.join(map(str, w['shape']))} (default_rng(0)); "
+                    "uniform actions, normal logits / uniform predictions generated on device",
+            "config": {"workload": w["name"], "num_envs_per_gpu": n_local, "num_envs_total": n_total,
+                       "sensor": list(w["sensor"]), "classes": w["classes"], "step_limit": 16,
+                       "reset_ms": reset_ms, "parallelism": f"env-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "image step (all kernels, HIP events around env.step)", "kernel_ms": step_ms,
+                         "bytes_per_launch": bpe * n_local},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            pool, labels = ds.device_pool()
+            n_cpu, s_cpu = (65536, 170) if w["kind"] == "cls" else (256, 2040)  # about 10 s of CPU work each
+            out["cpu_baseline"] = image_cpu_baseline(w, pool, labels, c, n_cpu, s_cpu)
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=505)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--num-envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--workload", default="lidar", choices=["lidar", *IMAGE_WORKLOADS])
+    ap.add_argument("--num-envs", type=int, default=None, help="envs per GPU (default: the workload's)")
+    ap.add_argument("--pool-len", type=int, default=None, help="image pool size (image workloads)")
     ap.add_argument("--beams", type=int, default=32)
     ap.add_argument("--map-size", type=int, default=64)
     ap.add_argument("--gather", action="store_true", help="all-gather step outputs across ranks (RCCL)")
@@ -116,8 +243,10 @@ def main():
     dev = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    if args.workload != "lidar":
+        return run_image(args, world, rank, dev)
 
-    n_local = args.num_envs
+    n_local = args.num_envs or 65536
     n_total = n_local * world
 
     def make_local(num_envs, env_offset):
