@@ -149,14 +149,33 @@ APG_DEV int generate_one(const Geo &g, Pcg64 &r, uint64_t *occ, uint16_t *stack,
   else return rooms_generate(r, occ, g.wpr, g.h, g.max_rooms, g.door_width, bt);
 }
 
+// Rooms maps are painted into the lane's LDS bitmap (row words are read-modify-written once per
+// primitive), then the wave copies its bitmaps out with coalesced stores.
+APG_DEV void copy_out_maps(const uint64_t *s_maps, unsigned long long done, size_t words, uint64_t *dst, int lane) {
+  while (done) {
+    const int j = __ffsll((long long)done) - 1;
+    done &= done - 1ULL;
+    for (size_t k = lane; k < words; k += 64) dst[(size_t)j * words + k] = s_maps[(size_t)j * words + k];
+  }
+}
+
 template <int GEN>
 __global__ __launch_bounds__(64) void k_map_generate(Geo g, const uint64_t *idx, int n, uint64_t *occ,
                                                      uint16_t *stack, uint32_t *err, BinomTable bt, int lanes) {
-  const int i = blockIdx.x * lanes + threadIdx.x;
-  if ((int)threadIdx.x >= lanes || i >= n) return;
-  Pcg64 r = seed_pcg64(idx[i]);
-  const int rc = generate_one<GEN>(g, r, occ + (size_t)i * g.h * g.wpr,
-                                   stack ? stack + (size_t)i * g.frames : nullptr, bt);
+  extern __shared__ uint64_t s_rows[];  // rooms: [lanes][h * wpr]
+  const int lane = threadIdx.x;
+  const int i = blockIdx.x * lanes + lane;
+  const bool active = lane < lanes && i < n;
+  const size_t words = (size_t)g.h * g.wpr;
+  int rc = 0;
+  if (active) {
+    Pcg64 r = seed_pcg64(idx[i]);
+    if constexpr (GEN == GEN_ROOMS)
+      rc = rooms_generate(r, s_rows + lane * words, g.wpr, g.h, g.max_rooms, g.door_width, bt);
+    else
+      rc = generate_one<GEN>(g, r, occ + (size_t)i * words, stack ? stack + (size_t)i * g.frames : nullptr, bt);
+  }
+  if constexpr (GEN == GEN_ROOMS) copy_out_maps(s_rows, __ballot(active), words, occ + (size_t)blockIdx.x * lanes * words, lane);
   if (rc != 0 && err) atomicOr(err, APG_ERR_MAPGEN);
 }
 
@@ -170,13 +189,16 @@ template <int GEN>
 __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, uint64_t seed, int use_seed,
                                                     int all, uint64_t *out_map_idx, uint32_t *err, BinomTable bt,
                                                     int lanes) {
+  extern __shared__ uint64_t s_rows[];  // rooms: [lanes][h * wpr]
   const int lane = threadIdx.x;
   const int e = blockIdx.x * lanes + lane;
   const bool mine = lane < lanes && e < g.n;
   const uint8_t f = mine ? S.flags[e] : 0;
   const bool active = mine && (all || (f & F_AUTORESET));
-  if (!active) return;
-  {
+  const unsigned long long todo = __ballot(active);
+  if (todo == 0ULL) return;
+  const size_t words = (size_t)g.h * g.wpr;
+  if (active) {
     Pcg64 rng;
     Pcg64 it;
     if (use_seed) {
@@ -191,9 +213,16 @@ __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, ui
     if constexpr (GEN != GEN_NONE) {
       midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
       Pcg64 map_rng = seed_pcg64(midx);  // FloorMapDataset*.get_data_point: default_rng(idx)
-      uint64_t *own = S.occ + (size_t)e * g.h * g.wpr;
-      int rc = generate_one<GEN>(g, map_rng, own, S.stack + (size_t)e * g.frames, bt);
-      if (place_start(rng, own, g.h, g.w, g.wpr, px, py) != 0) rc = -6;
+      int rc;
+      if constexpr (GEN == GEN_ROOMS) {
+        uint64_t *own = s_rows + lane * words;
+        rc = rooms_generate(map_rng, own, g.wpr, g.h, g.max_rooms, g.door_width, bt);
+        if (place_start(rng, own, g.h, g.w, g.wpr, px, py) != 0) rc = -6;
+      } else {
+        uint64_t *own = S.occ + (size_t)e * words;
+        rc = generate_one<GEN>(g, map_rng, own, S.stack + (size_t)e * g.frames, bt);
+        if (place_start(rng, own, g.h, g.w, g.wpr, px, py) != 0) rc = -6;
+      }
       if (rc != 0) atomicOr(err, APG_ERR_MAPGEN);
       *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
       S.map_idx[e] = midx;
@@ -210,6 +239,7 @@ __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, ui
     *reinterpret_cast<Pcg64 *>(&S.rng[e]) = rng;
     if (out_map_idx) out_map_idx[e] = midx;
   }
+  if constexpr (GEN == GEN_ROOMS) copy_out_maps(s_rows, todo, words, S.occ + (size_t)blockIdx.x * lanes * words, lane);
 }
 
 struct StepParams {
@@ -500,11 +530,23 @@ int gen_lanes(int n) {
   return lanes;
 }
 
+// Dynamic LDS of a map-generation launch: rooms bitmaps [lanes][h * wpr] (opted in above 64 KiB).
+template <class K>
+int gen_lds(K kernel, int gen, const Geo &g, int lanes, size_t &dyn) {
+  dyn = gen == GEN_ROOMS ? (size_t)lanes * g.h * g.wpr * sizeof(uint64_t) : 0;
+  if (dyn > 64 * 1024 &&
+      hipFuncSetAttribute((const void *)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) != hipSuccess)
+    return fail(APG_E_LAUNCH, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+  return APG_OK;
+}
+
 template <int GEN>
 int launch_reset_gen(const Geo &g, const apg_lidar_state *st, uint64_t seed, int use_seed, int all,
                      const apg_lidar_outputs *out, hipStream_t s) {
   const int lanes = GEN == GEN_NONE ? 64 : gen_lanes(g.n);
-  hipLaunchKernelGGL(k_lidar_reset<GEN>, dim3(grid_for(g.n, lanes)), dim3(64), 0, s, g, *st, seed, use_seed, all,
+  size_t dyn;
+  if (int rc = gen_lds(k_lidar_reset<GEN>, GEN, g, lanes, dyn)) return rc;
+  hipLaunchKernelGGL(k_lidar_reset<GEN>, dim3(grid_for(g.n, lanes)), dim3(64), dyn, s, g, *st, seed, use_seed, all,
                      out->map_idx, out->err, make_binom_table(), lanes);
   return check_launch("k_lidar_reset");
 }
@@ -520,7 +562,9 @@ template <int GEN>
 int launch_map_generate(const Geo &g, const uint64_t *idx, int n, uint64_t *occ, uint16_t *stack, uint32_t *err,
                         hipStream_t s) {
   const int lanes = gen_lanes(n);
-  hipLaunchKernelGGL(k_map_generate<GEN>, dim3(grid_for(n, lanes)), dim3(64), 0, s, g, idx, n, occ, stack, err,
+  size_t dyn;
+  if (int rc = gen_lds(k_map_generate<GEN>, GEN, g, lanes, dyn)) return rc;
+  hipLaunchKernelGGL(k_map_generate<GEN>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, idx, n, occ, stack, err,
                      make_binom_table(), lanes);
   return check_launch("k_map_generate");
 }

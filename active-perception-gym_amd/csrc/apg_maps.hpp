@@ -178,24 +178,28 @@ APG_DEV uint64_t span_mask(int s, int l, int k) {
   return (n >= 64 ? ~0ULL : ((1ULL << n) - 1ULL)) << (lo - 64 * k);
 }
 
-// word k of map row y: border | walls & ~doors
-APG_DEV uint64_t rooms_row_word(const RoomsPrims &P, int m, int y, int k) {
-  uint64_t v = (y == 0 || y == m - 1) ? span_mask(0, m, k) : (span_mask(0, 1, k) | span_mask(m - 1, 1, k));
+// Paint rows [m][wpr] = border | walls & ~doors, one primitive at a time (each primitive is read
+// once; the row words are read-modify-written, so `rows` should be LDS: see k_lidar_reset).
+APG_DEV void rooms_paint(const RoomsPrims &P, int m, int wpr, uint64_t *rows) {
+  for (int y = 0; y < m; y++)
+    for (int k = 0; k < wpr; k++)
+      rows[y * wpr + k] = (y == 0 || y == m - 1) ? span_mask(0, m, k) : (span_mask(0, 1, k) | span_mask(m - 1, 1, k));
   for (int i = 0; i < P.nw; i++) {
     const uint32_t wl = P.wall[i];
     const int fixed = (int)((wl >> 16) & 255u), st = (int)((wl >> 8) & 255u), len = (int)(wl & 255u);
-    if (wl >> 31) {
-      if (y >= st && y < st + len) v |= span_mask(fixed, 1, k);
-    } else if (y == fixed) {
-      v |= span_mask(st, len, k);
+    if (wl >> 31) {  // vertical: column `fixed`, rows [st, st + len)
+      const uint64_t bit = 1ULL << (fixed & 63);
+      for (int y = st; y < st + len; y++) rows[y * wpr + (fixed >> 6)] |= bit;
+    } else {
+      for (int k = 0; k < wpr; k++) rows[fixed * wpr + k] |= span_mask(st, len, k);
     }
   }
   for (int i = 0; i < P.nd; i++) {
     const uint32_t d = P.door[i];
     const int r0 = (int)(d >> 24), c0 = (int)((d >> 16) & 255u), hh = (int)((d >> 8) & 255u), ww = (int)(d & 255u);
-    if (y >= r0 && y < r0 + hh) v &= ~span_mask(c0, ww, k);
+    for (int y = r0; y < r0 + hh; y++)
+      for (int k = 0; k < wpr; k++) rows[y * wpr + k] &= ~span_mask(c0, ww, k);
   }
-  return v;
 }
 
 // generate + paint: occ rows [m][wpr]
@@ -203,8 +207,7 @@ APG_DEV int rooms_generate(Pcg64 &r, uint64_t *occ, int wpr, int m, int max_room
                            const BinomTable &bt) {
   RoomsPrims P;
   const int rc = rooms_primitives(r, m, max_rooms, door_width, bt, P);
-  for (int y = 0; y < m; y++)
-    for (int k = 0; k < wpr; k++) occ[y * wpr + k] = rooms_row_word(P, m, y, k);
+  rooms_paint(P, m, wpr, occ);
   return rc;
 }
 
