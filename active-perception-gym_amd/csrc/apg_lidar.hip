@@ -292,16 +292,18 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
       m &= m - 1ULL;
       const uint64_t *rows = S.occ + (size_t)(base + j) * words;
       float *dst = O.map_obs + (size_t)(base + j) * cells;
-      if ((cells & 3) == 0) {
+      if ((P.w & 3) == 0) {  // 4 cells of one row per float4: one row-word load, non-temporal stores
+        const int q = P.w >> 2;
         for (int k4 = tid; k4 < cells / 4; k4 += STEP_THREADS) {
-          float4 v;
-          float *pv = reinterpret_cast<float *>(&v);
-#pragma unroll
-          for (int u = 0; u < 4; u++) {
-            const int k = 4 * k4 + u, y = k / P.w, x = k - y * P.w;
-            pv[u] = ((rows[y * P.wpr + (x >> 6)] >> (x & 63)) & 1ULL) ? wall : 0.0f;
-          }
-          reinterpret_cast<float4 *>(dst)[k4] = v;
+          const int y = k4 / q, x = (k4 - y * q) * 4;
+          const uint32_t b = (uint32_t)(rows[y * P.wpr + (x >> 6)] >> (x & 63));
+          typedef float f4 __attribute__((ext_vector_type(4)));
+          f4 v;
+          v.x = (b & 1u) ? wall : 0.0f;
+          v.y = (b & 2u) ? wall : 0.0f;
+          v.z = (b & 4u) ? wall : 0.0f;
+          v.w = (b & 8u) ? wall : 0.0f;
+          __builtin_nontemporal_store(v, reinterpret_cast<f4 *>(dst) + k4);
         }
       } else {
         for (int k = tid; k < cells; k += STEP_THREADS) {
