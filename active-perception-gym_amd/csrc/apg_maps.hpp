@@ -41,7 +41,7 @@ APG_DEV int64_t pyfloordiv(int64_t a, int64_t b) {
   return q;
 }
 
-// distribute_integers(n, k) (rooms.py:36-40) with k <= 16
+// distribute_integers(n, k) (rooms.py:36-40) with k <= 17
 APG_DEV void distribute_integers(Pcg64 &r, int64_t n, int k, int64_t *out) {
   int64_t cuts[16];
   const int64_t nz = k > n ? k - n : 0;
@@ -120,9 +120,9 @@ APG_DEV int rooms_primitives(Pcg64 &r, int m, int max_rooms, int door_width, con
     int64_t mrl = pyfloordiv(n0 - min_size, min_size + 1) + 1;
     if (mr < mrl) mrl = mr;
     if (mrl <= 1) continue;
-    if (mrl > 16) return -2;
+    if (mrl > 17) return -2;  // max_rooms <= 17 (binomial table: mrl - 2 <= 15)
     const int k = (int)binomial_inv(r, mrl - 2, bt) + 2;
-    int64_t cap[16], sizes[16], starts[16], ends[16];
+    int64_t cap[17], sizes[17], starts[17], ends[17];
     distribute_integers(r, mrl, k, cap);
     distribute_integers(r, n0 - (int64_t)k * (1 + min_size) + 1, k, sizes);
     int64_t acc = 0;

@@ -52,9 +52,9 @@ def _p(a):
     return None if a is None else a.ctypes.data
 
 
-def rooms_map(idx: int, size: int) -> np.ndarray:
+def rooms_map(idx: int, size: int, max_rooms: int = 10, door_width: int = 3) -> np.ndarray:
     out = np.zeros((size, size), np.uint8)
-    if lib().orc_rooms_map(idx, size, size, 10, 3, _p(out)) != 0:
+    if lib().orc_rooms_map(idx, size, size, max_rooms, door_width, _p(out)) != 0:
         raise ValueError("rooms map must be square")
     return out
 

@@ -74,6 +74,18 @@ def test_device_maps_match_oracle_random_idx(gpu, oracle_mod, kind, size, count)
         assert np.array_equal(got[i], m.astype(bool)), (kind, size, int(idx[i]))
 
 
+@pytest.mark.parametrize("size,max_rooms,door_width", [(128, 17, 3), (128, 10, 3), (96, 17, 2), (48, 6, 4)])
+def test_device_rooms_parameters_match_oracle(gpu, oracle_mod, size, max_rooms, door_width):
+    import ap_gym_amd as ap
+
+    idx = np.random.default_rng(size + max_rooms).integers(0, 2**32, 1024).astype(np.uint64)
+    got = ap.FloorMapDatasetRooms(size, size, max_rooms=max_rooms, door_width=door_width).get_data_point_batch(
+        idx, device=gpu)
+    for i in range(0, 1024, 8):
+        m = oracle_mod.rooms_map(int(idx[i]), size, max_rooms, door_width)
+        assert np.array_equal(got[i], m.astype(bool)), (size, max_rooms, int(idx[i]))
+
+
 def _scan_gpu(gpu, maps_bool, map_index, segs):
     import torch
 
