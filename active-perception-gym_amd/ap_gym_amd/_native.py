@@ -50,17 +50,18 @@ class LidarConfig(ctypes.Structure):
                 ("map_kind", ctypes.c_int32), ("is_static", ctypes.c_int32), ("static_map_index", ctypes.c_int32),
                 ("beams", ctypes.c_int32), ("step_limit", ctypes.c_int32), ("max_rooms", ctypes.c_int32),
                 ("door_width", ctypes.c_int32), ("lidar_range", ctypes.c_float), ("loss_scale", ctypes.c_float),
-                ("loss_offset", ctypes.c_float), ("branching_prob", ctypes.c_double)]
+                ("loss_offset", ctypes.c_float), ("branching_prob", ctypes.c_double), ("log_stats", ctypes.c_int32)]
 
 
 class LidarState(ctypes.Structure):
     _fields_ = [(n, _vp) for n in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng", "occ", "scratch", "stack",
-                                   "map_idx", "beam_dirs")]
+                                   "map_idx", "beam_dirs", "stats_hist")]
 
 
 class LidarOutputs(ctypes.Structure):
     _fields_ = [(n, _vp) for n in ("lidar", "odometry", "time_step", "map_obs", "reward", "terminated", "truncated",
-                                   "base_reward", "target", "loss", "info_mask", "map_idx", "reset_mask", "err")]
+                                   "base_reward", "target", "loss", "info_mask", "map_idx", "reset_mask", "err",
+                                   "stats", "stats_len")]
 
 
 class LidarSizes(ctypes.Structure):
@@ -75,17 +76,19 @@ class ImageConfig(ctypes.Structure):
                                               "env_offset")] + [
         ("pool_len", ctypes.c_int64), ("sensor_scale", ctypes.c_double), ("max_step", ctypes.c_double * 2),
         ("cell", ctypes.c_double * 2), ("ce_scale", ctypes.c_double), ("ce_offset", ctypes.c_double),
-        ("mse_scale", ctypes.c_float), ("mse_offset", ctypes.c_float)]
+        ("mse_scale", ctypes.c_float), ("mse_offset", ctypes.c_float), ("log_stats", ctypes.c_int32)]
 
 
 class ImageState(ctypes.Structure):
     _fields_ = [(n, _vp) for n in ("pool", "pool_labels", "unique_grid", "index", "label", "inverted", "pos",
-                                   "target", "rng", "scratch_i64", "scratch_f64", "top_k", "rng_work")]
+                                   "target", "rng", "scratch_i64", "scratch_f64", "top_k", "rng_work",
+                                   "stats_hist")]
 
 
 class ImageOutputs(ctypes.Structure):
     _fields_ = [(n, _vp) for n in ("glimpse", "glimpse_pos", "time_step", "target_glimpse", "reward", "base_reward",
-                                   "target", "label_target", "loss_f64", "loss_f32", "err")]
+                                   "target", "label_target", "loss_f64", "loss_f32", "err", "stats",
+                                   "stats_idx")]
 
 
 # (name, restype, argtypes) for every symbol declared in include/apgym_capi.h

@@ -85,7 +85,8 @@ class _ImageVectorEnv:
 
     def __init__(self, num_envs: int, image_perception_config: ImagePerceptionConfig,
                  render_mode: str = "rgb_array", device=None, copy: bool = False, strict_errors: bool = False,
-                 array_backend: str = "numpy", num_envs_total: int | None = None, env_offset: int = 0):
+                 array_backend: str = "numpy", num_envs_total: int | None = None, env_offset: int = 0,
+                 log_stats: bool = False):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -103,6 +104,9 @@ class _ImageVectorEnv:
             raise ValueError("the shard [env_offset, env_offset + num_envs) must lie inside num_envs_total")
         self.render_mode = render_mode
         self.copy, self.strict_errors, self.array_backend = copy, strict_errors, array_backend
+        # the registered ids wrap the env in ActiveClassificationVectorLogWrapper /
+        # ActiveRegressionVectorLogWrapper (registration.py:185-192, 263-269): info["stats"]
+        self.log_stats = bool(log_stats)
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise ValueError("the image envs run on a GPU device (no CPU fallback)")
@@ -164,7 +168,7 @@ class _ImageVectorEnv:
             env_offset=self.env_offset, pool_len=m,
             sensor_scale=float(cfg.sensor_scale), max_step=(ctypes.c_double * 2)(*msl.tolist()),
             cell=(ctypes.c_double * 2)(*cell.tolist()), ce_scale=ce_scale, ce_offset=ce_offset,
-            mse_scale=mse_scale, mse_offset=mse_offset)
+            mse_scale=mse_scale, mse_offset=mse_offset, log_stats=int(self.log_stats))
 
         t, dev = torch, self.device
         gshape = (n, s0, s1, c)
@@ -187,13 +191,17 @@ class _ImageVectorEnv:
             target_out=t.zeros((n, 2), dtype=t.float32, device=dev),
             label_target=t.zeros(n, dtype=t.int32, device=dev),
             loss_f64=t.zeros(n, dtype=t.float64, device=dev), loss_f32=t.zeros(n, dtype=t.float32, device=dev),
-            err=t.zeros(1, dtype=t.int32, device=dev))
+            err=t.zeros(1, dtype=t.int32, device=dev),
+            stats_hist=(t.zeros((n, 2, int(cfg.step_limit)), dtype=t.float32, device=dev) if self.log_stats
+                        else None),
+            stats=t.zeros((4, n), dtype=t.float32, device=dev) if self.log_stats else None,
+            stats_idx=t.zeros((2, n), dtype=t.int32, device=dev) if self.log_stats else None)
         self._state = N.ImageState(*[N.ptr(T[k_]) for k_ in ("pool", "pool_labels", "unique_grid", "index", "label",
                                                               "inverted", "pos", "target", "rng", "scratch_i64",
-                                                              "scratch_f64", "top_k", "rng_work")])
+                                                              "scratch_f64", "top_k", "rng_work", "stats_hist")])
         self._out = N.ImageOutputs(*[N.ptr(T[k_]) for k_ in ("glimpse", "glimpse_pos", "time_step", "target_glimpse",
                                                               "reward", "base_reward", "target_out", "label_target",
-                                                              "loss_f64", "loss_f32", "err")])
+                                                              "loss_f64", "loss_f32", "err", "stats", "stats_idx")])
         self._err_host = t.zeros(1, dtype=t.int32).pin_memory()
         self._err_event = t.cuda.Event()
         self._err_pending = False
@@ -203,6 +211,7 @@ class _ImageVectorEnv:
         self._t_step = 0
         self._prev_done = False
         self._done_consts = None
+        self._stats_view = None
 
     # ------------------------------------------------------------------ properties
     @property
@@ -389,7 +398,74 @@ class _ImageVectorEnv:
         base = np.zeros(n) if resetting else T["base_reward"].cpu().numpy()
         info = {"index": T["index"].cpu().numpy(), "base_reward": base,
                 "prediction": {"target": target, "loss": loss}}
+        if self.log_stats and terminated:
+            info["stats"] = self._numpy_stats()
         return obs, reward, np.full(n, terminated), np.zeros(n, dtype=np.bool_), info
+
+    def _metric_names(self):
+        if self.kind == N.APG_IMAGE_CLASSIFY:
+            return ("correct_label_prob", "accuracy")
+        return ("euclidean_distance", "mse")
+
+    def _numpy_stats(self):
+        """update_info_metrics_vec (util.py:40-80) as the vector log wrappers call it on the step that
+        ends every env's episode (image episodes end together)."""
+        T = self._t
+        n, lim = self.num_envs, int(self.config.step_limit)
+        done = np.ones(n, dtype=np.bool_)
+        st = T["stats"].cpu().numpy()
+        hist = T["stats_hist"].cpu().numpy()
+        names = self._metric_names()
+        scalar: dict[str, Any] = {}
+        for j, nm in enumerate(names):
+            scalar[f"final_{nm}"] = st[j].copy()
+        for nm in names:
+            scalar[f"_final_{nm}"] = done
+        for j, nm in enumerate(names):
+            scalar[f"avg_{nm}"] = st[2 + j].copy()
+        for nm in names:
+            scalar[f"_avg_{nm}"] = done
+        vector: dict[str, Any] = {}
+        for j, nm in enumerate(names):
+            arr = np.empty(n, dtype=object)
+            for i in range(n):
+                arr[i] = list(hist[i, j, :lim])
+            vector[nm] = arr
+        for nm in names:
+            vector[f"_{nm}"] = done
+        if self.kind == N.APG_IMAGE_CLASSIFY:
+            idx = T["stats_idx"].cpu().numpy()
+            scalar.update(first_correct=idx[0].copy(), _first_correct=idx[0] >= 0,
+                          last_incorrect=idx[1].copy(), _last_incorrect=idx[1] >= 0)
+        return {"scalar": scalar, "_scalar": done, "vector": vector, "_vector": done}
+
+    def _torch_stats(self):
+        """Device form of info["stats"] (built once from persistent buffers): scalars [N] and the
+        per-step history [N, step_limit] of each metric as "vector"."""
+        if self._stats_view is None:
+            import torch
+
+            T = self._t
+            done = torch.ones(self.num_envs, dtype=torch.bool, device=self.device)
+            names = self._metric_names()
+            scalar, vector = {}, {}
+            for j, nm in enumerate(names):
+                scalar[f"final_{nm}"] = T["stats"][j]
+                scalar[f"_final_{nm}"] = done
+                scalar[f"avg_{nm}"] = T["stats"][2 + j]
+                scalar[f"_avg_{nm}"] = done
+                vector[nm] = T["stats_hist"][:, j]
+                vector[f"_{nm}"] = done
+            if self.kind == N.APG_IMAGE_CLASSIFY:
+                scalar.update(first_correct=T["stats_idx"][0], last_incorrect=T["stats_idx"][1])
+            self._stats_view = {"scalar": scalar, "_scalar": done, "vector": vector, "_vector": done}
+        if not self.copy:
+            return self._stats_view
+
+        def clone(d):
+            return {k: clone(v) if isinstance(v, dict) else v.clone() for k, v in d.items()}
+
+        return clone(self._stats_view)
 
     def _torch_step(self, resetting, terminated):
         import torch
@@ -408,6 +484,8 @@ class _ImageVectorEnv:
                                  torch.ones(n, dtype=torch.bool, device=self.device))
         term = self._c(self._done_consts[1 if terminated else 0])
         trunc = self._c(self._done_consts[0])
+        if self.log_stats and terminated:
+            info["stats"] = self._torch_stats()
         return self._torch_obs(), self._c(T["reward"]), term, trunc, info
 
     def render(self):

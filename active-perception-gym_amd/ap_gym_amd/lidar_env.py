@@ -11,7 +11,11 @@ HBM plus three kernels per step (include/apgym_capi.h):
   obs             {"lidar": f32[N,B], "odometry": f32[N,2], "map": f32[N,H,W,1] (dynamic maps),
                    "time_step": f32[N]}
   reward          float64 (SyncVectorEnv's reward array), base_reward - normalized MSE loss
-  info            {"base_reward", "prediction": {"target", "loss"}, "map_idx"} with `_key` masks
+  info            {"base_reward", "prediction": {"target", "loss"}, "map_idx"} with `_key` masks, and
+                  with log_stats=True (the registered ids, registration.py:348-355) the per-episode
+                  "stats" of ActiveRegressionLogWrapper (active_regression_env.py:131-159) for the
+                  envs whose episode ended: scalar avg_/final_ euclidean_distance and mse, vector
+                  lists of the per-step values
 
 Two I/O modes (constructor `array_backend`), inputs of either type are accepted:
   "numpy" (default) -> numpy out, host copies and host-side NaN checks, like the reference
@@ -44,6 +48,12 @@ def lidar_beam_directions(beams: int, lidar_range: float) -> np.ndarray:
     return np.ascontiguousarray(unscaled * lidar_range, dtype=np.float32)
 
 
+def torch_index(idx: np.ndarray, device):
+    import torch
+
+    return torch.as_tensor(idx, dtype=torch.int64, device=device)
+
+
 class LIDARLocalization2DVectorEnv:
     metadata = {"render_modes": ["rgb_array"], "render_fps": 4, "autoreset_mode": "NextStep"}
     ERROR_POLL_INTERVAL = 32
@@ -52,7 +62,7 @@ class LIDARLocalization2DVectorEnv:
                  static_map: bool = False, lidar_beam_count: int = 8, lidar_range: float = 5,
                  static_map_index: int = 0, prefetch: bool = True, prefetch_buffer_size: int = 128,
                  max_episode_steps: int = 100, device=None, env_offset: int = 0, copy: bool = False,
-                 strict_errors: bool = False, array_backend: str = "numpy"):
+                 strict_errors: bool = False, array_backend: str = "numpy", log_stats: bool = False):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -69,6 +79,7 @@ class LIDARLocalization2DVectorEnv:
         self.env_offset = int(env_offset)
         self.copy = copy
         self.strict_errors = strict_errors
+        self.log_stats = bool(log_stats)
         if array_backend not in ("numpy", "torch"):
             raise ValueError("array_backend must be 'numpy' or 'torch'")
         self.array_backend = array_backend
@@ -100,7 +111,7 @@ class LIDARLocalization2DVectorEnv:
                                   beams=self.lidar_beam_count, step_limit=self.max_episode_steps,
                                   max_rooms=p["max_rooms"], door_width=p["door_width"],
                                   lidar_range=float(np.float32(lidar_range)), loss_scale=scale, loss_offset=offset,
-                                  branching_prob=p["branching_prob"])
+                                  branching_prob=p["branching_prob"], log_stats=int(self.log_stats))
         L = N.lib()
         sizes = N.LidarSizes()
         N.check(L.apg_lidar_query_sizes(ctypes.byref(self._cfg), ctypes.byref(sizes)), "apg_lidar_query_sizes")
@@ -133,15 +144,21 @@ class LIDARLocalization2DVectorEnv:
             map_idx_out=t.zeros(n, dtype=t.int64, device=dev),
             reset_mask=t.zeros(n, dtype=t.bool, device=dev),
             err=t.zeros(1, dtype=t.int32, device=dev),
+            stats_hist=(t.zeros((n, 2, self.max_episode_steps), dtype=t.float32, device=dev) if self.log_stats
+                        else None),
+            stats=t.zeros((4, n), dtype=t.float32, device=dev) if self.log_stats else None,
+            stats_len=t.zeros(n, dtype=t.int32, device=dev) if self.log_stats else None,
         )
         T = self._t
         self._state = N.LidarState(*[N.ptr(T[k]) for k in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng",
-                                                            "occ", "scratch", "stack", "map_idx", "beam_dirs")])
+                                                            "occ", "scratch", "stack", "map_idx", "beam_dirs",
+                                                            "stats_hist")])
         self._out = N.LidarOutputs(N.ptr(T["lidar"]), N.ptr(T["odometry"]), N.ptr(T["time_step"]),
                                    N.ptr(T["map_obs"]), N.ptr(T["reward"]), N.ptr(T["terminated"]),
                                    N.ptr(T["truncated"]), N.ptr(T["base_reward"]), N.ptr(T["target"]),
                                    N.ptr(T["loss"]), N.ptr(T["info_mask"]), N.ptr(T["map_idx_out"]),
-                                   N.ptr(T["reset_mask"]), N.ptr(T["err"]))
+                                   N.ptr(T["reset_mask"]), N.ptr(T["err"]), N.ptr(T["stats"]),
+                                   N.ptr(T["stats_len"]))
         self._err_host = t.zeros(1, dtype=t.int32).pin_memory()
         self._err_event = t.cuda.Event()
         self._err_pending = False
@@ -149,6 +166,7 @@ class LIDARLocalization2DVectorEnv:
         self._seeded = False
         self._closed = False
         self._kernel_events = None
+        self._stats_view = None
         self._steps_since_poll = 0
         N.check(L.apg_lidar_init(ctypes.byref(self._cfg), ctypes.byref(self._state), self._stream()), "apg_lidar_init")
 
@@ -288,7 +306,61 @@ class LIDARLocalization2DVectorEnv:
                                "_loss": c(mask)},
                 "_prediction": c(mask),
                 "map_idx": c(T["map_idx_out"]), "_map_idx": c(T["reset_mask"])}
+        if self.log_stats:
+            info.update(self._torch_stats(c))
         return self._obs_out(), c(T["reward"]), c(T["terminated"]), c(T["truncated"]), info
+
+    # ------------------------------------------------------------------ episode statistics
+    STAT_NAMES = ("avg_euclidean_distance", "avg_mse", "final_euclidean_distance", "final_mse")
+
+    def _torch_stats(self, c):
+        """Device form of info["stats"]: scalars valid where `_stats` (= terminated: every episode of
+        these envs ends by termination, TimeLimit(issue_termination=True)); "vector" holds the
+        per-step history [N, max_episode_steps] of each metric with its valid length.  Built once
+        from persistent buffers (no per-step device work)."""
+        if self._stats_view is None:
+            T = self._t
+            done = T["terminated"]
+            scalar = {}
+            for j, name in enumerate(self.STAT_NAMES):
+                scalar[name] = T["stats"][j]
+                scalar["_" + name] = done
+            vector = {"euclidean_distance": T["stats_hist"][:, 0], "_euclidean_distance": done,
+                      "mse": T["stats_hist"][:, 1], "_mse": done, "length": T["stats_len"]}
+            self._stats_view = {"stats": {"scalar": scalar, "_scalar": done, "vector": vector, "_vector": done},
+                                "_stats": done}
+        if not self.copy:
+            return self._stats_view
+
+        def clone(d):
+            return {k: clone(v) if isinstance(v, dict) else v.clone() for k, v in d.items()}
+
+        return clone(self._stats_view)
+
+    def _numpy_stats(self, info: dict):
+        """SyncVectorEnv's merge of the sub-envs' ActiveRegressionLogWrapper stats (util.py:18-37):
+        python-float scalars -> float64 arrays, lists -> object arrays, `_key` masks."""
+        T = self._t
+        lens = T["stats_len"].cpu().numpy()
+        done = lens > 0
+        if not done.any():
+            return
+        st = T["stats"].cpu().numpy()
+        idx = np.nonzero(done)[0]
+        hist = T["stats_hist"][torch_index(idx, self.device)].cpu().numpy()
+        scalar: dict[str, Any] = {}
+        for j, name in enumerate(self.STAT_NAMES):
+            scalar[name] = np.where(done, st[j].astype(np.float64), 0.0)
+            scalar["_" + name] = done.copy()
+        vector: dict[str, Any] = {}
+        for m, name in enumerate(("euclidean_distance", "mse")):
+            arr = np.full(self.num_envs, None, dtype=object)
+            for row, i in enumerate(idx):
+                arr[i] = list(hist[row, m, :lens[i]])
+            vector[name] = arr
+            vector["_" + name] = done.copy()
+        info["stats"] = {"scalar": scalar, "_scalar": done.copy(), "vector": vector, "_vector": done.copy()}
+        info["_stats"] = done.copy()
 
     # ------------------------------------------------------------------ output assembly
     def _obs_out(self):
@@ -330,6 +402,8 @@ class LIDARLocalization2DVectorEnv:
             loss = np.where(mask, T["loss"].cpu().numpy(), np.float32(0))
             info["prediction"] = {"target": tgt, "_target": mask.copy(), "loss": loss, "_loss": mask.copy()}
             info["_prediction"] = mask.copy()
+        if self.log_stats:
+            self._numpy_stats(info)
         reset_mask = T["reset_mask"].cpu().numpy()
         if reset_mask.any():
             info["map_idx"] = np.where(reset_mask, T["map_idx_out"].cpu().numpy(), 0).astype(np.int64)

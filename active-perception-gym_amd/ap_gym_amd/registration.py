@@ -49,6 +49,7 @@ def _image(kind: str):
                 dataset = dataset_factory()
             image_perception_config = ImagePerceptionConfig(dataset=dataset, **(config_kwargs or {}))
         cls = ImageClassificationVectorEnv if kind == "cls" else ImageLocalizationVectorEnv
+        kwargs.setdefault("log_stats", True)  # the vector log wrapper of the registered ids
         return cls(num_envs, image_perception_config, **kwargs)
 
     return entry
@@ -79,7 +80,9 @@ def register_envs():
                              ("LIDARLocMaze-v0", FloorMapDatasetMaze, False),
                              ("LIDARLocRoomsStatic-v0", FloorMapDatasetRooms, True),
                              ("LIDARLocRooms-v0", FloorMapDatasetRooms, False)):
-        register(name, _lidar, kwargs=dict(dataset_factory=ds, static_map=static), max_episode_steps=100)
+        # TimeLimit + ActiveRegressionLogWrapper (registration.py:348-355): episode stats on
+        register(name, _lidar, kwargs=dict(dataset_factory=ds, static_map=static, log_stats=True),
+                 max_episode_steps=100)
     render_kw = dict(render_unvisited_opacity=0.5, render_visited_opacity=0.25)
     _register_image_ids("cls", "MNIST", lambda split: _hf("mnist", split, channels=1), dict(step_limit=16))
     _register_image_ids("cls", "CIFAR10", lambda split: _hf("cifar10", split, image_feature_name="img"),

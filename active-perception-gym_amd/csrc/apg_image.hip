@@ -22,53 +22,12 @@
 
 #include "../../include/apgym_capi.h"
 #include "apg_host.hpp"
+#include "apg_pairwise.hpp"
 #include "apg_rng.hpp"
 
 using namespace apg;
 
 namespace {
-
-// ------------------------------------------------------------------ numpy pairwise summation
-// numpy loops_utils.h.src pairwise_sum (PW_BLOCKSIZE 128) over n values x(i), f32 accumulators.
-// The leaf is kept out of line: the recursion below expands into one call per leaf.
-template <class F>
-__device__ __noinline__ float pw_leaf(const F &x, int off, int n) {
-  if (n < 8) {
-    float r = 0.0f;
-    for (int i = 0; i < n; i++) r = __fadd_rn(r, x(off + i));
-    return r;
-  }
-  float r0 = x(off), r1 = x(off + 1), r2 = x(off + 2), r3 = x(off + 3);
-  float r4 = x(off + 4), r5 = x(off + 5), r6 = x(off + 6), r7 = x(off + 7);
-  int i = 8;
-  for (; i < n - (n % 8); i += 8) {
-    r0 = __fadd_rn(r0, x(off + i));
-    r1 = __fadd_rn(r1, x(off + i + 1));
-    r2 = __fadd_rn(r2, x(off + i + 2));
-    r3 = __fadd_rn(r3, x(off + i + 3));
-    r4 = __fadd_rn(r4, x(off + i + 4));
-    r5 = __fadd_rn(r5, x(off + i + 5));
-    r6 = __fadd_rn(r6, x(off + i + 6));
-    r7 = __fadd_rn(r7, x(off + i + 7));
-  }
-  float res = __fadd_rn(__fadd_rn(__fadd_rn(r0, r1), __fadd_rn(r2, r3)), __fadd_rn(__fadd_rn(r4, r5), __fadd_rn(r6, r7)));
-  for (; i < n; i++) res = __fadd_rn(res, x(off + i));
-  return res;
-}
-
-template <int DEPTH, class F>
-APG_DEV float pw_sum(const F &x, int off, int n) {
-  if constexpr (DEPTH == 0) {
-    return pw_leaf(x, off, n);  // callers keep n <= 128 << MAX_PW_DEPTH
-  } else {
-    if (n <= 128) return pw_leaf(x, off, n);
-    int n2 = n / 2;
-    n2 -= n2 % 8;
-    return __fadd_rn(pw_sum<DEPTH - 1>(x, off, n2), pw_sum<DEPTH - 1>(x, off + n2, n - n2));
-  }
-}
-constexpr int MAX_PW_DEPTH = 7;  // n <= 128 * 2^7 = 16384 summands
-constexpr int MAX_PW_N = 128 << MAX_PW_DEPTH;
 
 // ------------------------------------------------------------------ geometry of a glimpse
 struct GlimpseGeo {
@@ -364,7 +323,7 @@ __global__ __launch_bounds__(256) void k_glimpse(GlimpseGeo g, const void *pool,
 
 // ------------------------------------------------------------------ k_image_env
 struct EnvArgs {
-  int n, kind, k, resetting;
+  int n, kind, k, resetting, log_stats, limit, t_new;
   double msl[2];
   double ce_scale, ce_offset;
   float mse_scale, mse_offset;
@@ -385,6 +344,49 @@ APG_DEV float ce_f32(const float *row, int k, int target) {
   const float s = pw_sum<MAX_PW_DEPTH>(ex, 0, k);
   const float out = __fsub_rn(__fsub_rn(row[target], m), logf(s));
   return -out;
+}
+
+// Vector log wrappers of the registered ids (active_classification_env.py:116-197,
+// active_regression_env.py:160-227, util.py:40-80): the per-step metric of the episode is recorded
+// at index t - 1 (the autoreset step clears the wrapper's deque and records nothing); on the
+// episode's last step final = value at t - 1 and avg = np.mean(list) (numpy's pairwise f32 mean).
+APG_DEV float episode_mean(const float *h, int len) {
+  return f32_div(__fadd_rn(0.0f, pw_sum_ptr(h, len)), (float)len);
+}
+
+APG_DEV void log_regression(const EnvArgs &a, int e, const apg_image_outputs &out, float *hist, float ed, float mse) {
+  if (!a.log_stats || a.resetting) return;
+  float *h0 = hist + (size_t)e * 2 * a.limit, *h1 = h0 + a.limit;
+  h0[a.t_new - 1] = ed;
+  h1[a.t_new - 1] = mse;
+  if (a.t_new < a.limit) return;
+  out.stats[e] = ed;
+  out.stats[(size_t)a.n + e] = mse;
+  out.stats[(size_t)2 * a.n + e] = episode_mean(h0, a.limit);
+  out.stats[(size_t)3 * a.n + e] = episode_mean(h1, a.limit);
+}
+
+APG_DEV void log_classification(const EnvArgs &a, int e, const apg_image_outputs &out, float *hist, float prob) {
+  if (!a.log_stats || a.resetting) return;
+  float *h = hist + (size_t)e * 2 * a.limit;
+  h[a.t_new - 1] = prob;
+  if (a.t_new < a.limit) return;
+  // accuracy = correct_label_prob > 1 / num_classes (the Python float compared as float32, NEP 50)
+  const float thr = (float)(1.0 / (double)a.k);
+  float *acc = h + a.limit;
+  int first_correct = -1, last_incorrect = -1;
+  for (int i = 0; i < a.limit; i++) {
+    const bool c = h[i] > thr;
+    acc[i] = c ? 1.0f : 0.0f;
+    if (c && first_correct < 0) first_correct = i;
+    if (!c) last_incorrect = i;
+  }
+  out.stats[e] = prob;
+  out.stats[(size_t)a.n + e] = acc[a.limit - 1];
+  out.stats[(size_t)2 * a.n + e] = episode_mean(h, a.limit);
+  out.stats[(size_t)3 * a.n + e] = episode_mean(acc, a.limit);
+  out.stats_idx[e] = first_correct;
+  out.stats_idx[(size_t)a.n + e] = last_incorrect;
 }
 
 // The per-env tail of ImagePerceptionModule.step (:197-213) + ActivePerceptionVectorEnv.step
@@ -427,7 +429,7 @@ APG_DEV uint32_t env_tail(const EnvArgs &a, int e, const float *__restrict__ act
 // Localization: one thread per env; MSE against the target before the autoreset update.
 __global__ __launch_bounds__(256) void k_image_env_loc(EnvArgs a, const float *__restrict__ act,
                                                        const float *__restrict__ pred, double *pos,
-                                                       apg_image_outputs out) {
+                                                       apg_image_outputs out, float *hist) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= a.n) return;
   uint32_t err = 0;
@@ -439,6 +441,7 @@ __global__ __launch_bounds__(256) void k_image_env_loc(EnvArgs a, const float *_
   const float mse = f32_div(__fadd_rn(__fadd_rn(0.0f, __fmul_rn(d0, d0)), __fmul_rn(d1, d1)), 2.0f);
   const float loss_f = __fadd_rn(__fmul_rn(mse, a.mse_scale), a.mse_offset);
   out.loss_f32[e] = loss_f;
+  log_regression(a, e, out, hist, norm_f32(d0, d1), mse);  // |target - prediction|: signs do not matter
   err |= env_tail(a, e, act, pos, out, (double)loss_f, loss_f);
   if (err) atomicOr(out.err, err);
 }
@@ -482,7 +485,7 @@ APG_DEV float pw_sum8(const float *x, int off, int n, int j) {
 constexpr int CLS_LANES = 8;
 __global__ __launch_bounds__(256) void k_image_env_cls(EnvArgs a, int envs_per_block, const float *__restrict__ act,
                                                        const float *__restrict__ pred, const int32_t *label,
-                                                       double *pos, apg_image_outputs out) {
+                                                       double *pos, apg_image_outputs out, float *hist) {
   extern __shared__ float s_logit[];  // [envs_per_block][k + 1]
   const int k = a.k, stride = k + 1;
   const int e0 = blockIdx.x * envs_per_block;
@@ -514,7 +517,8 @@ __global__ __launch_bounds__(256) void k_image_env_cls(EnvArgs a, int envs_per_b
   }
   if (nan || isinf(m)) m = 0.0f;  // x_max[~isfinite(x_max)] = 0
   const int32_t l = live ? label[e0 + grp] : 0;
-  const float xt = row[l < 0 ? 0 : (l >= k ? k - 1 : l)];
+  const int lc = l < 0 ? 0 : (l >= k ? k - 1 : l);
+  const float xt = row[lc];
   __syncthreads();
   if (live)  // lanes of the tail groups (grp >= ne) alias row 0 and must not write it
     for (int i = j; i < k; i += CLS_LANES) row[i] = expf(__fsub_rn(row[i], m));
@@ -527,6 +531,8 @@ __global__ __launch_bounds__(256) void k_image_env_cls(EnvArgs a, int envs_per_b
   const double loss_d = __dadd_rn(__dmul_rn((double)ce, a.ce_scale), a.ce_offset);
   out.loss_f64[e] = loss_d;
   out.label_target[e] = l;
+  // scipy.special.softmax(prediction)[label] = exp(x_l - max) / sum(exp(x - max)) (finite logits)
+  log_classification(a, e, out, hist, f32_div(row[lc], sum));
   err |= env_tail(a, e, act, pos, out, loss_d, 0.0f);
   if (err) atomicOr(out.err, err);
 }
@@ -694,6 +700,7 @@ int validate(const apg_image_config *c) {
   if (c->kind == APG_IMAGE_CLASSIFY && (c->num_classes <= 0 || c->num_classes > MAX_PW_N))
     return fail(APG_E_INVALID, "num_classes out of range");
   if (c->kind != APG_IMAGE_CLASSIFY && c->kind != APG_IMAGE_LOCALIZE) return fail(APG_E_INVALID, "unknown image env kind");
+  if (c->log_stats && c->step_limit > PW_PTR_MAX_N) return fail(APG_E_INVALID, "log_stats needs step_limit <= 968");
   if (c->env_offset < 0 || (int64_t)c->env_offset + c->num_envs > c->num_envs_total)
     return fail(APG_E_INVALID, "shard [env_offset, env_offset + num_envs) must lie inside num_envs_total");
   return APG_OK;
@@ -875,6 +882,8 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
                    apg_stream_t stream) {
   if (int rc = validate(c)) return rc;
   if (!action || !prediction) return fail(APG_E_INVALID, "null action/prediction");
+  if (c->log_stats && (!st->stats_hist || !out->stats || (c->kind == APG_IMAGE_CLASSIFY && !out->stats_idx)))
+    return fail(APG_E_INVALID, "log_stats needs stats_hist, stats (and stats_idx) buffers");
   hipStream_t s = (hipStream_t)stream;
   const int n = c->num_envs;
   int rc;
@@ -900,17 +909,20 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
   a.ce_offset = c->ce_offset;
   a.mse_scale = c->mse_scale;
   a.mse_offset = c->mse_offset;
+  a.log_stats = c->log_stats ? 1 : 0;
+  a.limit = c->step_limit;
   const int32_t t_new = prev_done ? 0 : t + 1;
+  a.t_new = t_new;
   a.time_value = (float)(((double)t_new / (double)c->step_limit) * 2.0 - 1.0);
   if (c->kind == APG_IMAGE_CLASSIFY) {
     int epb = 256 / CLS_LANES;
     while (epb > 1 && (size_t)epb * (c->num_classes + 1) * sizeof(float) > 64 * 1024) epb /= 2;
     const size_t lds = (size_t)epb * (c->num_classes + 1) * sizeof(float);
     hipLaunchKernelGGL(k_image_env_cls, dim3(grid_for(n, epb)), dim3(epb * CLS_LANES), lds, s, a, epb, action,
-                       prediction, st->label, st->pos, *out);
+                       prediction, st->label, st->pos, *out, st->stats_hist);
   } else {
     hipLaunchKernelGGL(k_image_env_loc, dim3(grid_for(n, 256)), dim3(256), 0, s, a, action, prediction, st->pos,
-                       *out);
+                       *out, st->stats_hist);
   }
   if ((rc = check_launch("k_image_env"))) return rc;
   // the target glimpse only changes with the target or the images, i.e. on the autoreset step

@@ -20,6 +20,7 @@
 #include "../../include/apgym_capi.h"
 #include "apg_host.hpp"
 #include "apg_maps.hpp"
+#include "apg_pairwise.hpp"
 #include "apg_scan.hpp"
 
 using namespace apg;
@@ -106,6 +107,7 @@ int validate(const apg_lidar_config *c) {
   if (!(c->lidar_range > 0.0f) || c->lidar_range > 10.0f)
     return fail(APG_E_INVALID, "lidar_range must be in (0, 10] (occupancy window of the fused step kernel)");
   if (c->step_limit <= 0) return fail(APG_E_INVALID, "step_limit must be positive");
+  if (c->log_stats && c->step_limit > PW_PTR_MAX_N) return fail(APG_E_INVALID, "log_stats needs step_limit <= 968");
   return APG_OK;
 }
 
@@ -243,9 +245,23 @@ __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, ui
 }
 
 struct StepParams {
-  int n, h, w, wpr, beams, step_limit, is_static, R, wrows;
+  int n, h, w, wpr, beams, step_limit, is_static, R, wrows, log_stats;
   float range, loss_scale, loss_offset;
 };
+
+// ActiveRegressionLogWrapper (active_regression_env.py:131-159): per step |target - prediction| and
+// mean((target - prediction)^2) in float32; at the episode end avg = float(np.mean(list)) (numpy's
+// pairwise float32 mean) and final = the last value.  Stats for the steps of this episode live in
+// hist[0 .. len) (euclidean distance) and hist[step_limit ..) (mse).
+APG_DEV void log_episode_stats(const StepParams &P, const apg_lidar_outputs &O, int e, const float *hist, int len) {
+  for (int m = 0; m < 2; m++) {
+    const float *h = hist + m * P.step_limit;
+    const float avg = f32_div(__fadd_rn(0.0f, pw_sum_ptr(h, len)), (float)len);
+    O.stats[(size_t)m * P.n + e] = avg;
+    O.stats[(size_t)(2 + m) * P.n + e] = h[len - 1];
+  }
+  O.stats_len[e] = len;
+}
 
 // Occupancy window per env, staged in LDS from the PRE-move position p0: the 32 x 32 cells
 // [floor(p0) - 15, floor(p0) + 17)^2 (zero outside the map).  A step moves the agent by at most
@@ -253,7 +269,7 @@ struct StepParams {
 // position p can touch lies within [floor(p) - R - 2, floor(p) + R + 1] (+1 column for the 2-bit
 // quad reads), i.e. within [floor(p0) - R - 5, floor(p0) + R + 5]: inside the window for R <= 10.
 #ifndef APG_STEP_MIN_WAVES
-#define APG_STEP_MIN_WAVES 1
+#define APG_STEP_MIN_WAVES 4  // keep k_lidar_step at <= 128 VGPRs: 4 waves per SIMD
 #endif
 __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step(StepParams P, apg_lidar_state S,
                                                              const float *__restrict__ act,
@@ -345,6 +361,7 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
         O.target[2 * e + 1] = 0.0f;
         O.loss[e] = 0.0f;
         O.info_mask[e] = 0;
+        if (P.log_stats) O.stats_len[e] = 0;
         f &= (uint8_t)~(F_JUST_RESET | F_AUTORESET);
       } else {
         float ax = act[2 * e], ay = act[2 * e + 1];
@@ -360,6 +377,7 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
           O.target[2 * e + 1] = 0.0f;
           O.loss[e] = 0.0f;
           O.info_mask[e] = 0;
+          if (P.log_stats) O.stats_len[e] = 0;
         } else {
           const float lpx = pos0, lpy = pos1;
           const float br = __fsub_rn(0.1f, __fmul_rn(0.001f, __fadd_rn(__fmul_rn(ax, ax), __fmul_rn(ay, ay))));
@@ -417,6 +435,13 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
           const float ex = __fsub_rn(prx, tgx), ey = __fsub_rn(pry, tgy);
           const float mse = f32_div(__fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey)), 2.0f);
           const float loss = __fadd_rn(__fmul_rn(mse, P.loss_scale), P.loss_offset);
+          if (P.log_stats) {
+            float *hist = S.stats_hist + (size_t)e * 2 * P.step_limit;
+            hist[el - 1] = norm_f32(ex, ey);  // |target - prediction|: the signs do not matter
+            hist[P.step_limit + el - 1] = mse;
+            if (term) log_episode_stats(P, O, e, hist, el);
+            else O.stats_len[e] = 0;
+          }
           O.base_reward[e] = br;
           O.target[2 * e] = tgx;
           O.target[2 * e + 1] = tgy;
@@ -586,6 +611,7 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   P.wpr = (cfg->width + 63) / 64;
   P.beams = cfg->beams;
   P.step_limit = cfg->step_limit;
+  P.log_stats = cfg->log_stats ? 1 : 0;
   P.is_static = cfg->is_static;
   P.R = (int)ceilf(cfg->lidar_range);
   P.wrows = MAX_WIN_ROWS;
@@ -644,6 +670,8 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
   int rc = validate(cfg);
   if (rc) return rc;
   if (!action || !prediction) return fail(APG_E_INVALID, "null action/prediction");
+  if (cfg->log_stats && (!st->stats_hist || !out->stats || !out->stats_len))
+    return fail(APG_E_INVALID, "log_stats needs stats_hist, stats and stats_len buffers");
   hipStream_t s = (hipStream_t)stream;
   Geo g = make_geo(cfg);
   if ((rc = launch_reset(g, st, 0, 0, 0, out, s))) return rc;

@@ -87,6 +87,7 @@ typedef struct apg_lidar_config {
   float lidar_range;
   float loss_scale, loss_offset;/* normalized MSE affine, as float32 (NEP 50) */
   double branching_prob;        /* FloorMapDatasetMaze parameter */
+  int32_t log_stats;            /* 1: ActiveRegressionLogWrapper episode statistics (registered ids) */
 } apg_lidar_config;
 
 /* Persistent per-env state.  Sizes come from apg_lidar_query_sizes(). */
@@ -102,6 +103,7 @@ typedef struct apg_lidar_state {
   uint16_t *stack;     /* [N][maze_frames] DFS frames, contiguous per env (dynamic maze only) */
   uint64_t *map_idx;   /* [N]   dataset index of the current map */
   const float *beam_dirs; /* [beams][2] lidar_directions (f32, computed by the host like the reference) */
+  float *stats_hist;   /* [N][2][step_limit] per-step euclidean_distance, mse of the episode (log_stats) */
 } apg_lidar_state;
 
 typedef struct apg_lidar_outputs {
@@ -119,6 +121,9 @@ typedef struct apg_lidar_outputs {
   uint64_t *map_idx;   /* [N] info["map_idx"] of envs that reset this step (others untouched) or NULL */
   uint8_t *reset_mask; /* [N] 1 where the env auto-reset this step (info["_map_idx"]) or NULL */
   uint32_t *err;       /* [1] OR-ed APG_ERR_* bits (never cleared by the library) */
+  float *stats;        /* [4][N] avg_euclidean_distance, avg_mse, final_euclidean_distance, final_mse
+                          of the episodes that ended this step (log_stats) */
+  int32_t *stats_len;  /* [N] length of the episode that ended this step, 0 = no stats (log_stats) */
 } apg_lidar_outputs;
 
 typedef struct apg_lidar_state_sizes {
@@ -203,6 +208,7 @@ typedef struct apg_image_config {
   double cell[2];             /* unique sampling max_grid_cell_size_norm */
   double ce_scale, ce_offset; /* normalized CrossEntropyLossFn affine (float64) */
   float mse_scale, mse_offset;/* normalized MSELossFn affine (float32, NEP 50) */
+  int32_t log_stats;          /* 1: the registered ids' vector log wrapper statistics */
 } apg_image_config;
 
 typedef struct apg_image_state {
@@ -219,6 +225,8 @@ typedef struct apg_image_state {
   double *scratch_f64;        /* [N_total][2] batch draws */
   int32_t *top_k;             /* [N][top_k] unique-sampling ranking (localize) */
   int64_t *rng_work;          /* apg_rng_fill_work_elems(N, max(pool_len, top_k, 2)) int64 */
+  float *stats_hist;          /* [N][2][step_limit] per-step metrics of the episode (log_stats):
+                                 classify: correct_label_prob; localize: euclidean_distance, mse */
 } apg_image_state;
 
 typedef struct apg_image_outputs {
@@ -233,6 +241,10 @@ typedef struct apg_image_outputs {
   double *loss_f64;           /* [N] classify: normalized cross entropy (float64) */
   float *loss_f32;            /* [N] localize: normalized MSE (float32) */
   uint32_t *err;              /* [1] OR-ed APG_ERR_* bits */
+  float *stats;               /* [4][N] on the episode's last step (log_stats): classify final/avg of
+                                 correct_label_prob, accuracy; localize final/avg of euclidean_distance, mse
+                                 (order: final m0, final m1, avg m0, avg m1) */
+  int32_t *stats_idx;         /* [2][N] classify: first_correct, last_incorrect (-1: none) */
 } apg_image_outputs;
 
 /* reset(seed=seed) seeding chain: np_random = default_rng(seed); module.seed(np_random.integers(0,

@@ -157,7 +157,7 @@ class ImageVectorEnvOracle:
     """Vector image env restated with numpy Generators (kind "cls" or "loc")."""
 
     def __init__(self, kind, pool, labels, num_classes, channels, num_envs, sensor=(5, 5), scale=1.0,
-                 step_limit=16, max_step_length=0.2, invert=False, top_k=10, rel=0.2):
+                 step_limit=16, max_step_length=0.2, invert=False, top_k=10, rel=0.2, log_stats=True):
         self.kind, self.n = kind, num_envs
         self.pool = images_f32(pool, channels)
         self.labels_pool = np.asarray(labels).astype(np.int32)
@@ -165,6 +165,7 @@ class ImageVectorEnvOracle:
         self.sensor, self.scale, self.limit = tuple(sensor), scale, step_limit
         self.msl = np.ones(2) * np.array(max_step_length)
         self.invert, self.top_k, self.rel = invert, top_k, rel
+        self.log_stats = log_stats
 
     # --- seeding chain: VectorEnv.reset(seed) -> _np_random setter -> module.seed
     def seed(self, seed):
@@ -204,7 +205,60 @@ class ImageVectorEnvOracle:
             self.target = np.clip(base + self.cur.uniform(-cell, cell, (self.n, 2)), -1, 1).astype(np.float32)
             self.env_prev_done = np.zeros(self.n, bool)
             obs["target_glimpse"] = glimpse(self.images, self.target, self.sensor, self.scale)
+        self.hist = [[] for _ in range(self.n)]
+        self.log_prev_done = np.zeros(self.n, bool)
         return obs, {"index": self.idx}
+
+    def _log(self, prediction, info, done):
+        """The registered ids' vector log wrapper (ActiveClassificationVectorLogWrapper,
+        active_classification_env.py:116-197 / ActiveRegressionVectorLogWrapper,
+        active_regression_env.py:160-227, util.py:40-80), restated."""
+        target = info["prediction"]["target"]
+        if self.kind == "cls":
+            prob = scipy.special.softmax(prediction, axis=-1)[np.arange(self.n), target]
+            vals = [(prob[i],) for i in range(self.n)]
+            names = ["correct_label_prob"]
+        else:
+            d = target - prediction
+            ed, ms = np.linalg.norm(d, axis=-1), np.mean(d ** 2, axis=-1)
+            vals = [(ed[i], ms[i]) for i in range(self.n)]
+            names = ["euclidean_distance", "mse"]
+        for i in range(self.n):
+            if self.log_prev_done[i]:
+                self.hist[i] = []
+            else:
+                self.hist[i].append(vals[i])
+        self.log_prev_done = done
+        if not done.any():
+            return info
+        metrics = {nm: [np.array([h[j] for h in self.hist[i]], np.float32) for i in range(self.n)]
+                   for j, nm in enumerate(names)}
+        if self.kind == "cls":
+            is_correct = [m > 1 / self.k for m in metrics["correct_label_prob"]]
+            metrics["accuracy"] = [c.astype(np.float32) for c in is_correct]
+        scalar, vector = {}, {}
+        for nm, per_env in metrics.items():
+            scalar[f"final_{nm}"] = np.array([e[-1] if t else np.nan for t, e in zip(done, per_env)], np.float32)
+            scalar[f"_final_{nm}"] = done
+        for nm, per_env in metrics.items():
+            scalar[f"avg_{nm}"] = np.array([np.mean(e) if t else np.nan for t, e in zip(done, per_env)], np.float32)
+            scalar[f"_avg_{nm}"] = done
+        for nm, per_env in metrics.items():
+            vector[nm] = np.array([(list(e) if t else []) for e, t in zip(per_env, done)] + [None], dtype=object)[:-1]
+            vector[f"_{nm}"] = done
+        if self.kind == "cls":
+            fc, fcv = np.full(self.n, -1, np.int32), np.zeros(self.n, bool)
+            li, liv = np.full(self.n, -1, np.int32), np.zeros(self.n, bool)
+            for i, c in enumerate(is_correct):
+                w = np.nonzero(c)[0]
+                if len(w):
+                    fc[i], fcv[i] = w[0], True
+                w = np.nonzero(~c)[0]
+                if len(w):
+                    li[i], liv[i] = w[-1], True
+            scalar.update(first_correct=fc, _first_correct=fcv, last_incorrect=li, _last_incorrect=liv)
+        info["stats"] = {"scalar": scalar, "_scalar": done, "vector": vector, "_vector": done}
+        return info
 
     def step(self, action, prediction):
         action = np.asarray(action, np.float32)
@@ -245,6 +299,8 @@ class ImageVectorEnvOracle:
             scale = 1 / (np.log(self.k) - 0.0)
             loss = ce * scale + (-0.0 * scale)
         info = {"index": self.idx, "base_reward": base, "prediction": {"target": target, "loss": loss}}
+        if self.log_stats:
+            info = self._log(prediction, info, term | trunc)
         return obs, base - loss, term, trunc, info
 
     @staticmethod

@@ -40,3 +40,29 @@ def gpu():
 
     ap_gym_amd._native.lib()
     return torch.device("cuda:0")
+
+
+def check_image_stats(st, g, t, rtol=0.0):
+    import numpy as np
+
+    """info["stats"] of the vector log wrappers against the reference fixture of step t."""
+    pre = f"stats_t{t}_"
+    for key, v in st["scalar"].items():
+        want = g[pre + "scalar_" + key]
+        assert np.asarray(v).dtype == want.dtype, key
+        if rtol and "correct_label_prob" in key:
+            np.testing.assert_allclose(v, want, rtol=rtol, atol=rtol, err_msg=key)
+        else:
+            assert np.array_equal(v, want, equal_nan=want.dtype.kind == "f"), key
+    assert {k for k in g.files if k.startswith(pre + "scalar_")} == {pre + "scalar_" + k for k in st["scalar"]}
+    for key, v in st["vector"].items():
+        if key.startswith("_"):
+            assert np.array_equal(v, g[pre + "vector_" + key]), key
+            continue
+        lens = g[pre + "vector_" + key + "_len"]
+        assert v.dtype == object and [len(x) for x in v] == list(lens), key
+        flat = np.array([x for lst in v for x in lst], np.float32)
+        if rtol and key == "correct_label_prob":
+            np.testing.assert_allclose(flat, g[pre + "vector_" + key], rtol=rtol, atol=rtol, err_msg=key)
+        else:
+            assert np.array_equal(flat, g[pre + "vector_" + key]), key

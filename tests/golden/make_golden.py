@@ -190,7 +190,10 @@ def run_lidar_env(name, dataset, static, beams, n_envs, steps, seed, action_mode
         actions = choices[arng.integers(0, len(choices), (steps, n_envs))]
     preds = arng.uniform(-1, 1, (steps, n_envs, 2)).astype(np.float32)
     rec = {k: [] for k in ("lidar", "odometry", "time_step", "map", "reward", "terminated", "truncated",
-                           "base_reward", "target", "loss", "info_mask")}
+                           "base_reward", "target", "loss", "info_mask", "stats_mask", "stats_avg_euclidean_distance",
+                           "stats_avg_mse", "stats_final_euclidean_distance", "stats_final_mse",
+                           "stats_len")}
+    vec = {"euclidean_distance": [], "mse": []}  # ActiveRegressionLogWrapper "vector" lists, concatenated
     reset_obs = obs
     reset_map_idx = np.asarray(info["map_idx"], dtype=np.int64)
     for t in range(steps):
@@ -210,7 +213,23 @@ def run_lidar_env(name, dataset, static, beams, n_envs, steps, seed, action_mode
                                       else np.zeros((n_envs, 2), np.float32), 0).astype(np.float32))
         rec["loss"].append(np.where(mask, info["prediction"]["loss"] if "prediction" in info
                                     else np.zeros(n_envs, np.float32), 0).astype(np.float32))
+        smask = info.get("_stats", np.zeros(n_envs, bool))
+        rec["stats_mask"].append(smask)
+        lens = np.zeros(n_envs, np.int32)
+        for key in ("avg_euclidean_distance", "avg_mse", "final_euclidean_distance", "final_mse"):
+            v = info["stats"]["scalar"][key] if smask.any() else np.zeros(n_envs)
+            assert not smask.any() or v.dtype == np.float64
+            rec["stats_" + key].append(np.where(smask, v, 0.0))
+        for i in np.nonzero(smask)[0]:
+            for key in vec:
+                lst = info["stats"]["vector"][key][i]
+                assert all(type(x) is np.float32 for x in lst)
+                vec[key].extend(lst)
+            lens[i] = len(info["stats"]["vector"]["mse"][i])
+        rec["stats_len"].append(lens)
     arrays = {k: np.stack(v) for k, v in rec.items() if v}
+    for key, v in vec.items():
+        arrays["stats_vector_" + key] = np.array(v, np.float32)
     arrays["reward_dtype"] = np.array(str(rew.dtype))
     arrays["base_reward_dtype"] = np.array(str(np.asarray(info.get("base_reward", np.zeros(1, np.float32))).dtype))
     arrays["lidar_dtype"] = np.array(str(obs["lidar"].dtype))
@@ -266,6 +285,9 @@ def run_image_env(name, kind, pool_shape, channels, num_classes, sensor, scale, 
     cfg = ipm.ImagePerceptionConfig(dataset=PoolDataset(), sensor_size=sensor, sensor_scale=scale,
                                     step_limit=step_limit, prefetch=False, randomly_invert_labels=invert)
     env = (ic.ImageClassificationVectorEnv if kind == "cls" else il.ImageLocalizationVectorEnv)(n_envs, cfg)
+    # the registered ids wrap the vector env in the vector log wrapper (registration.py:185-192, 263-269)
+    ap = sys.modules["ap_gym"]
+    env = (ap.ActiveClassificationVectorLogWrapper if kind == "cls" else ap.ActiveRegressionVectorLogWrapper)(env)
     obs, info = env.reset(seed=seed)
     arng = np.random.default_rng(11)
     actions = arng.uniform(-1.5, 1.5, (steps, n_envs, 2)).astype(np.float32)
@@ -291,6 +313,20 @@ def run_image_env(name, kind, pool_shape, channels, num_classes, sensor, scale, 
             v = np.asarray(v)
             rec.setdefault(k, []).append(v)
             rec.setdefault(k + "_dtype", []).append(str(v.dtype))
+        # vector log wrapper statistics (active_{classification,regression}_env.py, util.py:40-80)
+        smask = np.asarray(info["stats"]["_scalar"]) if "stats" in info else np.zeros(n_envs, bool)
+        rec.setdefault("stats_mask", []).append(smask)
+        if smask.any():
+            st = info["stats"]
+            for key, val in st["scalar"].items():
+                out.setdefault(f"stats_t{t}_scalar_{key}", np.asarray(val))
+            for key, val in st["vector"].items():
+                if key.startswith("_"):
+                    out[f"stats_t{t}_vector_{key}"] = np.asarray(val)
+                else:
+                    assert all(type(x) is np.float32 for lst in val for x in lst)
+                    out[f"stats_t{t}_vector_{key}_len"] = np.array([len(lst) for lst in val], np.int32)
+                    out[f"stats_t{t}_vector_{key}"] = np.array([x for lst in val for x in lst], np.float32)
     for k, v in rec.items():
         out["step_" + k] = np.array(v) if k.endswith("_dtype") else np.stack(v)
     env.close()

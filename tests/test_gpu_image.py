@@ -14,7 +14,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import check_image_stats, golden
 
 pytestmark = pytest.mark.gpu
 
@@ -234,13 +234,13 @@ def test_mse_loss_kernel_bit_exact(gpu, d):
 
 
 # ---------------------------------------------------------------------------------------- envs
-def _make_env(ap, g, backend="numpy", n=None, copy=False):
+def _make_env(ap, g, backend="numpy", n=None, copy=False, log_stats=False):
     h, w, c, k, s0, s1, lim, inv, n_g, _ = (int(v) for v in g["config"])
     ds = ap.ArrayImageClassificationDataset(g["pool"], g["labels"], k, c)
     cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=(s0, s1), sensor_scale=float(g["sensor_scale"]),
                                    step_limit=lim, randomly_invert_labels=bool(inv))
     cls = ap.ImageClassificationVectorEnv if str(g["kind"]) == "cls" else ap.ImageLocalizationVectorEnv
-    return cls(n or n_g, cfg, array_backend=backend, copy=copy)
+    return cls(n or n_g, cfg, array_backend=backend, copy=copy, log_stats=log_stats)
 
 
 def _assert_field(name, got, want, want_dtype, ce, key=None):
@@ -257,7 +257,7 @@ def test_image_env_matches_reference_trace(gpu, name):
     import ap_gym_amd as ap
 
     g = golden(f"image_{name}.npz")
-    env = _make_env(ap, g)
+    env = _make_env(ap, g, log_stats=True)
     ce = str(g["kind"]) == "cls"
     obs, info = env.reset(seed=int(g["seed"]))
     for k, v in obs.items():
@@ -269,9 +269,13 @@ def test_image_env_matches_reference_trace(gpu, name):
         fields = dict(obs, reward=rew, terminated=term, truncated=trunc, index=info["index"],
                       base_reward=info["base_reward"], target=info["prediction"]["target"],
                       loss=info["prediction"]["loss"])
-        assert set(fields) == {k[5:] for k in g.files if k.startswith("step_") and not k.endswith("_dtype")}
+        assert set(fields) | {"stats_mask"} == {k[5:] for k in g.files if k.startswith("step_") and not k.endswith("_dtype")}
         for k, v in fields.items():
             _assert_field(f"step{t}_{k}", v, g["step_" + k][t], g["step_" + k + "_dtype"][t], ce, key=k)
+        # vector log wrapper statistics (correct_label_prob uses the device exp: north-star tolerance)
+        assert ("stats" in info) == bool(g["step_stats_mask"][t].any())
+        if "stats" in info:
+            check_image_stats(info["stats"], g, t, rtol=CE_RTOL if ce else 0.0)
     env.close()
 
 

@@ -147,8 +147,9 @@ def test_vector_env_matches_reference_trace(gpu, name):
     d = golden(f"lidar_env_{name}.npz")
     n = d["actions"].shape[1]
     env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_ds(ap, kind, size), static_map=static,
-                                          lidar_beam_count=beams, device=gpu)
+                                          lidar_beam_count=beams, device=gpu, log_stats=True)
     obs, info = env.reset(seed=int(d["seed"]))
+    vec_off = 0
     assert np.array_equal(obs["lidar"], d["reset_lidar"])
     assert np.array_equal(obs["odometry"], d["reset_odometry"])
     assert np.array_equal(obs["time_step"], d["reset_time_step"])
@@ -174,6 +175,26 @@ def test_vector_env_matches_reference_trace(gpu, name):
         if not static:
             assert np.array_equal(np.packbits(obs["map"][..., 0] > 0, axis=-1), d["map"][t]), (name, t)
             assert set(np.unique(obs["map"])) <= {np.float32(0), np.float32(1) / np.float32(255)}
+        # ActiveRegressionLogWrapper episode statistics, merged by SyncVectorEnv
+        smask = d["stats_mask"][t]
+        if smask.any():
+            assert np.array_equal(info["_stats"], smask)
+            st = info["stats"]
+            assert np.array_equal(st["_scalar"], smask) and np.array_equal(st["_vector"], smask)
+            for key in ("avg_euclidean_distance", "avg_mse", "final_euclidean_distance", "final_mse"):
+                assert st["scalar"][key].dtype == np.float64
+                assert np.array_equal(st["scalar"][key], d["stats_" + key][t]), (name, t, key)
+                assert np.array_equal(st["scalar"]["_" + key], smask)
+            for i in np.nonzero(smask)[0]:
+                ln = int(d["stats_len"][t][i])
+                for key in ("euclidean_distance", "mse"):
+                    lst = st["vector"][key][i]
+                    assert len(lst) == ln and all(type(x) is np.float32 for x in lst)
+                    assert np.array_equal(np.array(lst), d["stats_vector_" + key][vec_off:vec_off + ln]), (name, t, i)
+                vec_off += ln
+        else:
+            assert "stats" not in info
+    assert vec_off == len(d["stats_vector_mse"])
     env.close()
 
 
@@ -183,17 +204,31 @@ def test_vector_env_matches_oracle(gpu, oracle_mod, kind, size, beams, n, steps)
     import ap_gym_amd as ap
 
     env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_ds(ap, kind, size), lidar_beam_count=beams,
-                                          device=gpu)
+                                          device=gpu, log_stats=True)
     ref = oracle_mod.OracleLidarVectorEnv(n, kind, size, False, 0, beams)
     obs, _ = env.reset(seed=123)
     ref.reset(123)
     assert np.array_equal(obs["lidar"], ref.lidar)
     rng = np.random.default_rng(9)
+    hist = [[] for _ in range(n)]  # ActiveRegressionLogWrapper metrics, restated per env
     for t in range(steps):
         a = rng.uniform(-1.5, 1.5, (n, 2)).astype(np.float32)
         p = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
         obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
         ref.step(a, p)
+        for i in np.nonzero(ref.info_mask)[0]:
+            d = ref.target[i] - p[i]
+            hist[i].append((np.linalg.norm(d), np.mean(d ** 2)))
+        done = (ref.terminated | ref.truncated).astype(bool)
+        assert np.array_equal(info.get("_stats", np.zeros(n, bool)), done), t
+        for i in np.nonzero(done)[0]:
+            ed = np.array([h[0] for h in hist[i]], np.float32)
+            ms = np.array([h[1] for h in hist[i]], np.float32)
+            sc = info["stats"]["scalar"]
+            assert sc["avg_euclidean_distance"][i] == float(np.mean(ed)) and sc["final_mse"][i] == float(ms[-1])
+            assert sc["avg_mse"][i] == float(np.mean(ms)) and sc["final_euclidean_distance"][i] == float(ed[-1])
+            assert np.array_equal(np.array(info["stats"]["vector"]["mse"][i]), ms)
+            hist[i] = []
         assert np.array_equal(obs["lidar"], ref.lidar), t
         assert np.array_equal(obs["odometry"], ref.odometry), t
         assert np.array_equal(obs["time_step"], ref.time_step), t

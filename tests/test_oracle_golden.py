@@ -10,7 +10,7 @@ CPU only.  These pin the restatement before it is trusted as the checker of the 
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import check_image_stats, golden
 
 ENV_CASES = {
     "rooms_static_b16": ("rooms", 32, True, 16),
@@ -119,6 +119,9 @@ def test_image_oracle_matches_reference_trace(name):
             v = np.asarray(v)
             assert np.array_equal(v, g["step_" + key][t]), (t, key)
             assert str(v.dtype) == g["step_" + key + "_dtype"][t], (t, key)
+        assert ("stats" in info) == bool(g["step_stats_mask"][t].any())
+        if "stats" in info:
+            check_image_stats(info["stats"], g, t)
 
 
 def test_pairwise_sum_matches_numpy_mean():
