@@ -50,7 +50,8 @@ class LidarConfig(ctypes.Structure):
                 ("map_kind", ctypes.c_int32), ("is_static", ctypes.c_int32), ("static_map_index", ctypes.c_int32),
                 ("beams", ctypes.c_int32), ("step_limit", ctypes.c_int32), ("max_rooms", ctypes.c_int32),
                 ("door_width", ctypes.c_int32), ("lidar_range", ctypes.c_float), ("loss_scale", ctypes.c_float),
-                ("loss_offset", ctypes.c_float), ("branching_prob", ctypes.c_double), ("log_stats", ctypes.c_int32)]
+                ("loss_offset", ctypes.c_float), ("branching_prob", ctypes.c_double), ("log_stats", ctypes.c_int32),
+                ("sparse", ctypes.c_int32)]
 
 
 class LidarState(ctypes.Structure):
@@ -61,7 +62,7 @@ class LidarState(ctypes.Structure):
 class LidarOutputs(ctypes.Structure):
     _fields_ = [(n, _vp) for n in ("lidar", "odometry", "time_step", "map_obs", "reward", "terminated", "truncated",
                                    "base_reward", "target", "loss", "info_mask", "map_idx", "reset_mask", "err",
-                                   "stats", "stats_len")]
+                                   "stats", "stats_len", "weight")]
 
 
 class LidarSizes(ctypes.Structure):
@@ -76,7 +77,8 @@ class ImageConfig(ctypes.Structure):
                                               "env_offset")] + [
         ("pool_len", ctypes.c_int64), ("sensor_scale", ctypes.c_double), ("max_step", ctypes.c_double * 2),
         ("cell", ctypes.c_double * 2), ("ce_scale", ctypes.c_double), ("ce_offset", ctypes.c_double),
-        ("mse_scale", ctypes.c_float), ("mse_offset", ctypes.c_float), ("log_stats", ctypes.c_int32)]
+        ("mse_scale", ctypes.c_float), ("mse_offset", ctypes.c_float), ("log_stats", ctypes.c_int32),
+        ("sparse", ctypes.c_int32)]
 
 
 class ImageState(ctypes.Structure):

@@ -30,7 +30,7 @@ import numpy as np
 
 from . import _native as N
 from .image_dataset import ImageClassificationDataset
-from .loss_fn import CrossEntropyLossFn, affine_f32, regression_loss
+from .loss_fn import CrossEntropyLossFn, WeightedLossFn, affine_f32, regression_loss
 from .spaces import ActivePerceptionActionSpace, Box, Dict, Discrete, ImageSpace, LogitSpace, MultiDiscrete, batch_space
 
 NAN_ACTION_MSG = "NaN values detected in action."
@@ -86,7 +86,7 @@ class _ImageVectorEnv:
     def __init__(self, num_envs: int, image_perception_config: ImagePerceptionConfig,
                  render_mode: str = "rgb_array", device=None, copy: bool = False, strict_errors: bool = False,
                  array_backend: str = "numpy", num_envs_total: int | None = None, env_offset: int = 0,
-                 log_stats: bool = False):
+                 log_stats: bool = False, sparse: bool = False):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -107,6 +107,9 @@ class _ImageVectorEnv:
         # the registered ids wrap the env in ActiveClassificationVectorLogWrapper /
         # ActiveRegressionVectorLogWrapper (registration.py:185-192, 263-269): info["stats"]
         self.log_stats = bool(log_stats)
+        # the "-sparse" ids wrap that in SparsifyVectorWrapper (sparsify_wrapper.py:23-92): target
+        # {"target", "weight" = terminated as float32}, reward = base_reward - loss * weight
+        self.sparse = bool(sparse)
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise ValueError("the image envs run on a GPU device (no CPU fallback)")
@@ -144,6 +147,12 @@ class _ImageVectorEnv:
             self.single_prediction_target_space = Discrete(k)
             self.prediction_target_space = MultiDiscrete([k] * n)
             self.loss_fn = CrossEntropyLossFn(num_classes=k).normalized
+        inner_loss = self.loss_fn
+        if self.sparse:
+            self.single_prediction_target_space = Dict({"target": self.single_prediction_target_space,
+                                                        "weight": Box(0, 1, (), np.float32)})
+            self.prediction_target_space = batch_space(self.single_prediction_target_space, n)
+            self.loss_fn = WeightedLossFn(inner_loss)
         self.single_observation_space = Dict(obs)
         self.observation_space = batch_space(self.single_observation_space, n)
         self.single_action_space = ActivePerceptionActionSpace(Box(-1, 1, (2,), np.float32), pred_space)
@@ -154,12 +163,12 @@ class _ImageVectorEnv:
                                           cfg.unique_sampling_max_grid_cell_size_rel)
         msl = np.ones(2) * np.array(cfg.max_step_length)
         if self.kind == N.APG_IMAGE_CLASSIFY:
-            ce = self.loss_fn
+            ce = inner_loss
             ce_scale, ce_offset = float(ce.scale), float(ce.offset)
             mse_scale, mse_offset = 1.0, 0.0
         else:
             ce_scale, ce_offset = 1.0, 0.0
-            mse_scale, mse_offset = affine_f32(self.loss_fn)
+            mse_scale, mse_offset = affine_f32(inner_loss)
         self._cfg = N.ImageConfig(
             num_envs=n, kind=self.kind, height=h, width=w, pool_channels=pc, channels=c,
             pool_dtype=N.APG_POOL_U8 if pool.dtype == np.uint8 else N.APG_POOL_F32, sensor_h=s0, sensor_w=s1,
@@ -168,7 +177,7 @@ class _ImageVectorEnv:
             env_offset=self.env_offset, pool_len=m,
             sensor_scale=float(cfg.sensor_scale), max_step=(ctypes.c_double * 2)(*msl.tolist()),
             cell=(ctypes.c_double * 2)(*cell.tolist()), ce_scale=ce_scale, ce_offset=ce_offset,
-            mse_scale=mse_scale, mse_offset=mse_offset, log_stats=int(self.log_stats))
+            mse_scale=mse_scale, mse_offset=mse_offset, log_stats=int(self.log_stats), sparse=int(self.sparse))
 
         t, dev = torch, self.device
         gshape = (n, s0, s1, c)
@@ -396,6 +405,8 @@ class _ImageVectorEnv:
             target = T["label_target"].cpu().numpy()
             loss = T["loss_f64"].cpu().numpy()
         base = np.zeros(n) if resetting else T["base_reward"].cpu().numpy()
+        if self.sparse:
+            target = {"target": target, "weight": np.full(n, terminated, dtype=np.float32)}
         info = {"index": T["index"].cpu().numpy(), "base_reward": base,
                 "prediction": {"target": target, "loss": loss}}
         if self.log_stats and terminated:
@@ -476,12 +487,17 @@ class _ImageVectorEnv:
             target, loss = T["target_out"], T["loss_f32"]
         else:
             target, loss = T["label_target"], T["loss_f64"]
-        info = {"index": self._c(T["index"]), "base_reward": self._c(T["base_reward"]),
-                "prediction": {"target": self._c(target), "loss": self._c(loss)}}
         # episodes end for the whole batch at once: terminated is all-True or all-False, never truncated
         if self._done_consts is None:
             self._done_consts = (torch.zeros(n, dtype=torch.bool, device=self.device),
-                                 torch.ones(n, dtype=torch.bool, device=self.device))
+                                 torch.ones(n, dtype=torch.bool, device=self.device),
+                                 torch.zeros(n, dtype=torch.float32, device=self.device),
+                                 torch.ones(n, dtype=torch.float32, device=self.device))
+        target = self._c(target)
+        if self.sparse:
+            target = {"target": target, "weight": self._c(self._done_consts[3 if terminated else 2])}
+        info = {"index": self._c(T["index"]), "base_reward": self._c(T["base_reward"]),
+                "prediction": {"target": target, "loss": self._c(loss)}}
         term = self._c(self._done_consts[1 if terminated else 0])
         trunc = self._c(self._done_consts[0])
         if self.log_stats and terminated:

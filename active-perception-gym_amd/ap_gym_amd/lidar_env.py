@@ -16,6 +16,12 @@ HBM plus three kernels per step (include/apgym_capi.h):
                   "stats" of ActiveRegressionLogWrapper (active_regression_env.py:131-159) for the
                   envs whose episode ended: scalar avg_/final_ euclidean_distance and mse, vector
                   lists of the per-step values
+  sparse=True     the "-sparse" ids (registration.py:115-142, SparsifyWrapper sparsify_wrapper.py:93-161
+                  on every sub-env): prediction target {"target", "weight" = 1.0 where terminated},
+                  reward = base_reward - loss * weight.  The reference's own LIDAR "-sparse" ids raise
+                  KeyError('prediction') in reset (SparsifyWrapper.reset needs info["prediction"], which
+                  LIDARLocalization2DEnv.reset does not return); this is their step semantics with a
+                  working reset (reset info as the dense ids)
 
 Two I/O modes (constructor `array_backend`), inputs of either type are accepted:
   "numpy" (default) -> numpy out, host copies and host-side NaN checks, like the reference
@@ -34,7 +40,7 @@ import numpy as np
 
 from . import _native as N
 from .floor_map import FloorMapDataset, FloorMapDatasetMaze, FloorMapDatasetRooms
-from .loss_fn import affine_f32, regression_loss
+from .loss_fn import WeightedLossFn, affine_f32, regression_loss
 from .spaces import ActivePerceptionActionSpace, Box, Dict, ImageSpace, batch_space
 
 NAN_ACTION_MSG = "NaN values detected in action."
@@ -62,7 +68,8 @@ class LIDARLocalization2DVectorEnv:
                  static_map: bool = False, lidar_beam_count: int = 8, lidar_range: float = 5,
                  static_map_index: int = 0, prefetch: bool = True, prefetch_buffer_size: int = 128,
                  max_episode_steps: int = 100, device=None, env_offset: int = 0, copy: bool = False,
-                 strict_errors: bool = False, array_backend: str = "numpy", log_stats: bool = False):
+                 strict_errors: bool = False, array_backend: str = "numpy", log_stats: bool = False,
+                 sparse: bool = False):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -80,6 +87,7 @@ class LIDARLocalization2DVectorEnv:
         self.copy = copy
         self.strict_errors = strict_errors
         self.log_stats = bool(log_stats)
+        self.sparse = bool(sparse)
         if array_backend not in ("numpy", "torch"):
             raise ValueError("array_backend must be 'numpy' or 'torch'")
         self.array_backend = array_backend
@@ -100,18 +108,23 @@ class LIDARLocalization2DVectorEnv:
                                                                Box(-1, 1, (2,), np.float32))
         self.action_space = batch_space(self.single_action_space, self.num_envs)
         self.single_prediction_target_space = Box(-1, 1, (2,), np.float32)
+        self.loss_fn = inner_loss = regression_loss(2, -1, 1)
+        if self.sparse:
+            self.single_prediction_target_space = Dict({"target": self.single_prediction_target_space,
+                                                        "weight": Box(0, 1, (), np.float32)})
+            self.loss_fn = WeightedLossFn(inner_loss)
         self.prediction_target_space = batch_space(self.single_prediction_target_space, self.num_envs)
-        self.loss_fn = regression_loss(2, -1, 1)
 
         # ---- native configuration
         p = dataset.native_params()
-        scale, offset = affine_f32(self.loss_fn)
+        scale, offset = affine_f32(inner_loss)
         self._cfg = N.LidarConfig(num_envs=self.num_envs, height=h, width=w, map_kind=dataset.map_kind,
                                   is_static=int(self.static_map), static_map_index=int(static_map_index),
                                   beams=self.lidar_beam_count, step_limit=self.max_episode_steps,
                                   max_rooms=p["max_rooms"], door_width=p["door_width"],
                                   lidar_range=float(np.float32(lidar_range)), loss_scale=scale, loss_offset=offset,
-                                  branching_prob=p["branching_prob"], log_stats=int(self.log_stats))
+                                  branching_prob=p["branching_prob"], log_stats=int(self.log_stats),
+                                  sparse=int(self.sparse))
         L = N.lib()
         sizes = N.LidarSizes()
         N.check(L.apg_lidar_query_sizes(ctypes.byref(self._cfg), ctypes.byref(sizes)), "apg_lidar_query_sizes")
@@ -148,6 +161,7 @@ class LIDARLocalization2DVectorEnv:
                         else None),
             stats=t.zeros((4, n), dtype=t.float32, device=dev) if self.log_stats else None,
             stats_len=t.zeros(n, dtype=t.int32, device=dev) if self.log_stats else None,
+            weight=t.zeros(n, dtype=t.float64, device=dev) if self.sparse else None,
         )
         T = self._t
         self._state = N.LidarState(*[N.ptr(T[k]) for k in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng",
@@ -158,7 +172,7 @@ class LIDARLocalization2DVectorEnv:
                                    N.ptr(T["truncated"]), N.ptr(T["base_reward"]), N.ptr(T["target"]),
                                    N.ptr(T["loss"]), N.ptr(T["info_mask"]), N.ptr(T["map_idx_out"]),
                                    N.ptr(T["reset_mask"]), N.ptr(T["err"]), N.ptr(T["stats"]),
-                                   N.ptr(T["stats_len"]))
+                                   N.ptr(T["stats_len"]), N.ptr(T["weight"]))
         self._err_host = t.zeros(1, dtype=t.int32).pin_memory()
         self._err_event = t.cuda.Event()
         self._err_pending = False
@@ -301,8 +315,11 @@ class LIDARLocalization2DVectorEnv:
         T = self._t
         mask = T["info_mask"]
         c = (lambda x: x.clone()) if self.copy else (lambda x: x)
+        target = c(T["target"])
+        if self.sparse:  # SyncVectorEnv merge of the sub-envs' {"target", "weight": float}
+            target = {"target": target, "_target": c(mask), "weight": c(T["weight"]), "_weight": c(mask)}
         info = {"base_reward": c(T["base_reward"]), "_base_reward": c(mask),
-                "prediction": {"target": c(T["target"]), "_target": c(mask), "loss": c(T["loss"]),
+                "prediction": {"target": target, "_target": c(mask), "loss": c(T["loss"]),
                                "_loss": c(mask)},
                 "_prediction": c(mask),
                 "map_idx": c(T["map_idx_out"]), "_map_idx": c(T["reset_mask"])}
@@ -400,6 +417,9 @@ class LIDARLocalization2DVectorEnv:
             info["_base_reward"] = mask.copy()
             tgt = np.where(mask[:, None], T["target"].cpu().numpy(), np.float32(0))
             loss = np.where(mask, T["loss"].cpu().numpy(), np.float32(0))
+            if self.sparse:
+                tgt = {"target": tgt, "_target": mask.copy(),
+                       "weight": np.where(mask, T["weight"].cpu().numpy(), 0.0), "_weight": mask.copy()}
             info["prediction"] = {"target": tgt, "_target": mask.copy(), "loss": loss, "_loss": mask.copy()}
             info["_prediction"] = mask.copy()
         if self.log_stats:

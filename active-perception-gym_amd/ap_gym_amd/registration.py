@@ -29,8 +29,23 @@ class EnvSpec:
 registry: dict[str, EnvSpec] = {}
 
 
-def register(id: str, vector_entry_point: Callable, kwargs: dict | None = None, max_episode_steps=None):
+def sparse_id(id: str) -> str:
+    """parse_env_id / get_env_id as registration.py:115-118 use them: "<name>-v<ver>" ->
+    "<name>-sparse-v<ver>" (namespace kept)."""
+    name, sep, version = id.rpartition("-v")
+    if not sep or not version.isdigit():
+        raise ValueError(f"malformed env id {id!r}")
+    return f"{name}-sparse-v{version}"
+
+
+def register(id: str, vector_entry_point: Callable, kwargs: dict | None = None, max_episode_steps=None,
+             register_sparse_version: bool = True):
+    """registration.py:87-142: every id also gets a "-sparse" variant whose loss (and so reward) is
+    masked to the last step of each episode (SparsifyVectorWrapper / SparsifyWrapper)."""
     registry[id] = EnvSpec(id, vector_entry_point, dict(kwargs or {}), max_episode_steps)
+    if register_sparse_version:
+        sid = sparse_id(id)
+        registry[sid] = EnvSpec(sid, vector_entry_point, dict(kwargs or {}, sparse=True), max_episode_steps)
 
 
 def _lidar(num_envs: int = 1, **kwargs):

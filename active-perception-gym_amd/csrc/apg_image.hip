@@ -328,6 +328,7 @@ struct EnvArgs {
   double ce_scale, ce_offset;
   float mse_scale, mse_offset;
   float time_value;
+  float loss_weight;  // 1, or for the -sparse ids terminated.astype(float32) (one value: episodes end together)
 };
 
 // scipy.special.log_softmax(row)[target] in float32 (x_max zeroed when not finite); -> -value
@@ -395,6 +396,11 @@ APG_DEV uint32_t env_tail(const EnvArgs &a, int e, const float *__restrict__ act
                           const apg_image_outputs &out, double loss_d, float loss_f) {
   uint32_t err = 0;
   double px = pos[2 * e], py = pos[2 * e + 1];
+  // WeightedLossFn (loss_fn.py:307-316): loss * weight; f64 * f32 -> f64 (classify), f32 * f32 (localize).
+  // weight 1 leaves the loss bit-identical (including inf / NaN), so the dense ids share this path.
+  loss_d = __dmul_rn(loss_d, (double)a.loss_weight);
+  loss_f = __fmul_rn(loss_f, a.loss_weight);
+  if (a.kind != APG_IMAGE_CLASSIFY) loss_d = (double)loss_f;
   if (a.resetting) {
     // module.reset() replaced the batch; base_reward = np.zeros(N) (float64)
     out.base_reward[e] = 0.0f;
@@ -914,6 +920,7 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
   const int32_t t_new = prev_done ? 0 : t + 1;
   a.t_new = t_new;
   a.time_value = (float)(((double)t_new / (double)c->step_limit) * 2.0 - 1.0);
+  a.loss_weight = !c->sparse ? 1.0f : (!prev_done && t_new >= c->step_limit ? 1.0f : 0.0f);
   if (c->kind == APG_IMAGE_CLASSIFY) {
     int epb = 256 / CLS_LANES;
     while (epb > 1 && (size_t)epb * (c->num_classes + 1) * sizeof(float) > 64 * 1024) epb /= 2;

@@ -245,7 +245,7 @@ __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, ui
 }
 
 struct StepParams {
-  int n, h, w, wpr, beams, step_limit, is_static, R, wrows, log_stats;
+  int n, h, w, wpr, beams, step_limit, is_static, R, wrows, log_stats, sparse;
   float range, loss_scale, loss_offset;
 };
 
@@ -362,6 +362,7 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
         O.loss[e] = 0.0f;
         O.info_mask[e] = 0;
         if (P.log_stats) O.stats_len[e] = 0;
+        if (P.sparse) O.weight[e] = 0.0;
         f &= (uint8_t)~(F_JUST_RESET | F_AUTORESET);
       } else {
         float ax = act[2 * e], ay = act[2 * e + 1];
@@ -378,6 +379,7 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
           O.loss[e] = 0.0f;
           O.info_mask[e] = 0;
           if (P.log_stats) O.stats_len[e] = 0;
+          if (P.sparse) O.weight[e] = 0.0;
         } else {
           const float lpx = pos0, lpy = pos1;
           const float br = __fsub_rn(0.1f, __fmul_rn(0.001f, __fadd_rn(__fmul_rn(ax, ax), __fmul_rn(ay, ay))));
@@ -446,7 +448,12 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
           O.target[2 * e] = tgx;
           O.target[2 * e + 1] = tgy;
           O.loss[e] = loss;
-          O.reward[e] = (double)__fsub_rn(br, loss);
+          if (P.sparse) {  // SparsifyWrapper: base_reward - loss * (1.0 if terminated else 0.0), in f32
+            O.weight[e] = term ? 1.0 : 0.0;
+            O.reward[e] = (double)__fsub_rn(br, __fmul_rn(loss, term ? 1.0f : 0.0f));
+          } else {
+            O.reward[e] = (double)__fsub_rn(br, loss);
+          }
           O.terminated[e] = term;
           O.truncated[e] = 0;
           O.info_mask[e] = 1;
@@ -612,6 +619,7 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   P.beams = cfg->beams;
   P.step_limit = cfg->step_limit;
   P.log_stats = cfg->log_stats ? 1 : 0;
+  P.sparse = cfg->sparse ? 1 : 0;
   P.is_static = cfg->is_static;
   P.R = (int)ceilf(cfg->lidar_range);
   P.wrows = MAX_WIN_ROWS;
@@ -672,6 +680,7 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
   if (!action || !prediction) return fail(APG_E_INVALID, "null action/prediction");
   if (cfg->log_stats && (!st->stats_hist || !out->stats || !out->stats_len))
     return fail(APG_E_INVALID, "log_stats needs stats_hist, stats and stats_len buffers");
+  if (cfg->sparse && !out->weight) return fail(APG_E_INVALID, "sparse needs the weight buffer");
   hipStream_t s = (hipStream_t)stream;
   Geo g = make_geo(cfg);
   if ((rc = launch_reset(g, st, 0, 0, 0, out, s))) return rc;

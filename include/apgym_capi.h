@@ -88,6 +88,8 @@ typedef struct apg_lidar_config {
   float loss_scale, loss_offset;/* normalized MSE affine, as float32 (NEP 50) */
   double branching_prob;        /* FloorMapDatasetMaze parameter */
   int32_t log_stats;            /* 1: ActiveRegressionLogWrapper episode statistics (registered ids) */
+  int32_t sparse;               /* 1: the -sparse ids (SparsifyWrapper, sparsify_wrapper.py:93-161):
+                                   reward = base_reward - loss * (terminated ? 1 : 0) */
 } apg_lidar_config;
 
 /* Persistent per-env state.  Sizes come from apg_lidar_query_sizes(). */
@@ -124,6 +126,7 @@ typedef struct apg_lidar_outputs {
   float *stats;        /* [4][N] avg_euclidean_distance, avg_mse, final_euclidean_distance, final_mse
                           of the episodes that ended this step (log_stats) */
   int32_t *stats_len;  /* [N] length of the episode that ended this step, 0 = no stats (log_stats) */
+  double *weight;      /* [N] sparse: info["prediction"]["target"]["weight"] (1.0 where terminated) or NULL */
 } apg_lidar_outputs;
 
 typedef struct apg_lidar_state_sizes {
@@ -209,6 +212,8 @@ typedef struct apg_image_config {
   double ce_scale, ce_offset; /* normalized CrossEntropyLossFn affine (float64) */
   float mse_scale, mse_offset;/* normalized MSELossFn affine (float32, NEP 50) */
   int32_t log_stats;          /* 1: the registered ids' vector log wrapper statistics */
+  int32_t sparse;             /* 1: the -sparse ids (SparsifyVectorWrapper, sparsify_wrapper.py:23-92):
+                                 reward = base_reward - loss * terminated */
 } apg_image_config;
 
 typedef struct apg_image_state {

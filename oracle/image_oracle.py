@@ -157,7 +157,8 @@ class ImageVectorEnvOracle:
     """Vector image env restated with numpy Generators (kind "cls" or "loc")."""
 
     def __init__(self, kind, pool, labels, num_classes, channels, num_envs, sensor=(5, 5), scale=1.0,
-                 step_limit=16, max_step_length=0.2, invert=False, top_k=10, rel=0.2, log_stats=True):
+                 step_limit=16, max_step_length=0.2, invert=False, top_k=10, rel=0.2, log_stats=True,
+                 sparse=False):
         self.kind, self.n = kind, num_envs
         self.pool = images_f32(pool, channels)
         self.labels_pool = np.asarray(labels).astype(np.int32)
@@ -166,6 +167,7 @@ class ImageVectorEnvOracle:
         self.msl = np.ones(2) * np.array(max_step_length)
         self.invert, self.top_k, self.rel = invert, top_k, rel
         self.log_stats = log_stats
+        self.sparse = sparse
 
     # --- seeding chain: VectorEnv.reset(seed) -> _np_random setter -> module.seed
     def seed(self, seed):
@@ -301,6 +303,11 @@ class ImageVectorEnvOracle:
         info = {"index": self.idx, "base_reward": base, "prediction": {"target": target, "loss": loss}}
         if self.log_stats:
             info = self._log(prediction, info, term | trunc)
+        if self.sparse:
+            # SparsifyVectorWrapper.step (sparsify_wrapper.py:61-87) with WeightedLossFn (loss_fn.py:307-316)
+            weight = term.astype(np.float32)
+            info["prediction"]["target"] = {"target": target, "weight": weight}
+            return obs, base - loss * weight, term, trunc, info
         return obs, base - loss, term, trunc, info
 
     @staticmethod

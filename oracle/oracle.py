@@ -85,7 +85,7 @@ class OracleLidarVectorEnv:
     """SyncVectorEnv(TimeLimit(LIDARLocalization2DEnv)) restated in C; numpy in/out."""
 
     def __init__(self, num_envs, map_kind="rooms", size=32, static_map=False, static_map_index=0, beams=8,
-                 lidar_range=5, step_limit=100):
+                 lidar_range=5, step_limit=100, sparse=False):
         self.n, self.h, self.w, self.beams = num_envs, size, size, beams
         self.static = static_map
         self.dirs = beam_directions(beams, lidar_range)
@@ -106,6 +106,8 @@ class OracleLidarVectorEnv:
         self.target = np.zeros((n, 2), np.float32)
         self.loss = np.zeros(n, np.float32)
         self.info_mask = np.zeros(n, np.uint8)
+        self.sparse = sparse
+        self.weight = np.zeros(n, np.float64)
 
     def close(self):
         if self._e:
@@ -121,10 +123,21 @@ class OracleLidarVectorEnv:
     def step(self, action, prediction) -> int:
         a = np.ascontiguousarray(action, np.float32)
         p = np.ascontiguousarray(prediction, np.float32)
-        return lib().orc_lidar_step(self._e, _p(a), _p(p), _p(self.lidar), _p(self.odometry), _p(self.time_step),
-                                    _p(self.map), _p(self.reward), _p(self.terminated), _p(self.truncated),
-                                    _p(self.base_reward), _p(self.target), _p(self.loss), _p(self.info_mask),
-                                    _p(self.map_idx))
+        rc = lib().orc_lidar_step(self._e, _p(a), _p(p), _p(self.lidar), _p(self.odometry), _p(self.time_step),
+                                  _p(self.map), _p(self.reward), _p(self.terminated), _p(self.truncated),
+                                  _p(self.base_reward), _p(self.target), _p(self.loss), _p(self.info_mask),
+                                  _p(self.map_idx))
+        if self.sparse:
+            # SparsifyWrapper.step per sub-env (sparsify_wrapper.py:137-151): weight = 1.0 if terminated
+            # else 0.0 (SyncVectorEnv merges the floats into float64); reward = base_reward - loss * weight
+            # in float32 (np.float32 loss times a Python float), stored as float64
+            m = self.info_mask.astype(bool)
+            w = np.where(self.terminated.astype(bool), np.float32(1.0), np.float32(0.0))
+            with np.errstate(invalid="ignore"):
+                r = (self.base_reward - self.loss * w).astype(np.float64)
+            self.weight = np.where(m, w.astype(np.float64), 0.0)
+            self.reward = np.where(m, r, 0.0)
+        return rc
 
     def state(self):
         n = self.n

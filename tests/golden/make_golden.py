@@ -166,16 +166,36 @@ def make_lidar_scan():
          distance=np.array(dist, np.float32))
 
 
-def run_lidar_env(name, dataset, static, beams, n_envs, steps, seed, action_mode):
+def _reset_prediction_info_shim(ap):
+    """Generation harness for the LIDAR "-sparse" fixtures only.  The reference's SparsifyWrapper.reset
+    reads info["prediction"]["target"] (sparsify_wrapper.py:128-135, 160), which
+    LIDARLocalization2DEnv.reset does not return (lidar_localization2d.py:315), so the reference's
+    LIDARLoc*-sparse ids raise KeyError in reset.  This wrapper, placed below SparsifyWrapper, adds
+    info["prediction"] = {"target": None} to reset infos so that the wrapper's unmodified step can
+    be recorded.  Step infos pass through untouched."""
+
+    class ResetPredictionInfo(ap.ActivePerceptionWrapper):
+        def reset(self, **kwargs):
+            obs, info = self.env.reset(**kwargs)
+            info["prediction"] = {"target": None}
+            return obs, info
+
+    return ResetPredictionInfo
+
+
+def run_lidar_env(name, dataset, static, beams, n_envs, steps, seed, action_mode, sparse=False):
     lmod = _lidar_module()
     gym = sys.modules["gymnasium"]
     ap = sys.modules["ap_gym"]
+    sw = refload.load("sparsify_wrapper") if sparse else None
 
     def mk():
         env = lmod.LIDARLocalization2DEnv(dataset=dataset, static_map=static, lidar_beam_count=beams,
                                           prefetch=False)
         env = ap.TimeLimit(env, max_episode_steps=100, issue_termination=True)
-        return ap.ActiveRegressionLogWrapper(env)
+        env = ap.ActiveRegressionLogWrapper(env)
+        # the "-sparse" ids (registration.py:115-142): SparsifyWrapper over the registered composition
+        return sw.SparsifyWrapper(_reset_prediction_info_shim(ap)(env)) if sparse else env
 
     venv = gym.vector.SyncVectorEnv([mk for _ in range(n_envs)])
     obs, info = venv.reset(seed=seed)
@@ -189,10 +209,13 @@ def run_lidar_env(name, dataset, static, beams, n_envs, steps, seed, action_mode
                             [-0.5, -0.5], [1, 0], [0, -1], [0, 0]], np.float32)
         actions = choices[arng.integers(0, len(choices), (steps, n_envs))]
     preds = arng.uniform(-1, 1, (steps, n_envs, 2)).astype(np.float32)
-    rec = {k: [] for k in ("lidar", "odometry", "time_step", "map", "reward", "terminated", "truncated",
+    if sparse:  # overflowing squared errors: loss inf, and inf * weight 0 is NaN in the sparse reward
+        preds[5::7, 0] = np.float32(1e20)
+    rec = {k: [] for k in ("weight",) if sparse}
+    rec.update({k: [] for k in ("lidar", "odometry", "time_step", "map", "reward", "terminated", "truncated",
                            "base_reward", "target", "loss", "info_mask", "stats_mask", "stats_avg_euclidean_distance",
                            "stats_avg_mse", "stats_final_euclidean_distance", "stats_final_mse",
-                           "stats_len")}
+                           "stats_len")})
     vec = {"euclidean_distance": [], "mse": []}  # ActiveRegressionLogWrapper "vector" lists, concatenated
     reset_obs = obs
     reset_map_idx = np.asarray(info["map_idx"], dtype=np.int64)
@@ -209,9 +232,18 @@ def run_lidar_env(name, dataset, static, beams, n_envs, steps, seed, action_mode
         mask = info.get("_base_reward", np.zeros(n_envs, bool))
         rec["info_mask"].append(mask)
         rec["base_reward"].append(np.where(mask, info.get("base_reward", np.zeros(n_envs, np.float32)), 0))
-        rec["target"].append(np.where(mask[:, None], info["prediction"]["target"] if "prediction" in info
+        tgt = info["prediction"]["target"] if "prediction" in info else None
+        if sparse and tgt is not None:
+            w = np.asarray(tgt["weight"])
+            # (autoreset envs carry the shim's reset info too; only the stepped envs are recorded)
+            assert w.dtype == np.float64 and np.all(tgt["_weight"][mask])
+            rec["weight"].append(np.where(mask, w, 0.0))
+            tgt = np.stack([np.zeros(2, np.float32) if v is None else v for v in tgt["target"]])
+        elif sparse:
+            rec["weight"].append(np.zeros(n_envs))
+        rec["target"].append(np.where(mask[:, None], tgt if tgt is not None
                                       else np.zeros((n_envs, 2), np.float32), 0).astype(np.float32))
-        rec["loss"].append(np.where(mask, info["prediction"]["loss"] if "prediction" in info
+        rec["loss"].append(np.where(mask, info["prediction"]["loss"] if "loss" in info.get("prediction", {})
                                     else np.zeros(n_envs, np.float32), 0).astype(np.float32))
         smask = info.get("_stats", np.zeros(n_envs, bool))
         rec["stats_mask"].append(smask)
@@ -262,7 +294,7 @@ def _image_modules():
 
 
 def run_image_env(name, kind, pool_shape, channels, num_classes, sensor, scale, step_limit, invert, n_envs,
-                  steps, seed, pool_len, pool_seed):
+                  steps, seed, pool_len, pool_seed, sparse=False):
     ipm, icd, ic, il = _image_modules()
     prng = np.random.default_rng(pool_seed)
     pool = prng.integers(0, 256, (pool_len, *pool_shape), dtype=np.uint8)
@@ -288,6 +320,8 @@ def run_image_env(name, kind, pool_shape, channels, num_classes, sensor, scale, 
     # the registered ids wrap the vector env in the vector log wrapper (registration.py:185-192, 263-269)
     ap = sys.modules["ap_gym"]
     env = (ap.ActiveClassificationVectorLogWrapper if kind == "cls" else ap.ActiveRegressionVectorLogWrapper)(env)
+    if sparse:  # the "-sparse" ids (registration.py:115-142)
+        env = refload.load("sparsify_wrapper").SparsifyVectorWrapper(env)
     obs, info = env.reset(seed=seed)
     arng = np.random.default_rng(11)
     actions = arng.uniform(-1.5, 1.5, (steps, n_envs, 2)).astype(np.float32)
@@ -295,6 +329,11 @@ def run_image_env(name, kind, pool_shape, channels, num_classes, sensor, scale, 
         preds = arng.standard_normal((steps, n_envs, num_classes)).astype(np.float32)
     else:
         preds = arng.uniform(-1, 1, (steps, n_envs, 2)).astype(np.float32)
+    if sparse:  # infinite losses: inf * weight 0 is NaN in the sparse reward
+        if kind == "cls":
+            preds[2::5, 0, 1:] = -np.inf
+        else:
+            preds[2::5, 0] = np.float32(1e20)
     out = {"pool": pool, "labels": labels, "actions": actions, "predictions": preds, "seed": np.array(seed),
            "config": np.array([pool_shape[0], pool_shape[1], channels, num_classes, sensor[0], sensor[1],
                                step_limit, int(invert), n_envs, steps], np.int64),
@@ -306,8 +345,12 @@ def run_image_env(name, kind, pool_shape, channels, num_classes, sensor, scale, 
     for t in range(steps):
         obs, rew, term, trunc, info = env.step({"action": actions[t], "prediction": preds[t]})
         fields = dict(obs)
+        tgt = info["prediction"]["target"]
+        if sparse:
+            fields["weight"] = np.asarray(tgt["weight"])
+            tgt = tgt["target"]
         fields.update(reward=rew, terminated=term, truncated=trunc, index=np.asarray(info["index"], np.int64),
-                      base_reward=np.asarray(info["base_reward"]), target=np.asarray(info["prediction"]["target"]),
+                      base_reward=np.asarray(info["base_reward"]), target=np.asarray(tgt),
                       loss=np.asarray(info["prediction"]["loss"]))
         for k, v in fields.items():
             v = np.asarray(v)
@@ -342,8 +385,18 @@ def make_image_env():
     run_image_env("loc_rect", "loc", (24, 20, 3), 3, 5, (4, 4), 1.25, 6, False, 4, 16, 9, 10, 105)
 
 
+def make_sparse_env():
+    """The "-sparse" ids (registration.py:115-142): SparsifyWrapper / SparsifyVectorWrapper."""
+    fm = refload.load("envs.floor_map")
+    run_lidar_env("maze21_b8_sparse", fm.FloorMapDatasetMaze(), False, 8, 8, 110, 7, "uniform", sparse=True)
+    run_image_env("cls_mnist_sparse", "cls", (28, 28), 1, 10, (5, 5), 1.0, 16, False, 8, 40, 0, 40, 100, sparse=True)
+    run_image_env("loc_rect_sparse", "loc", (24, 20, 3), 3, 5, (4, 4), 1.25, 6, False, 4, 16, 9, 10, 105,
+                  sparse=True)
+
+
 SECTIONS = {"rng": make_rng, "maps": make_maps, "loss": make_loss, "scan": make_lidar_scan,
-            "lidar": make_lidar_env, "image": make_image_env}
+            "lidar": make_lidar_env, "image": make_image_env,
+            "sparse": make_sparse_env}
 
 
 def main(argv):

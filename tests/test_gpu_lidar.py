@@ -21,6 +21,7 @@ ENV_CASES = {
     "maze21_b8": ("maze", 21, False, 8),
     "maze21_b8_grid": ("maze", 21, False, 8),
     "maze127_b64": ("maze", 127, False, 64),
+    "maze21_b8_sparse": ("maze", 21, False, 8),  # LIDARLocMaze-sparse-v0 (SparsifyWrapper per sub-env)
 }
 
 
@@ -146,8 +147,9 @@ def test_vector_env_matches_reference_trace(gpu, name):
     kind, size, static, beams = ENV_CASES[name]
     d = golden(f"lidar_env_{name}.npz")
     n = d["actions"].shape[1]
+    sparse = name.endswith("_sparse")
     env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_ds(ap, kind, size), static_map=static,
-                                          lidar_beam_count=beams, device=gpu, log_stats=True)
+                                          lidar_beam_count=beams, device=gpu, log_stats=True, sparse=sparse)
     obs, info = env.reset(seed=int(d["seed"]))
     vec_off = 0
     assert np.array_equal(obs["lidar"], d["reset_lidar"])
@@ -162,13 +164,18 @@ def test_vector_env_matches_reference_trace(gpu, name):
         assert np.array_equal(obs["lidar"], d["lidar"][t]), (name, t)
         assert np.array_equal(obs["odometry"], d["odometry"][t]), (name, t)
         assert np.array_equal(obs["time_step"], d["time_step"][t]), (name, t)
-        assert np.array_equal(rew, d["reward"][t]), (name, t)
+        assert np.array_equal(rew, d["reward"][t], equal_nan=True), (name, t)
         assert np.array_equal(term, d["terminated"][t]) and np.array_equal(trunc, d["truncated"][t]), (name, t)
         mask = d["info_mask"][t]
         if mask.any():
             assert np.array_equal(info["_base_reward"], mask)
             assert np.array_equal(info["base_reward"], d["base_reward"][t]), (name, t)
-            assert np.array_equal(info["prediction"]["target"], d["target"][t]), (name, t)
+            tgt = info["prediction"]["target"]
+            if sparse:  # {"target", "_target", "weight" (float64), "_weight"} as SyncVectorEnv merges them
+                assert np.array_equal(tgt["_target"], mask) and np.array_equal(tgt["_weight"], mask)
+                assert tgt["weight"].dtype == np.float64 and np.array_equal(tgt["weight"], d["weight"][t]), (name, t)
+                tgt = tgt["target"]
+            assert np.array_equal(tgt, d["target"][t]), (name, t)
             assert np.array_equal(info["prediction"]["loss"], d["loss"][t]), (name, t)
         else:
             assert "base_reward" not in info
@@ -198,14 +205,17 @@ def test_vector_env_matches_reference_trace(gpu, name):
     env.close()
 
 
-@pytest.mark.parametrize("kind,size,beams,n,steps", [("rooms", 64, 32, 1024, 230), ("maze", 21, 8, 1024, 120),
-                                                     ("maze", 127, 64, 64, 40), ("rooms", 32, 16, 512, 120)])
-def test_vector_env_matches_oracle(gpu, oracle_mod, kind, size, beams, n, steps):
+@pytest.mark.parametrize("kind,size,beams,n,steps,sparse", [("rooms", 64, 32, 1024, 230, False),
+                                                            ("maze", 21, 8, 1024, 120, False),
+                                                            ("maze", 127, 64, 64, 40, False),
+                                                            ("rooms", 32, 16, 512, 120, False),
+                                                            ("rooms", 64, 32, 1024, 120, True)])
+def test_vector_env_matches_oracle(gpu, oracle_mod, kind, size, beams, n, steps, sparse):
     import ap_gym_amd as ap
 
     env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_ds(ap, kind, size), lidar_beam_count=beams,
-                                          device=gpu, log_stats=True)
-    ref = oracle_mod.OracleLidarVectorEnv(n, kind, size, False, 0, beams)
+                                          device=gpu, log_stats=True, sparse=sparse)
+    ref = oracle_mod.OracleLidarVectorEnv(n, kind, size, False, 0, beams, sparse=sparse)
     obs, _ = env.reset(seed=123)
     ref.reset(123)
     assert np.array_equal(obs["lidar"], ref.lidar)
@@ -214,11 +224,14 @@ def test_vector_env_matches_oracle(gpu, oracle_mod, kind, size, beams, n, steps)
     for t in range(steps):
         a = rng.uniform(-1.5, 1.5, (n, 2)).astype(np.float32)
         p = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        if sparse:  # a few overflowing losses: inf * weight 0 is NaN in the sparse reward
+            p[rng.random(n) < 0.01] = np.float32(3e19)
         obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
         ref.step(a, p)
         for i in np.nonzero(ref.info_mask)[0]:
             d = ref.target[i] - p[i]
-            hist[i].append((np.linalg.norm(d), np.mean(d ** 2)))
+            with np.errstate(over="ignore"):
+                hist[i].append((np.linalg.norm(d), np.mean(d ** 2)))
         done = (ref.terminated | ref.truncated).astype(bool)
         assert np.array_equal(info.get("_stats", np.zeros(n, bool)), done), t
         for i in np.nonzero(done)[0]:
@@ -232,20 +245,25 @@ def test_vector_env_matches_oracle(gpu, oracle_mod, kind, size, beams, n, steps)
         assert np.array_equal(obs["lidar"], ref.lidar), t
         assert np.array_equal(obs["odometry"], ref.odometry), t
         assert np.array_equal(obs["time_step"], ref.time_step), t
-        assert np.array_equal(rew, ref.reward), t
+        assert np.array_equal(rew, ref.reward, equal_nan=True), t
         assert np.array_equal(term, ref.terminated.astype(bool)), t
+        if sparse and "prediction" in info:
+            m = ref.info_mask.astype(bool)
+            assert np.array_equal(info["prediction"]["target"]["weight"][m], ref.weight[m]), t
         assert np.array_equal(obs["map"][..., 0], ref.map), t
     env.close()
 
 
-def test_torch_backend_matches_numpy_backend(gpu):
+@pytest.mark.parametrize("env_id", ["LIDARLocRooms-v0", "LIDARLocRooms-sparse-v0"])
+def test_torch_backend_matches_numpy_backend(gpu, env_id):
     import torch
 
     import ap_gym_amd as ap
 
     kw = dict(num_envs=256, lidar_beam_count=32, dataset=ap.FloorMapDatasetRooms(64, 64), device=gpu)
-    e_np = ap.make_vec("LIDARLocRooms-v0", **kw)
-    e_t = ap.make_vec("LIDARLocRooms-v0", array_backend="torch", **kw)
+    e_np = ap.make_vec(env_id, **kw)
+    e_t = ap.make_vec(env_id, array_backend="torch", **kw)
+    assert e_np.sparse == env_id.endswith("-sparse-v0")
     e_np.reset(seed=5)
     e_t.reset(seed=5)
     rng = np.random.default_rng(2)
@@ -259,6 +277,11 @@ def test_torch_backend_matches_numpy_backend(gpu):
         assert np.array_equal(r1, r2.cpu().numpy())
         assert np.array_equal(te1, te2.cpu().numpy())
         assert np.array_equal(o1["map"], o2["map"].cpu().numpy())
+        if e_np.sparse and "prediction" in i1:
+            m = i1["_base_reward"]
+            w1, w2 = i1["prediction"]["target"]["weight"], i2["prediction"]["target"]["weight"].cpu().numpy()
+            assert np.array_equal(w1[m], w2[m]) and np.array_equal(w1[m], te1[m].astype(np.float64))
+            assert np.array_equal(i2["prediction"]["target"]["_weight"].cpu().numpy(), m)
     e_t.check_errors()
 
 

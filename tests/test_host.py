@@ -147,3 +147,58 @@ def test_image_registry_and_spaces():
     pool, lab = ds.device_pool()
     assert pool.dtype == np.uint8 and pool.shape == (20, 28, 28, 1)
     assert np.array_equal(imgs, pool[[0, 3]].astype(np.float32) / 255)
+
+
+def test_ctypes_layouts_match_the_c_header(tmp_path):
+    """Every ctypes mirror in _native.py has the size and field offsets gcc gives include/apgym_capi.h."""
+    import ctypes
+    import os
+    import shutil
+    import subprocess
+
+    from ap_gym_amd import _native as N
+
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    structs = {"apg_pcg64": N.Pcg64, "apg_lidar_config": N.LidarConfig, "apg_lidar_state": N.LidarState,
+               "apg_lidar_outputs": N.LidarOutputs, "apg_lidar_state_sizes": N.LidarSizes,
+               "apg_image_config": N.ImageConfig, "apg_image_state": N.ImageState,
+               "apg_image_outputs": N.ImageOutputs}
+    lines = ["#include <stdio.h>", "#include \"apgym_capi.h\"", "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'  printf("{cname} %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'  printf("{cname}.{fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                              text=True).stdout.splitlines())
+    for cname, py in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert int(got[f"{cname}.{fname}"]) == getattr(py, fname).offset, (cname, fname)
+
+
+def test_sparse_ids_and_weighted_loss():
+    """registration.py:115-142: every id has a "-sparse" twin; WeightedLossFn (loss_fn.py:292-349)."""
+    import ap_gym_amd as ap
+    from ap_gym_amd.registration import sparse_id
+
+    dense = [i for i in ap.registry if "-sparse-" not in i]
+    assert dense and all(sparse_id(i) in ap.registry for i in dense)
+    assert sparse_id("MNIST-train-v0") == "MNIST-train-sparse-v0"
+    assert ap.registry["LIDARLocRooms-sparse-v0"].kwargs["sparse"] is True
+    assert "sparse" not in ap.registry["LIDARLocRooms-v0"].kwargs
+    assert len(ap.registry) == 2 * len(dense)
+    inner = ap.MSELossFn(target_std=2 / np.sqrt(12)).normalized
+    fn = ap.WeightedLossFn(inner)
+    rng = np.random.default_rng(0)
+    p = rng.uniform(-1, 1, (6, 2)).astype(np.float32)
+    t = rng.uniform(-1, 1, (6, 2)).astype(np.float32)
+    w = np.array([0, 1, 0, 1, 1, 0], np.float32)
+    got = fn.numpy(p, {"target": t, "weight": w}, (6,))
+    assert np.array_equal(got, inner.numpy(p, t, (6,)) * w) and got.dtype == np.float32

@@ -19,6 +19,7 @@ ENV_CASES = {
     "maze21_b8": ("maze", 21, False, 8),
     "maze21_b8_grid": ("maze", 21, False, 8),
     "maze127_b64": ("maze", 127, False, 64),
+    "maze21_b8_sparse": ("maze", 21, False, 8),  # LIDARLocMaze-sparse-v0 (SparsifyWrapper per sub-env)
 }
 
 
@@ -76,7 +77,8 @@ def test_vector_env_trace(oracle_mod, name):
     kind, size, static, beams = ENV_CASES[name]
     d = golden(f"lidar_env_{name}.npz")
     n = d["actions"].shape[1]
-    env = oracle_mod.OracleLidarVectorEnv(n, kind, size, static, 0, beams)
+    sparse = name.endswith("_sparse")
+    env = oracle_mod.OracleLidarVectorEnv(n, kind, size, static, 0, beams, sparse=sparse)
     env.reset(int(d["seed"]))
     assert np.array_equal(env.lidar, d["reset_lidar"])
     assert np.array_equal(env.odometry, d["reset_odometry"])
@@ -88,13 +90,16 @@ def test_vector_env_trace(oracle_mod, name):
                          ("reward", env.reward), ("terminated", env.terminated.astype(bool)),
                          ("truncated", env.truncated.astype(bool)), ("base_reward", env.base_reward),
                          ("target", env.target), ("loss", env.loss), ("info_mask", env.info_mask.astype(bool))):
-            assert np.array_equal(got, d[key][t]), f"{name} step {t} {key}"
+            assert np.array_equal(got, d[key][t], equal_nan=got.dtype.kind == "f"), f"{name} step {t} {key}"
+        if sparse:
+            assert np.array_equal(env.weight, d["weight"][t]), f"{name} step {t} weight"
         if not static:
             assert np.array_equal(np.packbits(env.map > 0, axis=-1), d["map"][t]), f"{name} step {t} map"
     assert str(d["reward_dtype"]) == "float64" and str(d["base_reward_dtype"]) == "float32"
 
 
-IMAGE_CASES = ["cls_mnist", "cls_tin", "cls_gray3_rect", "loc_mnist", "loc_tin12", "loc_rect"]
+IMAGE_CASES = ["cls_mnist", "cls_tin", "cls_gray3_rect", "loc_mnist", "loc_tin12", "loc_rect",
+               "cls_mnist_sparse", "loc_rect_sparse"]  # *_sparse: SparsifyVectorWrapper over the log wrapper
 
 
 @pytest.mark.parametrize("name", IMAGE_CASES)
@@ -105,19 +110,26 @@ def test_image_oracle_matches_reference_trace(name):
     g = golden(f"image_{name}.npz")
     h, w, c, k, s0, s1, lim, inv, n, steps = (int(v) for v in g["config"])
     env = io.ImageVectorEnvOracle(str(g["kind"]), g["pool"], g["labels"], k, c, n, (s0, s1),
-                                  float(g["sensor_scale"]), lim, invert=bool(inv))
+                                  float(g["sensor_scale"]), lim, invert=bool(inv), sparse=name.endswith("_sparse"))
     obs, info = env.reset(int(g["seed"]))
     for key, v in obs.items():
         assert np.array_equal(v, g["reset_" + key]) and v.dtype == g["reset_" + key].dtype, key
     assert np.array_equal(info["index"], g["reset_index"])
     for t in range(steps):
-        obs, rew, term, trunc, info = env.step(g["actions"][t], g["predictions"][t])
+        with np.errstate(invalid="ignore", over="ignore"):
+            obs, rew, term, trunc, info = env.step(g["actions"][t], g["predictions"][t])
+        tgt = info["prediction"]["target"]
         fields = dict(obs, reward=rew, terminated=term, truncated=trunc, index=info["index"],
-                      base_reward=info["base_reward"], target=info["prediction"]["target"],
-                      loss=info["prediction"]["loss"])
+                      base_reward=info["base_reward"], loss=info["prediction"]["loss"])
+        if isinstance(tgt, dict):
+            fields.update(target=tgt["target"], weight=tgt["weight"])
+        else:
+            fields["target"] = tgt
+        assert set(k for k in fields) == set(k[5:] for k in g.files if k.startswith("step_") and
+                                             not k.endswith("_dtype") and k != "step_stats_mask")
         for key, v in fields.items():
             v = np.asarray(v)
-            assert np.array_equal(v, g["step_" + key][t]), (t, key)
+            assert np.array_equal(v, g["step_" + key][t], equal_nan=v.dtype.kind == "f"), (t, key)
             assert str(v.dtype) == g["step_" + key + "_dtype"][t], (t, key)
         assert ("stats" in info) == bool(g["step_stats_mask"][t].any())
         if "stats" in info:
