@@ -48,7 +48,7 @@ int check_launch(const char *what) {
 namespace {
 
 constexpr uint8_t F_AUTORESET = 1, F_JUST_RESET = 2, F_FIRST = 4;
-constexpr int EPB = 64;        // envs per step workgroup
+constexpr int EPB = 64;        // envs per step workgroup (= one wave: lane = env in phases 1 and 2a)
 constexpr int STEP_THREADS = 256;
 constexpr int MAX_WIN_ROWS = 32;
 constexpr int WIN_STRIDE = MAX_WIN_ROWS + 1;  // LDS words per env window (+1: lanes = envs hit distinct banks)
@@ -279,6 +279,8 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
   __shared__ int s_x0[EPB], s_y0[EPB];
   __shared__ uint32_t s_win[EPB * WIN_STRIDE];
   __shared__ float s_lid[EPB * (MAX_STAGED_BEAMS + 1)];
+  __shared__ uint16_t s_queue[EPB * MAX_STAGED_BEAMS];  // phase 2b work list: (beam << 6) | env
+  __shared__ int s_qn;
   const int tid = threadIdx.x;
   const int base = blockIdx.x * EPB;
   const size_t words = (size_t)P.h * P.wpr;
@@ -294,7 +296,10 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
       rs = (S.flags[e] & F_JUST_RESET) != 0;
     }
     const unsigned long long m = __ballot(rs);
-    if (tid == 0) s_reset = m;
+    if (tid == 0) {
+      s_reset = m;
+      s_qn = 0;
+    }
   }
   __syncthreads();
   // map obs of the envs that reset this step: bool map / 255 (lidar_localization2d.py:299), written by
@@ -482,25 +487,47 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
   }
   __syncthreads();
 
-  // ---------------- phase 2: lane = env, wave = beam index (all 64 lanes of a wave cast the same
-  // beam direction, so trip counts and branch paths agree across lanes); results staged in LDS and
-  // written out coalesced.
+  // ---------------- phase 2a: lane = env, wave = beam index (all 64 lanes of a wave cast the same
+  // beam direction).  Beams whose bounding box holds no occupied cell are SCAN_EMPTY and finish
+  // here; the others are queued (env, beam) in LDS, grouped by beam, for 2b.
   const int el = tid & (EPB - 1), e = base + el;
   const bool staged = P.beams <= MAX_STAGED_BEAMS;
-  if (e < P.n) {
-    const float px = s_pos[el][0], py = s_pos[el][1];
-    const RowsWindow rw{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
-    for (int beam = tid / EPB; beam < P.beams; beam += STEP_THREADS / EPB) {
+  const float px = s_pos[el][0], py = s_pos[el][1];
+  const RowsWindow rw{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
+  for (int beam = tid / EPB; beam < P.beams; beam += STEP_THREADS / EPB) {
+    bool walk = false;
+    if (e < P.n) {
       const float qx = __fadd_rn(px, S.beam_dirs[2 * beam]), qy = __fadd_rn(py, S.beam_dirs[2 * beam + 1]);
-      const float d = lidar_scan(rw, px, py, qx, qy).dist;
-      const float v = fminf(fmaxf(f32_div(d, P.range), -1.0f), 1.0f);
-      if (staged)
-        s_lid[el * (MAX_STAGED_BEAMS + 1) + beam] = v;
-      else
-        O.lidar[(size_t)e * P.beams + beam] = v;
+      walk = scan_may_hit(rw, px, py, qx, qy);
+      if (!walk || !staged) {
+        const float d = walk ? lidar_scan_walk(rw, px, py, qx, qy).dist : scan_empty(px, py, qx, qy).dist;
+        const float v = fminf(fmaxf(f32_div(d, P.range), -1.0f), 1.0f);
+        if (staged)
+          s_lid[el * (MAX_STAGED_BEAMS + 1) + beam] = v;
+        else
+          O.lidar[(size_t)e * P.beams + beam] = v;
+      }
+    }
+    if (staged) {
+      const unsigned long long m = __ballot(walk);
+      int qbase = 0;
+      if (el == 0 && m) qbase = atomicAdd(&s_qn, __popcll(m));
+      qbase = __shfl(qbase, 0);
+      if (walk) s_queue[qbase + __popcll(m & ((1ULL << el) - 1ULL))] = (uint16_t)((beam << 6) | el);
     }
   }
   if (staged) {
+    __syncthreads();
+    // ---------------- phase 2b: the queued scans, densely over all lanes of the workgroup
+    const int nq = s_qn;
+    for (int i = tid; i < nq; i += STEP_THREADS) {
+      const int ent = s_queue[i], qe = ent & (EPB - 1), beam = ent >> 6;
+      const float qpx = s_pos[qe][0], qpy = s_pos[qe][1];
+      const RowsWindow qrw{&s_win[qe * WIN_STRIDE], s_x0[qe], s_y0[qe], P.wrows};
+      const float qx = __fadd_rn(qpx, S.beam_dirs[2 * beam]), qy = __fadd_rn(qpy, S.beam_dirs[2 * beam + 1]);
+      const float d = lidar_scan_walk(qrw, qpx, qpy, qx, qy).dist;
+      s_lid[qe * (MAX_STAGED_BEAMS + 1) + beam] = fminf(fmaxf(f32_div(d, P.range), -1.0f), 1.0f);
+    }
     __syncthreads();
     const int nenv = P.n - base < EPB ? P.n - base : EPB;
     for (int i = tid; i < nenv * P.beams; i += STEP_THREADS) {

@@ -38,8 +38,31 @@ APG_DEV unsigned quad_status(const Rows &rows, int i0, int di, int j0, int dj) {
   return ((b0 | b1) != 0u ? 1u : 0u) | ((b0 == m && b1 == m) ? 2u : 0u);
 }
 
+// Cheap conservative pre-test: can any occupied cell's closed box meet the segment?  Every closed
+// unit box [i, i+1] x [j, j+1] meeting the segment meets its bounding box, i.e. has
+// i in [ceil(min x) - 1, floor(max x)] and j in [ceil(min y) - 1, floor(max y)].  When none of those
+// cells is occupied the intersection is empty and the scan is SCAN_EMPTY with |q - p| (exactly what
+// the walk below returns for it).  Rows/columns are read through the same window as the walk.
 template <class Rows>
-APG_DEV ScanOut lidar_scan(const Rows &rows, float fpx, float fpy, float fqx, float fqy) {
+APG_DEV bool scan_may_hit(const Rows &rows, float fpx, float fpy, float fqx, float fqy) {
+  const int i0 = (int)ceilf(fminf(fpx, fqx)) - 1, i1 = (int)floorf(fmaxf(fpx, fqx));
+  const int j0 = (int)ceilf(fminf(fpy, fqy)) - 1, j1 = (int)floorf(fmaxf(fpy, fqy));
+  const int wdt = i1 - i0 + 1;  // <= lidar range + 2 < 32
+  const uint32_t mask = ((1u << wdt) - 1u) << (i0 - rows.x0);
+  uint32_t acc = 0u;
+  for (int j = j0; j <= j1; j++) acc |= rows.row(j);
+  return (acc & mask) != 0u;
+}
+
+APG_DEV ScanOut scan_empty(float fpx, float fpy, float fqx, float fqy) {
+  ScanOut o;
+  o.kind = SCAN_EMPTY;
+  o.dist = norm_f32(__fsub_rn(fqx, fpx), __fsub_rn(fqy, fpy));
+  return o;
+}
+
+template <class Rows>
+APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fqx, float fqy) {
   const double px = fpx, py = fpy, qx = fqx, qy = fqy;
   const int sx = (fqx > fpx) - (fqx < fpx), sy = (fqy > fpy) - (fqy < fpy);
   const float flpx = floorf(fpx), flpy = floorf(fpy), flqx = floorf(fqx), flqy = floorf(fqy);
@@ -227,6 +250,12 @@ APG_DEV ScanOut lidar_scan(const Rows &rows, float fpx, float fpy, float fqx, fl
     o.dist = d > 0.0f ? d : 0.0f;
   }
   return o;
+}
+
+template <class Rows>
+APG_DEV ScanOut lidar_scan(const Rows &rows, float fpx, float fpy, float fqx, float fqy) {
+  if (!scan_may_hit(rows, fpx, fpy, fqx, fqy)) return scan_empty(fpx, fpy, fqx, fqy);
+  return lidar_scan_walk(rows, fpx, fpy, fqx, fqy);
 }
 
 // ------------------------------------------------------------------ occupancy row sources
