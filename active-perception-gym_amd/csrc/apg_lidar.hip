@@ -277,9 +277,13 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
                                                              apg_lidar_outputs O) {
   __shared__ float s_pos[EPB][2];
   __shared__ int s_x0[EPB], s_y0[EPB];
-  __shared__ uint32_t s_win[EPB * WIN_STRIDE];
-  __shared__ float s_lid[EPB * (MAX_STAGED_BEAMS + 1)];
-  __shared__ uint16_t s_queue[EPB * MAX_STAGED_BEAMS];  // phase 2b work list: (beam << 6) | env
+  // dynamic LDS (step_lds_bytes): occupancy windows, then (beams <= MAX_STAGED_BEAMS) the lidar rows
+  // staged for coalesced stores and the phase-2b work list of (beam << 6) | env entries
+  extern __shared__ uint32_t s_dyn[];
+  uint32_t *s_win = s_dyn;
+  const int LS = P.beams + 1;  // odd row stride: lanes = envs hit distinct banks
+  float *s_lid = reinterpret_cast<float *>(s_dyn + EPB * WIN_STRIDE);
+  uint16_t *s_queue = reinterpret_cast<uint16_t *>(s_lid + EPB * LS);
   __shared__ int s_qn;
   const int tid = threadIdx.x;
   const int base = blockIdx.x * EPB;
@@ -503,7 +507,7 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
         const float d = walk ? lidar_scan_walk(rw, px, py, qx, qy).dist : scan_empty(px, py, qx, qy).dist;
         const float v = fminf(fmaxf(f32_div(d, P.range), -1.0f), 1.0f);
         if (staged)
-          s_lid[el * (MAX_STAGED_BEAMS + 1) + beam] = v;
+          s_lid[el * LS + beam] = v;
         else
           O.lidar[(size_t)e * P.beams + beam] = v;
       }
@@ -526,13 +530,13 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
       const RowsWindow qrw{&s_win[qe * WIN_STRIDE], s_x0[qe], s_y0[qe], P.wrows};
       const float qx = __fadd_rn(qpx, S.beam_dirs[2 * beam]), qy = __fadd_rn(qpy, S.beam_dirs[2 * beam + 1]);
       const float d = lidar_scan_walk(qrw, qpx, qpy, qx, qy).dist;
-      s_lid[qe * (MAX_STAGED_BEAMS + 1) + beam] = fminf(fmaxf(f32_div(d, P.range), -1.0f), 1.0f);
+      s_lid[qe * LS + beam] = fminf(fmaxf(f32_div(d, P.range), -1.0f), 1.0f);
     }
     __syncthreads();
     const int nenv = P.n - base < EPB ? P.n - base : EPB;
     for (int i = tid; i < nenv * P.beams; i += STEP_THREADS) {
       const int l = i / P.beams, beam = i - l * P.beams;
-      O.lidar[(size_t)base * P.beams + i] = s_lid[l * (MAX_STAGED_BEAMS + 1) + beam];
+      O.lidar[(size_t)base * P.beams + i] = s_lid[l * LS + beam];
     }
   }
 }
@@ -636,6 +640,12 @@ int launch_map_generate_any(const Geo &g, const uint64_t *idx, int n, uint64_t *
   return launch_map_generate<GEN_ROOMS>(g, idx, n, occ, stack, err, s);
 }
 
+size_t step_lds_bytes(int beams) {
+  size_t b = (size_t)EPB * WIN_STRIDE * sizeof(uint32_t);
+  if (beams <= MAX_STAGED_BEAMS) b += (size_t)EPB * (beams + 1) * sizeof(float) + (size_t)EPB * beams * sizeof(uint16_t);
+  return b;
+}
+
 int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *act,
                        const float *pred, const apg_lidar_outputs *out, hipStream_t s) {
   StepParams P;
@@ -653,7 +663,8 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   P.range = cfg->lidar_range;
   P.loss_scale = cfg->loss_scale;
   P.loss_offset = cfg->loss_offset;
-  hipLaunchKernelGGL(k_lidar_step, dim3(grid_for(P.n, EPB)), dim3(STEP_THREADS), 0, s, P, *st, act, pred, *out);
+  hipLaunchKernelGGL(k_lidar_step, dim3(grid_for(P.n, EPB)), dim3(STEP_THREADS), step_lds_bytes(P.beams), s, P, *st,
+                     act, pred, *out);
   return check_launch("k_lidar_step");
 }
 
