@@ -48,8 +48,12 @@ int check_launch(const char *what) {
 namespace {
 
 constexpr uint8_t F_AUTORESET = 1, F_JUST_RESET = 2, F_FIRST = 4;
-constexpr int EPB = 64;        // envs per step workgroup (= one wave: lane = env in phases 1 and 2a)
-constexpr int STEP_THREADS = 256;
+#ifndef APG_STEP_EPB
+#define APG_STEP_EPB 64
+#endif
+constexpr int EPB = APG_STEP_EPB;        // envs per step workgroup (lane = env in phases 1 and 2a)
+constexpr int STEP_THREADS = 4 * EPB;    // phase 2a: 4 beams at a time per env
+static_assert(EPB == 16 || EPB == 32 || EPB == 64, "EPB: power of two, at most one wave");
 constexpr int MAX_WIN_ROWS = 32;
 constexpr int WIN_STRIDE = MAX_WIN_ROWS + 1;  // LDS words per env window (+1: lanes = envs hit distinct banks)
 constexpr int MAX_STAGED_BEAMS = 64;          // lidar rows staged in LDS for coalesced stores
@@ -481,13 +485,7 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
       s_pos[tid][0] = pos0;
       s_pos[tid][1] = pos1;
     }
-    // one atomic per wave for the error word
-    const unsigned long long any = __ballot(errbits != 0);
-    if (any) {
-      uint32_t bits = errbits;
-      for (int off = 32; off > 0; off >>= 1) bits |= __shfl_xor(bits, off);
-      if ((tid & 63) == 0) atomicOr(O.err, bits);
-    }
+    if (errbits) atomicOr(O.err, errbits);  // rare: NaN inputs only
   }
   __syncthreads();
 
@@ -513,11 +511,12 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
       }
     }
     if (staged) {
+      const int lane = tid & 63;
       const unsigned long long m = __ballot(walk);
       int qbase = 0;
-      if (el == 0 && m) qbase = atomicAdd(&s_qn, __popcll(m));
+      if (lane == 0 && m) qbase = atomicAdd(&s_qn, __popcll(m));
       qbase = __shfl(qbase, 0);
-      if (walk) s_queue[qbase + __popcll(m & ((1ULL << el) - 1ULL))] = (uint16_t)((beam << 6) | el);
+      if (walk) s_queue[qbase + __popcll(m & ((1ULL << lane) - 1ULL))] = (uint16_t)((beam << 6) | el);
     }
   }
   if (staged) {
