@@ -11,6 +11,11 @@ no CPU fallback.
 """
 
 from . import _native  # noqa: F401
+from .circle_square import (  # noqa: F401
+    CircleSquareDataset,
+    CircleSquareHideAndSeekVectorWrapper,
+    DoubleCircleSquareDataset,
+)
 from .floor_map import FloorMapDataset, FloorMapDatasetMaze, FloorMapDatasetRooms  # noqa: F401
 from .image_dataset import (  # noqa: F401
     ArrayImageClassificationDataset,

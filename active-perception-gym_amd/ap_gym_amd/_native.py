@@ -27,6 +27,8 @@ APG_IMAGE_CLASSIFY = 0
 APG_IMAGE_LOCALIZE = 1
 APG_POOL_U8 = 0
 APG_POOL_F32 = 1
+APG_DS_CIRCLE_SQUARE = 0
+APG_DS_DOUBLE_CIRCLE_SQUARE = 1
 
 
 class NativeLibraryError(RuntimeError):
@@ -93,6 +95,19 @@ class ImageOutputs(ctypes.Structure):
                                    "stats_idx")]
 
 
+class CircleSquareConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("kind", "height", "width", "show_gradient_a", "show_gradient_b",
+                                              "pad_")] + [
+        ("num_positions", ctypes.c_int64), ("half_extent", ctypes.c_double), ("max_dist", ctypes.c_double)]
+
+
+class HideAndSeekArgs(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("num_envs", "height", "width", "resetting", "terminated",
+                                              "mask_prediction", "sparse", "pad_")] + [
+        ("lim", ctypes.c_double * 2)] + [(n, _vp) for n in ("index", "glimpse_pos", "base_reward_in", "reward_in",
+                                                              "loss", "base_reward_out", "reward_out", "additional")]
+
+
 # (name, restype, argtypes) for every symbol declared in include/apgym_capi.h
 SYMBOLS = [
     ("apg_version", ctypes.c_char_p, []),
@@ -128,6 +143,9 @@ SYMBOLS = [
                                    _vp]),
     ("apg_loss_mse", ctypes.c_int, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_float, ctypes.c_float, _vp,
                                     _vp]),
+    ("apg_circle_square_pool", ctypes.c_int, [ctypes.POINTER(CircleSquareConfig), _vp, ctypes.c_int64,
+                                              ctypes.c_int64, _vp, _vp, _vp]),
+    ("apg_hide_and_seek_reward", ctypes.c_int, [ctypes.POINTER(HideAndSeekArgs), _vp]),
 ]
 
 _lib = None

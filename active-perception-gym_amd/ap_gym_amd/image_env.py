@@ -115,8 +115,14 @@ class _ImageVectorEnv:
             raise ValueError("the image envs run on a GPU device (no CPU fallback)")
         ds = cfg.dataset
         ds.load()
-        pool, labels = ds.device_pool()
-        m, h, w, pc = pool.shape
+        if hasattr(ds, "device_pool_tensors"):  # procedural datasets render their pool on the device
+            pool_t, labels_t = ds.device_pool_tensors(self.device)
+            pool_is_u8 = pool_t.dtype == torch.uint8
+        else:
+            pool, labels = ds.device_pool()
+            pool_t, labels_t = None, None
+            pool_is_u8 = pool.dtype == np.uint8
+        m, h, w, pc = (pool_t if pool_t is not None else pool).shape
         c = int(ds.num_channels)
         if c not in (1, 3):
             raise ValueError(f"Target channels must be either 1 or 3 but is {c}.")
@@ -171,7 +177,7 @@ class _ImageVectorEnv:
             mse_scale, mse_offset = affine_f32(inner_loss)
         self._cfg = N.ImageConfig(
             num_envs=n, kind=self.kind, height=h, width=w, pool_channels=pc, channels=c,
-            pool_dtype=N.APG_POOL_U8 if pool.dtype == np.uint8 else N.APG_POOL_F32, sensor_h=s0, sensor_w=s1,
+            pool_dtype=N.APG_POOL_U8 if pool_is_u8 else N.APG_POOL_F32, sensor_h=s0, sensor_w=s1,
             step_limit=int(cfg.step_limit), num_classes=k, invert_labels=int(bool(cfg.randomly_invert_labels)),
             top_k=int(cfg.unique_sampling_top_k), unique_points=int(grid.shape[0]), num_envs_total=nt,
             env_offset=self.env_offset, pool_len=m,
@@ -183,7 +189,8 @@ class _ImageVectorEnv:
         gshape = (n, s0, s1, c)
         work = max(N.lib().apg_rng_fill_work_elems(nt, b) for b in (m, int(cfg.unique_sampling_top_k), 2))
         self._t = T = dict(
-            pool=t.from_numpy(pool).to(dev), pool_labels=t.from_numpy(labels).to(dev),
+            pool=pool_t if pool_t is not None else t.from_numpy(pool).to(dev),
+            pool_labels=labels_t if labels_t is not None else t.from_numpy(labels).to(dev),
             unique_grid=t.from_numpy(grid).to(dev),
             index=t.zeros(n, dtype=t.int64, device=dev), label=t.zeros(n, dtype=t.int32, device=dev),
             inverted=t.zeros(n, dtype=t.int32, device=dev), pos=t.zeros((n, 2), dtype=t.float64, device=dev),

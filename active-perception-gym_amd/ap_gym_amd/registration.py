@@ -1,4 +1,4 @@
-"""Env ids of the hot path and make_vec (ap_gym/envs/registration.py:145-192, 319-356, 516-690, 753-767).
+"""Env ids of the hot path and make_vec (ap_gym/envs/registration.py:145-192, 319-512, 516-690, 753-767).
 
 Only the ids whose step is accelerated by this backend are registered.  `make_vec(id, num_envs,
 **kwargs)` accepts the same keyword overrides as the reference (dataset, lidar_beam_count,
@@ -70,6 +70,44 @@ def _image(kind: str):
     return entry
 
 
+def _hide_and_seek(mask_prediction: bool):
+    """registration.py:471-512: CircleSquareHideAndSeekVectorWrapper(ImageClassificationVectorEnv), with the
+    classification log wrapper outside it for the prediction variant only."""
+
+    def entry(num_envs: int = 1, sparse: bool = False, **kwargs):
+        from .circle_square import CircleSquareHideAndSeekVectorWrapper
+
+        kwargs.setdefault("log_stats", not mask_prediction)
+        inner = _image("cls")(num_envs=num_envs, **kwargs)
+        return CircleSquareHideAndSeekVectorWrapper(inner, mask_prediction=mask_prediction, sparse=sparse)
+
+    return entry
+
+
+def _circle_square(double: bool, size: int, show_gradient: bool):
+    def factory():
+        from .circle_square import CircleSquareDataset, DoubleCircleSquareDataset
+
+        if double:
+            return DoubleCircleSquareDataset(image_shape=(size, size), show_gradient_a=show_gradient,
+                                             show_gradient_b=show_gradient)
+        return CircleSquareDataset(image_shape=(size, size), show_gradient=show_gradient)
+
+    return factory
+
+
+def _register_circle_square(size: int, show_gradient: bool, suffix: str, step_limit: int = 16):
+    # register_circle_square (registration.py:358-406)
+    cfg = dict(step_limit=step_limit)
+    register(f"CircleSquare{suffix}-v0", _image("cls"),
+             kwargs=dict(dataset_factory=_circle_square(False, size, show_gradient), config_kwargs=dict(cfg)))
+    register(f"CircleSquareInverted{suffix}-v0", _image("cls"),
+             kwargs=dict(dataset_factory=_circle_square(False, size, show_gradient),
+                         config_kwargs=dict(cfg, randomly_invert_labels=True)))
+    register(f"DoubleCircleSquare{suffix}-v0", _image("cls"),
+             kwargs=dict(dataset_factory=_circle_square(True, size, show_gradient), config_kwargs=dict(cfg)))
+
+
 def _hf(name: str, split: str, **kw):
     def factory():
         from .image_dataset import HuggingfaceImageClassificationDataset
@@ -98,6 +136,15 @@ def register_envs():
         # TimeLimit + ActiveRegressionLogWrapper (registration.py:348-355): episode stats on
         register(name, _lidar, kwargs=dict(dataset_factory=ds, static_map=static, log_stats=True),
                  max_episode_steps=100)
+    # registration.py:409-512: the CircleSquare family (procedural datasets rendered on the device)
+    for size, grad, suffix, limit in ((28, True, "", 16), (28, True, "-s28", 16), (20, True, "-s20", 16),
+                                      (15, True, "-s15", 16), (28, False, "-nograd", 16),
+                                      (20, False, "-s20-nograd", 16), (15, False, "-s15-nograd", 16),
+                                      (28, True, "-t32", 32), (28, True, "-t64", 64)):
+        _register_circle_square(size, grad, suffix, limit)
+    for name, mask in (("CircleSquareHideAndSeek-v0", False), ("CircleSquareHideAndSeekNoPrediction-v0", True)):
+        register(name, _hide_and_seek(mask),
+                 kwargs=dict(dataset_factory=_circle_square(False, 28, True), config_kwargs=dict(step_limit=32)))
     render_kw = dict(render_unvisited_opacity=0.5, render_visited_opacity=0.25)
     _register_image_ids("cls", "MNIST", lambda split: _hf("mnist", split, channels=1), dict(step_limit=16))
     _register_image_ids("cls", "CIFAR10", lambda split: _hf("cifar10", split, image_feature_name="img"),

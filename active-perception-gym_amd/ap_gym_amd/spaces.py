@@ -18,6 +18,7 @@ try:  # pragma: no cover - gymnasium is absent in the build image
     Dict = _gym.spaces.Dict
     Discrete = _gym.spaces.Discrete
     MultiDiscrete = _gym.spaces.MultiDiscrete
+    Tuple = _gym.spaces.Tuple
     HAVE_GYMNASIUM = True
 except ImportError:
     HAVE_GYMNASIUM = False
@@ -74,6 +75,20 @@ except ImportError:
 
         def __repr__(self):
             return "Dict(" + ", ".join(f"{k!r}: {v}" for k, v in self.spaces.items()) + ")"
+
+    class Tuple(Space):  # type: ignore[no-redef]
+        def __init__(self, spaces=()):
+            super().__init__(None, None)
+            self.spaces = tuple(spaces)
+
+        def __getitem__(self, i):
+            return self.spaces[i]
+
+        def __len__(self):
+            return len(self.spaces)
+
+        def __repr__(self):
+            return "Tuple(" + ", ".join(str(v) for v in self.spaces) + ")"
 
 
 class LogitSpace(Box):
@@ -140,4 +155,6 @@ def batch_space(space, n: int):
         return batch_box(space, n)
     if isinstance(space, Discrete):
         return MultiDiscrete(np.full(n, space.n))
+    if isinstance(space, Tuple):  # gymnasium batches a Tuple element-wise (Tuple(()) stays empty)
+        return Tuple(tuple(batch_space(v, n) for v in space.spaces))
     raise TypeError(f"cannot batch {type(space).__name__}")

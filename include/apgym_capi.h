@@ -43,6 +43,11 @@
  *       ImagePerceptionModule.sample_unique_glimpse_positions  image_perception_module.py:253-277.
  *   apg_loss_ce / apg_loss_mse
  *       CrossEntropyLossFn.numpy / MSELossFn.numpy + LossFnAffineTransformation (loss_fn.py).
+ *   apg_circle_square_pool
+ *       CircleSquareDataset / DoubleCircleSquareDataset get_data_point_batch
+ *       ap_gym/envs/image/circle_square_dataset.py:32-178 (+ _process_imgs_np float64 -> float32).
+ *   apg_hide_and_seek_reward
+ *       CircleSquareHideAndSeekVectorWrapper.step  ap_gym/envs/circle_square_catch_or_flee.py:69-98.
  */
 #ifndef APGYM_CAPI_H
 #define APGYM_CAPI_H
@@ -283,6 +288,50 @@ int apg_loss_ce(const float *logits, const int32_t *target, int32_t n, int32_t k
                 double *out, apg_stream_t stream);
 int apg_loss_mse(const float *pred, const float *target, int32_t n, int32_t d, float scale, float offset,
                  float *out, apg_stream_t stream);
+
+/* ---------------------------------------------------------------- procedural CircleSquare datasets */
+#define APG_DS_CIRCLE_SQUARE 0        /* CircleSquareDataset        circle_square_dataset.py:79-113 */
+#define APG_DS_DOUBLE_CIRCLE_SQUARE 1 /* DoubleCircleSquareDataset  circle_square_dataset.py:116-178 */
+
+typedef struct apg_circle_square_config {
+  int32_t kind;                       /* APG_DS_* */
+  int32_t height, width;              /* image_shape */
+  int32_t show_gradient_a;            /* CircleSquare: show_gradient; Double: show_gradient_a */
+  int32_t show_gradient_b;            /* Double: show_gradient_b */
+  int32_t pad_;
+  int64_t num_positions;              /* Double: len(positions) (valid coordinate pairs) */
+  double half_extent;                 /* object_extents / 2 */
+  double max_dist;                    /* np.sqrt(np.sum(np.array(image_shape) ** 2)) */
+} apg_circle_square_config;
+
+/* Data points [first, first + count) rendered into pool[count][H][W] (float32, one channel) and
+ * labels[count] (int32), i.e. get_data_point_batch(arange(first, first + count)).  Double:
+ * positions[num_positions][2][2] int16 (row, col) pairs in the reference's order. */
+int apg_circle_square_pool(const apg_circle_square_config *cfg, const int16_t *positions, int64_t first,
+                           int64_t count, float *pool, int32_t *labels, apg_stream_t stream);
+
+/* CircleSquareHideAndSeekVectorWrapper.step (circle_square_catch_or_flee.py:69-98) on the inner
+ * ImageClassificationVectorEnv's step outputs (+ SparsifyVectorWrapper for the -sparse ids). */
+typedef struct apg_hide_and_seek_args {
+  int32_t num_envs;
+  int32_t height, width;              /* CircleSquareDataset image_shape */
+  int32_t resetting;                  /* the inner step was the batch autoreset (base_reward = f64 zeros) */
+  int32_t terminated;                 /* the inner step terminated the batch */
+  int32_t mask_prediction;            /* NoPrediction variant: reward = base_reward */
+  int32_t sparse;                     /* -sparse ids: reward = base_reward - loss * terminated */
+  int32_t pad_;
+  double lim[2];                      /* sensor_pos_lim_pixels (x, y) */
+  const int64_t *index;               /* [N] info["index"] */
+  const float *glimpse_pos;           /* [N][2] obs["glimpse_pos"] */
+  const float *base_reward_in;        /* [N] inner info["base_reward"] (unused when resetting) */
+  const double *reward_in;            /* [N] inner reward */
+  const double *loss;                 /* [N] inner normalized CE (sparse) */
+  double *base_reward_out;            /* [N] new info["base_reward"] (float32 values unless resetting) */
+  double *reward_out;                 /* [N] new reward */
+  double *additional;                 /* [N] sign * distance */
+} apg_hide_and_seek_args;
+
+int apg_hide_and_seek_reward(const apg_hide_and_seek_args *args, apg_stream_t stream);
 
 #ifdef __cplusplus
 }

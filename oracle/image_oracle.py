@@ -317,3 +317,67 @@ class ImageVectorEnvOracle:
         bg = float(np.mean(std ** 2))
         scale = 1 / (bg - 0.0)
         return np.mean((prediction - target) ** 2, axis=-1) * scale + (-0.0 * scale)
+
+
+# ------------------------------------------------------------------ CircleSquare datasets (test oracle)
+def circle_square_positions(image_shape, object_extents=8) -> np.ndarray:
+    """DoubleCircleSquareDataset's valid coordinate pairs (circle_square_dataset.py:129-146), [P, 2, 2]."""
+    h, w = image_shape
+    coords = np.stack(np.meshgrid(np.arange(h), np.arange(w), indexing="ij"), axis=-1).reshape(-1, 2)
+    pairs = np.stack(np.broadcast_arrays(coords[:, None], coords[None, :]), axis=-2).reshape(-1, 2, 2)
+    valid = ((np.abs(pairs[:, 0] - pairs[:, 1]) >= object_extents + 1).any(axis=-1)
+             & (pairs[:, 0, 0] <= pairs[:, 1, 0])
+             & ((pairs[:, 0, 0] < pairs[:, 1, 0]) | (pairs[:, 0, 1] <= pairs[:, 1, 1])))
+    return pairs[valid]
+
+
+def _cs_object(coords, pos, label, ext):
+    """_draw_object (circle_square_dataset.py:32-55), vectorised over a batch of positions/labels."""
+    p = pos[:, None, None, :]
+    half = ext / 2
+    rect = ((p[..., 0] - half <= coords[..., 0]) & (coords[..., 0] <= p[..., 0] + half)
+            & (p[..., 1] - half <= coords[..., 1]) & (coords[..., 1] <= p[..., 1] + half))
+    circ = np.linalg.norm(p - coords, axis=-1) <= half
+    return np.where((np.asarray(label) == 0)[:, None, None], rect, circ)
+
+
+def circle_square_images(kind: str, image_shape, idx, show_gradient_a=True, show_gradient_b=True, object_extents=8,
+                         positions=None):
+    """get_data_point_batch of CircleSquareDataset ("single") / DoubleCircleSquareDataset ("double")
+    (circle_square_dataset.py:98-107, 149-172; float64 arithmetic, then float32): images [n, H, W, 1],
+    labels int32."""
+    idx = np.asarray(idx, np.int64)
+    h, w = image_shape
+    coords = np.stack(np.meshgrid(np.arange(h), np.arange(w), indexing="ij"), axis=-1)
+    max_dist = np.sqrt(np.sum(np.array(image_shape) ** 2))
+    if kind == "single":
+        label, rest = idx % 2, idx // 2
+        pos = np.stack([(rest // w) % h, rest % w], axis=-1)
+        if show_gradient_a:
+            img = 1 - np.linalg.norm(pos[:, None, None, :] - coords, axis=-1) / max_dist
+        else:
+            img = np.zeros((idx.shape[0], h, w))
+        img[_cs_object(coords, pos, label, object_extents)] = 1.0
+        labels = label
+    else:
+        if positions is None:
+            positions = circle_square_positions(image_shape, object_extents)
+        l1, l2, pi = idx % 2, (idx // 2) % 2, (idx // 4) % len(positions)
+        p1, p2 = positions[pi, 0], positions[pi, 1]
+        n1 = np.linalg.norm(p1[:, None, None, :] - coords, axis=-1)
+        n2 = np.linalg.norm(p2[:, None, None, :] - coords, axis=-1)
+        img = 1 - np.minimum(n1 * show_gradient_a, n2 * show_gradient_b) / max_dist
+        img[_cs_object(coords, p1, l1, object_extents) | _cs_object(coords, p2, l2, object_extents)] = 1.0
+        labels = np.where(l1 == l2, l1, 2)
+    return img.astype(np.float32)[..., None], labels.astype(np.int32)
+
+
+def hide_and_seek_additional_reward(index, glimpse_pos, image_shape, sensor, scale):
+    """CircleSquareHideAndSeekVectorWrapper.step's additional reward (circle_square_catch_or_flee.py:79-92)."""
+    h, w = image_shape
+    index = np.asarray(index)
+    label, rest = index % 2, index // 2
+    positions = np.stack([(rest // w) % h, rest % w], axis=-1)
+    sign = label * 2 - 1
+    positions_norm = np.flip(positions, axis=-1) / sensor_pos_lim((h, w), sensor, scale) - 1
+    return sign * np.linalg.norm(glimpse_pos - positions_norm, axis=-1)

@@ -322,6 +322,16 @@ def run_image_env(name, kind, pool_shape, channels, num_classes, sensor, scale, 
     env = (ap.ActiveClassificationVectorLogWrapper if kind == "cls" else ap.ActiveRegressionVectorLogWrapper)(env)
     if sparse:  # the "-sparse" ids (registration.py:115-142)
         env = refload.load("sparsify_wrapper").SparsifyVectorWrapper(env)
+    out = {"pool": pool, "labels": labels,
+           "config": np.array([pool_shape[0], pool_shape[1], channels, num_classes, sensor[0], sensor[1],
+                               step_limit, int(invert), n_envs, steps], np.int64),
+           "sensor_scale": np.array(scale, np.float64), "kind": np.array(kind)}
+    _trace_image_env(env, kind, n_envs, num_classes, steps, seed, sparse, out)
+    save(f"image_{name}.npz", **out)
+
+
+def _trace_image_env(env, kind, n_envs, num_classes, steps, seed, sparse, out, mask_prediction=False):
+    """Reset with `seed`, step with seeded actions/predictions, record every output into `out`."""
     obs, info = env.reset(seed=seed)
     arng = np.random.default_rng(11)
     actions = arng.uniform(-1.5, 1.5, (steps, n_envs, 2)).astype(np.float32)
@@ -334,21 +344,22 @@ def run_image_env(name, kind, pool_shape, channels, num_classes, sensor, scale, 
             preds[2::5, 0, 1:] = -np.inf
         else:
             preds[2::5, 0] = np.float32(1e20)
-    out = {"pool": pool, "labels": labels, "actions": actions, "predictions": preds, "seed": np.array(seed),
-           "config": np.array([pool_shape[0], pool_shape[1], channels, num_classes, sensor[0], sensor[1],
-                               step_limit, int(invert), n_envs, steps], np.int64),
-           "sensor_scale": np.array(scale, np.float64), "kind": np.array(kind)}
+    out.update(actions=actions, predictions=preds, seed=np.array(seed))
     for k, v in obs.items():
         out[f"reset_{k}"] = np.asarray(v)
     out["reset_index"] = np.asarray(info["index"], np.int64)
     rec = {}
     for t in range(steps):
-        obs, rew, term, trunc, info = env.step({"action": actions[t], "prediction": preds[t]})
+        pred_t = () if mask_prediction else preds[t]
+        obs, rew, term, trunc, info = env.step({"action": actions[t], "prediction": pred_t})
         fields = dict(obs)
         tgt = info["prediction"]["target"]
         if sparse:
             fields["weight"] = np.asarray(tgt["weight"])
             tgt = tgt["target"]
+        if mask_prediction:
+            assert tgt == ()
+            tgt = np.zeros(0)
         fields.update(reward=rew, terminated=term, truncated=trunc, index=np.asarray(info["index"], np.int64),
                       base_reward=np.asarray(info["base_reward"]), target=np.asarray(tgt),
                       loss=np.asarray(info["prediction"]["loss"]))
@@ -373,7 +384,6 @@ def run_image_env(name, kind, pool_shape, channels, num_classes, sensor, scale, 
     for k, v in rec.items():
         out["step_" + k] = np.array(v) if k.endswith("_dtype") else np.stack(v)
     env.close()
-    save(f"image_{name}.npz", **out)
 
 
 def make_image_env():
@@ -394,9 +404,88 @@ def make_sparse_env():
                   sparse=True)
 
 
+# --------------------------------------------------------------------------- CircleSquare family
+def _circle_square_modules():
+    ipm, icd, ic, il = _image_modules()
+    csd = refload.load("envs.image.circle_square_dataset")
+    return ipm, ic, csd
+
+
+def make_circle_square():
+    """circle_square_dataset.py renders (sampled data points of every registered shape) and traces of
+    the CircleSquare ids (registration.py:358-512), incl. CircleSquareHideAndSeekVectorWrapper."""
+    ipm, ic, csd = _circle_square_modules()
+    out = {}
+    rng = np.random.default_rng(21)
+    cases = [("cs28g", csd.CircleSquareDataset(image_shape=(28, 28), show_gradient=True)),
+             ("cs20n", csd.CircleSquareDataset(image_shape=(20, 20), show_gradient=False)),
+             ("cs15g", csd.CircleSquareDataset(image_shape=(15, 15), show_gradient=True)),
+             ("csrect", csd.CircleSquareDataset(image_shape=(12, 17), show_gradient=True, object_extents=5)),
+             ("dcs15g", csd.DoubleCircleSquareDataset(image_shape=(15, 15))),
+             ("dcs15n", csd.DoubleCircleSquareDataset(image_shape=(15, 15), show_gradient_a=False,
+                                                      show_gradient_b=False)),
+             ("dcs15ab", csd.DoubleCircleSquareDataset(image_shape=(15, 15), show_gradient_a=True,
+                                                       show_gradient_b=False)),
+             ("dcs20g", csd.DoubleCircleSquareDataset(image_shape=(20, 20))),
+             ("dcs28g", csd.DoubleCircleSquareDataset(image_shape=(28, 28)))]
+    for name, ds in cases:
+        n = len(ds)
+        idx = np.unique(np.concatenate([np.arange(min(n, 8)), [n - 1, n // 2],
+                                        rng.integers(0, n, 56)])).astype(np.int64)
+        imgs, labels = ds.get_data_point_batch(idx)
+        out[f"{name}_len"] = np.array(n, np.int64)
+        out[f"{name}_idx"] = idx
+        out[f"{name}_images"] = np.asarray(imgs, np.float32)
+        out[f"{name}_labels"] = np.asarray(labels, np.int32)
+        if isinstance(ds, csd.CircleSquareDataset):
+            pos, lab = ds.get_object_position_and_label(idx)
+            out[f"{name}_obj_pos"] = np.asarray(pos, np.int64)
+            out[f"{name}_obj_label"] = np.asarray(lab, np.int64)
+    save("circle_square_data.npz", **out)
+
+    ap = sys.modules["ap_gym"]
+    hs = refload.load("envs.circle_square_catch_or_flee")
+    sp = refload.load("sparsify_wrapper")
+
+    def trace(name, ds, step_limit, invert, n_envs, steps, seed, wrap=None, sparse=False, mask=False,
+              log=True):
+        cfg = ipm.ImagePerceptionConfig(dataset=ds, step_limit=step_limit, prefetch=False,
+                                        randomly_invert_labels=invert)
+        env = ic.ImageClassificationVectorEnv(n_envs, cfg)
+        if wrap is not None:
+            env = wrap(env)
+        if log:
+            env = ap.ActiveClassificationVectorLogWrapper(env)
+        if sparse:
+            env = sp.SparsifyVectorWrapper(env)
+        k = ds.num_classes
+        res = {"config": np.array([step_limit, int(invert), n_envs, steps, k], np.int64)}
+        _trace_image_env(env, "cls", n_envs, k, steps, seed, sparse, res, mask_prediction=mask)
+        save(f"cs_env_{name}.npz", **res)
+
+    trace("cs28", csd.CircleSquareDataset(image_shape=(28, 28)), 16, False, 6, 36, 0)
+    trace("csinv15n", csd.CircleSquareDataset(image_shape=(15, 15), show_gradient=False), 16, True, 5, 36, 3)
+    trace("dcs15", csd.DoubleCircleSquareDataset(image_shape=(15, 15)), 16, False, 5, 20, 4)
+    trace("hs28", csd.CircleSquareDataset(image_shape=(28, 28)), 32, False, 6, 70, 5,
+          wrap=hs.CircleSquareHideAndSeekVectorWrapper)
+    trace("hs28_sparse", csd.CircleSquareDataset(image_shape=(28, 28)), 32, False, 4, 40, 6,
+          wrap=hs.CircleSquareHideAndSeekVectorWrapper, sparse=True)
+    # the NoPrediction variant: the reference's reset raises KeyError('prediction') (its reset info has
+    # no "prediction" entry, circle_square_catch_or_flee.py:61-64); record that
+    env = hs.CircleSquareHideAndSeekVectorWrapper(
+        ic.ImageClassificationVectorEnv(3, ipm.ImagePerceptionConfig(dataset=csd.CircleSquareDataset(), step_limit=32,
+                                                                     prefetch=False)), mask_prediction=True)
+    try:
+        env.reset(seed=0)
+        reset_error = ""
+    except KeyError as e:
+        reset_error = f"KeyError:{e.args[0]}"
+    save("cs_env_hs_noprediction_reset.npz", reset_error=np.array(reset_error))
+
+
 SECTIONS = {"rng": make_rng, "maps": make_maps, "loss": make_loss, "scan": make_lidar_scan,
             "lidar": make_lidar_env, "image": make_image_env,
-            "sparse": make_sparse_env}
+            "sparse": make_sparse_env, "circle_square": make_circle_square}
 
 
 def main(argv):

@@ -147,3 +147,57 @@ def test_pairwise_sum_matches_numpy_mean():
         n = int(np.prod(shape))
         got = (np.float32(0) + io.pairwise_sum_f32(x.reshape(64, n))) / np.float32(n)
         assert np.array_equal(got, want), shape
+
+
+# ---------------------------------------------------------------------------- CircleSquare family
+CS_DATA_CASES = {  # golden prefix: (kind, shape, show_gradient_a, show_gradient_b, object_extents)
+    "cs28g": ("single", (28, 28), True, True, 8), "cs20n": ("single", (20, 20), False, False, 8),
+    "cs15g": ("single", (15, 15), True, True, 8), "csrect": ("single", (12, 17), True, True, 5),
+    "dcs15g": ("double", (15, 15), True, True, 8), "dcs15n": ("double", (15, 15), False, False, 8),
+    "dcs15ab": ("double", (15, 15), True, False, 8), "dcs20g": ("double", (20, 20), True, True, 8),
+    "dcs28g": ("double", (28, 28), True, True, 8),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CS_DATA_CASES))
+def test_circle_square_oracle_matches_reference_renders(name):
+    from oracle import image_oracle as io
+
+    g = golden("circle_square_data.npz")
+    kind, shape, ga, gb, ext = CS_DATA_CASES[name]
+    if kind == "double":
+        assert int(g[f"{name}_len"]) == 4 * len(io.circle_square_positions(shape, ext))
+    else:
+        assert int(g[f"{name}_len"]) == 2 * shape[0] * shape[1]
+    imgs, labels = io.circle_square_images(kind, shape, g[f"{name}_idx"], ga, gb, ext)
+    assert np.array_equal(imgs, g[f"{name}_images"])
+    assert np.array_equal(labels, g[f"{name}_labels"])
+
+
+def test_circle_square_host_api_matches_reference():
+    """Index packing and get_object_position_and_label of the product's dataset classes (host logic)."""
+    import ap_gym_amd as ap
+
+    g = golden("circle_square_data.npz")
+    for name, (kind, shape, ga, gb, ext) in CS_DATA_CASES.items():
+        if kind == "single":
+            ds = ap.CircleSquareDataset(show_gradient=ga, image_shape=shape, object_extents=ext)
+            pos, lab = ds.get_object_position_and_label(g[f"{name}_idx"])
+            assert np.array_equal(pos, g[f"{name}_obj_pos"]) and np.array_equal(lab, g[f"{name}_obj_label"])
+        else:
+            ds = ap.DoubleCircleSquareDataset(ga, gb, image_shape=shape, object_extents=ext)
+        assert len(ds) == int(g[f"{name}_len"]) and ds.num_classes == (2 if kind == "single" else 3)
+        assert ds._unpack(ds._pack([1, 0, 3])) == [1, 0, 3]
+
+
+def test_hide_and_seek_oracle_matches_reference_autoreset_steps():
+    """On the batch autoreset step the inner base_reward is float64 zeros, so the reference's
+    info["base_reward"] is exactly the additional reward."""
+    from oracle import image_oracle as io
+
+    g = golden("cs_env_hs28.npz")
+    lim = int(g["config"][0])
+    for t in (lim, 2 * lim + 1):
+        assert str(g["step_base_reward_dtype"][t]) == "float64"
+        add = io.hide_and_seek_additional_reward(g["step_index"][t], g["step_glimpse_pos"][t], (28, 28), (5, 5), 1.0)
+        assert np.array_equal(add, g["step_base_reward"][t])
