@@ -25,6 +25,7 @@ from .image_dataset import (  # noqa: F401
 )
 from .image_env import ImageClassificationVectorEnv, ImageLocalizationVectorEnv, ImagePerceptionConfig  # noqa: F401
 from .lidar_env import LIDARLocalization2DVectorEnv, lidar_beam_directions  # noqa: F401
+from .light_dark_env import LightDarkVectorEnv  # noqa: F401
 from .loss_fn import (  # noqa: F401
     CrossEntropyLossFn,
     LambdaLossFn,

@@ -108,6 +108,21 @@ class HideAndSeekArgs(ctypes.Structure):
                                                               "loss", "base_reward_out", "reward_out", "additional")]
 
 
+class LightDarkConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("num_envs", "step_limit", "log_stats", "sparse")] + [
+        ("loss_scale", ctypes.c_float), ("loss_offset", ctypes.c_float)]
+
+
+class LightDarkState(ctypes.Structure):
+    _fields_ = [(n, _vp) for n in ("pos", "elapsed", "flags", "rng", "stats_hist")]
+
+
+class LightDarkOutputs(ctypes.Structure):
+    _fields_ = [(n, _vp) for n in ("noisy_position", "time_step", "reward", "terminated", "truncated", "base_reward",
+                                   "target", "loss", "info_mask", "reset_mask", "err", "stats", "stats_len",
+                                   "weight")]
+
+
 # (name, restype, argtypes) for every symbol declared in include/apgym_capi.h
 SYMBOLS = [
     ("apg_version", ctypes.c_char_p, []),
@@ -146,6 +161,11 @@ SYMBOLS = [
     ("apg_circle_square_pool", ctypes.c_int, [ctypes.POINTER(CircleSquareConfig), _vp, ctypes.c_int64,
                                               ctypes.c_int64, _vp, _vp, _vp]),
     ("apg_hide_and_seek_reward", ctypes.c_int, [ctypes.POINTER(HideAndSeekArgs), _vp]),
+    ("apg_light_dark_reset", ctypes.c_int, [ctypes.POINTER(LightDarkConfig), ctypes.POINTER(LightDarkState),
+                                            ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(LightDarkOutputs), _vp]),
+    ("apg_light_dark_step", ctypes.c_int, [ctypes.POINTER(LightDarkConfig), ctypes.POINTER(LightDarkState), _vp, _vp,
+                                           ctypes.POINTER(LightDarkOutputs), _vp]),
+    ("apg_standard_normal_draws", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, _vp]),
 ]
 
 _lib = None

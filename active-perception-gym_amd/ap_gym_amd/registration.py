@@ -70,6 +70,12 @@ def _image(kind: str):
     return entry
 
 
+def _light_dark(num_envs: int = 1, **kwargs):
+    from .light_dark_env import LightDarkVectorEnv
+
+    return LightDarkVectorEnv(num_envs=num_envs, **kwargs)
+
+
 def _hide_and_seek(mask_prediction: bool):
     """registration.py:471-512: CircleSquareHideAndSeekVectorWrapper(ImageClassificationVectorEnv), with the
     classification log wrapper outside it for the prediction variant only."""
@@ -136,6 +142,8 @@ def register_envs():
         # TimeLimit + ActiveRegressionLogWrapper (registration.py:348-355): episode stats on
         register(name, _lidar, kwargs=dict(dataset_factory=ds, static_map=static, log_stats=True),
                  max_episode_steps=100)
+    # registration.py:640-647: TimeLimit(50) + ActiveRegressionLogWrapper over LightDarkEnv
+    register("LightDark-v0", _light_dark, kwargs=dict(log_stats=True), max_episode_steps=50)
     # registration.py:409-512: the CircleSquare family (procedural datasets rendered on the device)
     for size, grad, suffix, limit in ((28, True, "", 16), (28, True, "-s28", 16), (20, True, "-s20", 16),
                                       (15, True, "-s15", 16), (28, False, "-nograd", 16),

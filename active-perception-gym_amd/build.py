@@ -17,8 +17,9 @@ CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "ap_gym_amd", "_lib")
 OUT = os.path.join(OUT_DIR, "libapgym_hip.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
-SOURCES = ["apg_lidar.hip", "apg_image.hip", "apg_circle_square.hip"]
-HEADERS = ["apg_device.hpp", "apg_maps.hpp", "apg_scan.hpp", "apg_rng.hpp", "apg_host.hpp", "apg_pairwise.hpp"]
+SOURCES = ["apg_lidar.hip", "apg_image.hip", "apg_circle_square.hip", "apg_light_dark.hip"]
+HEADERS = ["apg_device.hpp", "apg_maps.hpp", "apg_scan.hpp", "apg_rng.hpp", "apg_host.hpp", "apg_pairwise.hpp",
+           "apg_ziggurat.hpp"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = [

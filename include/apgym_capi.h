@@ -48,6 +48,12 @@
  *       ap_gym/envs/image/circle_square_dataset.py:32-178 (+ _process_imgs_np float64 -> float32).
  *   apg_hide_and_seek_reward
  *       CircleSquareHideAndSeekVectorWrapper.step  ap_gym/envs/circle_square_catch_or_flee.py:69-98.
+ *   apg_light_dark_reset / apg_light_dark_step
+ *       SyncVectorEnv over ActiveRegressionLogWrapper(TimeLimit(50)(LightDarkEnv)) as registered at
+ *       ap_gym/envs/registration.py:640-647; LightDarkEnv.reset/_step/__get_obs
+ *       ap_gym/envs/light_dark.py:93-155.
+ *   apg_standard_normal_draws
+ *       numpy Generator.standard_normal (ziggurat, distributions.c) as LightDarkEnv draws it (test entry).
  */
 #ifndef APGYM_CAPI_H
 #define APGYM_CAPI_H
@@ -332,6 +338,48 @@ typedef struct apg_hide_and_seek_args {
 } apg_hide_and_seek_args;
 
 int apg_hide_and_seek_reward(const apg_hide_and_seek_args *args, apg_stream_t stream);
+
+/* ---------------------------------------------------------------- LightDark-v0 */
+typedef struct apg_light_dark_config {
+  int32_t num_envs;
+  int32_t step_limit;                 /* TimeLimit max_episode_steps (50 for LightDark-v0) */
+  int32_t log_stats;                  /* 1: ActiveRegressionLogWrapper episode statistics */
+  int32_t sparse;                     /* 1: LightDark-sparse-v0 (SparsifyWrapper): reward = base - loss * terminated */
+  float loss_scale, loss_offset;      /* normalized MSE affine, as float32 (NEP 50) */
+} apg_light_dark_config;
+
+typedef struct apg_light_dark_state {
+  float *pos;                         /* [N][2] agent position */
+  int32_t *elapsed;                   /* [N] TimeLimit._elapsed_steps */
+  uint8_t *flags;                     /* [N] bit0: the env is reset by the next step (NEXT_STEP autoreset) */
+  apg_pcg64 *rng;                     /* [N] env np_random */
+  float *stats_hist;                  /* [N][2][step_limit] per-step euclidean_distance, mse (log_stats) */
+} apg_light_dark_state;
+
+typedef struct apg_light_dark_outputs {
+  float *noisy_position;              /* [N][2] obs["noisy_position"] */
+  float *time_step;                   /* [N] obs["time_step"] */
+  double *reward;                     /* [N] float64 like SyncVectorEnv */
+  uint8_t *terminated, *truncated;    /* [N] */
+  float *base_reward;                 /* [N] info["base_reward"] */
+  float *target;                      /* [N][2] info["prediction"]["target"] (the pre-move position) */
+  float *loss;                        /* [N] info["prediction"]["loss"] */
+  uint8_t *info_mask;                 /* [N] 1 where the step info carries base_reward/prediction */
+  uint8_t *reset_mask;                /* [N] 1 where the env auto-reset this step */
+  uint32_t *err;                      /* [1] OR-ed APG_ERR_* bits */
+  float *stats;                       /* [4][N] avg/avg/final/final (euclidean_distance, mse) of ended episodes */
+  int32_t *stats_len;                 /* [N] episode length where an episode ended this step, else 0 */
+  double *weight;                     /* [N] sparse: 1.0 where terminated */
+} apg_light_dark_outputs;
+
+/* reset(seed): sub-env i seeded with seed + i when use_seed (else the streams continue). */
+int apg_light_dark_reset(const apg_light_dark_config *cfg, const apg_light_dark_state *st, uint64_t seed,
+                         int use_seed, const apg_light_dark_outputs *out, apg_stream_t stream);
+/* step({"action", "prediction"}) with NEXT_STEP autoreset. */
+int apg_light_dark_step(const apg_light_dark_config *cfg, const apg_light_dark_state *st, const float *action,
+                        const float *prediction, const apg_light_dark_outputs *out, apg_stream_t stream);
+/* n draws of Generator.standard_normal from default_rng(seeds[i]) for each of m seeds -> out[m][n]. */
+int apg_standard_normal_draws(const uint64_t *seeds, int m, int n, double *out, apg_stream_t stream);
 
 #ifdef __cplusplus
 }

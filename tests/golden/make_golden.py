@@ -483,9 +483,82 @@ def make_circle_square():
     save("cs_env_hs_noprediction_reset.npz", reset_error=np.array(reset_error))
 
 
+# --------------------------------------------------------------------------- LightDark
+def run_light_dark(name, n_envs, steps, seed, action_scale, sparse=False):
+    """LightDark-v0 as registered (registration.py:640-647): TimeLimit(50, issue_termination=True) +
+    ActiveRegressionLogWrapper over LightDarkEnv, vectorised by the SyncVectorEnv restatement."""
+    ap = refload.load_core()
+    ld = refload.load("envs.light_dark")
+    gym = sys.modules["gymnasium"]
+    sw = refload.load("sparsify_wrapper") if sparse else None
+
+    def mk():
+        env = ap.TimeLimit(ld.LightDarkEnv(), max_episode_steps=50, issue_termination=True)
+        env = ap.ActiveRegressionLogWrapper(env)
+        return sw.SparsifyWrapper(_reset_prediction_info_shim(ap)(env)) if sparse else env
+
+    venv = gym.vector.SyncVectorEnv([mk for _ in range(n_envs)])
+    obs, info = venv.reset(seed=seed)
+    arng = np.random.default_rng(2)
+    actions = arng.uniform(-action_scale, action_scale, (steps, n_envs, 2)).astype(np.float32)
+    preds = arng.uniform(-1, 1, (steps, n_envs, 2)).astype(np.float32)
+    if sparse:
+        preds[5::7, 0] = np.float32(1e20)
+    out = {"actions": actions, "predictions": preds, "seed": np.array(seed),
+           "reset_noisy_position": obs["noisy_position"], "reset_time_step": obs["time_step"],
+           "reset_info_keys": np.array(sorted(info.keys()), dtype=str)}
+    rec = {}
+    vec = {"euclidean_distance": [], "mse": []}
+    for t in range(steps):
+        obs, rew, term, trunc, info = venv.step({"action": actions[t], "prediction": preds[t]})
+        mask = info.get("_base_reward", np.zeros(n_envs, bool))
+        fields = {"noisy_position": obs["noisy_position"], "time_step": obs["time_step"], "reward": rew,
+                  "terminated": term, "truncated": trunc, "info_mask": mask,
+                  "base_reward": np.where(mask, info.get("base_reward", np.zeros(n_envs, np.float32)), 0)
+                  .astype(np.float32)}
+        tgt = info["prediction"]["target"] if "prediction" in info else None
+        if sparse:
+            w = np.asarray(tgt["weight"]) if tgt is not None else np.zeros(n_envs)
+            fields["weight"] = np.where(mask, w, 0.0)
+            tgt = (np.stack([np.zeros(2, np.float32) if v is None else v for v in tgt["target"]])
+                   if tgt is not None else None)
+        fields["target"] = np.where(mask[:, None], tgt if tgt is not None else np.zeros((n_envs, 2), np.float32),
+                                    0).astype(np.float32)
+        fields["loss"] = np.where(mask, info["prediction"]["loss"] if "loss" in info.get("prediction", {})
+                                  else np.zeros(n_envs, np.float32), 0).astype(np.float32)
+        smask = info.get("_stats", np.zeros(n_envs, bool))
+        fields["stats_mask"] = smask
+        lens = np.zeros(n_envs, np.int32)
+        for key in ("avg_euclidean_distance", "avg_mse", "final_euclidean_distance", "final_mse"):
+            v = info["stats"]["scalar"][key] if smask.any() else np.zeros(n_envs)
+            fields["stats_" + key] = np.where(smask, v, 0.0)
+        for i in np.nonzero(smask)[0]:
+            for key in vec:
+                lst = info["stats"]["vector"][key][i]
+                assert all(type(x) is np.float32 for x in lst)
+                vec[key].extend(lst)
+            lens[i] = len(info["stats"]["vector"]["mse"][i])
+        fields["stats_len"] = lens
+        for k, v in fields.items():
+            rec.setdefault(k, []).append(np.asarray(v))
+    for k, v in rec.items():
+        out["step_" + k] = np.stack(v)
+    for key, v in vec.items():
+        out["stats_vector_" + key] = np.array(v, np.float32)
+    out["reward_dtype"] = np.array(str(rew.dtype))
+    save(f"light_dark_{name}.npz", **out)
+
+
+def make_light_dark():
+    run_light_dark("n8", 8, 130, 0, 1.0)
+    run_light_dark("n6_wide", 6, 120, 5, 3.0)
+    run_light_dark("n5_sparse", 5, 110, 2, 2.0, sparse=True)
+
+
 SECTIONS = {"rng": make_rng, "maps": make_maps, "loss": make_loss, "scan": make_lidar_scan,
             "lidar": make_lidar_env, "image": make_image_env,
-            "sparse": make_sparse_env, "circle_square": make_circle_square}
+            "sparse": make_sparse_env, "circle_square": make_circle_square,
+            "light_dark": make_light_dark}
 
 
 def main(argv):

@@ -201,3 +201,45 @@ def test_hide_and_seek_oracle_matches_reference_autoreset_steps():
         assert str(g["step_base_reward_dtype"][t]) == "float64"
         add = io.hide_and_seek_additional_reward(g["step_index"][t], g["step_glimpse_pos"][t], (28, 28), (5, 5), 1.0)
         assert np.array_equal(add, g["step_base_reward"][t])
+
+
+# ---------------------------------------------------------------------------- LightDark
+LIGHT_DARK_CASES = {"n8": False, "n6_wide": False, "n5_sparse": True}
+
+
+def check_light_dark_step(g, t, got, rtol=0.0):
+    """One step of a LightDark vector env (oracle or GPU, numpy-mode dict form) against the fixture."""
+    for key in ("noisy_position", "time_step", "reward", "terminated", "truncated", "info_mask"):
+        assert np.array_equal(got[key], g["step_" + key][t], equal_nan=got[key].dtype.kind == "f"), (t, key)
+    m = g["step_info_mask"][t]
+    for key in ("base_reward", "loss"):
+        assert np.array_equal(np.where(m, got[key], 0), g["step_" + key][t], equal_nan=True), (t, key)
+    assert np.array_equal(np.where(m[:, None], got["target"], 0), g["step_target"][t]), t
+    if "step_weight" in g.files:
+        assert np.array_equal(np.where(m, got["weight"], 0.0), g["step_weight"][t]), t
+    assert np.array_equal(got["stats_len"], g["step_stats_len"][t]), t
+    names = ("avg_euclidean_distance", "avg_mse", "final_euclidean_distance", "final_mse")
+    for j, key in enumerate(names):
+        assert np.array_equal(np.where(got["stats_len"] > 0, got["stats"][j], 0.0), g["step_stats_" + key][t]), (t, key)
+
+
+@pytest.mark.parametrize("name", sorted(LIGHT_DARK_CASES))
+def test_light_dark_oracle_matches_reference_trace(name):
+    from oracle.light_dark_oracle import LightDarkVectorOracle
+
+    g = golden(f"light_dark_{name}.npz")
+    steps, n = g["actions"].shape[:2]
+    ref = LightDarkVectorOracle(n, 50, sparse=LIGHT_DARK_CASES[name])
+    obs = ref.reset(int(g["seed"]))
+    assert np.array_equal(obs["noisy_position"], g["reset_noisy_position"])
+    assert np.array_equal(obs["time_step"], g["reset_time_step"])
+    vec = {"euclidean_distance": [], "mse": []}
+    for t in range(steps):
+        out = ref.step(g["actions"][t], g["predictions"][t])
+        check_light_dark_step(g, t, out)
+        for i in sorted(out["stats_vectors"]):
+            ed, ms = out["stats_vectors"][i]
+            vec["euclidean_distance"] += ed
+            vec["mse"] += ms
+    for key, v in vec.items():
+        assert np.array_equal(np.array(v, np.float32), g["stats_vector_" + key]), key
