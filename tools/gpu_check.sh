@@ -1,0 +1,7 @@
+#!/bin/bash
+# Round-end style GPU check: parity tests, smoke, default bench (logs under gpurun_out/).
+set -e
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1
