@@ -44,18 +44,25 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str | None = None) -> str:
+    """Build the library; `extra_flags`/`out` make tuning variants (e.g. -DAPG_STEP_PROFILE into tune/)."""
     os.makedirs(OUT_DIR, exist_ok=True)
-    if not force and not _stale():
+    variant = out is not None
+    out = out or OUT
+    if not force and not variant and not _stale():
         return OUT
-    cmd = [HIPCC, *FLAGS, "-I", INCLUDE, "-o", OUT + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    cmd = [HIPCC, *FLAGS, *extra_flags, "-I", INCLUDE, "-o", out + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
     if verbose:
         cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose="--verbose" in sys.argv))
+    args = sys.argv[1:]
+    out_arg = next((a.split("=", 1)[1] for a in args if a.startswith("--out=")), None)
+    defs = [a for a in args if a.startswith("-D")]
+    print(build(force="--force" in args, verbose="--verbose" in args, extra_flags=defs, out=out_arg))

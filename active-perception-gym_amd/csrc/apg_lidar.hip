@@ -272,6 +272,13 @@ APG_DEV void log_episode_stats(const StepParams &P, const apg_lidar_outputs &O, 
 // ~2 cells (clamped move <= 1, slide <= 1), and every cell a scan of length <= R from the new
 // position p can touch lies within [floor(p) - R - 2, floor(p) + R + 1] (+1 column for the 2-bit
 // quad reads), i.e. within [floor(p0) - R - 5, floor(p0) + R + 5]: inside the window for R <= 10.
+#ifdef APG_STEP_PROFILE  // tuning builds only (tools/step_phase_profile.py): per-workgroup phase timestamps
+__device__ unsigned long long g_step_prof[16384][8];
+#define STEP_MARK(k) \
+  if (threadIdx.x == 0 && blockIdx.x < 16384) g_step_prof[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();
+#else
+#define STEP_MARK(k)
+#endif
 #ifndef APG_STEP_MIN_WAVES
 #define APG_STEP_MIN_WAVES 4  // keep k_lidar_step at <= 128 VGPRs: 4 waves per SIMD
 #endif
@@ -292,6 +299,10 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
   const int tid = threadIdx.x;
   const int base = blockIdx.x * EPB;
   const size_t words = (size_t)P.h * P.wpr;
+  STEP_MARK(0)
+#ifdef APG_STEP_PROFILE
+  const unsigned long long prof_clk0 = __builtin_amdgcn_s_memtime();
+#endif
 
   // ---------------- phase 0: window origins from the pre-move positions; which envs reset
   __shared__ unsigned long long s_reset;
@@ -354,6 +365,7 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
     s_win[el * WIN_STRIDE + row] = v;
   }
   __syncthreads();
+  STEP_MARK(1)
 
   // ---------------- phase 1: one lane per env
   if (tid < EPB) {
@@ -488,6 +500,7 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
     if (errbits) atomicOr(O.err, errbits);  // rare: NaN inputs only
   }
   __syncthreads();
+  STEP_MARK(2)
 
   // ---------------- phase 2a: lane = env, wave = beam index (all 64 lanes of a wave cast the same
   // beam direction).  Beams whose bounding box holds no occupied cell are SCAN_EMPTY and finish
@@ -521,6 +534,7 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
   }
   if (staged) {
     __syncthreads();
+    STEP_MARK(3)
     // ---------------- phase 2b: the queued scans, densely over all lanes of the workgroup
     const int nq = s_qn;
     for (int i = tid; i < nq; i += STEP_THREADS) {
@@ -532,12 +546,21 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
       s_lid[qe * LS + beam] = fminf(fmaxf(f32_div(d, P.range), -1.0f), 1.0f);
     }
     __syncthreads();
+    STEP_MARK(4)
     const int nenv = P.n - base < EPB ? P.n - base : EPB;
     for (int i = tid; i < nenv * P.beams; i += STEP_THREADS) {
       const int l = i / P.beams, beam = i - l * P.beams;
       O.lidar[(size_t)base * P.beams + i] = s_lid[l * LS + beam];
     }
   }
+#ifdef APG_STEP_PROFILE
+  __syncthreads();
+  STEP_MARK(5)
+  if (threadIdx.x == 0 && blockIdx.x < 16384) {
+    g_step_prof[blockIdx.x][6] = s_qn;
+    g_step_prof[blockIdx.x][7] = __builtin_amdgcn_s_memtime() - prof_clk0;
+  }
+#endif
 }
 
 __global__ void k_scan_batch(const uint64_t *occ, const int32_t *map_index, int h, int w, int wpr,
@@ -774,4 +797,9 @@ int apg_rng_draws(const uint64_t *seeds, int m, int kind, int64_t a, int64_t b, 
   return check_launch("k_rng_draws");
 }
 
+#ifdef APG_STEP_PROFILE
+int apg_debug_step_profile(void *dst, size_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_step_prof), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 }  // extern "C"

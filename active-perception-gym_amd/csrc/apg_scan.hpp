@@ -124,34 +124,6 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
   auto dist_f32 = [&](double x, double y) -> float {
     return norm_f32(__fsub_rn((float)x, fpx), __fsub_rn((float)y, fpy));
   };
-  // close the piece [previous node, new node] (status cur_in)
-  auto close_piece = [&]() {
-    if (cur_in) {
-      if (n_lines == 0) {
-        l0_t = pv_t;
-        l0_a = pv_a;
-        l0_b = pv_b;
-      } else {
-        double x, y;
-        node_coord(pv_t, pv_a, pv_b, x, y);
-        later_line = fminf(later_line, dist_f32(x, y));
-      }
-      n_lines++;
-    } else if (pv_onb && !pv_left_in) {
-      if (n_points == 0) {
-        p0_t = pv_t;
-        p0_a = pv_a;
-        p0_b = pv_b;
-      } else {
-        double x, y;
-        node_coord(pv_t, pv_a, pv_b, x, y);
-        later_point = fminf(later_point, dist_f32(x, y));
-      }
-      n_points++;
-    }
-    pv_left_in = cur_in;
-  };
-
   const int ntot = nxl + nyl;
   int xi = 0, yi = 0;
   while (xi + yi < ntot) {
@@ -208,7 +180,26 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
   }
   // q: always a node
   const unsigned qst = quad_status(rows, qxi ? iqx - 1 : iqx, qxi ? 1 : 0, qyi ? iqy - 1 : iqy, qyi ? 1 : 0);
-  close_piece();
+  {  // close the last piece [previous node, q] (predicated like the loop body: no pointer selects)
+    const bool is_line = cur_in, is_point = !cur_in && pv_onb && !pv_left_in;
+    if ((is_line && n_lines > 0) || (is_point && n_points > 0)) {
+      double x, y;
+      node_coord(pv_t, pv_a, pv_b, x, y);
+      const float d = dist_f32(x, y);
+      if (is_line) later_line = fminf(later_line, d);
+      else later_point = fminf(later_point, d);
+    }
+    const bool first_line = is_line && n_lines == 0, first_point = is_point && n_points == 0;
+    l0_t = first_line ? pv_t : l0_t;
+    l0_a = first_line ? pv_a : l0_a;
+    l0_b = first_line ? pv_b : l0_b;
+    p0_t = first_point ? pv_t : p0_t;
+    p0_a = first_point ? pv_a : p0_a;
+    p0_b = first_point ? pv_b : p0_b;
+    n_lines += is_line ? 1 : 0;
+    n_points += is_point ? 1 : 0;
+    pv_left_in = cur_in;
+  }
   pv_t = 4;
   pv_onb = qst == 1u;
   if (pv_onb && !pv_left_in) {

@@ -1,0 +1,63 @@
+"""Phase timeline of k_lidar_step (tuning aid): needs a library built with -DAPG_STEP_PROFILE, e.g.
+
+    python active-perception-gym_amd/build.py -DAPG_STEP_PROFILE --out=tune/libprof.so
+    APG_LIBRARY=tune/libprof.so python tools/step_phase_profile.py
+
+Marks per workgroup (s_memrealtime, 100 MHz): 0 start, 1 windows staged, 2 move phase done,
+3 beam pre-test done, 4 queued walks done, 5 end; slot 6 = queued walks.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "active-perception-gym_amd"))
+import ap_gym_amd as ap  # noqa: E402
+from ap_gym_amd import _native as N  # noqa: E402
+
+n = int(os.environ.get("NENV", 65536))
+M = int(os.environ.get("MAP", 64))  # bench.py's workload: BASELINE config 2 (64x64 rooms, 32 beams)
+env = ap.make_vec("LIDARLocRooms-v0", num_envs=n, lidar_beam_count=32, dataset=ap.FloorMapDatasetRooms(M, M),
+                  array_backend="torch")
+env.reset(seed=0)
+g = torch.Generator(device="cuda")
+g.manual_seed(0)
+for t in range(int(os.environ.get("WARM", 30))):
+    a = torch.rand((n, 2), device="cuda", generator=g) * 2 - 1
+    env.step({"action": a, "prediction": a})
+torch.cuda.synchronize()
+if not hasattr(N.lib(), "apg_debug_step_profile"):
+    sys.exit("library built without -DAPG_STEP_PROFILE: only the warm-up steps ran")
+N.lib().apg_debug_step_profile.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+for rep in range(3):
+    a = torch.rand((n, 2), device="cuda", generator=g) * 2 - 1
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    env.step({"action": a, "prediction": a})
+    ev1.record()
+    torch.cuda.synchronize()
+    print(f"rep {rep}: events around env.step {ev0.elapsed_time(ev1) * 1000:.1f} us")
+    nwg = (n + 63) // 64
+    buf = np.zeros((16384, 8), np.uint64)
+    assert N.lib().apg_debug_step_profile(buf.ctypes.data, buf.nbytes) == 0
+    b = buf[:nwg].astype(np.int64)
+    t0 = b[:, 0].min()
+
+    def us(x):
+        return x * 0.01  # 100 MHz ticks -> us
+
+    off = b[:, 0] - t0
+    print(f"rep {rep}: kernel span {us(b[:, 5].max() - t0):.1f} us; WG start offsets p50/p99/max "
+          f"{us(np.percentile(off, 50)):.1f}/{us(np.percentile(off, 99)):.1f}/{us(off.max()):.1f}; "
+          f"WG end p50/max {us(np.percentile(b[:, 5] - t0, 50)):.1f}/{us((b[:, 5] - t0).max()):.1f}")
+    names = ["stage windows", "move (phase 1)", "pre-test (2a)", "walks (2b)", "store"]
+    for k in range(5):
+        d = us(b[:, k + 1] - b[:, k])
+        print(f"   {names[k]:16s} p50 {np.percentile(d, 50):6.2f}  p90 {np.percentile(d, 90):6.2f}  max {d.max():6.2f} us")
+    mhz = np.median(b[:, 7] / np.maximum(b[:, 5] - b[:, 0], 1)) * 100
+    print(f"   shader clock / realtime x 100 MHz: {mhz:.0f} MHz")
+    q = b[:, 6]
+    print(f"   queued walks per WG: mean {q.mean():.0f} p90 {np.percentile(q, 90):.0f} max {q.max()}")
