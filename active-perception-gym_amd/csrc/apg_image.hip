@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/apgym_capi.h"
@@ -634,6 +635,236 @@ __global__ __launch_bounds__(UNIQ_THREADS) void k_unique(GlimpseGeo g, const voi
   }
 }
 
+// ---- k_unique_blk: the same ranking, register-blocked (the path for L = G*G*C <= 2048).
+// The P glimpses of an env are computed once into a per-workgroup global slot; pairs are then
+// processed as (32-row A tile) x (64-row B tile), leaf by leaf of numpy's pairwise sum over L: each
+// thread owns a 2 x 4 block of pairs (A rows ia, ia+16; B rows ib + 16j) with the leaf's eight
+// strided accumulators per pair in packed f32 registers, so one LDS read feeds 2 or 4 pairs.  Leaf
+// results are combined in the recursion's post order through a small shifting stack (the combine
+// counts come from the host, UniqPlan).  Per-point minima are kept on the pair TOTALS and divided
+// by L at the end: rounding x / L is monotone, so min(x) / L == min(x / L) bit for bit.
+constexpr int UQ_TA = 32, UQ_TB = 64, UQ_THREADS = 256, UQ_MAX_LEAVES = 16, UQ_MAX_L = 2048;
+struct UniqPlan {
+  int nleaves, ls;  // leaves of the pairwise sum over L; LDS row stride (>= longest leaf, ls % 8 == 4)
+  int16_t off[UQ_MAX_LEAVES], len[UQ_MAX_LEAVES];
+  int8_t comb[UQ_MAX_LEAVES];  // combines of the two top partial sums right after leaf j
+};
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <int SD>
+__global__ __launch_bounds__(UQ_THREADS, 3) void k_unique_blk(GlimpseGeo g, const void *pool, const int64_t *index,
+                                                           const double *grid, int n, int P, int k, int32_t *top_k,
+                                                           float *uniq, float *scratch, UniqPlan plan) {
+  extern __shared__ float s_dyn[];  // [UQ_TA + UQ_TB][ls] leaf tiles, then s_min[P]
+  __shared__ float s_lut[256];
+  load_u8_table(s_lut);
+  const int L = g.s0 * g.s1 * g.c, ls = plan.ls;
+  float *s_a = s_dyn, *s_b = s_dyn + UQ_TA * ls;
+  uint32_t *s_min = reinterpret_cast<uint32_t *>(s_dyn + (UQ_TA + UQ_TB) * ls);
+  float *glim = scratch + (size_t)blockIdx.x * P * L;
+  const int tid = threadIdx.x, ia = tid >> 4, ib = tid & 15;
+  const int per = g.s0 * g.s1;
+  const bool vec4 = L % 4 == 0;  // glimpse rows 16-byte aligned (leaf offsets are multiples of 8)
+  for (int e = blockIdx.x; e < n; e += gridDim.x) {
+    const int64_t base = index[e] * g.img_elems;
+    __syncthreads();  // the previous env's ranking is done with s_min
+    for (int q = tid; q < P * per; q += UQ_THREADS) {
+      const int p = q / per, pix = q - p * per;
+      float v[3];
+      glimpse_pixel(g, pool, s_lut, base, grid[2 * p], grid[2 * p + 1], pix / g.s1, pix % g.s1, v);
+      for (int ch = 0; ch < g.c; ch++) glim[(size_t)p * L + pix * g.c + ch] = v[ch];
+    }
+    for (int p = tid; p < P; p += UQ_THREADS) s_min[p] = 0x7f800000u;  // +inf
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // read the slot's fresh glimpses, not stale L1 lines
+    for (int A0 = 0; A0 < P; A0 += UQ_TA) {
+      for (int B0 = A0; B0 < P; B0 += UQ_TB) {
+        float st[SD][8];  // partial sums of the pairwise tree, st[0] on top; pair index i * 4 + j
+#pragma unroll
+        for (int d = 0; d < SD; d++)
+#pragma unroll
+          for (int q = 0; q < 8; q++) st[d][q] = 0.0f;
+        for (int lf = 0; lf < plan.nleaves; lf++) {
+          const int lo = plan.off[lf], ln = plan.len[lf];
+          // stage the leaf's columns of the 96 tile rows: 32 lanes per row (4 columns each), 8 rows at a
+          // time; the loads of each half of the rows are all issued before its first LDS store
+          __syncthreads();  // tiles free
+#pragma unroll 1
+          for (int half = 0; half < 2; half++) {
+            constexpr int RPASS = UQ_THREADS / 32, NPASS = (UQ_TA + UQ_TB) / RPASS / 2;
+            const int c4 = tid & 31, c = 4 * c4, r0 = (tid >> 5) + half * RPASS * NPASS;
+            f4 v[NPASS];
+            if (vec4) {
+#pragma unroll
+              for (int rr = 0; rr < NPASS; rr++) {
+                const int r = r0 + RPASS * rr, p = r < UQ_TA ? A0 + r : B0 + (r - UQ_TA);
+                v[rr] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+                if (c < ln && p < P) v[rr] = *reinterpret_cast<const f4 *>(glim + (size_t)p * L + lo + c);
+              }
+            } else {
+#pragma unroll
+              for (int rr = 0; rr < NPASS; rr++) {
+                const int r = r0 + RPASS * rr, p = r < UQ_TA ? A0 + r : B0 + (r - UQ_TA);
+                const float *src = glim + (size_t)p * L + lo + c;
+                const bool ok = p < P;
+                v[rr].x = ok && c < ln ? src[0] : 0.0f;
+                v[rr].y = ok && c + 1 < ln ? src[1] : 0.0f;
+                v[rr].z = ok && c + 2 < ln ? src[2] : 0.0f;
+                v[rr].w = ok && c + 3 < ln ? src[3] : 0.0f;
+              }
+            }
+#pragma unroll
+            for (int rr = 0; rr < NPASS; rr++) {
+              const int r = r0 + RPASS * rr;
+              if (c < ln) *reinterpret_cast<f4 *>(s_dyn + r * ls + c) = v[rr];
+            }
+          }
+          __syncthreads();
+          const float *pa0 = s_a + ia * ls, *pa1 = s_a + (ia + 16) * ls;
+          const float *pb0 = s_b + ib * ls, *pb1 = s_b + (ib + 16) * ls, *pb2 = s_b + (ib + 32) * ls,
+                      *pb3 = s_b + (ib + 48) * ls;
+          // acc[i][j][h]: a row i, b row j, strided accumulators (2h, 2h+1) packed: the 16-byte row reads
+          // land in register pairs the packed f32 ops take as they are
+          f2 acc[2][4][4];
+#pragma unroll
+          for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+              for (int h = 0; h < 4; h++) acc[i][j][h] = f2{0.0f, 0.0f};
+          const int groups = ln >> 3;
+          for (int gi = 0; gi < groups; gi++) {
+            const int c = gi * 8;
+            f2 av[2][4], bv[4][4];
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+              const float *pa = i ? pa1 : pa0;
+              const f4 lo4 = *reinterpret_cast<const f4 *>(pa + c), hi4 = *reinterpret_cast<const f4 *>(pa + c + 4);
+              av[i][0] = lo4.xy;
+              av[i][1] = lo4.zw;
+              av[i][2] = hi4.xy;
+              av[i][3] = hi4.zw;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+              const float *pb = j == 0 ? pb0 : (j == 1 ? pb1 : (j == 2 ? pb2 : pb3));
+              const f4 lo4 = *reinterpret_cast<const f4 *>(pb + c), hi4 = *reinterpret_cast<const f4 *>(pb + c + 4);
+              bv[j][0] = lo4.xy;
+              bv[j][1] = lo4.zw;
+              bv[j][2] = hi4.xy;
+              bv[j][3] = hi4.zw;
+            }
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+              for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int h = 0; h < 4; h++) {
+                  const f2 d = bv[j][h] - av[i][h];
+                  acc[i][j][h] = acc[i][j][h] + d * d;
+                }
+          }
+          // leaf sums: ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) (0 for a leaf shorter than 8), in-order tail
+          float res[8];
+#pragma unroll
+          for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+              const f2 *r = acc[i][j];
+              const float t = __fadd_rn(__fadd_rn(__fadd_rn(r[0].x, r[0].y), __fadd_rn(r[1].x, r[1].y)),
+                                        __fadd_rn(__fadd_rn(r[2].x, r[2].y), __fadd_rn(r[3].x, r[3].y)));
+              res[i * 4 + j] = groups ? t : 0.0f;
+            }
+          for (int c = groups * 8; c < ln; c++) {
+            const float a[2] = {pa0[c], pa1[c]};
+            const float b[4] = {pb0[c], pb1[c], pb2[c], pb3[c]};
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+              for (int j = 0; j < 4; j++) {
+                const float d = __fsub_rn(b[j], a[i]);
+                res[i * 4 + j] = __fadd_rn(res[i * 4 + j], __fmul_rn(d, d));
+              }
+          }
+          // push, then the post-order combines (left = st[1], right = st[0])
+#pragma unroll
+          for (int d = SD - 1; d > 0; d--)
+#pragma unroll
+            for (int q = 0; q < 8; q++) st[d][q] = st[d - 1][q];
+#pragma unroll
+          for (int q = 0; q < 8; q++) st[0][q] = res[q];
+          for (int cb = 0; cb < plan.comb[lf]; cb++) {
+#pragma unroll
+            for (int q = 0; q < 8; q++) st[0][q] = __fadd_rn(st[1][q], st[0][q]);
+#pragma unroll
+            for (int d = 1; d < SD - 1; d++)
+#pragma unroll
+              for (int q = 0; q < 8; q++) st[d][q] = st[d + 1][q];
+          }
+        }
+        // per-point minima over the valid pairs a < b < P (totals are >= 0: unsigned order == float order)
+        const int a[2] = {A0 + ia, A0 + ia + 16};
+        const int b[4] = {B0 + ib, B0 + ib + 16, B0 + ib + 32, B0 + ib + 48};
+        uint32_t colmin[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+          uint32_t rowmin = 0xffffffffu;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            if (a[i] < b[j] && b[j] < P) {
+              const uint32_t bits = __float_as_uint(st[0][i * 4 + j]);
+              rowmin = bits < rowmin ? bits : rowmin;
+              colmin[j] = bits < colmin[j] ? bits : colmin[j];
+            }
+          }
+          if (rowmin != 0xffffffffu) atomicMin(&s_min[a[i]], rowmin);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (colmin[j] != 0xffffffffu) atomicMin(&s_min[b[j]], colmin[j]);
+      }
+    }
+    __syncthreads();
+    // np.mean = (0 + total) / L on the minimum total of each point
+    const float lden = (float)L;
+    for (int p = tid; p < P; p += UQ_THREADS) {
+      const float m = f32_div(__fadd_rn(0.0f, __uint_as_float(s_min[p])), lden);
+      s_min[p] = __float_as_uint(m);
+      if (uniq) uniq[(size_t)e * P + p] = m;
+    }
+    __syncthreads();
+    if (tid < 64) {  // top k by descending uniqueness, exact ties by ascending index
+      const int lane = tid;
+      for (int r = 0; r < k; r++) {
+        uint32_t best = 0;
+        int bi = 0x7fffffff;
+        for (int p = lane; p < P; p += 64) {
+          const uint32_t v = s_min[p];
+          if (v != 0xffffffffu && (bi == 0x7fffffff || v > best)) {
+            best = v;
+            bi = p;
+          }
+        }
+        for (int d = 32; d >= 1; d >>= 1) {
+          const uint32_t ob = __shfl_xor(best, d, 64);
+          const int oi = __shfl_xor(bi, d, 64);
+          if (oi != 0x7fffffff && (bi == 0x7fffffff || ob > best || (ob == best && oi < bi))) {
+            best = ob;
+            bi = oi;
+          }
+        }
+        if (lane == 0) {
+          top_k[(size_t)e * k + r] = bi;
+          s_min[bi] = 0xffffffffu;  // taken
+        }
+        __builtin_amdgcn_wave_barrier();
+        __threadfence_block();
+      }
+    }
+  }
+}
+
 // target = clip(grid[top_k[sel]] + jitter, -1, 1).astype(float32)  (:281-292, image_localization.py:139-143)
 __global__ void k_unique_finish(int n, int offset, int k, const int32_t *top_k, const int64_t *sel,
                                 const double *grid, const double *jitter, float *target) {
@@ -776,9 +1007,90 @@ int unique_tile_rows(int L) {
   return T;
 }
 
+// numpy's pairwise recursion over L as a leaf list with post-order combine counts; returns the
+// partial-sum stack depth it needs, or 0 when it does not fit the blocked kernel
+int unique_plan(int L, UniqPlan &pl) {
+  memset(&pl, 0, sizeof(pl));
+  int depth = 0, maxdepth = 0, longest = 0;
+  bool ok = true;
+  auto rec = [&](auto &&self, int off, int len) -> void {
+    if (len <= 128) {
+      if (pl.nleaves >= UQ_MAX_LEAVES) {
+        ok = false;
+        return;
+      }
+      pl.off[pl.nleaves] = (int16_t)off;
+      pl.len[pl.nleaves] = (int16_t)len;
+      pl.nleaves++;
+      longest = len > longest ? len : longest;
+      depth++;
+      maxdepth = depth > maxdepth ? depth : maxdepth;
+      return;
+    }
+    int n2 = len / 2;
+    n2 -= n2 % 8;
+    self(self, off, n2);
+    self(self, off + n2, len - n2);
+    if (!ok) return;
+    pl.comb[pl.nleaves - 1]++;
+    depth--;
+  };
+  rec(rec, 0, L);
+  if (!ok || L > UQ_MAX_L) return 0;
+  pl.ls = ((longest + 3) / 4) * 4;
+  if (pl.ls % 8 == 0) pl.ls += 4;  // ls / 4 odd: the 16-byte row reads of 16 lanes hit distinct banks
+  return maxdepth;
+}
+
+float *unique_scratch(size_t bytes) {  // per-device slot buffer of k_unique_blk, grown on demand (resets only)
+  static float *buf[64] = {};
+  static size_t cap[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (cap[dev] < bytes) {
+    if (buf[dev]) (void)hipFree(buf[dev]);
+    buf[dev] = nullptr;
+    cap[dev] = 0;
+    if (hipMalloc(reinterpret_cast<void **>(&buf[dev]), bytes) != hipSuccess) return nullptr;
+    cap[dev] = bytes;
+  }
+  return buf[dev];
+}
+
+template <int SD>
+int launch_unique_blk(const GlimpseGeo &g, const void *pool, const int64_t *index, const double *grid, int n, int P,
+                      int k, int32_t *top_k, float *uniq, const UniqPlan &pl, hipStream_t s) {
+  const int L = g.s0 * g.s1 * g.c;
+  const size_t dyn = ((size_t)(UQ_TA + UQ_TB) * pl.ls + P) * sizeof(float);
+  if (dyn > 64 * 1024 &&
+      hipFuncSetAttribute((const void *)k_unique_blk<SD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) !=
+          hipSuccess)
+    return fail(APG_E_LAUNCH, "hipFuncSetAttribute(k_unique_blk) failed");
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_unique_blk<SD>, UQ_THREADS, dyn) != hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return fail(APG_E_LAUNCH, "k_unique_blk occupancy query failed");
+  int blocks = (per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1);
+  if (const char *cap = getenv("APG_UNIQUE_GRID")) blocks = atoi(cap) > 0 ? atoi(cap) : blocks;  // tests: striding
+  if (blocks > n) blocks = n;
+  float *scratch = unique_scratch((size_t)blocks * P * L * sizeof(float));
+  if (!scratch) return fail(APG_E_LAUNCH, "hipMalloc of the uniqueness glimpse slots failed");
+  hipLaunchKernelGGL(k_unique_blk<SD>, dim3(blocks), dim3(UQ_THREADS), dyn, s, g, pool, index, grid, n, P, k, top_k,
+                     uniq, scratch, pl);
+  return check_launch("k_unique_blk");
+}
+
 int launch_unique(const GlimpseGeo &g, const void *pool, const int64_t *index, const double *grid, int n, int P,
                   int k, int32_t *top_k, float *uniq, hipStream_t s) {
   const int L = g.s0 * g.s1 * g.c;
+  if (P > UNIQ_MAX_POINTS) return fail(APG_E_INVALID, "too many unique-sampling grid points");
+  if (k < 1 || k > P) return fail(APG_E_INVALID, "top_k must be in [1, P]");
+  UniqPlan pl;
+  const int sd = getenv("APG_UNIQUE_GENERIC") ? 0 : unique_plan(L, pl);
+  if (sd >= 1 && sd <= 2) return launch_unique_blk<2>(g, pool, index, grid, n, P, k, top_k, uniq, pl, s);
+  if (sd == 3) return launch_unique_blk<3>(g, pool, index, grid, n, P, k, top_k, uniq, pl, s);
+  if (sd >= 4 && sd <= 5) return launch_unique_blk<5>(g, pool, index, grid, n, P, k, top_k, uniq, pl, s);
   const int T = unique_tile_rows(L);
   if (T < 1) return fail(APG_E_INVALID, "glimpse too large for the uniqueness tiles");
   if (P > UNIQ_MAX_POINTS) return fail(APG_E_INVALID, "too many unique-sampling grid points");

@@ -172,9 +172,18 @@ def test_glimpse_out_of_bounds_flags_like_scipy(gpu):
             assert not bits & N.APG_ERR_OOB_Y
 
 
-@pytest.mark.parametrize("h,w,c,sensor,n", [(28, 28, 1, (5, 5), 24), (32, 32, 3, (6, 6), 6), (64, 64, 3, (12, 12), 2)])
-def test_unique_top_k_matches_oracle(gpu, h, w, c, sensor, n):
+# L = G*G*C: 25 and 108 (one leaf of numpy's pairwise sum), 432 (4 leaves), 300 (leaf tail), 4 (a leaf
+# shorter than 8), 768 (deeper combine stack); knobs: the generic kernel, and few workgroups (env striding)
+@pytest.mark.parametrize("h,w,c,sensor,n,knob", [(28, 28, 1, (5, 5), 24, None), (32, 32, 3, (6, 6), 6, None),
+                                                 (64, 64, 3, (12, 12), 2, None), (32, 32, 3, (10, 10), 4, None),
+                                                 (16, 16, 1, (2, 2), 3, None), (64, 64, 3, (16, 16), 2, None),
+                                                 (64, 64, 3, (12, 12), 2, "APG_UNIQUE_GENERIC=1"),
+                                                 (28, 28, 1, (5, 5), 24, "APG_UNIQUE_GRID=5")])
+def test_unique_top_k_matches_oracle(gpu, h, w, c, sensor, n, knob, monkeypatch):
     import torch
+
+    if knob:
+        monkeypatch.setenv(*knob.split("="))
 
     from ap_gym_amd import _native as N
     from ap_gym_amd.image_env import unique_sampling_grid
