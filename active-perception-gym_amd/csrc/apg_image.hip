@@ -17,6 +17,7 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (see build.py).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -61,8 +62,11 @@ GlimpseGeo make_geo(const apg_image_config *c) {
 // float32(v) / 255 for v = 0..255 (_process_imgs_np), staged in LDS by every glimpse workgroup:
 // the f64 quotient rounded once more to f32 equals numpy's correctly rounded f32 division for all
 // 256 values (checked bit for bit by the glimpse parity tests, which cover every u8 value)
+APG_DEV float u8_value(unsigned v) { return (float)__dmul_rn((double)v, 1.0 / 255.0); }
 APG_DEV void load_u8_table(float *lut) {
-  for (int v = threadIdx.x; v < 256; v += blockDim.x) lut[v] = (float)__ddiv_rn((double)v, 255.0);
+  // v * (1/255) in f64 rounds to the same f32 as the correctly rounded v / 255 for every v in 0..255
+  // (checked exhaustively against numpy on the host); cheaper than an f64 division per entry
+  for (int v = threadIdx.x; v < 256; v += blockDim.x) lut[v] = u8_value((unsigned)v);
   __syncthreads();
 }
 
@@ -319,6 +323,116 @@ __global__ __launch_bounds__(256) void k_glimpse(GlimpseGeo g, const void *pool,
   float v[3];
   const uint32_t bad = glimpse_pixel(g, pool, s_lut, index[e] * g.img_elems, px, py, i, j, v);
   for (int ch = 0; ch < g.c; ch++) out[(size_t)t * g.c + ch] = v[ch];
+  if (bad) atomicOr(err, bad);
+}
+
+// k_glimpse_sep: the same pixels, UPB glimpse units (env x position) per workgroup, using that the
+// bilinear coordinates are separable: the row interval / weight of pixel (i, j) depends on i only and
+// the column ones on j only, so they are computed once per unit row and column (G0 + G1 values instead
+// of G0 * G1) and shared through LDS; each pixel then forms its four weights and reads its taps.
+// Divisions by the launch-invariant unit and row sizes use host-computed reciprocals (FastDiv).
+constexpr int GS_THREADS = 256, GS_MAX_UNITS = 64, GS_MAX_SIDE = 256;
+struct FastDiv {  // n / d for n < 2^32 / d: (n * ceil(2^32 / d)) >> 32
+  uint32_t d, m;
+  APG_DEV uint32_t div(uint32_t n) const { return d == 1 ? n : __umulhi(n, m); }
+};
+FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  f.m = d <= 1 ? 0u : (uint32_t)((((uint64_t)1 << 32) + d - 1) / d);
+  return f;
+}
+
+struct Axis {  // one sampling coordinate: grid interval, fractional weight, 1 - weight
+  int idx;
+  double w, nw;
+};
+
+template <class PosT>
+__global__ __launch_bounds__(GS_THREADS) void k_glimpse_sep(GlimpseGeo g, const void *pool, const int64_t *index,
+                                                            const PosT *pos, int npos, int units, int upb,
+                                                            FastDiv per_div, FastDiv s1_div, FastDiv side_div,
+                                                            float *out, uint32_t *err) {
+  __shared__ float s_lut[256];
+  extern __shared__ Axis s_ax[];  // [unit][rows s0 | columns s1]
+  __shared__ int64_t s_base[GS_MAX_UNITS];
+  const int tid = threadIdx.x;
+  for (int v = tid; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
+  const int u0 = blockIdx.x * upb, nu = units - u0 < upb ? units - u0 : upb;
+  const int side = g.s0 + g.s1;
+  uint32_t bad = 0;
+  for (int q = tid; q < nu * side; q += GS_THREADS) {
+    const int u = (int)side_div.div((uint32_t)q), k = q - u * side;
+    const bool row = k < g.s0;
+    const int t = row ? k : k - g.s0;
+    const double p = (double)pos[2 * (u0 + u) + (row ? 1 : 0)];
+    // flip(denormalize(pos)) + offsets (glimpse_pixel): rows use pos[1], columns pos[0]
+    const double off = __dmul_rn(__dsub_rn((double)t, ((double)(row ? g.s0 : g.s1) - 1.0) / 2.0), g.scale);
+    const double c = __dadd_rn(__dmul_rn(p, row ? g.lim_y : g.lim_x), off);
+    const double lim = row ? g.cy : g.cx;
+    if (!(c >= -lim && c <= lim)) bad |= row ? APG_ERR_OOB_Y : APG_ERR_OOB_X;
+    Axis ax;
+    ax.idx = grid_interval(c, lim, row ? g.h : g.w, ax.w);
+    ax.nw = __dsub_rn(1.0, ax.w);
+    s_ax[q] = ax;
+    if (k == 0) s_base[u] = index[(u0 + u) / npos] * g.img_elems;
+  }
+  __syncthreads();
+  const int per = g.s0 * g.s1;
+  for (int q = tid; q < nu * per; q += GS_THREADS) {
+    const int u = (int)per_div.div((uint32_t)q), pix = q - u * per;
+    const int i = (int)s1_div.div((uint32_t)pix), j = pix - i * g.s1;
+    const Axis ay = s_ax[u * side + i], axx = s_ax[u * side + g.s0 + j];
+    // hypercube order of _evaluate_linear: (i0, j0), (i0, j0+1), (i0+1, j0), (i0+1, j0+1); w = (1*wy)*wx
+    const double w00 = __dmul_rn(ay.nw, axx.nw), w01 = __dmul_rn(ay.nw, axx.w), w10 = __dmul_rn(ay.w, axx.nw),
+                 w11 = __dmul_rn(ay.w, axx.w);
+    const int64_t r0 = s_base[u] + ((int64_t)ay.idx * g.w + axx.idx) * g.pc, r1 = r0 + (int64_t)g.w * g.pc;
+    float *dst = out + ((size_t)u0 * per + q) * g.c;
+    // u8 pools: the 2 * pc tap bytes of each row are contiguous; read them with aligned dword loads
+    // (at most three per row, only the ones they occupy) instead of one byte load per tap
+    uint32_t rw0[3] = {0, 0, 0}, rw1[3] = {0, 0, 0};
+    int o0 = 0, o1 = 0;
+    if (!g.pool_f32) {
+      const uint8_t *im = static_cast<const uint8_t *>(pool);
+      const uintptr_t a0 = reinterpret_cast<uintptr_t>(im + r0), a1 = reinterpret_cast<uintptr_t>(im + r1);
+      o0 = (int)(a0 & 3u);
+      o1 = (int)(a1 & 3u);
+      const uint32_t *d0 = reinterpret_cast<const uint32_t *>(a0 - o0), *d1 = reinterpret_cast<const uint32_t *>(a1 - o1);
+      const int span = 2 * g.pc;
+      rw0[0] = d0[0];
+      rw1[0] = d1[0];
+      if (o0 + span > 4) rw0[1] = d0[1];
+      if (o1 + span > 4) rw1[1] = d1[1];
+      if (o0 + span > 8) rw0[2] = d0[2];
+      if (o1 + span > 8) rw1[2] = d1[2];
+    }
+    auto tap = [&](const uint32_t *w, int k) {  // byte k of the loaded dwords
+      const uint32_t word = k < 4 ? w[0] : (k < 8 ? w[1] : w[2]);
+      return s_lut[(word >> (8 * (k & 3))) & 0xffu];
+    };
+    for (int ch = 0; ch < g.c; ch++) {
+      const int cc = g.pc == 1 ? 0 : ch;
+      float t00, t01, t10, t11;
+      if (g.pool_f32) {
+        const float *im = static_cast<const float *>(pool);
+        t00 = im[r0 + cc];
+        t01 = im[r0 + g.pc + cc];
+        t10 = im[r1 + cc];
+        t11 = im[r1 + g.pc + cc];
+      } else {
+        t00 = tap(rw0, o0 + cc);
+        t01 = tap(rw0, o0 + g.pc + cc);
+        t10 = tap(rw1, o1 + cc);
+        t11 = tap(rw1, o1 + g.pc + cc);
+      }
+      double v = __dadd_rn(0.0, __dmul_rn((double)t00, w00));
+      v = __dadd_rn(v, __dmul_rn((double)t01, w01));
+      v = __dadd_rn(v, __dmul_rn((double)t10, w10));
+      v = __dadd_rn(v, __dmul_rn((double)t11, w11));
+      v = v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);  // np.clip(0, 1)
+      dst[ch] = (float)v;
+    }
+  }
   if (bad) atomicOr(err, bad);
 }
 
@@ -996,6 +1110,15 @@ int launch_glimpse(const GlimpseGeo &g, const void *pool, const int64_t *index, 
                    float *out, uint32_t *err, hipStream_t s) {
   const int64_t total = (int64_t)n * npos * g.s0 * g.s1;
   if (total >= (int64_t)1 << 31) return fail(APG_E_INVALID, "glimpse batch too large (>= 2**31 pixels)");
+  if (g.s0 <= GS_MAX_SIDE && g.s1 <= GS_MAX_SIDE && !getenv("APG_GLIMPSE_GENERIC")) {
+    const int per = g.s0 * g.s1, units = n * npos;
+    const int upb = std::max(1, std::min(GS_MAX_UNITS, (4 * GS_THREADS + per - 1) / per));
+    const size_t dyn = (size_t)upb * (g.s0 + g.s1) * sizeof(Axis);
+    hipLaunchKernelGGL(k_glimpse_sep<PosT>, dim3(grid_for(units, upb)), dim3(GS_THREADS), dyn, s, g, pool, index, pos,
+                       npos, units, upb, make_fastdiv((uint32_t)per), make_fastdiv((uint32_t)g.s1),
+                       make_fastdiv((uint32_t)(g.s0 + g.s1)), out, err);
+    return check_launch("k_glimpse_sep");
+  }
   hipLaunchKernelGGL(k_glimpse<PosT>, dim3(grid_for(total, 256)), dim3(256), 0, s, g, pool, index, pos, npos,
                      (int)total, out, err);
   return check_launch("k_glimpse");

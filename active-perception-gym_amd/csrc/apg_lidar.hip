@@ -296,6 +296,7 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
   float *s_lid = reinterpret_cast<float *>(s_dyn + EPB * WIN_STRIDE);
   uint16_t *s_queue = reinterpret_cast<uint16_t *>(s_lid + EPB * LS);
   __shared__ int s_qn;
+  __shared__ float s_dirs[MAX_STAGED_BEAMS][2];  // beam_dirs, read inside the beam loops (LDS, not HBM latency)
   const int tid = threadIdx.x;
   const int base = blockIdx.x * EPB;
   const size_t words = (size_t)P.h * P.wpr;
@@ -306,6 +307,7 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
 
   // ---------------- phase 0: window origins from the pre-move positions; which envs reset
   __shared__ unsigned long long s_reset;
+  if (P.beams <= MAX_STAGED_BEAMS && tid < 2 * P.beams) s_dirs[tid >> 1][tid & 1] = S.beam_dirs[tid];
   if (tid < EPB) {
     const int e = base + tid;
     bool rs = false;
@@ -512,7 +514,9 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
   for (int beam = tid / EPB; beam < P.beams; beam += STEP_THREADS / EPB) {
     bool walk = false;
     if (e < P.n) {
-      const float qx = __fadd_rn(px, S.beam_dirs[2 * beam]), qy = __fadd_rn(py, S.beam_dirs[2 * beam + 1]);
+      const float dx = staged ? s_dirs[beam][0] : S.beam_dirs[2 * beam];
+      const float dy = staged ? s_dirs[beam][1] : S.beam_dirs[2 * beam + 1];
+      const float qx = __fadd_rn(px, dx), qy = __fadd_rn(py, dy);
       walk = scan_may_hit(rw, px, py, qx, qy);
       if (!walk || !staged) {
         const float d = walk ? lidar_scan_walk(rw, px, py, qx, qy).dist : scan_empty(px, py, qx, qy).dist;
@@ -541,7 +545,7 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
       const int ent = s_queue[i], qe = ent & (EPB - 1), beam = ent >> 6;
       const float qpx = s_pos[qe][0], qpy = s_pos[qe][1];
       const RowsWindow qrw{&s_win[qe * WIN_STRIDE], s_x0[qe], s_y0[qe], P.wrows};
-      const float qx = __fadd_rn(qpx, S.beam_dirs[2 * beam]), qy = __fadd_rn(qpy, S.beam_dirs[2 * beam + 1]);
+      const float qx = __fadd_rn(qpx, s_dirs[beam][0]), qy = __fadd_rn(qpy, s_dirs[beam][1]);
       const float d = lidar_scan_walk(qrw, qpx, qpy, qx, qy).dist;
       s_lid[qe * LS + beam] = fminf(fmaxf(f32_div(d, P.range), -1.0f), 1.0f);
     }
