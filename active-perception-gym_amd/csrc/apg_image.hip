@@ -410,6 +410,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_glimpse_sep(GlimpseGeo g, const 
       const uint32_t word = k < 4 ? w[0] : (k < 8 ? w[1] : w[2]);
       return s_lut[(word >> (8 * (k & 3))) & 0xffu];
     };
+    float res[3];
     for (int ch = 0; ch < g.c; ch++) {
       const int cc = g.pc == 1 ? 0 : ch;
       float t00, t01, t10, t11;
@@ -430,7 +431,15 @@ __global__ __launch_bounds__(GS_THREADS) void k_glimpse_sep(GlimpseGeo g, const 
       v = __dadd_rn(v, __dmul_rn((double)t10, w10));
       v = __dadd_rn(v, __dmul_rn((double)t11, w11));
       v = v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);  // np.clip(0, 1)
-      dst[ch] = (float)v;
+      res[ch] = (float)v;
+    }
+    if (g.c == 3) {
+      struct F3 {
+        float x, y, z;
+      };
+      *reinterpret_cast<F3 *>(dst) = F3{res[0], res[1], res[2]};  // one 12-byte store per pixel
+    } else {
+      for (int ch = 0; ch < g.c; ch++) dst[ch] = res[ch];
     }
   }
   if (bad) atomicOr(err, bad);
@@ -444,6 +453,7 @@ struct EnvArgs {
   float mse_scale, mse_offset;
   float time_value;
   float loss_weight;  // 1, or for the -sparse ids terminated.astype(float32) (one value: episodes end together)
+  const float *copy_target;  // localize, steps without a target refresh: prediction_target = target.copy() here
 };
 
 // scipy.special.log_softmax(row)[target] in float32 (x_max zeroed when not finite); -> -value
@@ -556,7 +566,12 @@ __global__ __launch_bounds__(256) void k_image_env_loc(EnvArgs a, const float *_
   uint32_t err = 0;
   const float p0 = pred[2 * e], p1 = pred[2 * e + 1];
   if (p0 != p0 || p1 != p1) err |= APG_ERR_NAN_PREDICTION;  // 1 - |pred - target| / 2 is NaN
-  const float t0 = out.target[2 * e], t1 = out.target[2 * e + 1];
+  if (a.copy_target) {  // k_loc_target folded in (no refresh this step)
+    out.target[2 * e] = a.copy_target[2 * e];
+    out.target[2 * e + 1] = a.copy_target[2 * e + 1];
+  }
+  const float t0 = a.copy_target ? a.copy_target[2 * e] : out.target[2 * e];
+  const float t1 = a.copy_target ? a.copy_target[2 * e + 1] : out.target[2 * e + 1];
   const float d0 = __fsub_rn(p0, t0), d1 = __fsub_rn(p1, t1);
   // np.mean(f32 [2]): (0 + d0^2 + d1^2) / 2, then * scale + offset in f32
   const float mse = f32_div(__fadd_rn(__fadd_rn(0.0f, __fmul_rn(d0, d0)), __fmul_rn(d1, d1)), 2.0f);
@@ -1334,9 +1349,11 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
       const double low[2] = {-1.0, -1.0}, range[2] = {2.0, 2.0};
       if ((rc = launch_uniform(st->rng + 0, c->num_envs_total, 2, low, range, st->scratch_f64, s))) return rc;
     }
-    hipLaunchKernelGGL(k_loc_target, dim3(grid_for(n, 256)), dim3(256), 0, s, n, c->env_offset, prev_done,
-                       st->scratch_f64, st->target, out->target);
-    if ((rc = check_launch("k_loc_target"))) return rc;
+    if (prev_done) {  // otherwise the copy is folded into k_image_env_loc
+      hipLaunchKernelGGL(k_loc_target, dim3(grid_for(n, 256)), dim3(256), 0, s, n, c->env_offset, prev_done,
+                         st->scratch_f64, st->target, out->target);
+      if ((rc = check_launch("k_loc_target"))) return rc;
+    }
   }
   if (prev_done && (rc = module_reset(c, st, out, s))) return rc;
   EnvArgs a;
@@ -1356,6 +1373,7 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
   a.t_new = t_new;
   a.time_value = (float)(((double)t_new / (double)c->step_limit) * 2.0 - 1.0);
   a.loss_weight = !c->sparse ? 1.0f : (!prev_done && t_new >= c->step_limit ? 1.0f : 0.0f);
+  a.copy_target = c->kind == APG_IMAGE_LOCALIZE && !prev_done ? st->target : nullptr;
   if (c->kind == APG_IMAGE_CLASSIFY) {
     int epb = 256 / CLS_LANES;
     while (epb > 1 && (size_t)epb * (c->num_classes + 1) * sizeof(float) > 64 * 1024) epb /= 2;
