@@ -17,3 +17,8 @@ for c in FETCH_SIZE WRITE_SIZE; do
     python $R/bench.py --no-cpu-baseline > $O/pmc_$c.log 2>&1
 done
 python $R/profiles/traffic.py $O > $O/traffic_lidar_step.json
+# image workloads (BASELINE configs 4, 5): kernel stats of the benches
+for w in mnist tinyimagenet-loc; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats_$w -o run --output-format csv -- \
+    python $R/bench.py --workload $w --no-cpu-baseline > $O/bench_stats_$w.json 2> $O/bench_stats_$w.err
+done
