@@ -67,6 +67,12 @@ class LidarOutputs(ctypes.Structure):
                                    "stats", "stats_len", "weight")]
 
 
+class LidarRenderState(ctypes.Structure):
+    _fields_ = [("num_tracked", ctypes.c_int32), ("scan_points", ctypes.c_int32)] + [
+        (n, _vp) for n in ("env", "scan_xy", "scan_norm", "obs_map", "traj", "traj_len", "pose", "has_last",
+                           "lidar_dist")]
+
+
 class LidarSizes(ctypes.Structure):
     _fields_ = [("occ_bytes", ctypes.c_size_t), ("scratch_bytes", ctypes.c_size_t),
                 ("stack_bytes", ctypes.c_size_t), ("wpr", ctypes.c_int32), ("maze_frames", ctypes.c_int32)]
@@ -139,6 +145,8 @@ SYMBOLS = [
                                         ctypes.c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp]),
     ("apg_lidar_scan_batch", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp,
                                             _vp]),
+    ("apg_lidar_render_track", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(LidarState), _vp,
+                                              ctypes.POINTER(LidarOutputs), ctypes.POINTER(LidarRenderState), _vp]),
     ("apg_rng_draws", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                      _vp, _vp]),
     ("apg_rng_fill_work_elems", ctypes.c_int64, [ctypes.c_int64, ctypes.c_uint64]),

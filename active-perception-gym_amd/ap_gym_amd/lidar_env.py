@@ -69,7 +69,7 @@ class LIDARLocalization2DVectorEnv:
                  static_map_index: int = 0, prefetch: bool = True, prefetch_buffer_size: int = 128,
                  max_episode_steps: int = 100, device=None, env_offset: int = 0, copy: bool = False,
                  strict_errors: bool = False, array_backend: str = "numpy", log_stats: bool = False,
-                 sparse: bool = False):
+                 sparse: bool = False, render_envs=None):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -183,6 +183,77 @@ class LIDARLocalization2DVectorEnv:
         self._stats_view = None
         self._steps_since_poll = 0
         N.check(L.apg_lidar_init(ctypes.byref(self._cfg), ctypes.byref(self._state), self._stream()), "apg_lidar_init")
+        self._setup_render(render_envs)
+
+    # ------------------------------------------------------------------ render state
+    def _setup_render(self, render_envs):
+        """Device buffers of the render-only state of the tracked sub-envs (apg_lidar_render_track).
+        render_envs=None tracks every sub-env up to render.DEFAULT_TRACKED of them, else none."""
+        import torch
+
+        from .render import tracked_envs
+
+        self.render_envs = tracked_envs(render_envs, self.num_envs)
+        self._r = self._rstate = None
+        k = len(self.render_envs)
+        if not k:
+            return
+        ang = np.linspace(-np.pi, np.pi, self.lidar_beam_count, dtype=np.float32, endpoint=False)
+        unscaled = np.stack([np.cos(ang), np.sin(ang)], axis=-1)
+        scan = np.arange(0, self.lidar_range, 0.05)[None, :, None] * unscaled[:, None]  # lidar_localization2d.py:188-191
+        h, w, dev = self.dataset.map_height, self.dataset.map_width, self.device
+        f32, i32 = torch.float32, torch.int32
+        self._r = R = dict(
+            env=torch.as_tensor(self.render_envs.astype(np.int32), device=dev),
+            scan_xy=torch.as_tensor(np.ascontiguousarray(scan, dtype=np.float64), device=dev),
+            scan_norm=torch.as_tensor(np.ascontiguousarray(np.linalg.norm(scan, axis=-1), dtype=np.float64), device=dev),
+            obs_map=torch.zeros((k, h, (w + 31) // 32), dtype=i32, device=dev),
+            traj=torch.zeros((k, self.max_episode_steps, 3), dtype=f32, device=dev),
+            traj_len=torch.zeros(k, dtype=i32, device=dev),
+            pose=torch.zeros((k, 6), dtype=f32, device=dev),
+            has_last=torch.zeros(k, dtype=i32, device=dev),
+            lidar_dist=torch.zeros((k, self.lidar_beam_count), dtype=f32, device=dev))
+        self._rstate = N.LidarRenderState(k, scan.shape[1], *[N.ptr(R[n]) for n in (
+            "env", "scan_xy", "scan_norm", "obs_map", "traj", "traj_len", "pose", "has_last", "lidar_dist")])
+
+    def _track_render(self, prediction):
+        if self._rstate is not None:
+            N.check(N.lib().apg_lidar_render_track(ctypes.byref(self._cfg), ctypes.byref(self._state),
+                                                   N.ptr(prediction), ctypes.byref(self._out),
+                                                   ctypes.byref(self._rstate), self._stream()),
+                    "apg_lidar_render_track")
+
+    def _occupancy(self, envs: np.ndarray) -> np.ndarray:
+        """Current maps (bool [len(envs), H, W]) of the given sub-envs, unpacked from the bit rows."""
+        h, w = self.dataset.map_height, self.dataset.map_width
+        wpr = (w + 63) // 64
+        rows = self._t["occ"].view(-1, h * wpr)
+        sel = np.zeros(len(envs), np.int64) if self.static_map else envs
+        words = rows[torch_index(sel, self.device)].cpu().numpy()
+        bits = np.unpackbits(words.view(np.uint8).reshape(len(envs), h, wpr * 8), axis=-1, bitorder="little")
+        return bits[..., :w].astype(bool)
+
+    def render(self):
+        """SyncVectorEnv.render(): a tuple with one rgb_array frame per tracked sub-env, drawn from the
+        device render state like LIDARLocalization2DEnv.render (lidar_localization2d.py:391-494)."""
+        from .render import lidar_frame, no_tracked_error
+
+        if self._rstate is None:
+            raise no_tracked_error()
+        if not self._seeded:
+            raise RuntimeError("render() needs reset() first")
+        R = {k: self._r[k].cpu().numpy() for k in ("obs_map", "traj", "traj_len", "pose", "has_last", "lidar_dist")}
+        w = self.dataset.map_width
+        seen = np.unpackbits(R["obs_map"].view(np.uint8), axis=-1, bitorder="little")[..., :w].astype(bool)
+        occ = self._occupancy(self.render_envs)
+        dirs = self._t["beam_dirs"].cpu().numpy()
+        frames = []
+        for j in range(len(self.render_envs)):
+            p = R["pose"][j]
+            last = bool(R["has_last"][j])
+            frames.append(lidar_frame(occ[j], seen[j], R["traj"][j, :R["traj_len"][j]], R["lidar_dist"][j], dirs,
+                                      p[4:6], p[0:2] if last else None, p[2:4] if last else None))
+        return tuple(frames)
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
@@ -265,6 +336,7 @@ class LIDARLocalization2DVectorEnv:
             raise ValueError("seed must be a non-negative int")
         N.check(N.lib().apg_lidar_reset(ctypes.byref(self._cfg), ctypes.byref(self._state), s, int(use_seed),
                                         ctypes.byref(self._out), self._stream()), "apg_lidar_reset")
+        self._track_render(None)
         self._seeded = True
         self._autoreset_host[:] = False
         T = self._t
@@ -309,6 +381,7 @@ class LIDARLocalization2DVectorEnv:
             rc = N.lib().apg_lidar_step_profiled(ctypes.byref(self._cfg), ctypes.byref(self._state), N.ptr(a_t),
                                                  N.ptr(p_t), ctypes.byref(self._out), self._stream(), ev_b, ev_e)
         N.check(rc, "apg_lidar_step")
+        self._track_render(p_t)
         if numpy_mode:
             return self._numpy_step_result()
         self._post_launch_error_copy()
@@ -430,9 +503,6 @@ class LIDARLocalization2DVectorEnv:
             info["_map_idx"] = reset_mask
         self._autoreset_host = term | trunc
         return obs, reward, term, trunc, info
-
-    def render(self):
-        raise NotImplementedError("rendering is not part of the MI355X hot path (SURVEY §8(f) item 2)")
 
     def close(self, **kwargs):
         if not self._closed:

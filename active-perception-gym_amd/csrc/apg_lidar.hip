@@ -578,6 +578,96 @@ __global__ void k_scan_batch(const uint64_t *occ, const int32_t *map_index, int 
   if (kind) kind[i] = o.kind;
 }
 
+// ------------------------------------------------------------------ render tracking (render path only)
+// LIDARLocalization2DEnv keeps render-only state the hot kernels do not: the observation_map of every
+// cell its beams saw (__get_obs, lidar_localization2d.py:239-261), the trajectory deque (:327, :377-380),
+// the last lidar readings (:242) and last pos / prediction (:326-327).  One workgroup per tracked env
+// rebuilds it after every reset / step from the new position: each beam re-scanned with the reference's
+// contact point, the contact cell and the non-occluded scan points OR-ed into an observation bitmap.
+constexpr int RT_THREADS = 256;
+constexpr int RT_MAX_BEAMS = 1024;
+
+__global__ __launch_bounds__(RT_THREADS) void k_lidar_render_track(StepParams P, apg_lidar_state S, const float *pred,
+                                                                 apg_lidar_outputs O, apg_lidar_render_state R) {
+  __shared__ float s_dist[RT_MAX_BEAMS];
+  const int t = blockIdx.x, e = R.env[t];
+  const int wpr32 = (P.w + 31) / 32;
+  uint32_t *om = R.obs_map + (size_t)t * P.h * wpr32;
+  float *pose = R.pose + 6 * (size_t)t;
+  const bool was_reset = O.reset_mask[e] != 0;
+  const float px = S.pos[2 * e], py = S.pos[2 * e + 1];
+  if (was_reset)
+    for (int k = threadIdx.x; k < P.h * wpr32; k += RT_THREADS) om[k] = 0u;  // np.zeros_like(map) (:301)
+  if (threadIdx.x == 0) {
+    if (was_reset) {  // trajectory.clear(); last_pred = last_pos = None (:312-313)
+      R.traj_len[t] = 0;
+      R.has_last[t] = 0;
+    } else if (pred) {
+      const float lx = pose[4], ly = pose[5];  // last_pos = pos.copy() before the move (:327)
+      const float ax = pred[2 * e], ay = pred[2 * e + 1];
+      pose[0] = lx;
+      pose[1] = ly;
+      // last_pred = (prediction + 1) / 2 * map_size (:323-326); / 2 == * 0.5 exactly
+      pose[2] = __fmul_rn(__fmul_rn(__fadd_rn(ax, 1.0f), 0.5f), (float)P.w);
+      pose[3] = __fmul_rn(__fmul_rn(__fadd_rn(ay, 1.0f), 0.5f), (float)P.h);
+      // prediction_quality = 1 - |prediction - normalized_last_pos| / 0.25 (:377-380); the step's target is
+      // normalized_last_pos, and / 0.25 == * 4 exactly
+      const float d = norm_f32(__fsub_rn(ax, O.target[2 * e]), __fsub_rn(ay, O.target[2 * e + 1]));
+      const float q = __fsub_rn(1.0f, __fmul_rn(d, 4.0f));
+      const int k = R.traj_len[t];
+      if (k < P.step_limit) {
+        float *tr = R.traj + ((size_t)t * P.step_limit + k) * 3;
+        tr[0] = lx;
+        tr[1] = ly;
+        tr[2] = q > 1.0f ? 1.0f : q;  // np.minimum(quality, 1)
+        R.traj_len[t] = k + 1;
+      }
+      R.has_last[t] = 1;
+    }
+  }
+  __syncthreads();
+  const uint64_t *occ = S.occ + (P.is_static ? 0 : (size_t)e * P.h * P.wpr);
+  for (int b = threadIdx.x; b < P.beams; b += RT_THREADS) {
+    const float qx = __fadd_rn(px, S.beam_dirs[2 * b]), qy = __fadd_rn(py, S.beam_dirs[2 * b + 1]);
+    const RowsGlobal rg{occ, P.h, P.wpr, (int)floorf(fminf(px, qx)) - 1};
+    ScanContact c{(double)qx, (double)qy, true};
+    const float dist = lidar_scan_walk<RowsGlobal, true>(rg, px, py, qx, qy, &c).dist;
+    s_dist[b] = dist;
+    R.lidar_dist[(size_t)t * P.beams + b] = dist;
+    if (dist < norm_f32(__fsub_rn(qx, px), __fsub_rn(qy, py))) {
+      // coords = floor(contact); coords[exact & (target < pos)] -= 1 (:529-533), in the contact's dtype
+      int ix, iy;
+      if (c.is_f32) {
+        const float cx = (float)c.x, cy = (float)c.y, fx = floorf(cx), fy = floorf(cy);
+        ix = (int)fx - ((fabsf(__fsub_rn(fx, cx)) < 1e-5f && qx < px) ? 1 : 0);
+        iy = (int)fy - ((fabsf(__fsub_rn(fy, cy)) < 1e-5f && qy < py) ? 1 : 0);
+      } else {
+        const double fx = floor(c.x), fy = floor(c.y);
+        ix = (int)fx - ((fabs(__dsub_rn(fx, c.x)) < 1e-5 && qx < px) ? 1 : 0);
+        iy = (int)fy - ((fabs(__dsub_rn(fy, c.y)) < 1e-5 && qy < py) ? 1 : 0);
+      }
+      if (ix >= 0 && iy >= 0 && ix < P.w && iy < P.h) atomicOr(&om[iy * wpr32 + (ix >> 5)], 1u << (ix & 31));
+    }
+  }
+  __syncthreads();
+  // scan points within the measured distance and in bounds (:250-261); the reference tests (x, y) against
+  // map.shape = (H, W), i.e. x < H and y < W, and indexes [y, x]
+  const int npts = P.beams * R.scan_points;
+  for (int k = threadIdx.x; k < npts; k += RT_THREADS) {
+    if (!(R.scan_norm[k] <= (double)s_dist[k / R.scan_points])) continue;
+    const double fx = floor(__dadd_rn((double)px, R.scan_xy[2 * k]));
+    const double fy = floor(__dadd_rn((double)py, R.scan_xy[2 * k + 1]));
+    if (fx < 0.0 || fy < 0.0 || fx >= (double)P.h || fy >= (double)P.w || fx >= (double)P.w || fy >= (double)P.h)
+      continue;
+    const int ix = (int)fx, iy = (int)fy;
+    atomicOr(&om[iy * wpr32 + (ix >> 5)], 1u << (ix & 31));
+  }
+  if (threadIdx.x == 0) {
+    pose[4] = px;
+    pose[5] = py;
+  }
+}
+
 __global__ void k_rng_draws(const uint64_t *seeds, int m, int kind, int64_t a, int64_t b, int n,
                             double *out, BinomTable bt) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -790,6 +880,31 @@ int apg_lidar_scan_batch(const uint64_t *occ, const int32_t *map_index, int h, i
   hipLaunchKernelGGL(k_scan_batch, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, occ, map_index, h,
                      w, (w + 63) / 64, seg, n, dist, kind);
   return check_launch("k_scan_batch");
+}
+
+int apg_lidar_render_track(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *prediction,
+                           const apg_lidar_outputs *out, const apg_lidar_render_state *rs, apg_stream_t stream) {
+  int rc = validate(cfg);
+  if (rc) return rc;
+  if (!st || !out || !rs || !out->reset_mask || !out->target)
+    return fail(APG_E_INVALID, "render tracking needs the state, reset_mask and target buffers");
+  if (rs->num_tracked <= 0) return APG_OK;
+  if (cfg->beams > RT_MAX_BEAMS) return fail(APG_E_INVALID, "render tracking supports at most 1024 beams");
+  if (rs->scan_points < 0 || !rs->env || !rs->obs_map || !rs->traj || !rs->traj_len || !rs->pose ||
+      !rs->has_last || !rs->lidar_dist || (rs->scan_points > 0 && (!rs->scan_xy || !rs->scan_norm)))
+    return fail(APG_E_INVALID, "null render state buffer");
+  StepParams P;
+  memset(&P, 0, sizeof(P));
+  P.n = cfg->num_envs;
+  P.h = cfg->height;
+  P.w = cfg->width;
+  P.wpr = (cfg->width + 63) / 64;
+  P.beams = cfg->beams;
+  P.step_limit = cfg->step_limit;
+  P.is_static = cfg->is_static;
+  hipLaunchKernelGGL(k_lidar_render_track, dim3(rs->num_tracked), dim3(RT_THREADS), 0, (hipStream_t)stream, P, *st,
+                     prediction, *out, *rs);
+  return check_launch("k_lidar_render_track");
 }
 
 int apg_rng_draws(const uint64_t *seeds, int m, int kind, int64_t a, int64_t b, int n, double *out,

@@ -28,6 +28,13 @@ struct ScanOut {
   int kind;
 };
 
+// The reference's `contact_point` of a hit (render path only, lidar_localization2d.py:506-525): the
+// LineString entry node in float64, the nearest Multi* node in float32, p for a Point.
+struct ScanContact {
+  double x, y;
+  bool is_f32;
+};
+
 // closure quad of cells [i0, i0+di] x [j0, j0+dj] (di, dj in {0, 1}); returns bit0 = any, bit1 = all
 template <class Rows>
 APG_DEV unsigned quad_status(const Rows &rows, int i0, int di, int j0, int dj) {
@@ -61,8 +68,11 @@ APG_DEV ScanOut scan_empty(float fpx, float fpy, float fqx, float fqy) {
   return o;
 }
 
-template <class Rows>
-APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fqx, float fqy) {
+// kContact (render path): also report the reference's contact point in *contact; the hot path
+// instantiates kContact = false, which compiles to the distance-only walk.
+template <class Rows, bool kContact = false>
+APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fqx, float fqy,
+                                ScanContact *contact = nullptr) {
   const double px = fpx, py = fpy, qx = fqx, qy = fqy;
   const int sx = (fqx > fpx) - (fqx < fpx), sy = (fqy > fpy) - (fqy < fpy);
   const float flpx = floorf(fpx), flpy = floorf(fpy), flqx = floorf(fqx), flqy = floorf(fqy);
@@ -104,6 +114,7 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
   int n_lines = 0, n_points = 0;
   int l0_t = 0, l0_a = 0, l0_b = 0, p0_t = 0, p0_a = 0, p0_b = 0;
   float later_line = __builtin_inff(), later_point = __builtin_inff();
+  float ll_x = 0.0f, ll_y = 0.0f, lp_x = 0.0f, lp_y = 0.0f;  // kContact: f32 nodes of those minima
 
   auto node_coord = [&](int t, int a, int b, double &x, double &y) {
     if (t == 0) {
@@ -155,6 +166,10 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
       double x, y;
       node_coord(pv_t, pv_a, pv_b, x, y);
       const float d = dist_f32(x, y);
+      if constexpr (kContact) {  // np.argmin: the first of equal minima
+        if (is_line && d < later_line) ll_x = (float)x, ll_y = (float)y;
+        if (!is_line && d < later_point) lp_x = (float)x, lp_y = (float)y;
+      }
       if (is_line) later_line = fminf(later_line, d);
       else later_point = fminf(later_point, d);
     }
@@ -186,6 +201,10 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
       double x, y;
       node_coord(pv_t, pv_a, pv_b, x, y);
       const float d = dist_f32(x, y);
+      if constexpr (kContact) {
+        if (is_line && d < later_line) ll_x = (float)x, ll_y = (float)y;
+        if (!is_line && d < later_point) lp_x = (float)x, lp_y = (float)y;
+      }
       if (is_line) later_line = fminf(later_line, d);
       else later_point = fminf(later_point, d);
     }
@@ -206,7 +225,11 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
     if (n_points == 0) {
       p0_t = 4;
     } else {
-      later_point = fminf(later_point, dist_f32(qx, qy));
+      const float d = dist_f32(qx, qy);
+      if constexpr (kContact) {
+        if (d < later_point) lp_x = fqx, lp_y = fqy;
+      }
+      later_point = fminf(later_point, d);
     }
     n_points++;
   }
@@ -225,20 +248,32 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
       const double dx = __dsub_rn(x, px), dy = __dsub_rn(y, py);
       const double d = __dsub_rn(__dsqrt_rn(__fma_rn(dy, dy, __dmul_rn(dx, dx))), 1e-3);
       o.dist = (float)(d > 0.0 ? d : 0.0);
+      if constexpr (kContact) *contact = ScanContact{x, y, false};
     } else {
       o.kind = SCAN_MULTILINE;
-      const float d = __fsub_rn(fminf(dist_f32(x, y), later_line), 0.001f);
+      const float d0 = dist_f32(x, y);
+      const float d = __fsub_rn(fminf(d0, later_line), 0.001f);
       o.dist = d > 0.0f ? d : 0.0f;
+      if constexpr (kContact) {
+        const bool later = later_line < d0;
+        *contact = ScanContact{later ? ll_x : (float)x, later ? ll_y : (float)y, true};
+      }
     }
   } else if (n_points == 1) {
     o.kind = SCAN_POINT;
     o.dist = 0.0f;
+    if constexpr (kContact) *contact = ScanContact{fpx, fpy, true};
   } else if (n_points > 1) {
     double x, y;
     node_coord(p0_t, p0_a, p0_b, x, y);
     o.kind = SCAN_MULTIPOINT;
-    const float d = __fsub_rn(fminf(dist_f32(x, y), later_point), 0.001f);
+    const float d0 = dist_f32(x, y);
+    const float d = __fsub_rn(fminf(d0, later_point), 0.001f);
     o.dist = d > 0.0f ? d : 0.0f;
+    if constexpr (kContact) {
+      const bool later = later_point < d0;
+      *contact = ScanContact{later ? lp_x : (float)x, later ? lp_y : (float)y, true};
+    }
   }
   return o;
 }

@@ -21,6 +21,9 @@
  *       FloorMapDatasetMaze.get_data_point   ap_gym/envs/floor_map/floor_map_dataset_maze.py:24-55
  *   apg_lidar_scan_batch
  *       LIDARLocalization2DEnv.__lidar_scan  ap_gym/envs/lidar_localization2d.py:496-536
+ *   apg_lidar_render_track
+ *       the render-only state of LIDARLocalization2DEnv (observation_map, trajectory, last readings)
+ *       ap_gym/envs/lidar_localization2d.py:239-261, 312-313, 326-327, 377-380 used by render() :391-494.
  *   apg_rng_draws
  *       numpy Generator(PCG64(SeedSequence(seed))) draws as used by the above (test entry point).
  *   apg_rng_fill
@@ -178,6 +181,29 @@ int apg_map_generate(int map_kind, const uint64_t *idx, int n, int h, int w, int
 /* n segments seg[n][4] = (px, py, qx, qy) against map map_index[n] of occ[*][h][wpr]. */
 int apg_lidar_scan_batch(const uint64_t *occ, const int32_t *map_index, int h, int w,
                          const float *seg, int n, float *dist, int32_t *kind, apg_stream_t stream);
+
+/* ---------------------------------------------------------------- LIDAR render path (not the hot path)
+ * Render-only state of the tracked sub-envs: what LIDARLocalization2DEnv keeps for render()
+ * (ap_gym/envs/lidar_localization2d.py:391-494) — observation_map (:239-261, :301), the trajectory deque
+ * (:312, :327, :377-380), the last lidar readings (:242) and last pos / prediction (:313, :326-327). */
+typedef struct apg_lidar_render_state {
+  int32_t num_tracked;       /* T */
+  int32_t scan_points;       /* P = len(np.arange(0, lidar_range, 0.05)) */
+  const int32_t *env;        /* [T] tracked sub-env indices (< num_envs) */
+  const double *scan_xy;     /* [beams][P][2] scan_points (float64, computed by the host like :188-191) */
+  const double *scan_norm;   /* [beams][P] np.linalg.norm(scan_points, axis=-1) */
+  uint32_t *obs_map;         /* [T][H][ceil(W/32)] observation_map, bit x%32 of word x/32 */
+  float *traj;               /* [T][step_limit][3] trajectory rows: last_pos x, y, min(prediction_quality, 1) */
+  int32_t *traj_len;         /* [T] */
+  float *pose;               /* [T][6] last_pos (x, y), last_pred (x, y), pos (x, y) */
+  int32_t *has_last;         /* [T] 0 after a reset (last_pos = last_pred = None) */
+  float *lidar_dist;         /* [T][beams] distances of the last observation */
+} apg_lidar_render_state;
+
+/* After apg_lidar_reset (prediction = NULL) or apg_lidar_step (its prediction): update the render state
+ * of the tracked sub-envs from st->pos, out->reset_mask and out->target (both required). */
+int apg_lidar_render_track(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *prediction,
+                           const apg_lidar_outputs *out, const apg_lidar_render_state *rs, apg_stream_t stream);
 
 /* n draws of `kind` (0 next64, 1 next32, 2 random, 3 integers(a,b), 4 integers(0,2**32,endpoint),
  * 5 binomial(a, 0.3)) from default_rng(seed[i]) for each of m seeds; out[m][n] as float64. */

@@ -555,10 +555,44 @@ def make_light_dark():
     run_light_dark("n5_sparse", 5, 110, 2, 2.0, sparse=True)
 
 
+# --------------------------------------------------------------------------- render
+def run_lidar_render(name, dataset, static, beams, n_envs, steps, seed, render_at):
+    """Frames of the reference's LIDARLocalization2DEnv.render() (lidar_localization2d.py:391-494) for every
+    sub-env of the registered composition, after reset (step 0) and after the steps in `render_at`."""
+    lmod = _lidar_module()
+    gym = sys.modules["gymnasium"]
+    ap = sys.modules["ap_gym"]
+
+    def mk():
+        env = lmod.LIDARLocalization2DEnv(dataset=dataset, static_map=static, lidar_beam_count=beams, prefetch=False)
+        return ap.TimeLimit(env, max_episode_steps=100, issue_termination=True)
+
+    venv = gym.vector.SyncVectorEnv([mk for _ in range(n_envs)])
+    venv.reset(seed=seed)
+    arng = np.random.default_rng(4)
+    actions = arng.uniform(-1.5, 1.5, (steps, n_envs, 2)).astype(np.float32)
+    preds = arng.uniform(-1, 1, (steps, n_envs, 2)).astype(np.float32)
+    frames = []
+    if 0 in render_at:
+        frames.append(np.stack([e.render() for e in venv.envs]))
+    for t in range(steps):
+        venv.step({"action": actions[t], "prediction": preds[t]})
+        if t + 1 in render_at:
+            frames.append(np.stack([e.render() for e in venv.envs]))
+    save(f"render_lidar_{name}.npz", actions=actions, predictions=preds, seed=np.array(seed),
+         render_at=np.array(sorted(render_at)), frames=np.stack(frames))
+
+
+def make_render():
+    fm = refload.load("envs.floor_map")
+    run_lidar_render("rooms32_b8", fm.FloorMapDatasetRooms(32, 32), False, 8, 3, 104, 5, {0, 1, 2, 40, 100, 101, 104})
+    run_lidar_render("maze21_b16_static", fm.FloorMapDatasetMaze(), True, 16, 2, 30, 9, {0, 3, 30})
+
+
 SECTIONS = {"rng": make_rng, "maps": make_maps, "loss": make_loss, "scan": make_lidar_scan,
             "lidar": make_lidar_env, "image": make_image_env,
             "sparse": make_sparse_env, "circle_square": make_circle_square,
-            "light_dark": make_light_dark}
+            "light_dark": make_light_dark, "render": make_render}
 
 
 def main(argv):

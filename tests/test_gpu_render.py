@@ -1,0 +1,78 @@
+"""GPU parity of render(): frames of the tracked sub-envs against the reference's own render() frames.
+
+tests/golden/render_lidar_*.npz hold LIDARLocalization2DEnv.render() (lidar_localization2d.py:391-494)
+frames of every sub-env of the registered composition (make_golden.py `render`), after reset and after
+selected steps, including the steps around a TimeLimit autoreset.  The render state (observation_map,
+trajectory, last readings) is kept on the device by k_lidar_render_track; the frames must match pixel
+for pixel.
+"""
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+LIDAR_CASES = {"rooms32_b8": ("rooms", 32, False, 8), "maze21_b16_static": ("maze", 21, True, 16)}
+
+
+def _lidar_env(ap, gpu, name, n, backend="numpy", **kw):
+    kind, size, static, beams = LIDAR_CASES[name]
+    ds = ap.FloorMapDatasetRooms(size, size) if kind == "rooms" else ap.FloorMapDatasetMaze(size, size)
+    return ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=ds, static_map=static, lidar_beam_count=beams,
+                                           device=gpu, array_backend=backend, **kw)
+
+
+def _check_frames(got, want, where):
+    got = np.stack(got)
+    assert got.shape == want.shape and got.dtype == np.uint8, (where, got.shape, want.shape)
+    bad = np.argwhere(np.any(got != want, axis=-1))
+    assert bad.size == 0, (where, len(bad), bad[:8])
+
+
+@pytest.mark.parametrize("backend", ["numpy", "torch"])
+@pytest.mark.parametrize("name", sorted(LIDAR_CASES))
+def test_lidar_render_matches_reference(gpu, name, backend):
+    import torch
+
+    import ap_gym_amd as ap
+
+    d = golden(f"render_lidar_{name}.npz")
+    n = d["actions"].shape[1]
+    env = _lidar_env(ap, gpu, name, n, backend)
+    env.reset(seed=int(d["seed"]))
+    at = [int(x) for x in d["render_at"]]
+    k = 0
+    if 0 in at:
+        _check_frames(env.render(), d["frames"][k], (name, 0))
+        k += 1
+    for t in range(d["actions"].shape[0]):
+        a, p = d["actions"][t], d["predictions"][t]
+        if backend == "torch":
+            a, p = torch.as_tensor(a, device=gpu), torch.as_tensor(p, device=gpu)
+        env.step({"action": a, "prediction": p})
+        if t + 1 in at:
+            _check_frames(env.render(), d["frames"][k], (name, t + 1))
+            k += 1
+    assert k == len(at)
+    env.close()
+
+
+def test_lidar_render_subset_and_untracked(gpu):
+    """render_envs picks the tracked sub-envs (frames equal to those of full tracking); with none tracked
+    (the default above 64 sub-envs) render() raises instead of returning stale frames."""
+    import ap_gym_amd as ap
+
+    d = golden("render_lidar_rooms32_b8.npz")
+    n = d["actions"].shape[1]
+    env = _lidar_env(ap, gpu, "rooms32_b8", n, render_envs=[2, 0])
+    env.reset(seed=int(d["seed"]))
+    for t in range(40):
+        env.step({"action": d["actions"][t], "prediction": d["predictions"][t]})
+    k = [int(x) for x in d["render_at"]].index(40)
+    _check_frames(env.render(), d["frames"][k][[2, 0]], "subset")
+    big = _lidar_env(ap, gpu, "rooms32_b8", 65)
+    big.reset(seed=0)
+    with pytest.raises(RuntimeError, match="render_envs"):
+        big.render()

@@ -165,7 +165,8 @@ def test_ctypes_layouts_match_the_c_header(tmp_path):
                "apg_image_config": N.ImageConfig, "apg_image_state": N.ImageState,
                "apg_image_outputs": N.ImageOutputs, "apg_circle_square_config": N.CircleSquareConfig,
                "apg_hide_and_seek_args": N.HideAndSeekArgs, "apg_light_dark_config": N.LightDarkConfig,
-               "apg_light_dark_state": N.LightDarkState, "apg_light_dark_outputs": N.LightDarkOutputs}
+               "apg_light_dark_state": N.LightDarkState, "apg_light_dark_outputs": N.LightDarkOutputs,
+               "apg_lidar_render_state": N.LidarRenderState}
     lines = ["#include <stdio.h>", "#include \"apgym_capi.h\"", "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'  printf("{cname} %zu\\n", sizeof({cname}));')
