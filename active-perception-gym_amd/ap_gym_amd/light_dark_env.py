@@ -43,7 +43,7 @@ class LightDarkVectorEnv:
 
     def __init__(self, num_envs: int = 1, render_mode: str = "rgb_array", max_episode_steps: int = 50, device=None,
                  env_offset: int = 0, copy: bool = False, strict_errors: bool = False, array_backend: str = "numpy",
-                 log_stats: bool = False, sparse: bool = False):
+                 log_stats: bool = False, sparse: bool = False, render_envs=None):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -106,6 +106,11 @@ class LightDarkVectorEnv:
         self._seeded = False
         self._closed = False
         self._stats_view = None
+        from .render import tracked_envs
+
+        self.render_envs = tracked_envs(render_envs, n)
+        self._render_state = [dict(traj=[], pos=None, last_obs=None, last_pos=None, last_pred=None)
+                              for _ in self.render_envs]
 
     # ------------------------------------------------------------------ properties
     @property
@@ -179,6 +184,7 @@ class LightDarkVectorEnv:
             raise ValueError("seed must be a non-negative int")
         N.check(N.lib().apg_light_dark_reset(ctypes.byref(self._cfg), ctypes.byref(self._state), s, int(use_seed),
                                              ctypes.byref(self._out), self._stream()), "apg_light_dark_reset")
+        self._track_render(None)
         self._seeded = True
         self._autoreset_host[:] = False
         if self.array_backend == "numpy":
@@ -217,6 +223,7 @@ class LightDarkVectorEnv:
         N.check(N.lib().apg_light_dark_step(ctypes.byref(self._cfg), ctypes.byref(self._state), N.ptr(a_t),
                                             N.ptr(p_t), ctypes.byref(self._out), self._stream()),
                 "apg_light_dark_step")
+        self._track_render(p_np if numpy_mode else p_t)
         if numpy_mode:
             return self._numpy_step()
         self._post_launch_error_copy()
@@ -309,8 +316,47 @@ class LightDarkVectorEnv:
                 info.update(self._stats_view)
         return self._torch_obs(), c(T["reward"]), c(T["terminated"]), c(T["truncated"]), info
 
+    # ------------------------------------------------------------------ render
+    def _track_render(self, prediction):
+        """Host copy of the render-only state of the tracked sub-envs (light_dark.py:102-150): position,
+        last observation, last pos / prediction and the (last_pos, prediction_quality) trajectory."""
+        if not len(self.render_envs):
+            return
+        import torch
+
+        T = self._t
+        idx = torch.as_tensor(self.render_envs, dtype=torch.int64, device=self.device)
+        pos = T["pos"][idx].cpu().numpy()
+        noisy = T["noisy_position"][idx].cpu().numpy()
+        if prediction is None:  # reset(): every sub-env reset
+            reset = np.ones(len(self.render_envs), dtype=bool)
+        else:
+            reset = T["reset_mask"][idx].cpu().numpy()
+            tgt = T["target"][idx].cpu().numpy()
+            pred = (prediction[idx].cpu().numpy() if isinstance(prediction, torch.Tensor)
+                    else np.asarray(prediction)[self.render_envs])
+        for j, r in enumerate(self._render_state):
+            if reset[j]:  # trajectory.clear(); last_pred = last_pos = None (:119-120)
+                r["traj"] = []
+                r["last_pos"] = r["last_pred"] = None
+            else:  # :129-130, :146-149
+                last_pos, last_pred = tgt[j].copy(), pred[j].copy()
+                quality = np.maximum(1 - np.linalg.norm(last_pred - last_pos) / 0.5, 0)
+                r["traj"].append((last_pos, quality))
+                r["last_pos"], r["last_pred"] = last_pos, last_pred
+            r["pos"], r["last_obs"] = pos[j].copy(), noisy[j].copy()
+
     def render(self):
-        raise NotImplementedError("rendering is not part of the MI355X hot path (SURVEY §8(f) item 2)")
+        """SyncVectorEnv.render(): one rgb_array frame per tracked sub-env, drawn like LightDarkEnv.render
+        (light_dark.py:152-243)."""
+        from .render import light_dark_frame, no_tracked_error
+
+        if not len(self.render_envs):
+            raise no_tracked_error()
+        if not self._seeded:
+            raise RuntimeError("render() needs reset() first")
+        return tuple(light_dark_frame(r["pos"], r["last_obs"], r["last_pos"], r["last_pred"], r["traj"])
+                     for r in self._render_state)
 
     def close(self, **kwargs):
         if not self._closed:

@@ -86,3 +86,57 @@ def lidar_frame(occ, seen, traj, lidar_dist, lidar_directions, pos, last_pos, la
         _disc(draw, last_pos, radius, scale, COLOR_AGENT + (100,))
     _disc(draw, pos, radius, scale, COLOR_AGENT)
     return np.array(img)
+
+
+# ---------------------------------------------------------------------------------------- LightDark
+LIGHT_POS = np.array([0, -0.7], dtype=np.float32)
+LIGHT_HEIGHT = 0.2
+_light_dark_base = None
+
+
+def light_dark_brightness(pos):
+    """light_dark.py:96-100: h^2 / (|pos - light|^2 + h^2)."""
+    return LIGHT_HEIGHT**2 / (np.sum((pos - LIGHT_POS) ** 2, axis=-1) + LIGHT_HEIGHT**2)
+
+
+def light_dark_base() -> np.ndarray:
+    """light_dark.py:72-81: the 500 x 500 brightness background (0.1 ambient), computed once."""
+    global _light_dark_base
+    if _light_dark_base is None:
+        res = 500
+        gx, gy = np.meshgrid(np.linspace(-1, 1, res), np.linspace(-1, 1, res), indexing="ij")
+        b = light_dark_brightness(np.stack([gy, gx], axis=-1))
+        _light_dark_base = np.broadcast_to(((b * 0.9 + 0.1) * 255).astype(np.uint8)[..., None], (res, res, 3))
+    return _light_dark_base
+
+
+def light_dark_frame(pos, last_obs, last_pos, last_pred, traj) -> np.ndarray:
+    """One LightDarkEnv frame: noise disc, trajectory coloured by prediction quality, observation and
+    prediction markers.  pos / last_obs / last_pos / last_pred float32 [2] (the last two None after a
+    reset); traj: list of (last_pos float32 [2], quality float32)."""
+    from PIL import Image, ImageDraw
+
+    img = Image.fromarray(light_dark_base())
+    draw = ImageDraw.Draw(img, mode="RGBA")
+    dot = 0.01 * img.size[0]
+    size = np.array(img.size[::-1])
+
+    def px(p):
+        return (p + 1) / 2 * size
+
+    c = px(pos)
+    std = (1 - light_dark_brightness(pos)) * 0.3 / 2 * size
+    draw.ellipse([tuple(c - std), tuple(c + std)], fill=COLOR_OBS_PRIMARY + (30,), outline=None)
+    for (pa, _), (pb, qb) in zip(traj[:-1], traj[1:]):
+        a, b = px(pa), px(pb)
+        draw.line((a[0], a[1], b[0], b[1]), width=2, fill=quality_color(qb))
+    o = px(last_obs)
+    draw.line((tuple(c), tuple(o)), fill=COLOR_OBS_PRIMARY + (80,))
+    draw.ellipse([tuple(o - dot), tuple(o + dot)], fill=COLOR_OBS_PRIMARY + (100,), outline=None)
+    if last_pred is not None:
+        lp, ls = px(last_pred), px(last_pos)
+        draw.line((tuple(ls), tuple(lp)), fill=COLOR_PRED + (80,))
+        draw.ellipse([tuple(lp - dot), tuple(lp + dot)], fill=COLOR_PRED + (100,), outline=None)
+        draw.ellipse([tuple(ls - dot), tuple(ls + dot)], fill=COLOR_AGENT + (100,), outline=None)
+    draw.ellipse([tuple(c - dot), tuple(c + dot)], fill=COLOR_AGENT, outline=None)
+    return np.array(img)

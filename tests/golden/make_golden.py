@@ -583,7 +583,31 @@ def run_lidar_render(name, dataset, static, beams, n_envs, steps, seed, render_a
          render_at=np.array(sorted(render_at)), frames=np.stack(frames))
 
 
+def run_light_dark_render(name, n_envs, steps, seed, action_scale, render_at):
+    """Frames of the reference's LightDarkEnv.render() (light_dark.py:152-243) for every sub-env of
+    TimeLimit(50, issue_termination=True) over LightDarkEnv, after reset (step 0) and the steps in render_at."""
+    ap = refload.load_core()
+    ld = refload.load("envs.light_dark")
+    gym = sys.modules["gymnasium"]
+    venv = gym.vector.SyncVectorEnv([lambda: ap.TimeLimit(ld.LightDarkEnv(), max_episode_steps=50,
+                                                          issue_termination=True) for _ in range(n_envs)])
+    venv.reset(seed=seed)
+    arng = np.random.default_rng(6)
+    actions = arng.uniform(-action_scale, action_scale, (steps, n_envs, 2)).astype(np.float32)
+    preds = arng.uniform(-1, 1, (steps, n_envs, 2)).astype(np.float32)
+    frames = []
+    if 0 in render_at:
+        frames.append(np.stack([e.render() for e in venv.envs]))
+    for t in range(steps):
+        venv.step({"action": actions[t], "prediction": preds[t]})
+        if t + 1 in render_at:
+            frames.append(np.stack([e.render() for e in venv.envs]))
+    save(f"render_light_dark_{name}.npz", actions=actions, predictions=preds, seed=np.array(seed),
+         render_at=np.array(sorted(render_at)), frames=np.stack(frames))
+
+
 def make_render():
+    run_light_dark_render("n3", 3, 54, 2, 1.5, {0, 1, 2, 20, 50, 51, 54})
     fm = refload.load("envs.floor_map")
     run_lidar_render("rooms32_b8", fm.FloorMapDatasetRooms(32, 32), False, 8, 3, 104, 5, {0, 1, 2, 40, 100, 101, 104})
     run_lidar_render("maze21_b16_static", fm.FloorMapDatasetMaze(), True, 16, 2, 30, 9, {0, 3, 30})

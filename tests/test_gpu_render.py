@@ -76,3 +76,31 @@ def test_lidar_render_subset_and_untracked(gpu):
     big.reset(seed=0)
     with pytest.raises(RuntimeError, match="render_envs"):
         big.render()
+
+
+@pytest.mark.parametrize("backend", ["numpy", "torch"])
+def test_light_dark_render_matches_reference(gpu, backend):
+    """LightDarkEnv.render() frames (light_dark.py:152-243) of every sub-env of TimeLimit(50) over
+    LightDarkEnv, across an autoreset, from the host copy of the tracked render state."""
+    import torch
+
+    import ap_gym_amd as ap
+
+    d = golden("render_light_dark_n3.npz")
+    n = d["actions"].shape[1]
+    env = ap.LightDarkVectorEnv(num_envs=n, device=gpu, array_backend=backend)
+    env.reset(seed=int(d["seed"]))
+    at = [int(x) for x in d["render_at"]]
+    k = 0
+    if 0 in at:
+        _check_frames(env.render(), d["frames"][k], ("light_dark", 0))
+        k += 1
+    for t in range(d["actions"].shape[0]):
+        a, p = d["actions"][t], d["predictions"][t]
+        if backend == "torch":
+            a, p = torch.as_tensor(a, device=gpu), torch.as_tensor(p, device=gpu)
+        env.step({"action": a, "prediction": p})
+        if t + 1 in at:
+            _check_frames(env.render(), d["frames"][k], ("light_dark", t + 1))
+            k += 1
+    assert k == len(at)
