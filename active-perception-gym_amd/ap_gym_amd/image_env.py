@@ -86,7 +86,7 @@ class _ImageVectorEnv:
     def __init__(self, num_envs: int, image_perception_config: ImagePerceptionConfig,
                  render_mode: str = "rgb_array", device=None, copy: bool = False, strict_errors: bool = False,
                  array_backend: str = "numpy", num_envs_total: int | None = None, env_offset: int = 0,
-                 log_stats: bool = False, sparse: bool = False):
+                 log_stats: bool = False, sparse: bool = False, render_envs=None):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -228,6 +228,12 @@ class _ImageVectorEnv:
         self._prev_done = False
         self._done_consts = None
         self._stats_view = None
+        from .render import tracked_envs
+
+        self.render_envs = tracked_envs(render_envs, n)
+        self._pool_host = pool if pool_t is None else None  # render: images of the tracked envs
+        self._visits = [[] for _ in self.render_envs]  # (pre-step position f64 [2], quality) since the reset
+        self._last_prediction = None
 
     # ------------------------------------------------------------------ properties
     @property
@@ -313,6 +319,8 @@ class _ImageVectorEnv:
                                   self._stream()), "apg_image_reset")
         self._t_step = 0
         self._prev_done = False
+        self._visits = [[] for _ in self.render_envs]  # module.reset clears the overlay (:184-186)
+        self._last_prediction = None
         if self.array_backend == "numpy":
             self.check_errors(block=True)
             return self._numpy_obs(), {"index": self._t["index"].cpu().numpy()}
@@ -348,6 +356,7 @@ class _ImageVectorEnv:
             a_t = torch.as_tensor(a, dtype=torch.float32, device=self.device).reshape(n, 2).contiguous()
             p_t = torch.as_tensor(p, dtype=torch.float32, device=self.device).reshape(n, pdim).contiguous()
         resetting = self._prev_done
+        self._track_render(p_np if numpy_mode else p_t, resetting)
         N.check(N.lib().apg_image_step(ctypes.byref(self._cfg), ctypes.byref(self._state), N.ptr(a_t), N.ptr(p_t),
                                        int(self._t_step), int(resetting), ctypes.byref(self._out), self._stream()),
                 "apg_image_step")
@@ -511,8 +520,120 @@ class _ImageVectorEnv:
             info["stats"] = self._torch_stats()
         return self._torch_obs(), self._c(T["reward"]), term, trunc, info
 
+    # ------------------------------------------------------------------ render
+    def _track_render(self, prediction, resetting: bool):
+        """Visitation overlay history of the tracked envs (image_perception_module.py:196, 219-234): the
+        module records the sensor rectangle at the position *before* the step with the prediction quality,
+        then (on the batch autoreset) clears the overlay.  Kept as (position, quality) rows and replayed
+        by render()."""
+        if not len(self.render_envs):
+            return
+        import torch
+
+        if isinstance(prediction, torch.Tensor):
+            self._last_prediction = prediction[torch.as_tensor(self.render_envs, device=self.device)].cpu().numpy()
+        else:
+            self._last_prediction = np.asarray(prediction)[self.render_envs].copy()
+        if resetting:  # the overlay written by this step is cleared by module.reset() right after
+            self._visits = [[] for _ in self.render_envs]
+            return
+        idx = torch.as_tensor(self.render_envs, device=self.device)
+        pos = self._t["pos"][idx].cpu().numpy()
+        p = self._last_prediction
+        if self.kind == N.APG_IMAGE_CLASSIFY:  # softmax(prediction)[label] (image_classification.py:114-116)
+            from scipy.special import softmax
+
+            lab = self._t["label"][idx].cpu().numpy()
+            quality = softmax(p, axis=-1)[np.arange(len(p)), lab]
+        else:  # 1 - |prediction - target| / sqrt(4) (image_localization.py:157-159)
+            quality = 1 - np.linalg.norm(p - self._t["target"][idx].cpu().numpy(), axis=-1) / np.sqrt(4)
+        for j, v in enumerate(self._visits):
+            v.append((pos[j].copy(), quality[j]))
+
+    def _render_geometry(self):
+        """render_size / render_scaling / sensor_pos_lim_pixels as the module derives them
+        (image_perception_module.py:167-171, 403-445, 464-465)."""
+        h, w = self.image_size
+        s0, s1 = (int(v) for v in self.config.sensor_size)
+        width = max(128, s1)
+        scaling = width / w
+        size = (width, int(round(scaling * h)))
+        eff = np.array(self.config.sensor_size) * self.config.sensor_scale
+        lim = (np.flip(np.array([h, w])) - 1) / 2 - (eff - 1) / 2
+        border = max(1, int(round(1 / 128 * size[0])))
+        return size, scaling, eff, lim, border
+
     def render(self):
-        raise NotImplementedError("rendering is not part of the MI355X hot path (SURVEY §8(f) item 2)")
+        """rgb_array frames [len(render_envs), H_r, W_r, 3] like ImagePerceptionModule.render
+        (image_perception_module.py:333-401) plus, for localization, ImageLocalizationVectorEnv.render
+        (image_localization.py:183-223)."""
+        from PIL import Image, ImageDraw
+
+        from .render import COLOR_AGENT, COLOR_PRED, no_tracked_error, quality_color
+
+        if not len(self.render_envs):
+            raise no_tracked_error()
+        if not self._seeded:
+            raise RuntimeError("render() needs reset() first")
+        import torch
+
+        size, scaling, eff, lim, border = self._render_geometry()
+        cfg = self.config
+
+        def to_render(pn):
+            return pn * lim * scaling + np.array(size) / 2
+
+        idx = torch.as_tensor(self.render_envs, device=self.device)
+        index = self._t["index"][idx].cpu().numpy()
+        pool = self._pool_host if self._pool_host is not None else self._t["pool"][
+            torch.as_tensor(index, device=self.device)].cpu().numpy()
+        imgs = pool[index] if self._pool_host is not None else pool
+        if imgs.dtype == np.uint8:
+            imgs = imgs.astype(np.float32) / 255
+        if imgs.shape[-1] == 1 and int(self.config.dataset.num_channels) == 3:
+            imgs = np.repeat(imgs, 3, axis=-1)
+        if imgs.shape[-1] == 1:
+            imgs = imgs[..., 0]
+        pos_now = self._t["pos"][idx].cpu().numpy()
+        targets = self._t["target"][idx].cpu().numpy() if self.kind == N.APG_IMAGE_LOCALIZE else None
+        rect = eff * scaling
+        frames = []
+        for j in range(len(self.render_envs)):
+            counts = np.zeros((size[1], size[0]), dtype=np.int32)
+            qmap = np.zeros((size[1], size[0]), dtype=np.float32)
+            rs = np.round(np.flip(rect)).astype(np.int32)
+            for pn, q in self._visits[j]:  # __update_visitation_overlay (:219-234)
+                pi = np.round(to_render(pn)).astype(np.int32)
+                xs = np.clip(pi[0] + np.arange(rs[0]) - rs[0] // 2, 0, size[0] - 1)
+                ys = np.clip(pi[1] + np.arange(rs[1]) - rs[1] // 2, 0, size[1] - 1)
+                counts[ys[:, None], xs[None, :]] += 1
+                qmap[ys[:, None], xs[None, :]] = np.clip(q, 0, 1)
+            visited = counts > 0
+            ol = (visited[..., None] * np.concatenate(
+                [np.stack(quality_color(qmap[None]))[..., :3].reshape(size[1], size[0], 3),
+                 np.full_like(qmap[..., None], int(255 * cfg.render_visited_opacity))], axis=-1)
+                  + ~visited[..., None] * (0, 0, 0, int(255 * cfg.render_unvisited_opacity))).round().astype(np.uint8)
+            img = Image.fromarray((imgs[j] * 255).astype(np.uint8)).resize(
+                size, resample=Image.Resampling.NEAREST).convert("RGB")
+            if cfg.display_visitation:
+                alpha = ol[..., -1:] / 255
+                img = Image.fromarray((np.array(img) * (1 - alpha) + alpha * ol[..., :-1]).astype(np.uint8))
+            draw = ImageDraw.Draw(img, "RGBA")
+            c = to_render(pos_now[j])
+            box = np.concatenate([c - rect / 2, c + rect / 2])
+            draw.rectangle(tuple(box + border), outline=(0, 0, 0, 80), width=border)
+            draw.rectangle(tuple(box), outline=COLOR_AGENT, width=border)
+            if targets is not None:
+                t_c = to_render(targets[j])
+                draw.rectangle((tuple(t_c - rect / 2), tuple(t_c + rect / 2)), outline=COLOR_PRED + (100,),
+                               width=border)
+                if self._last_prediction is not None:
+                    lp = to_render(self._last_prediction[j])
+                    lp_box = np.concatenate([lp - rect / 2, lp + rect / 2])
+                    draw.rectangle(tuple(lp_box), outline=COLOR_PRED, width=border)
+                    draw.rectangle(tuple(lp_box + border), outline=(0, 0, 0, 80), width=border)
+            frames.append(np.asarray(img))
+        return np.asarray(frames)
 
     def close(self, **kwargs):
         if not self._closed:

@@ -606,7 +606,58 @@ def run_light_dark_render(name, n_envs, steps, seed, action_scale, render_at):
          render_at=np.array(sorted(render_at)), frames=np.stack(frames))
 
 
+def run_image_render(name, kind, pool_shape, channels, num_classes, sensor, scale, step_limit, n_envs, steps, seed,
+                     pool_len, pool_seed, opacity, render_at):
+    """Frames of the reference's ImageClassificationVectorEnv / ImageLocalizationVectorEnv render()
+    (image_perception_module.py:333-401, image_localization.py:183-223) on a synthetic uint8 pool, after
+    reset (step 0) and the steps in render_at (crossing the batch autoreset)."""
+    ipm, icd, ic, il = _image_modules()
+    prng = np.random.default_rng(pool_seed)
+    pool = prng.integers(0, 256, (pool_len, *pool_shape), dtype=np.uint8)
+    labels = prng.integers(0, num_classes, pool_len).astype(np.int64)
+
+    class PoolDataset(icd.ImageClassificationDataset):
+        def _get_length(self):
+            return pool_len
+
+        def _get_num_classes(self):
+            return num_classes
+
+        def _get_num_channels(self):
+            return channels
+
+        def _get_data_point_batch(self, idx):
+            return pool[np.asarray(idx)], labels[np.asarray(idx)]
+
+    kw = {} if opacity is None else dict(render_unvisited_opacity=opacity[0], render_visited_opacity=opacity[1])
+    cfg = ipm.ImagePerceptionConfig(dataset=PoolDataset(), sensor_size=sensor, sensor_scale=scale,
+                                    step_limit=step_limit, prefetch=False, **kw)
+    env = (ic.ImageClassificationVectorEnv if kind == "cls" else il.ImageLocalizationVectorEnv)(n_envs, cfg)
+    env.reset(seed=seed)
+    arng = np.random.default_rng(12)
+    actions = arng.uniform(-1.5, 1.5, (steps, n_envs, 2)).astype(np.float32)
+    if kind == "cls":
+        preds = (arng.standard_normal((steps, n_envs, num_classes)) * 2).astype(np.float32)
+    else:
+        preds = arng.uniform(-1, 1, (steps, n_envs, 2)).astype(np.float32)
+    frames = [env.render()] if 0 in render_at else []
+    for t in range(steps):
+        env.step({"action": actions[t], "prediction": preds[t]})
+        if t + 1 in render_at:
+            frames.append(env.render())
+    save(f"render_image_{name}.npz", pool=pool, labels=labels,
+         config=np.array([channels, num_classes, sensor[0], sensor[1], step_limit, n_envs], np.int64),
+         sensor_scale=np.array(scale, np.float64), kind=np.array(kind),
+         opacity=np.array(opacity if opacity is not None else (0.0, 0.3), np.float64), actions=actions,
+         predictions=preds, seed=np.array(seed), render_at=np.array(sorted(render_at)), frames=np.stack(frames))
+
+
 def make_render():
+    run_image_render("cls_mnist", "cls", (28, 28), 1, 10, (5, 5), 1.0, 8, 3, 12, 0, 20, 200, (0.5, 0.25),
+                     {0, 1, 5, 8, 9, 12})
+    run_image_render("cls_gray3_rect", "cls", (20, 24), 3, 4, (5, 5), 1.5, 6, 2, 9, 5, 10, 201, None, {0, 3, 6, 7})
+    run_image_render("loc_tin12", "loc", (64, 64, 3), 3, 200, (12, 12), 1.0, 5, 2, 8, 4, 6, 202, (0.5, 0.25),
+                     {0, 2, 5, 6, 8})
     run_light_dark_render("n3", 3, 54, 2, 1.5, {0, 1, 2, 20, 50, 51, 54})
     fm = refload.load("envs.floor_map")
     run_lidar_render("rooms32_b8", fm.FloorMapDatasetRooms(32, 32), False, 8, 3, 104, 5, {0, 1, 2, 40, 100, 101, 104})
