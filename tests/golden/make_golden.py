@@ -664,10 +664,60 @@ def make_render():
     run_lidar_render("maze21_b16_static", fm.FloorMapDatasetMaze(), True, 16, 2, 30, 9, {0, 3, 30})
 
 
+# --------------------------------------------------------------------------- HF data ingestion
+def write_hf_parquet(root, images, labels, label_names, splits):
+    """A local Hugging Face dataset directory (data/<split>-00000-of-00001.parquet, PNG-encoded images,
+    ClassLabel labels) that `datasets.load_dataset(root)` loads offline.  Shared with tests/test_host.py
+    (which rebuilds the same directory from the fixture's arrays)."""
+    from datasets import ClassLabel, Dataset, Features, Image
+
+    feats = Features({"image": Image(), "label": ClassLabel(names=list(label_names))})
+    os.makedirs(os.path.join(root, "data"), exist_ok=True)
+    start = 0
+    for split, n in splits:
+        ims = [images[i] for i in range(start, start + n)]
+        Dataset.from_dict({"image": ims, "label": [int(v) for v in labels[start:start + n]]}, features=feats).to_parquet(
+            os.path.join(root, "data", f"{split}-00000-of-00001.parquet"))
+        start += n
+
+
+def make_hf():
+    """The reference's HuggingfaceImageClassificationDataset (huggingface_image_classification_dataset.py)
+    on small local datasets: lengths, class counts, filter_labels remapping and processed batches."""
+    import tempfile
+
+    refload.load_core()
+    hf = refload.load("envs.image.huggingface_image_classification_dataset")
+    out = {}
+    rng = np.random.default_rng(21)
+    for name, shape, channels in (("rgb", (9, 7, 3), 3), ("grey", (8, 8), 1), ("grey_to_rgb", (8, 8), 3)):
+        images = rng.integers(0, 256, (18, *shape), dtype=np.uint8)
+        labels = rng.integers(0, 5, 18)
+        names = ["zero", "one", "two", "three", "four"]
+        out[f"{name}_images"], out[f"{name}_labels"] = images, labels
+        out[f"{name}_channels"] = np.array(channels)
+        with tempfile.TemporaryDirectory() as root:
+            write_hf_parquet(root, images, labels, names, (("train", 12), ("test", 6)))
+            for split in ("train", "test"):
+                for filt in (None, ["three", "one"]):
+                    ds = hf.HuggingfaceImageClassificationDataset(root, channels=channels, split=split,
+                                                                  filter_labels=filt)
+                    ds.load()
+                    key = f"{name}_{split}_{'filt' if filt else 'all'}"
+                    idx = np.arange(len(ds))[::-1]
+                    imgs, labs = ds.get_data_point_batch(idx)
+                    out[key + "_len"] = np.array(len(ds))
+                    out[key + "_num_classes"] = np.array(ds.num_classes)
+                    out[key + "_idx"] = idx
+                    out[key + "_batch_images"] = np.asarray(imgs)
+                    out[key + "_batch_labels"] = np.asarray(labs)
+    save("hf_dataset.npz", **out)
+
+
 SECTIONS = {"rng": make_rng, "maps": make_maps, "loss": make_loss, "scan": make_lidar_scan,
             "lidar": make_lidar_env, "image": make_image_env,
             "sparse": make_sparse_env, "circle_square": make_circle_square,
-            "light_dark": make_light_dark, "render": make_render}
+            "light_dark": make_light_dark, "render": make_render, "hf": make_hf}
 
 
 def main(argv):
