@@ -652,7 +652,34 @@ def run_image_render(name, kind, pool_shape, channels, num_classes, sensor, scal
          predictions=preds, seed=np.array(seed), render_at=np.array(sorted(render_at)), frames=np.stack(frames))
 
 
+def run_circle_square_render(name, double, shape, step_limit, n_envs, steps, seed, render_at):
+    """render() frames of CircleSquareHideAndSeek over ImageClassificationVectorEnv on the procedural
+    CircleSquare / DoubleCircleSquare datasets (float32 images), registered render opacities."""
+    ipm, ic, csd = _circle_square_modules()
+    hs = refload.load("envs.circle_square_catch_or_flee")
+    ds = csd.DoubleCircleSquareDataset(image_shape=shape) if double else csd.CircleSquareDataset(image_shape=shape)
+    cfg = ipm.ImagePerceptionConfig(dataset=ds, step_limit=step_limit, prefetch=False, render_unvisited_opacity=0.5,
+                                    render_visited_opacity=0.25)
+    env = ic.ImageClassificationVectorEnv(n_envs, cfg)
+    if not double:
+        env = hs.CircleSquareHideAndSeekVectorWrapper(env)
+    env.reset(seed=seed)
+    arng = np.random.default_rng(13)
+    actions = arng.uniform(-1.5, 1.5, (steps, n_envs, 2)).astype(np.float32)
+    preds = (arng.standard_normal((steps, n_envs, ds.num_classes)) * 2).astype(np.float32)
+    frames = [env.render()] if 0 in render_at else []
+    for t in range(steps):
+        env.step({"action": actions[t], "prediction": preds[t]})
+        if t + 1 in render_at:
+            frames.append(env.render())
+    save(f"render_cs_{name}.npz", config=np.array([int(double), shape[0], shape[1], step_limit, n_envs], np.int64),
+         actions=actions, predictions=preds, seed=np.array(seed), render_at=np.array(sorted(render_at)),
+         frames=np.stack(frames))
+
+
 def make_render():
+    run_circle_square_render("hs28", False, (28, 28), 6, 3, 9, 3, {0, 2, 6, 7, 9})
+    run_circle_square_render("dcs15", True, (15, 15), 4, 2, 6, 1, {0, 3, 5})
     run_image_render("cls_mnist", "cls", (28, 28), 1, 10, (5, 5), 1.0, 8, 3, 12, 0, 20, 200, (0.5, 0.25),
                      {0, 1, 5, 8, 9, 12})
     run_image_render("cls_gray3_rect", "cls", (20, 24), 3, 4, (5, 5), 1.5, 6, 2, 9, 5, 10, 201, None, {0, 3, 6, 7})

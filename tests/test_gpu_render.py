@@ -140,3 +140,31 @@ def test_image_render_matches_reference(gpu, name, backend):
             _check_frames(env.render(), g["frames"][j], (name, t + 1))
             j += 1
     assert j == len(at)
+
+
+@pytest.mark.parametrize("name", ["hs28", "dcs15"])
+def test_circle_square_render_matches_reference(gpu, name):
+    """render() of the CircleSquare family (float32 pools rendered on the device; the hide-and-seek
+    wrapper passes render() through to the inner ImageClassificationVectorEnv)."""
+    import ap_gym_amd as ap
+
+    g = golden(f"render_cs_{name}.npz")
+    double, h, w, lim, n = (int(v) for v in g["config"])
+    ds = ap.DoubleCircleSquareDataset(image_shape=(h, w)) if double else ap.CircleSquareDataset(image_shape=(h, w))
+    cfg = ap.ImagePerceptionConfig(dataset=ds, step_limit=lim, render_unvisited_opacity=0.5,
+                                   render_visited_opacity=0.25)
+    env = ap.ImageClassificationVectorEnv(n, cfg, device=gpu)
+    if not double:
+        env = ap.CircleSquareHideAndSeekVectorWrapper(env)
+    env.reset(seed=int(g["seed"]))
+    at = [int(x) for x in g["render_at"]]
+    j = 0
+    if 0 in at:
+        _check_frames(env.render(), g["frames"][j], (name, 0))
+        j += 1
+    for t in range(g["actions"].shape[0]):
+        env.step({"action": g["actions"][t], "prediction": g["predictions"][t]})
+        if t + 1 in at:
+            _check_frames(env.render(), g["frames"][j], (name, t + 1))
+            j += 1
+    assert j == len(at)
