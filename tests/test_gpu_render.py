@@ -168,3 +168,26 @@ def test_circle_square_render_matches_reference(gpu, name):
             _check_frames(env.render(), g["frames"][j], (name, t + 1))
             j += 1
     assert j == len(at)
+
+
+def test_lidar_render_large_batch_tracks_chosen_envs(gpu):
+    """At N = 8192 (default: nothing tracked) render_envs=[5, 8000] gives the frames of those sub-envs:
+    sub-env i depends only on seed + i, so a 1-env batch seeded with seed + i renders the same frames."""
+    import ap_gym_amd as ap
+
+    seed, steps = 3, 30
+    big = _lidar_env(ap, gpu, "rooms32_b8", 8192, render_envs=[5, 8000])
+    big.reset(seed=seed)
+    small = [_lidar_env(ap, gpu, "rooms32_b8", 1) for _ in range(2)]
+    for e, i in zip(small, (5, 8000)):
+        e.reset(seed=seed + i)
+    rng = np.random.default_rng(9)
+    for _ in range(steps):
+        a = rng.uniform(-1.5, 1.5, (8192, 2)).astype(np.float32)
+        p = rng.uniform(-1, 1, (8192, 2)).astype(np.float32)
+        big.step({"action": a, "prediction": p})
+        for e, i in zip(small, (5, 8000)):
+            e.step({"action": a[i:i + 1], "prediction": p[i:i + 1]})
+    got = big.render()
+    for j, e in enumerate(small):
+        _check_frames(got[j:j + 1], np.stack(e.render()), ("large batch", j))
