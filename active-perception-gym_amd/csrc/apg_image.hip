@@ -673,6 +673,68 @@ __global__ __launch_bounds__(256) void k_image_env_cls(EnvArgs a, int envs_per_b
   if (err) atomicOr(out.err, err);
 }
 
+// Classification for few classes (K <= CLS1_MAX_K, e.g. MNIST / CIFAR-10): thread = env.  With 8 lanes
+// per env most lanes idle for K = 10 and the tail (loss, stats, move) runs on one lane of eight; here a
+// 128-thread block stages its 128 rows of logits in LDS with coalesced loads and every thread evaluates
+// its own row: max, exp, numpy's pairwise sum (n <= 128: 8 strided accumulators, ((0+1)+(2+3))+((4+5)+(6+7)),
+// then the tail — the order pw_leaf8 distributes over 8 lanes), log, with the same device libm calls.
+constexpr int CLS1_ENVS = 128;
+constexpr int CLS1_MAX_K = 16;
+__global__ __launch_bounds__(CLS1_ENVS) void k_image_env_cls1(EnvArgs a, const float *__restrict__ act,
+                                                             const float *__restrict__ pred, const int32_t *label,
+                                                             double *pos, apg_image_outputs out, float *hist) {
+  extern __shared__ float s_logit[];  // [CLS1_ENVS][k + 1]
+  const int k = a.k, stride = k + 1;
+  const int e0 = blockIdx.x * CLS1_ENVS;
+  const int ne = a.n - e0 < CLS1_ENVS ? a.n - e0 : CLS1_ENVS;
+  for (int q = threadIdx.x; q < ne * k; q += CLS1_ENVS) {
+    const int r = q / k;
+    s_logit[r * stride + (q - r * k)] = pred[(size_t)e0 * k + q];
+  }
+  __syncthreads();
+  if ((int)threadIdx.x >= ne) return;
+  float *row = s_logit + threadIdx.x * stride;
+  float m = -INFINITY;
+  bool nan = false, pos_inf = false, all_neg_inf = true;
+  for (int i = 0; i < k; i++) {
+    const float v = row[i];
+    nan |= v != v;
+    pos_inf |= v == INFINITY;
+    all_neg_inf &= v == -INFINITY;
+    m = v > m ? v : m;
+  }
+  if (nan || isinf(m)) m = 0.0f;  // x_max[~isfinite(x_max)] = 0
+  const int e = e0 + threadIdx.x;
+  const int32_t l = label[e];
+  const int lc = l < 0 ? 0 : (l >= k ? k - 1 : l);
+  const float xt = row[lc];
+  for (int i = 0; i < k; i++) row[i] = expf(__fsub_rn(row[i], m));
+  float sum = 0.0f;
+  if (k < 8) {
+    for (int i = 0; i < k; i++) sum = __fadd_rn(sum, row[i]);
+  } else {
+    float r[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) r[j] = row[j];
+    int i = 8;
+    for (; i < k - (k % 8); i += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) r[j] = __fadd_rn(r[j], row[i + j]);
+    }
+    sum = __fadd_rn(__fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3])),
+                    __fadd_rn(__fadd_rn(r[4], r[5]), __fadd_rn(r[6], r[7])));
+    for (; i < k; i++) sum = __fadd_rn(sum, row[i]);
+  }
+  uint32_t err = (nan || pos_inf || all_neg_inf) ? APG_ERR_NAN_PREDICTION : 0u;
+  const float ce = -__fsub_rn(__fsub_rn(xt, m), logf(sum));
+  const double loss_d = __dadd_rn(__dmul_rn((double)ce, a.ce_scale), a.ce_offset);
+  out.loss_f64[e] = loss_d;
+  out.label_target[e] = l;
+  log_classification(a, e, out, hist, f32_div(row[lc], sum));
+  err |= env_tail(a, e, act, pos, out, loss_d, 0.0f);
+  if (err) atomicOr(out.err, err);
+}
+
 // ------------------------------------------------------------------ k_unique
 constexpr int UNIQ_THREADS = 256;
 constexpr int UNIQ_LDS_FLOATS = 24 * 1024;  // 96 KiB of glimpse tiles (two tiles)
@@ -1374,7 +1436,11 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
   a.time_value = (float)(((double)t_new / (double)c->step_limit) * 2.0 - 1.0);
   a.loss_weight = !c->sparse ? 1.0f : (!prev_done && t_new >= c->step_limit ? 1.0f : 0.0f);
   a.copy_target = c->kind == APG_IMAGE_LOCALIZE && !prev_done ? st->target : nullptr;
-  if (c->kind == APG_IMAGE_CLASSIFY) {
+  if (c->kind == APG_IMAGE_CLASSIFY && c->num_classes <= CLS1_MAX_K && !getenv("APG_CLS_LANES8")) {
+    const size_t lds = (size_t)CLS1_ENVS * (c->num_classes + 1) * sizeof(float);
+    hipLaunchKernelGGL(k_image_env_cls1, dim3(grid_for(n, CLS1_ENVS)), dim3(CLS1_ENVS), lds, s, a, action, prediction,
+                       st->label, st->pos, *out, st->stats_hist);
+  } else if (c->kind == APG_IMAGE_CLASSIFY) {
     int epb = 256 / CLS_LANES;
     while (epb > 1 && (size_t)epb * (c->num_classes + 1) * sizeof(float) > 64 * 1024) epb /= 2;
     const size_t lds = (size_t)epb * (c->num_classes + 1) * sizeof(float);
