@@ -331,7 +331,7 @@ __global__ __launch_bounds__(256) void k_glimpse(GlimpseGeo g, const void *pool,
 // the column ones on j only, so they are computed once per unit row and column (G0 + G1 values instead
 // of G0 * G1) and shared through LDS; each pixel then forms its four weights and reads its taps.
 // Divisions by the launch-invariant unit and row sizes use host-computed reciprocals (FastDiv).
-constexpr int GS_THREADS = 256, GS_MAX_UNITS = 64, GS_MAX_SIDE = 256;
+constexpr int GS_THREADS = 256, GS_MAX_UNITS = 128, GS_MAX_SIDE = 256;
 struct FastDiv {  // n / d for n < 2^32 / d: (n * ceil(2^32 / d)) >> 32
   uint32_t d, m;
   APG_DEV uint32_t div(uint32_t n) const { return d == 1 ? n : __umulhi(n, m); }
@@ -1189,7 +1189,9 @@ int launch_glimpse(const GlimpseGeo &g, const void *pool, const int64_t *index, 
   if (total >= (int64_t)1 << 31) return fail(APG_E_INVALID, "glimpse batch too large (>= 2**31 pixels)");
   if (g.s0 <= GS_MAX_SIDE && g.s1 <= GS_MAX_SIDE && !getenv("APG_GLIMPSE_GENERIC")) {
     const int per = g.s0 * g.s1, units = n * npos;
-    const int upb = std::max(1, std::min(GS_MAX_UNITS, (4 * GS_THREADS + per - 1) / per));
+    // pixels per thread of a workgroup (tuning knob APG_GLIMPSE_PPT; output does not depend on it)
+    static const int ppt = getenv("APG_GLIMPSE_PPT") ? std::max(1, atoi(getenv("APG_GLIMPSE_PPT"))) : 4;
+    const int upb = std::max(1, std::min(GS_MAX_UNITS, (ppt * GS_THREADS + per - 1) / per));
     const size_t dyn = (size_t)upb * (g.s0 + g.s1) * sizeof(Axis);
     hipLaunchKernelGGL(k_glimpse_sep<PosT>, dim3(grid_for(units, upb)), dim3(GS_THREADS), dyn, s, g, pool, index, pos,
                        npos, units, upb, make_fastdiv((uint32_t)per), make_fastdiv((uint32_t)g.s1),
