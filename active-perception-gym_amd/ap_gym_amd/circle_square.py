@@ -28,6 +28,7 @@ from . import _native as N
 from .image_dataset import ImageClassificationDataset
 from .loss_fn import WeightedLossFn, ZeroLossFn
 from .spaces import ActivePerceptionActionSpace, Box, Dict, Tuple, batch_space
+from .vector_env import VectorEnv
 
 
 class BaseCircleSquareDataset(ImageClassificationDataset):
@@ -184,7 +185,7 @@ class DoubleCircleSquareDataset(BaseCircleSquareDataset):
                                     max_dist=float(np.sqrt(np.sum(np.array(self._image_shape) ** 2))))
 
 
-class CircleSquareHideAndSeekVectorWrapper:
+class CircleSquareHideAndSeekVectorWrapper(VectorEnv):
     """circle_square_catch_or_flee.py:20-107 over the GPU ImageClassificationVectorEnv.
 
     reward += sign * |glimpse_pos - object position (normalized)|, sign = +1 for circles (label 1),
@@ -245,6 +246,14 @@ class CircleSquareHideAndSeekVectorWrapper:
     @property
     def config(self):
         return self.env.config
+
+    @property
+    def render_mode(self):
+        return self.env.render_mode
+
+    @property
+    def closed(self):
+        return self.env.closed
 
     @property
     def prediction_space(self):
@@ -312,4 +321,5 @@ class CircleSquareHideAndSeekVectorWrapper:
         return self.env.render()
 
     def close(self, **kwargs):
-        self.env.close(**kwargs)
+        if "env" in self.__dict__:
+            self.env.close(**kwargs)

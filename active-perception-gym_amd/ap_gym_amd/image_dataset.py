@@ -93,6 +93,39 @@ class ImageClassificationDataset:
         return np.ascontiguousarray(imgs), np.asarray(labels).astype(np.int32)
 
 
+class ForeignDatasetView(ImageClassificationDataset):
+    """Any object with the reference dataset interface (`load`, `__len__`, `num_classes`,
+    `num_channels`, `_get_data_point_batch`) -- e.g. a subclass of the reference's own
+    ImageClassificationDataset (image_classification_dataset.py:12-98) -- seen as a pool dataset:
+    `device_pool()` fetches every data point once through its `_get_data_point_batch`."""
+
+    def __init__(self, inner):
+        self.inner = inner
+
+    def load(self):
+        if hasattr(self.inner, "load"):
+            self.inner.load()
+
+    def _get_length(self):
+        return len(self.inner)
+
+    def _get_num_classes(self):
+        return int(self.inner.num_classes)
+
+    def _get_num_channels(self):
+        return int(self.inner.num_channels)
+
+    def _get_data_point_batch(self, idx):
+        return self.inner._get_data_point_batch(idx)
+
+
+def as_pool_dataset(ds):
+    """`ds` itself when it can hand the envs its pool, else a ForeignDatasetView of it."""
+    if hasattr(ds, "device_pool") or hasattr(ds, "device_pool_tensors"):
+        return ds
+    return ForeignDatasetView(ds)
+
+
 class ArrayImageClassificationDataset(ImageClassificationDataset):
     """In-memory dataset: images [M, H, W] or [M, H, W, C] (uint8 or float), labels [M]."""
 

@@ -29,9 +29,10 @@ from typing import Any, Sequence
 import numpy as np
 
 from . import _native as N
-from .image_dataset import ImageClassificationDataset
+from .image_dataset import ImageClassificationDataset, as_pool_dataset
 from .loss_fn import CrossEntropyLossFn, WeightedLossFn, affine_f32, regression_loss
 from .spaces import ActivePerceptionActionSpace, Box, Dict, Discrete, ImageSpace, LogitSpace, MultiDiscrete, batch_space
+from .vector_env import VectorEnv
 
 NAN_ACTION_MSG = "NaN values detected in action."
 NAN_PREDICTION_MSG = "NaN values detected in prediction."
@@ -78,7 +79,7 @@ def softmax_nan_rows(logits: np.ndarray) -> np.ndarray:
     return np.isnan(logits).any(-1) | np.isposinf(logits).any(-1) | np.isneginf(logits).all(-1)
 
 
-class _ImageVectorEnv:
+class _ImageVectorEnv(VectorEnv):
     metadata = {"render_modes": ["rgb_array"], "render_fps": 2, "autoreset_mode": "NextStep"}
     ERROR_POLL_INTERVAL = 32
     kind: int
@@ -113,7 +114,7 @@ class _ImageVectorEnv:
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise ValueError("the image envs run on a GPU device (no CPU fallback)")
-        ds = cfg.dataset
+        ds = as_pool_dataset(cfg.dataset)
         ds.load()
         if hasattr(ds, "device_pool_tensors"):  # procedural datasets render their pool on the device
             pool_t, labels_t = ds.device_pool_tensors(self.device)
@@ -636,8 +637,9 @@ class _ImageVectorEnv:
         return np.asarray(frames)
 
     def close(self, **kwargs):
-        if not self._closed:
+        if not getattr(self, "_closed", True):
             self._closed = True
+            self.closed = True
             self._t = {}
 
 

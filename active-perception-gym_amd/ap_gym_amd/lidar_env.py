@@ -20,8 +20,10 @@ HBM plus three kernels per step (include/apgym_capi.h):
                   on every sub-env): prediction target {"target", "weight" = 1.0 where terminated},
                   reward = base_reward - loss * weight.  The reference's own LIDAR "-sparse" ids raise
                   KeyError('prediction') in reset (SparsifyWrapper.reset needs info["prediction"], which
-                  LIDARLocalization2DEnv.reset does not return); this is their step semantics with a
-                  working reset (reset info as the dense ids)
+                  LIDARLocalization2DEnv.reset does not return), and so does this env by default (after
+                  resetting its state, as the reference's first sub-env does).  sparse_reset_info=True
+                  opts into a working reset (reset info as the dense ids) with the wrapper's step
+                  semantics
 
 Two I/O modes (constructor `array_backend`), inputs of either type are accepted:
   "numpy" (default) -> numpy out, host copies and host-side NaN checks, like the reference
@@ -42,6 +44,7 @@ from . import _native as N
 from .floor_map import FloorMapDataset, FloorMapDatasetMaze, FloorMapDatasetRooms
 from .loss_fn import WeightedLossFn, affine_f32, regression_loss
 from .spaces import ActivePerceptionActionSpace, Box, Dict, ImageSpace, batch_space
+from .vector_env import VectorEnv
 
 NAN_ACTION_MSG = "NaN values detected in action."
 NAN_PREDICTION_MSG = "NaN values detected in prediction."
@@ -60,7 +63,27 @@ def torch_index(idx: np.ndarray, device):
     return torch.as_tensor(idx, dtype=torch.int64, device=device)
 
 
-class LIDARLocalization2DVectorEnv:
+def lidar_spaces(num_envs: int, height: int, width: int, beams: int, static_map: bool, sparse: bool) -> dict:
+    """Spaces and loss of the LIDAR ids (lidar_localization2d.py:144-227, time_limit.py:64-70,
+    active_regression_env.py:55-76; sparse: sparsify_wrapper.py:93-127)."""
+    obs = {"lidar": Box(0, 1, (beams,), np.float32), "odometry": Box(-1, 1, (2,), np.float32)}
+    if not static_map:
+        obs["map"] = ImageSpace(width=width, height=height, channels=1)
+    obs["time_step"] = Box(-1.0, 1.0, (), np.float32)
+    single_obs = Dict(obs)
+    single_act = ActivePerceptionActionSpace(Box(-1, 1, (2,), np.float32), Box(-1, 1, (2,), np.float32))
+    single_target = Box(-1, 1, (2,), np.float32)
+    loss_fn = inner_loss = regression_loss(2, -1, 1)
+    if sparse:
+        single_target = Dict({"target": single_target, "weight": Box(0, 1, (), np.float32)})
+        loss_fn = WeightedLossFn(inner_loss)
+    return dict(single_observation_space=single_obs, observation_space=batch_space(single_obs, num_envs),
+                single_action_space=single_act, action_space=batch_space(single_act, num_envs),
+                single_prediction_target_space=single_target,
+                prediction_target_space=batch_space(single_target, num_envs), loss_fn=loss_fn, inner_loss=inner_loss)
+
+
+class LIDARLocalization2DVectorEnv(VectorEnv):
     metadata = {"render_modes": ["rgb_array"], "render_fps": 4, "autoreset_mode": "NextStep"}
     ERROR_POLL_INTERVAL = 32
 
@@ -69,7 +92,7 @@ class LIDARLocalization2DVectorEnv:
                  static_map_index: int = 0, prefetch: bool = True, prefetch_buffer_size: int = 128,
                  max_episode_steps: int = 100, device=None, env_offset: int = 0, copy: bool = False,
                  strict_errors: bool = False, array_backend: str = "numpy", log_stats: bool = False,
-                 sparse: bool = False, render_envs=None):
+                 sparse: bool = False, render_envs=None, sparse_reset_info: bool = False):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -88,6 +111,7 @@ class LIDARLocalization2DVectorEnv:
         self.strict_errors = strict_errors
         self.log_stats = bool(log_stats)
         self.sparse = bool(sparse)
+        self.sparse_reset_info = bool(sparse_reset_info)
         if array_backend not in ("numpy", "torch"):
             raise ValueError("array_backend must be 'numpy' or 'torch'")
         self.array_backend = array_backend
@@ -96,24 +120,10 @@ class LIDARLocalization2DVectorEnv:
             raise ValueError("LIDARLocalization2DVectorEnv runs on a GPU device (no CPU fallback)")
         h, w = dataset.map_height, dataset.map_width
 
-        # ---- spaces (lidar_localization2d.py:144-227, time_limit.py:64-70, active_regression_env.py:55-76)
-        obs = {"lidar": Box(0, 1, (self.lidar_beam_count,), np.float32),
-               "odometry": Box(-1, 1, (2,), np.float32)}
-        if not self.static_map:
-            obs["map"] = ImageSpace(width=w, height=h, channels=1)
-        obs["time_step"] = Box(-1.0, 1.0, (), np.float32)
-        self.single_observation_space = Dict(obs)
-        self.observation_space = batch_space(self.single_observation_space, self.num_envs)
-        self.single_action_space = ActivePerceptionActionSpace(Box(-1, 1, (2,), np.float32),
-                                                               Box(-1, 1, (2,), np.float32))
-        self.action_space = batch_space(self.single_action_space, self.num_envs)
-        self.single_prediction_target_space = Box(-1, 1, (2,), np.float32)
-        self.loss_fn = inner_loss = regression_loss(2, -1, 1)
-        if self.sparse:
-            self.single_prediction_target_space = Dict({"target": self.single_prediction_target_space,
-                                                        "weight": Box(0, 1, (), np.float32)})
-            self.loss_fn = WeightedLossFn(inner_loss)
-        self.prediction_target_space = batch_space(self.single_prediction_target_space, self.num_envs)
+        sp = lidar_spaces(self.num_envs, h, w, self.lidar_beam_count, self.static_map, self.sparse)
+        inner_loss = sp.pop("inner_loss")
+        for k, v in sp.items():
+            setattr(self, k, v)
 
         # ---- native configuration
         p = dataset.native_params()
@@ -339,6 +349,10 @@ class LIDARLocalization2DVectorEnv:
         self._track_render(None)
         self._seeded = True
         self._autoreset_host[:] = False
+        if self.sparse and not self.sparse_reset_info:
+            # SparsifyWrapper.reset (sparsify_wrapper.py:128-135) reads info["prediction"], which
+            # LIDARLocalization2DEnv.reset never returns (lidar_localization2d.py:315)
+            raise KeyError("prediction")
         T = self._t
         if self.array_backend == "numpy":
             self.check_errors(block=True)
@@ -505,8 +519,9 @@ class LIDARLocalization2DVectorEnv:
         return obs, reward, term, trunc, info
 
     def close(self, **kwargs):
-        if not self._closed:
+        if not getattr(self, "_closed", True):
             self._closed = True
+            self.closed = True
             self._t = {}
 
     def __repr__(self):

@@ -31,12 +31,13 @@ import numpy as np
 from . import _native as N
 from .loss_fn import WeightedLossFn, affine_f32, regression_loss
 from .spaces import ActivePerceptionActionSpace, Box, Dict, batch_space
+from .vector_env import VectorEnv
 
 NAN_ACTION_MSG = "NaN values detected in action."
 NAN_PREDICTION_MSG = "NaN values detected in prediction."
 
 
-class LightDarkVectorEnv:
+class LightDarkVectorEnv(VectorEnv):
     metadata = {"render_modes": ["rgb_array"], "render_fps": 4, "autoreset_mode": "NextStep"}
     ERROR_POLL_INTERVAL = 32
     STAT_NAMES = ("avg_euclidean_distance", "avg_mse", "final_euclidean_distance", "final_mse")
@@ -359,8 +360,9 @@ class LightDarkVectorEnv:
                      for r in self._render_state)
 
     def close(self, **kwargs):
-        if not self._closed:
+        if not getattr(self, "_closed", True):
             self._closed = True
+            self.closed = True
             self._t = {}
 
     def __repr__(self):

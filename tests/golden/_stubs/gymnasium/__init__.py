@@ -4,6 +4,7 @@ the build container when generating golden fixtures (gymnasium is not installed 
 Restated behaviour that affects values (everything else is a no-op placeholder):
   * Env.reset(seed) -> np_random = Generator(PCG64(SeedSequence(seed)))   (gymnasium/utils/seeding.py)
   * Wrapper forwarding of reset/step/spaces/np_random                    (gymnasium/core.py)
+  * register / make / make_vec with gymnasium's vector-entry-point rules     (gymnasium/envs/registration.py)
   * SyncVectorEnv with NEXT_STEP autoreset, seed+i per sub-env, info merging with `_key` masks,
     float64 rewards / bool flags                                          (gymnasium/vector/sync_vector_env.py)
 """
@@ -25,13 +26,4 @@ class VectorizeMode(enum.Enum):
     VECTOR_ENTRY_POINT = "vector_entry_point"
 
 
-def register(*args, **kwargs):  # registry is not needed for fixture generation
-    return None
-
-
-def make(*args, **kwargs):
-    raise NotImplementedError("gymnasium stub: make() is not available")
-
-
-def make_vec(*args, **kwargs):
-    raise NotImplementedError("gymnasium stub: make_vec() is not available")
+from .envs.registration import make, make_vec, register, registry  # noqa: E402,F401

@@ -149,7 +149,8 @@ def test_vector_env_matches_reference_trace(gpu, name):
     n = d["actions"].shape[1]
     sparse = name.endswith("_sparse")
     env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_ds(ap, kind, size), static_map=static,
-                                          lidar_beam_count=beams, device=gpu, log_stats=True, sparse=sparse)
+                                          lidar_beam_count=beams, device=gpu, log_stats=True, sparse=sparse,
+                                          sparse_reset_info=sparse)
     obs, info = env.reset(seed=int(d["seed"]))
     vec_off = 0
     assert np.array_equal(obs["lidar"], d["reset_lidar"])
@@ -214,7 +215,8 @@ def test_vector_env_matches_oracle(gpu, oracle_mod, kind, size, beams, n, steps,
     import ap_gym_amd as ap
 
     env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_ds(ap, kind, size), lidar_beam_count=beams,
-                                          device=gpu, log_stats=True, sparse=sparse)
+                                          device=gpu, log_stats=True, sparse=sparse,
+                                          sparse_reset_info=sparse)
     ref = oracle_mod.OracleLidarVectorEnv(n, kind, size, False, 0, beams, sparse=sparse)
     obs, _ = env.reset(seed=123)
     ref.reset(123)
@@ -261,6 +263,10 @@ def test_torch_backend_matches_numpy_backend(gpu, env_id):
     import ap_gym_amd as ap
 
     kw = dict(num_envs=256, lidar_beam_count=32, dataset=ap.FloorMapDatasetRooms(64, 64), device=gpu)
+    if env_id.endswith("-sparse-v0"):
+        with pytest.raises(KeyError, match="prediction"):  # the reference's own -sparse LIDAR reset
+            ap.make_vec(env_id, **kw).reset(seed=5)
+        kw["sparse_reset_info"] = True
     e_np = ap.make_vec(env_id, **kw)
     e_t = ap.make_vec(env_id, array_backend="torch", **kw)
     assert e_np.sparse == env_id.endswith("-sparse-v0")
