@@ -1,7 +1,12 @@
-"""ctypes binding of the gfx950 C ABI (include/apgym_capi.h) in _lib/libapgym_hip.so.
+"""Bindings of the gfx950 C ABI (include/apgym_capi.h) in _lib/libapgym_hip.so.
 
-The library is the ONLY compute path of this package: there is no CPU fallback.  `lib()` raises
-NativeLibraryError when the shared object is missing or cannot be loaded, and every op calls it.
+* `lib()` — ctypes over every entry point (setup, tests, render, utility calls);
+* `torch_ops()` — the TORCH_LIBRARY(apgym) custom ops of _lib/libapgym_torch.so
+  (csrc/apg_torch_ops.cpp), which the envs' reset/step hot path calls: one C++ op call per step,
+  launched on PyTorch's current HIP stream (CUDA-graph capturable).
+
+The library is the ONLY compute path of this package: there is no CPU fallback.  Both loaders raise
+NativeLibraryError when their shared object is missing or cannot be loaded.
 """
 
 from __future__ import annotations
@@ -12,6 +17,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "_lib")
 LIB_PATH = os.environ.get("APG_LIBRARY") or os.path.join(LIB_DIR, "libapgym_hip.so")  # override: tuning builds
+TORCH_LIB_PATH = os.path.join(LIB_DIR, "libapgym_torch.so")
 
 APG_OK = 0
 APG_ERR_NAN_ACTION = 1
@@ -197,6 +203,35 @@ def lib():
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+_torch_ops = None
+
+
+def torch_ops():
+    """torch.ops.apgym (loads _lib/libapgym_torch.so once, after the C-ABI library it links)."""
+    global _torch_ops
+    if _torch_ops is None:
+        import torch
+
+        lib()  # the ops library resolves libapgym_hip.so through its rpath; load (and check) it first
+        if not os.path.exists(TORCH_LIB_PATH):
+            raise NativeLibraryError(f"{TORCH_LIB_PATH} not found: build it with "
+                                     "`python -c 'import __graft_entry__ as g; g.build()'`")
+        try:
+            torch.ops.load_library(TORCH_LIB_PATH)
+        except OSError as e:  # pragma: no cover - depends on the ROCm runtime
+            raise NativeLibraryError(f"cannot load {TORCH_LIB_PATH}: {e}") from e
+        _torch_ops = torch.ops.apgym
+    return _torch_ops
+
+
+def op_buffers(tensors, device):
+    """Buffer list for an env handle: None -> a 0-element tensor (NULL in the C struct)."""
+    import torch
+
+    empty = torch.empty(0, dtype=torch.uint8, device=device)
+    return [empty if t is None else t for t in tensors]
 
 
 def check(rc: int, what: str = "apg call") -> None:

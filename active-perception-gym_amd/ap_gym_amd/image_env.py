@@ -219,6 +219,20 @@ class _ImageVectorEnv(VectorEnv):
         self._out = N.ImageOutputs(*[N.ptr(T[k_]) for k_ in ("glimpse", "glimpse_pos", "time_step", "target_glimpse",
                                                               "reward", "base_reward", "target_out", "label_target",
                                                               "loss_f64", "loss_f32", "err", "stats", "stats_idx")])
+        c = self._cfg
+        self._ops = N.torch_ops()  # torch.ops.apgym: the reset/step hot path
+        self._h = t.classes.apgym.ImageEnv(
+            [c.num_envs, c.kind, c.height, c.width, c.pool_channels, c.channels, c.pool_dtype, c.sensor_h,
+             c.sensor_w, c.step_limit, c.num_classes, c.invert_labels, c.top_k, c.unique_points, c.num_envs_total,
+             c.env_offset, c.pool_len, c.log_stats, c.sparse],
+            [c.sensor_scale, c.max_step[0], c.max_step[1], c.cell[0], c.cell[1], c.ce_scale, c.ce_offset,
+             c.mse_scale, c.mse_offset],
+            N.op_buffers([T[k_] for k_ in ("pool", "pool_labels", "unique_grid", "index", "label", "inverted", "pos",
+                                           "target", "rng", "scratch_i64", "scratch_f64", "top_k", "rng_work",
+                                           "stats_hist")], dev),
+            N.op_buffers([T[k_] for k_ in ("glimpse", "glimpse_pos", "time_step", "target_glimpse", "reward",
+                                           "base_reward", "target_out", "label_target", "loss_f64", "loss_f32", "err",
+                                           "stats", "stats_idx")], dev))
         self._err_host = t.zeros(1, dtype=t.int32).pin_memory()
         self._err_event = t.cuda.Event()
         self._err_pending = False
@@ -316,8 +330,7 @@ class _ImageVectorEnv(VectorEnv):
             N.check(L.apg_image_seed(ctypes.byref(self._cfg), ctypes.byref(self._state), int(seed), self._stream()),
                     "apg_image_seed")
             self._seeded = True
-        N.check(L.apg_image_reset(ctypes.byref(self._cfg), ctypes.byref(self._state), ctypes.byref(self._out),
-                                  self._stream()), "apg_image_reset")
+        self._ops.image_reset(self._h)
         self._t_step = 0
         self._prev_done = False
         self._visits = [[] for _ in self.render_envs]  # module.reset clears the overlay (:184-186)
@@ -358,9 +371,7 @@ class _ImageVectorEnv(VectorEnv):
             p_t = torch.as_tensor(p, dtype=torch.float32, device=self.device).reshape(n, pdim).contiguous()
         resetting = self._prev_done
         self._track_render(p_np if numpy_mode else p_t, resetting)
-        N.check(N.lib().apg_image_step(ctypes.byref(self._cfg), ctypes.byref(self._state), N.ptr(a_t), N.ptr(p_t),
-                                       int(self._t_step), int(resetting), ctypes.byref(self._out), self._stream()),
-                "apg_image_step")
+        self._ops.image_step(self._h, a_t, p_t, int(self._t_step), bool(resetting))
         if resetting:
             self._t_step = 0
             terminated = False

@@ -183,6 +183,17 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
                                    N.ptr(T["loss"]), N.ptr(T["info_mask"]), N.ptr(T["map_idx_out"]),
                                    N.ptr(T["reset_mask"]), N.ptr(T["err"]), N.ptr(T["stats"]),
                                    N.ptr(T["stats_len"]), N.ptr(T["weight"]))
+        c = self._cfg
+        self._ops = N.torch_ops()  # torch.ops.apgym: the reset/step hot path
+        self._h = t.classes.apgym.LidarEnv(
+            [c.num_envs, c.height, c.width, c.map_kind, c.is_static, c.static_map_index, c.beams, c.step_limit,
+             c.max_rooms, c.door_width, c.log_stats, c.sparse],
+            [c.lidar_range, c.loss_scale, c.loss_offset, c.branching_prob],
+            N.op_buffers([T[k] for k in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng", "occ", "scratch",
+                                         "stack", "map_idx", "beam_dirs", "stats_hist")], dev),
+            N.op_buffers([T[k] for k in ("lidar", "odometry", "time_step", "map_obs", "reward", "terminated",
+                                         "truncated", "base_reward", "target", "loss", "info_mask", "map_idx_out",
+                                         "reset_mask", "err", "stats", "stats_len", "weight")], dev))
         self._err_host = t.zeros(1, dtype=t.int32).pin_memory()
         self._err_event = t.cuda.Event()
         self._err_pending = False
@@ -289,6 +300,38 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
     def single_inner_action_space(self):
         return self.single_action_space["action"]
 
+    def capture_step_graph(self, action, prediction):
+        """Capture one device step (torch.ops.apgym.lidar_step on the static `action` / `prediction`
+        tensors, float32 [N, 2] on the env's device) into a torch.cuda.CUDAGraph (a hipGraph).  Each
+        `graph.replay()` is one env step reading the tensors' current contents; its results land in the
+        persistent output buffers (`device_outputs()`).  NaN checks run on the device as usual
+        (`check_errors()`); the host-side bookkeeping of `step()` (render tracking, lazy error polling)
+        is not part of the graph."""
+        import torch
+
+        if not self._seeded:
+            raise RuntimeError("capture_step_graph() needs reset() first")
+        for name, x in (("action", action), ("prediction", prediction)):
+            if not (isinstance(x, torch.Tensor) and x.dtype == torch.float32 and x.is_contiguous()
+                    and x.device == self.device and x.numel() == 2 * self.num_envs):
+                raise ValueError(f"{name} must be a contiguous float32 [num_envs, 2] tensor on {self.device}")
+        graph = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side), torch.cuda.graph(graph, stream=side):
+            self._ops.lidar_step(self._h, action, prediction)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        return graph
+
+    def device_outputs(self) -> dict:
+        """The persistent device buffers every step writes (obs, reward, flags, info fields)."""
+        T = self._t
+        out = {k: T[k] for k in ("lidar", "odometry", "time_step", "reward", "terminated", "truncated", "base_reward",
+                                 "target", "loss", "info_mask", "reset_mask")}
+        if not self.static_map:
+            out["map"] = T["map_obs"]
+        return out
+
     def set_kernel_timing_events(self, begin=None, end=None):
         """Record hipEvent_t handles `begin`/`end` around the fused step kernel of the next step
         (bench.py's live per-launch timing).  None disables."""
@@ -344,8 +387,7 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         s = (int(seed) + self.env_offset) if use_seed else 0
         if s < 0 or s + self.num_envs > 2**64:
             raise ValueError("seed must be a non-negative int")
-        N.check(N.lib().apg_lidar_reset(ctypes.byref(self._cfg), ctypes.byref(self._state), s, int(use_seed),
-                                        ctypes.byref(self._out), self._stream()), "apg_lidar_reset")
+        self._ops.lidar_reset(self._h, s if s < 2**63 else s - 2**64, bool(use_seed))
         self._track_render(None)
         self._seeded = True
         self._autoreset_host[:] = False
@@ -388,13 +430,12 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             a_t = torch.as_tensor(a, dtype=torch.float32, device=self.device).contiguous()
             p_t = torch.as_tensor(p, dtype=torch.float32, device=self.device).contiguous()
         if self._kernel_events is None:
-            rc = N.lib().apg_lidar_step(ctypes.byref(self._cfg), ctypes.byref(self._state), N.ptr(a_t), N.ptr(p_t),
-                                        ctypes.byref(self._out), self._stream())
+            self._ops.lidar_step(self._h, a_t, p_t)
         else:
             ev_b, ev_e = self._kernel_events
-            rc = N.lib().apg_lidar_step_profiled(ctypes.byref(self._cfg), ctypes.byref(self._state), N.ptr(a_t),
-                                                 N.ptr(p_t), ctypes.byref(self._out), self._stream(), ev_b, ev_e)
-        N.check(rc, "apg_lidar_step")
+            N.check(N.lib().apg_lidar_step_profiled(ctypes.byref(self._cfg), ctypes.byref(self._state), N.ptr(a_t),
+                                                    N.ptr(p_t), ctypes.byref(self._out), self._stream(), ev_b, ev_e),
+                    "apg_lidar_step")
         self._track_render(p_t)
         if numpy_mode:
             return self._numpy_step_result()

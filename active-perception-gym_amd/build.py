@@ -2,8 +2,9 @@
 
     python active-perception-gym_amd/build.py [--force] [--verbose]
 
-Output: active-perception-gym_amd/ap_gym_amd/_lib/libapgym_hip.so (git-ignored; travels to the
-GPU box with the gpurun snapshot).
+Outputs (git-ignored; they travel to the GPU box with the gpurun snapshot):
+  active-perception-gym_amd/ap_gym_amd/_lib/libapgym_hip.so    the gfx950 kernels + C ABI
+  active-perception-gym_amd/ap_gym_amd/_lib/libapgym_torch.so  TORCH_LIBRARY(apgym) ops over that C ABI
 """
 
 from __future__ import annotations
@@ -35,6 +36,39 @@ FLAGS = [
 ]
 
 
+TORCH_OUT = os.path.join(OUT_DIR, "libapgym_torch.so")
+TORCH_SRC = os.path.join(CSRC, "apg_torch_ops.cpp")
+
+
+def _torch_stale() -> bool:
+    if not os.path.exists(TORCH_OUT):
+        return True
+    t = os.path.getmtime(TORCH_OUT)
+    return any(os.path.getmtime(d) > t for d in (TORCH_SRC, OUT, os.path.join(INCLUDE, "apgym_capi.h"),
+                                                  os.path.abspath(__file__)))
+
+
+def build_torch_ops(force: bool = False) -> str:
+    """Host-only C++ against torch's headers (hipcc for the HIP stream API), linked to
+    libapgym_hip.so next to it ($ORIGIN) and to torch's libraries."""
+    if not force and not _torch_stale():
+        return TORCH_OUT
+    import torch
+    from torch.utils import cpp_extension as ce
+
+    torch_lib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = [HIPCC, "-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+           f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=apgym_torch",
+           *[f"-I{p}" for p in ce.include_paths(device_type="cuda")], "-I", INCLUDE,
+           "-o", TORCH_OUT + ".tmp", TORCH_SRC,
+           f"-L{OUT_DIR}", "-lapgym_hip", f"-L{torch_lib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch",
+           "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{torch_lib}"]
+    subprocess.run(cmd, check=True)
+    os.replace(TORCH_OUT + ".tmp", TORCH_OUT)
+    return TORCH_OUT
+
+
 def _stale() -> bool:
     if not os.path.exists(OUT):
         return True
@@ -61,8 +95,14 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str |
     return out
 
 
+def build_all(force: bool = False) -> tuple[str, str]:
+    return build(force=force), build_torch_ops(force=force)
+
+
 if __name__ == "__main__":
     args = sys.argv[1:]
     out_arg = next((a.split("=", 1)[1] for a in args if a.startswith("--out=")), None)
     defs = [a for a in args if a.startswith("-D")]
     print(build(force="--force" in args, verbose="--verbose" in args, extra_flags=defs, out=out_arg))
+    if out_arg is None:
+        print(build_torch_ops(force="--force" in args))

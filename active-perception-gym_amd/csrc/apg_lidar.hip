@@ -185,12 +185,56 @@ __global__ __launch_bounds__(64) void k_map_generate(Geo g, const uint64_t *idx,
   if (rc != 0 && err) atomicOr(err, APG_ERR_MAPGEN);
 }
 
-// One wave per `lanes` (<= 64) envs.  Envs pending autoreset (or all, for reset(seed)) draw their
-// next map index, generate the map and draw the start cell (the float32 map observation is expanded
-// by the following k_lidar_step, whose workgroups have the bandwidth for it).  Map generation is a
-// long serial, divergent chain per env whose speed is set by instruction latency, not by lanes, so
-// the host spreads the envs over as many waves as fit on the chip at once (pick_lanes).  Waves with
-// nothing to reset exit after one flag load.
+// reset of env e (lidar_localization2d.py:293-315 with the _np_random setter :547-557 on reset(seed)):
+// reseed (use_seed) or continue the env's streams, next map index from the DatasetIterator stream,
+// map generation into `own` (rooms: the caller's LDS bitmap; maze: the env's occupancy rows), start
+// cell draw.  Returns the env's new flags.
+template <int GEN>
+APG_DEV uint8_t reset_one(const Geo &g, const apg_lidar_state &S, int e, uint8_t f, bool use_seed, uint64_t seed,
+                          uint64_t *own, uint64_t *out_map_idx, uint32_t *err, const BinomTable &bt) {
+  Pcg64 rng;
+  Pcg64 it;
+  if (use_seed) {
+    rng = seed_pcg64(seed + (uint64_t)e);
+    if constexpr (GEN != GEN_NONE) it = seed_pcg64(bounded_u64(rng, 0x100000000ULL));  // integers(0, 2**32, endpoint=True)
+  } else {
+    rng = *reinterpret_cast<const Pcg64 *>(&S.rng[e]);
+    if constexpr (GEN != GEN_NONE) it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[e]);
+  }
+  uint64_t midx;
+  float px = 0.5f, py = 0.5f;
+  if constexpr (GEN != GEN_NONE) {
+    midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
+    Pcg64 map_rng = seed_pcg64(midx);  // FloorMapDataset*.get_data_point: default_rng(idx)
+    int rc;
+    if constexpr (GEN == GEN_ROOMS)
+      rc = rooms_generate(map_rng, own, g.wpr, g.h, g.max_rooms, g.door_width, bt);
+    else
+      rc = generate_one<GEN>(g, map_rng, own, S.stack + (size_t)e * g.frames, bt);
+    if (place_start(rng, own, g.h, g.w, g.wpr, px, py) != 0) rc = -6;
+    if (rc != 0) atomicOr(err, APG_ERR_MAPGEN);
+    *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
+    S.map_idx[e] = midx;
+  } else {
+    midx = S.map_idx[e];
+    if (place_start(rng, S.occ, g.h, g.w, g.wpr, px, py) != 0) atomicOr(err, APG_ERR_MAPGEN);
+  }
+  S.pos[2 * e] = px;
+  S.pos[2 * e + 1] = py;
+  S.init_pos[2 * e] = px;
+  S.init_pos[2 * e + 1] = py;
+  S.elapsed[e] = 0;
+  const uint8_t nf = (uint8_t)((f & F_AUTORESET) | F_JUST_RESET | F_FIRST);
+  S.flags[e] = nf;
+  *reinterpret_cast<Pcg64 *>(&S.rng[e]) = rng;
+  if (out_map_idx) out_map_idx[e] = midx;
+  return nf;
+}
+
+// reset(seed) of all envs (and, for maps too large for the fused step kernel's LDS, the autoresets):
+// one wave per `lanes` (<= 64) envs.  Map generation is a long serial, divergent chain per env whose
+// speed is set by instruction latency, not by lanes, so the host spreads the envs over as many waves
+// as fit on the chip at once (gen_lanes).  Waves with nothing to reset exit after one flag load.
 template <int GEN>
 __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, uint64_t seed, int use_seed,
                                                     int all, uint64_t *out_map_idx, uint32_t *err, BinomTable bt,
@@ -205,45 +249,8 @@ __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, ui
   if (todo == 0ULL) return;
   const size_t words = (size_t)g.h * g.wpr;
   if (active) {
-    Pcg64 rng;
-    Pcg64 it;
-    if (use_seed) {
-      rng = seed_pcg64(seed + (uint64_t)e);
-      if constexpr (GEN != GEN_NONE) it = seed_pcg64(bounded_u64(rng, 0x100000000ULL));  // integers(0, 2**32, endpoint=True)
-    } else {
-      rng = *reinterpret_cast<const Pcg64 *>(&S.rng[e]);
-      if constexpr (GEN != GEN_NONE) it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[e]);
-    }
-    uint64_t midx;
-    float px = 0.5f, py = 0.5f;
-    if constexpr (GEN != GEN_NONE) {
-      midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
-      Pcg64 map_rng = seed_pcg64(midx);  // FloorMapDataset*.get_data_point: default_rng(idx)
-      int rc;
-      if constexpr (GEN == GEN_ROOMS) {
-        uint64_t *own = s_rows + lane * words;
-        rc = rooms_generate(map_rng, own, g.wpr, g.h, g.max_rooms, g.door_width, bt);
-        if (place_start(rng, own, g.h, g.w, g.wpr, px, py) != 0) rc = -6;
-      } else {
-        uint64_t *own = S.occ + (size_t)e * words;
-        rc = generate_one<GEN>(g, map_rng, own, S.stack + (size_t)e * g.frames, bt);
-        if (place_start(rng, own, g.h, g.w, g.wpr, px, py) != 0) rc = -6;
-      }
-      if (rc != 0) atomicOr(err, APG_ERR_MAPGEN);
-      *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
-      S.map_idx[e] = midx;
-    } else {
-      midx = S.map_idx[e];
-      if (place_start(rng, S.occ, g.h, g.w, g.wpr, px, py) != 0) atomicOr(err, APG_ERR_MAPGEN);
-    }
-    S.pos[2 * e] = px;
-    S.pos[2 * e + 1] = py;
-    S.init_pos[2 * e] = px;
-    S.init_pos[2 * e + 1] = py;
-    S.elapsed[e] = 0;
-    S.flags[e] = (uint8_t)((f & F_AUTORESET) | F_JUST_RESET | F_FIRST);
-    *reinterpret_cast<Pcg64 *>(&S.rng[e]) = rng;
-    if (out_map_idx) out_map_idx[e] = midx;
+    uint64_t *own = GEN == GEN_ROOMS ? s_rows + lane * words : S.occ + (size_t)e * words;
+    reset_one<GEN>(g, S, e, f, use_seed != 0, seed, own, out_map_idx, err, bt);
   }
   if constexpr (GEN == GEN_ROOMS) copy_out_maps(s_rows, todo, words, S.occ + (size_t)blockIdx.x * lanes * words, lane);
 }
@@ -282,10 +289,15 @@ __device__ unsigned long long g_step_prof[16384][8];
 #ifndef APG_STEP_MIN_WAVES
 #define APG_STEP_MIN_WAVES 4  // keep k_lidar_step at <= 128 VGPRs: 4 waves per SIMD
 #endif
-__global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step(StepParams P, apg_lidar_state S,
+// GEN / FUSED: FUSED instances start with phase R, the NEXT_STEP autoresets of the envs whose episode
+// ended at the previous step (map generation of kind GEN, start cell), so a step is one launch; the
+// unfused instance (reset(seed)'s observation pass, and autoresets of rooms maps too large for the LDS
+// budget, which k_lidar_reset does first) skips it.
+template <int GEN, bool FUSED>
+__global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step(StepParams P, Geo g, apg_lidar_state S,
                                                              const float *__restrict__ act,
                                                              const float *__restrict__ pred,
-                                                             apg_lidar_outputs O) {
+                                                             apg_lidar_outputs O, BinomTable bt) {
   __shared__ float s_pos[EPB][2];
   __shared__ int s_x0[EPB], s_y0[EPB];
   // dynamic LDS (step_lds_bytes): occupancy windows, then (beams <= MAX_STAGED_BEAMS) the lidar rows
@@ -305,8 +317,41 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
   const unsigned long long prof_clk0 = __builtin_amdgcn_s_memtime();
 #endif
 
-  // ---------------- phase 0: window origins from the pre-move positions; which envs reset
+  // ---------------- phase R: NEXT_STEP autoresets (fused instances).  Envs are spread 16 per wave over
+  // the four waves (map generation is a serial divergent chain per env, latency-bound: more waves in
+  // flight, fewer lanes each).  Rooms maps are painted in LDS (aliasing the windows, which are staged
+  // later) and copied out with the map observation; maze maps go straight to the occupancy rows.
   __shared__ unsigned long long s_reset;
+  if constexpr (FUSED) {
+    __shared__ unsigned long long s_pend;
+    if (tid < EPB) {
+      const int e = base + tid;
+      const bool pend = e < P.n && (S.flags[e] & F_AUTORESET);
+      const unsigned long long m = __ballot(pend);
+      if (tid == 0) s_pend = m;
+    }
+    __syncthreads();
+    const unsigned long long pend = s_pend;
+    if (pend != 0ULL) {
+      uint64_t *s_maps = reinterpret_cast<uint64_t *>(s_dyn);  // rooms: [EPB][h * wpr]
+      const int lane = tid & 63, el = (tid >> 6) * (EPB / 4) + lane;
+      if (lane < EPB / 4 && ((pend >> el) & 1ULL)) {
+        const int e = base + el;
+        uint64_t *own = GEN == GEN_ROOMS ? s_maps + (size_t)el * words : S.occ + (size_t)e * words;
+        reset_one<GEN>(g, S, e, S.flags[e], false, 0, own, O.map_idx, O.err, bt);
+      }
+      __syncthreads();
+      if constexpr (GEN == GEN_ROOMS) {  // occupancy rows out, coalesced over the workgroup
+        for (int k = tid; k < EPB * (int)words; k += STEP_THREADS) {
+          const int el2 = k / (int)words;
+          if (((pend >> el2) & 1ULL) && base + el2 < P.n) S.occ[(size_t)base * words + k] = s_maps[k];
+        }
+        __syncthreads();
+      }
+    }
+  }
+
+  // ---------------- phase 0: window origins from the pre-move positions; which envs reset
   if (P.beams <= MAX_STAGED_BEAMS && tid < 2 * P.beams) s_dirs[tid >> 1][tid & 1] = S.beam_dirs[tid];
   if (tid < EPB) {
     const int e = base + tid;
@@ -762,8 +807,19 @@ size_t step_lds_bytes(int beams) {
   return b;
 }
 
+// Rooms maps of a fused step workgroup live in its dynamic LDS during phase R: keep that within the
+// budget of four resident workgroups per CU (the step kernel's occupancy); larger rooms maps take
+// the two-launch path (k_lidar_reset, then the unfused step kernel).
+constexpr size_t FUSED_ROOMS_LDS_MAX = 36 * 1024;
+size_t fused_rooms_lds(const Geo &g) { return (size_t)EPB * g.h * g.wpr * sizeof(uint64_t); }
+int step_gen(const Geo &g) {
+  if (g.is_static) return GEN_NONE;
+  if (g.kind == APG_MAP_MAZE) return GEN_MAZE;
+  return fused_rooms_lds(g) <= FUSED_ROOMS_LDS_MAX ? GEN_ROOMS : -1;  // -1: not fusable
+}
+
 int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *act,
-                       const float *pred, const apg_lidar_outputs *out, hipStream_t s) {
+                       const float *pred, const apg_lidar_outputs *out, hipStream_t s, bool fused) {
   StepParams P;
   P.n = cfg->num_envs;
   P.h = cfg->height;
@@ -779,8 +835,25 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   P.range = cfg->lidar_range;
   P.loss_scale = cfg->loss_scale;
   P.loss_offset = cfg->loss_offset;
-  hipLaunchKernelGGL(k_lidar_step, dim3(grid_for(P.n, EPB)), dim3(STEP_THREADS), step_lds_bytes(P.beams), s, P, *st,
-                     act, pred, *out);
+  const Geo g = make_geo(cfg);
+  const dim3 grid(grid_for(P.n, EPB)), block(STEP_THREADS);
+  const BinomTable bt = make_binom_table();
+  size_t lds = step_lds_bytes(P.beams);
+  const int gen = fused ? step_gen(g) : -1;
+  if (gen == GEN_ROOMS && fused_rooms_lds(g) > lds) lds = fused_rooms_lds(g);
+  switch (gen) {
+    case GEN_NONE:
+      hipLaunchKernelGGL((k_lidar_step<GEN_NONE, true>), grid, block, lds, s, P, g, *st, act, pred, *out, bt);
+      break;
+    case GEN_ROOMS:
+      hipLaunchKernelGGL((k_lidar_step<GEN_ROOMS, true>), grid, block, lds, s, P, g, *st, act, pred, *out, bt);
+      break;
+    case GEN_MAZE:
+      hipLaunchKernelGGL((k_lidar_step<GEN_MAZE, true>), grid, block, lds, s, P, g, *st, act, pred, *out, bt);
+      break;
+    default:
+      hipLaunchKernelGGL((k_lidar_step<GEN_NONE, false>), grid, block, lds, s, P, g, *st, act, pred, *out, bt);
+  }
   return check_launch("k_lidar_step");
 }
 
@@ -823,7 +896,7 @@ int apg_lidar_reset(const apg_lidar_config *cfg, const apg_lidar_state *st, uint
   hipStream_t s = (hipStream_t)stream;
   Geo g = make_geo(cfg);
   if ((rc = launch_reset(g, st, seed, use_seed, 1, out, s))) return rc;
-  return launch_step_kernel(cfg, st, nullptr, nullptr, out, s);
+  return launch_step_kernel(cfg, st, nullptr, nullptr, out, s, false);
 }
 
 int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
@@ -837,9 +910,12 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
   if (cfg->sparse && !out->weight) return fail(APG_E_INVALID, "sparse needs the weight buffer");
   hipStream_t s = (hipStream_t)stream;
   Geo g = make_geo(cfg);
-  if ((rc = launch_reset(g, st, 0, 0, 0, out, s))) return rc;
+  // one launch per step: the fused step kernel performs the NEXT_STEP autoresets itself; only rooms
+  // maps beyond its LDS budget are generated by k_lidar_reset first
+  const bool fused = step_gen(g) >= 0;
+  if (!fused && (rc = launch_reset(g, st, 0, 0, 0, out, s))) return rc;
   if (ev_begin && hipEventRecord((hipEvent_t)ev_begin, s) != hipSuccess) return fail(APG_E_LAUNCH, "hipEventRecord");
-  rc = launch_step_kernel(cfg, st, action, prediction, out, s);
+  rc = launch_step_kernel(cfg, st, action, prediction, out, s, fused);
   if (rc == APG_OK && ev_end && hipEventRecord((hipEvent_t)ev_end, s) != hipSuccess)
     return fail(APG_E_LAUNCH, "hipEventRecord");
   return rc;

@@ -345,3 +345,40 @@ def test_full_size_properties(gpu, oracle_mod):
             assert int(reset_now.sum()) >= 0.99 * n and bool((rew[reset_now] == 0).all())
     env.check_errors()
     assert resets == 2
+
+
+@pytest.mark.parametrize("kind,size,beams", [("rooms", 64, 32), ("maze", 21, 8)])
+def test_step_through_ops_and_graph_replay(gpu, kind, size, beams):
+    """The hot path is torch.ops.apgym.lidar_step; one step captured in a torch.cuda.CUDAGraph (hipGraph)
+    and replayed over 230 steps (two autoreset bursts, fused into the step kernel) is bit-identical to
+    eager env.step."""
+    import torch
+
+    import ap_gym_amd as ap
+
+    n = 512
+    kw = dict(num_envs=n, lidar_beam_count=beams, dataset=_ds(ap, kind, size), device=gpu, array_backend="torch")
+    eager = ap.make_vec(f"LIDARLoc{'Rooms' if kind == 'rooms' else 'Maze'}-v0", **kw)
+    graphed = ap.make_vec(f"LIDARLoc{'Rooms' if kind == 'rooms' else 'Maze'}-v0", **kw)
+    assert eager._ops is torch.ops.apgym
+    eager.reset(seed=11)
+    graphed.reset(seed=11)
+    a_buf = torch.zeros((n, 2), dtype=torch.float32, device=gpu)
+    p_buf = torch.zeros((n, 2), dtype=torch.float32, device=gpu)
+    graph = graphed.capture_step_graph(a_buf, p_buf)
+    g = torch.Generator(device=gpu).manual_seed(3)
+    out_g = graphed.device_outputs()
+    for t in range(230):
+        a = torch.rand((n, 2), device=gpu, generator=g) * 2.2 - 1.1
+        p = torch.rand((n, 2), device=gpu, generator=g) * 2 - 1
+        obs, rew, term, trunc, info = eager.step({"action": a, "prediction": p})
+        a_buf.copy_(a)
+        p_buf.copy_(p)
+        graph.replay()
+        for k, v in (("lidar", obs["lidar"]), ("odometry", obs["odometry"]), ("time_step", obs["time_step"]),
+                     ("reward", rew), ("terminated", term), ("base_reward", info["base_reward"]),
+                     ("target", info["prediction"]["target"]), ("loss", info["prediction"]["loss"])):
+            assert torch.equal(out_g[k], v), (t, k)
+        assert torch.equal(graphed._t["map_obs"], obs["map"]), t
+    eager.check_errors()
+    graphed.check_errors()

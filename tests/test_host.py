@@ -205,3 +205,19 @@ def test_sparse_ids_and_weighted_loss():
     w = np.array([0, 1, 0, 1, 1, 0], np.float32)
     got = fn.numpy(p, {"target": t, "weight": w}, (6,))
     assert np.array_equal(got, inner.numpy(p, t, (6,)) * w) and got.dtype == np.float32
+
+
+def test_torch_ops_library_registers_the_ops():
+    """libapgym_torch.so (csrc/apg_torch_ops.cpp) loads on a CPU-only host and registers
+    TORCH_LIBRARY(apgym) ops and env handle classes (no GPU call is made)."""
+    import torch
+
+    from ap_gym_amd import _native as N
+
+    ops = N.torch_ops()
+    assert ops is torch.ops.apgym
+    for name in ("lidar_reset", "lidar_step", "image_reset", "image_step"):
+        assert callable(getattr(ops, name)), name
+    assert torch.classes.apgym.LidarEnv is not None and torch.classes.apgym.ImageEnv is not None
+    with pytest.raises(RuntimeError, match="12 ints"):
+        torch.classes.apgym.LidarEnv([1], [0.0], [], [])
