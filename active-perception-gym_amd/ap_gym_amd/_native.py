@@ -251,3 +251,19 @@ def stream_handle(device) -> int:
     import torch
 
     return torch.cuda.current_stream(device).cuda_stream
+
+
+_hip = None
+
+
+def event_record(event, stream) -> None:
+    """hipEventRecord(event, stream) through the HIP runtime torch already loaded (bench timing of
+    the step op on its own stream; torch.cuda.Event would only see torch's current stream object)."""
+    global _hip
+    if _hip is None:
+        h = ctypes.CDLL("libamdhip64.so")
+        h.hipEventRecord.argtypes = [_vp, _vp]
+        h.hipEventRecord.restype = ctypes.c_int
+        _hip = h
+    if _hip.hipEventRecord(event, stream) != 0:
+        raise ApgError("hipEventRecord failed")

@@ -333,8 +333,9 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         return out
 
     def set_kernel_timing_events(self, begin=None, end=None):
-        """Record hipEvent_t handles `begin`/`end` around the fused step kernel of the next step
-        (bench.py's live per-launch timing).  None disables."""
+        """Record hipEvent_t handles `begin`/`end` around the step op (torch.ops.apgym.lidar_step: the
+        fused step kernel, one launch) of the next step, on its stream (bench.py's live per-launch
+        timing).  None disables."""
         self._kernel_events = None if begin is None else (begin, end)
 
     def _raise_error_bits(self, bits: int):
@@ -431,11 +432,12 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             p_t = torch.as_tensor(p, dtype=torch.float32, device=self.device).contiguous()
         if self._kernel_events is None:
             self._ops.lidar_step(self._h, a_t, p_t)
-        else:
+        else:  # bench timing: hipEvents on the op's stream around the step launch(es)
             ev_b, ev_e = self._kernel_events
-            N.check(N.lib().apg_lidar_step_profiled(ctypes.byref(self._cfg), ctypes.byref(self._state), N.ptr(a_t),
-                                                    N.ptr(p_t), ctypes.byref(self._out), self._stream(), ev_b, ev_e),
-                    "apg_lidar_step")
+            s = self._stream()
+            N.event_record(ev_b, s)
+            self._ops.lidar_step(self._h, a_t, p_t)
+            N.event_record(ev_e, s)
         self._track_render(p_t)
         if numpy_mode:
             return self._numpy_step_result()

@@ -4,12 +4,14 @@
 //                   DatasetIterator stream, rooms/maze generation, start-cell draw
 //                   (lidar_localization2d.py:293-315, :547-557; dataset_iterator.py:26-32)
 //                   The same wave then rewrites the float32 map obs of each env that reset (:299).
-//   k_lidar_step    64 envs per 256-thread workgroup.  Phase 1 (lane = env): autoreset bookkeeping,
-//                   NaN check, reward, move + collide + slide, termination, target, normalized MSE,
-//                   TimeLimit (lidar_localization2d.py:317-389, time_limit.py:118-139,
-//                   active_perception_env.py:101-121).  Phase 2 (lane = beam): each env's 32-column
-//                   occupancy window is staged in LDS, then every beam runs the exact scan
-//                   (:238-277, :496-536).
+//   k_lidar_step    256 envs per 1024-thread workgroup (one per CU; 64 / 256 threads for small
+//                   batches).  Phase R: the NEXT_STEP autoresets (map generation, start cell).
+//                   Phase 1 (env-major, 16 envs per wave): autoreset bookkeeping, NaN check, reward,
+//                   move + collide + slide, termination, target, normalized MSE, TimeLimit
+//                   (lidar_localization2d.py:317-389, time_limit.py:118-139,
+//                   active_perception_env.py:101-121).  Phase 2: each env's 32 x 32 occupancy window
+//                   is staged in LDS, every beam runs the exact scan (:238-277, :496-536): a bounding-
+//                   box pre-test, then the queued walks spread over the workgroup's waves.
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (see build.py).
 #include <hip/hip_runtime.h>
 
@@ -48,12 +50,6 @@ int check_launch(const char *what) {
 namespace {
 
 constexpr uint8_t F_AUTORESET = 1, F_JUST_RESET = 2, F_FIRST = 4;
-#ifndef APG_STEP_EPB
-#define APG_STEP_EPB 64
-#endif
-constexpr int EPB = APG_STEP_EPB;        // envs per step workgroup (lane = env in phases 1 and 2a)
-constexpr int STEP_THREADS = 4 * EPB;    // phase 2a: 4 beams at a time per env
-static_assert(EPB == 16 || EPB == 32 || EPB == 64, "EPB: power of two, at most one wave");
 constexpr int MAX_WIN_ROWS = 32;
 constexpr int WIN_STRIDE = MAX_WIN_ROWS + 1;  // LDS words per env window (+1: lanes = envs hit distinct banks)
 constexpr int MAX_STAGED_BEAMS = 64;          // lidar rows staged in LDS for coalesced stores
@@ -279,6 +275,14 @@ APG_DEV void log_episode_stats(const StepParams &P, const apg_lidar_outputs &O, 
 // ~2 cells (clamped move <= 1, slide <= 1), and every cell a scan of length <= R from the new
 // position p can touch lies within [floor(p) - R - 2, floor(p) + R + 1] (+1 column for the 2-bit
 // quad reads), i.e. within [floor(p0) - R - 5, floor(p0) + R + 5]: inside the window for R <= 10.
+// APG_STEP_STOP=k (tuning builds only, tools/phase_pmc.py): the kernel returns after phase mark k, so
+// PMC counts of the variants split the instruction mix by phase.  Outputs are then meaningless.
+#ifdef APG_STEP_STOP
+#define STEP_STOP(k) \
+  if (APG_STEP_STOP == (k)) return;
+#else
+#define STEP_STOP(k)
+#endif
 #ifdef APG_STEP_PROFILE  // tuning builds only (tools/step_phase_profile.py): per-workgroup phase timestamps
 __device__ unsigned long long g_step_prof[16384][8];
 #define STEP_MARK(k) \
@@ -289,99 +293,287 @@ __device__ unsigned long long g_step_prof[16384][8];
 #ifndef APG_STEP_MIN_WAVES
 #define APG_STEP_MIN_WAVES 4  // keep k_lidar_step at <= 128 VGPRs: 4 waves per SIMD
 #endif
+
+// Workgroup shape of a k_lidar_step instance: EPB envs, 4 threads per env (phase 2a: 4 beams at a
+// time per env), W waves.  Phases R and 1 are "env-major": env slot el runs on wave el % W, lane
+// el / W, i.e. every wave carries EPB / W = 16 envs, so the serial per-env chains (map generation,
+// the move scans) run on all W waves at once instead of on the first EPB / 64.
+template <int EPB>
+struct StepShape {
+  static constexpr int T = 4 * EPB, W = T / 64, LPW = EPB / W;
+  static_assert(EPB == 64 || EPB == 256, "EPB: 64 (256 threads) or 256 (1024 threads)");
+  static_assert(LPW == 16, "16 envs per wave in the env-major phases");
+};
+constexpr int PRIM_STRIDE = 33;  // LDS words per env of the rooms primitives: nw | nd << 8, 16 walls, 16 doors
+constexpr int MAX_MAP_ROWS = 128;
+
+APG_DEV int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+APG_DEV int wave_inclusive_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// position of the k-th set bit (k < popcount(m)) of m
+APG_DEV int select_bit(uint64_t m, int k) {
+  for (int i = 0; i < k; i++) m &= m - 1ULL;
+  return __ffsll((long long)m) - 1;
+}
+
+// Row y of a rooms map painted from its primitives (rooms_paint's result, one row at a time): border
+// | walls & ~doors.  Word k covers columns [64k, 64k + 64).
+APG_DEV uint64_t rooms_row_word(const uint32_t *pr, int m, int y, int k) {
+  const int nw = (int)(pr[0] & 255u), nd = (int)(pr[0] >> 8);
+  uint64_t v = (y == 0 || y == m - 1) ? span_mask(0, m, k) : (span_mask(0, 1, k) | span_mask(m - 1, 1, k));
+  for (int i = 0; i < nw; i++) {
+    const uint32_t wl = pr[1 + i];
+    const int fixed = (int)((wl >> 16) & 255u), st = (int)((wl >> 8) & 255u), len = (int)(wl & 255u);
+    if (wl >> 31) {
+      if (y >= st && y < st + len && (fixed >> 6) == k) v |= 1ULL << (fixed & 63);
+    } else if (fixed == y) {
+      v |= span_mask(st, len, k);
+    }
+  }
+  for (int i = 0; i < nd; i++) {
+    const uint32_t d = pr[17 + i];
+    const int r0 = (int)(d >> 24), c0 = (int)((d >> 16) & 255u), hh = (int)((d >> 8) & 255u), ww = (int)(d & 255u);
+    if (y >= r0 && y < r0 + hh) v &= ~span_mask(c0, ww, k);
+  }
+  return v;
+}
+
 // GEN / FUSED: FUSED instances start with phase R, the NEXT_STEP autoresets of the envs whose episode
 // ended at the previous step (map generation of kind GEN, start cell), so a step is one launch; the
-// unfused instance (reset(seed)'s observation pass, and autoresets of rooms maps too large for the LDS
-// budget, which k_lidar_reset does first) skips it.
-template <int GEN, bool FUSED>
-__global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step(StepParams P, Geo g, apg_lidar_state S,
-                                                             const float *__restrict__ act,
-                                                             const float *__restrict__ pred,
-                                                             apg_lidar_outputs O, BinomTable bt) {
+// unfused instance (reset(seed)'s observation pass after k_lidar_reset) skips it.
+template <int GEN, bool FUSED, int EPB>
+__global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(StepParams P, Geo g, apg_lidar_state S,
+                                                                 const float *__restrict__ act,
+                                                                 const float *__restrict__ pred,
+                                                                 apg_lidar_outputs O, BinomTable bt) {
+  using SS = StepShape<EPB>;
+  constexpr int T = SS::T, W = SS::W, LPW = SS::LPW;
   __shared__ float s_pos[EPB][2];
   __shared__ int s_x0[EPB], s_y0[EPB];
+  __shared__ uint16_t s_rlist[EPB];  // envs that reset this step (map obs pass)
+  __shared__ uint32_t s_start[EPB];  // rooms autoreset: start cell y << 8 | x, or ~0u (no free cell)
+  __shared__ int s_cnt[4];           // 0: reset-list length, 1: queued walks, 2: walk cursor
+  __shared__ float s_dirs[MAX_STAGED_BEAMS][2];  // beam_dirs, read inside the beam loops (LDS, not HBM latency)
   // dynamic LDS (step_lds_bytes): occupancy windows, then (beams <= MAX_STAGED_BEAMS) the lidar rows
-  // staged for coalesced stores and the phase-2b work list of (beam << 6) | env entries
+  // staged for coalesced stores and the phase-2b work list of (beam << 8) | env entries.  Phase R
+  // (rooms) uses the same bytes first for the primitives and each wave's map rows.
   extern __shared__ uint32_t s_dyn[];
   uint32_t *s_win = s_dyn;
   const int LS = P.beams + 1;  // odd row stride: lanes = envs hit distinct banks
   float *s_lid = reinterpret_cast<float *>(s_dyn + EPB * WIN_STRIDE);
   uint16_t *s_queue = reinterpret_cast<uint16_t *>(s_lid + EPB * LS);
-  __shared__ int s_qn;
-  __shared__ float s_dirs[MAX_STAGED_BEAMS][2];  // beam_dirs, read inside the beam loops (LDS, not HBM latency)
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int base = blockIdx.x * EPB;
   const size_t words = (size_t)P.h * P.wpr;
+  // env-major slot of this thread (phases R, 0, 1)
+  const bool env_thread = lane < LPW;
+  const int my_el = lane * W + wave, my_e = base + my_el;
+  const bool my_valid = env_thread && my_e < P.n;
   STEP_MARK(0)
 #ifdef APG_STEP_PROFILE
   const unsigned long long prof_clk0 = __builtin_amdgcn_s_memtime();
 #endif
 
-  // ---------------- phase R: NEXT_STEP autoresets (fused instances).  Envs are spread 16 per wave over
-  // the four waves (map generation is a serial divergent chain per env, latency-bound: more waves in
-  // flight, fewer lanes each).  Rooms maps are painted in LDS (aliasing the windows, which are staged
-  // later) and copied out with the map observation; maze maps go straight to the occupancy rows.
-  __shared__ unsigned long long s_reset;
-  if constexpr (FUSED) {
-    __shared__ unsigned long long s_pend;
-    if (tid < EPB) {
-      const int e = base + tid;
-      const bool pend = e < P.n && (S.flags[e] & F_AUTORESET);
-      const unsigned long long m = __ballot(pend);
-      if (tid == 0) s_pend = m;
+  if (tid == 0) {
+    s_cnt[0] = 0;
+    s_cnt[1] = 0;
+    s_cnt[2] = 0;
+  }
+  // Phases 0 and 1 run lane = env on the first EPB / 64 waves (thread tid owns env base + tid).  Its
+  // inputs are loaded here, before any barrier, so their latency overlaps phase R and the window loads
+  // (reloaded after phase R where resets happened).
+  const int oe = base + tid;
+  const bool own = tid < EPB && oe < P.n;
+  uint8_t pf_f = 0;
+  float pf_px = 0.0f, pf_py = 0.0f, pf_ax = 0.0f, pf_ay = 0.0f, pf_prx = 0.0f, pf_pry = 0.0f, pf_ix = 0.0f,
+        pf_iy = 0.0f;
+  int pf_el = 0;
+  if (own) {
+    pf_f = S.flags[oe];
+    pf_px = S.pos[2 * oe];
+    pf_py = S.pos[2 * oe + 1];
+    pf_ix = S.init_pos[2 * oe];
+    pf_iy = S.init_pos[2 * oe + 1];
+    pf_el = S.elapsed[oe];
+    if (act) {
+      pf_ax = act[2 * oe];
+      pf_ay = act[2 * oe + 1];
+      pf_prx = pred[2 * oe];
+      pf_pry = pred[2 * oe + 1];
     }
-    __syncthreads();
-    const unsigned long long pend = s_pend;
-    if (pend != 0ULL) {
-      uint64_t *s_maps = reinterpret_cast<uint64_t *>(s_dyn);  // rooms: [EPB][h * wpr]
-      const int lane = tid & 63, el = (tid >> 6) * (EPB / 4) + lane;
-      if (lane < EPB / 4 && ((pend >> el) & 1ULL)) {
-        const int e = base + el;
-        uint64_t *own = GEN == GEN_ROOMS ? s_maps + (size_t)el * words : S.occ + (size_t)e * words;
-        reset_one<GEN>(g, S, e, S.flags[e], false, 0, own, O.map_idx, O.err, bt);
-      }
-      __syncthreads();
-      if constexpr (GEN == GEN_ROOMS) {  // occupancy rows out, coalesced over the workgroup
-        for (int k = tid; k < EPB * (int)words; k += STEP_THREADS) {
-          const int el2 = k / (int)words;
-          if (((pend >> el2) & 1ULL) && base + el2 < P.n) S.occ[(size_t)base * words + k] = s_maps[k];
+  }
+  if constexpr (!FUSED) __syncthreads();
+
+  // ---------------- phase R: NEXT_STEP autoresets (fused instances), env-major.  The barrier of
+  // __syncthreads_or also publishes the counters above.
+  if constexpr (FUSED) {
+    const uint8_t f0 = my_valid ? S.flags[my_e] : 0;
+    const bool pend = my_valid && (f0 & F_AUTORESET);
+    if (__syncthreads_or(pend)) {
+      if constexpr (GEN == GEN_ROOMS) {
+        // R1: the env's streams, its next map index and the map's primitives (into LDS)
+        uint32_t *s_prims = s_dyn;
+        uint64_t *s_mrow = reinterpret_cast<uint64_t *>(s_dyn + ((EPB * PRIM_STRIDE + 1) & ~1));
+        Pcg64 rng, it;
+        uint64_t midx = 0;
+        if (pend) {
+          rng = *reinterpret_cast<const Pcg64 *>(&S.rng[my_e]);
+          it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[my_e]);
+          midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
+          Pcg64 map_rng = seed_pcg64(midx);  // FloorMapDatasetRooms.get_data_point: default_rng(idx)
+          RoomsPrims pr;
+          const int rc = rooms_primitives(map_rng, g.h, g.max_rooms, g.door_width, bt, pr);
+          if (rc != 0) atomicOr(O.err, APG_ERR_MAPGEN);
+          uint32_t *q = s_prims + my_el * PRIM_STRIDE;
+          q[0] = (uint32_t)pr.nw | ((uint32_t)pr.nd << 8);
+          for (int i = 0; i < pr.nw; i++) q[1 + i] = pr.wall[i];
+          for (int i = 0; i < pr.nd; i++) q[17 + i] = pr.door[i];
         }
         __syncthreads();
+        // R2: each wave paints the maps of its own envs one after the other, lane = row: occupancy rows
+        // out (coalesced), the f32 map obs from the wave's row copy in LDS, the free-cell count and the
+        // start cell (place_start: the pick-th free cell in row-major order, drawn by the env's lane)
+        uint64_t *mrow = s_mrow + (size_t)wave * MAX_MAP_ROWS * 2;
+        const int m = P.h, wpr = P.wpr;
+        for (int j = 0; j < LPW; j++) {
+          if (!__shfl((int)pend, j)) continue;  // wave-uniform
+          const int el = j * W + wave, e = base + el;
+          const uint32_t *pr = s_prims + el * PRIM_STRIDE;
+          uint64_t *dst = S.occ + (size_t)e * words;
+          int fr[2] = {0, 0};
+          uint64_t rw[2][2] = {{0ULL, 0ULL}, {0ULL, 0ULL}};
+#pragma unroll
+          for (int rr = 0; rr < 2; rr++) {
+            const int y = lane + 64 * rr;
+            if (y < m) {
+              int occ = 0;
+              for (int k = 0; k < wpr; k++) {
+                const uint64_t v = rooms_row_word(pr, m, y, k);
+                rw[rr][k] = v;
+                dst[y * wpr + k] = v;
+                mrow[y * 2 + k] = v;
+                occ += __popcll(v);
+              }
+              fr[rr] = P.w - occ;
+            }
+          }
+          const int nfree = wave_sum(fr[0] + fr[1]);
+          long long pick = -1;
+          if (lane == j && nfree > 0) pick = (long long)integers(rng, 0, nfree);
+          pick = __shfl(pick, j);
+          int off = 0;
+          if (lane == 0) s_start[el] = ~0u;
+#pragma unroll
+          for (int rr = 0; rr < 2; rr++) {
+            const int incl = wave_inclusive_scan(fr[rr], lane) + off;
+            const int excl = incl - fr[rr];
+            if (pick >= excl && pick < incl) {  // the pick-th free cell is in this lane's row
+              int k2 = (int)(pick - excl), x = -1;
+              for (int k = 0; k < wpr && x < 0; k++) {
+                const int lo = 64 * k;
+                const uint64_t valid = P.w - lo >= 64 ? ~0ULL : ((1ULL << (P.w - lo)) - 1ULL);
+                const uint64_t fm = ~rw[rr][k] & valid;
+                const int c = __popcll(fm);
+                if (k2 < c) x = lo + select_bit(fm, k2);
+                else k2 -= c;
+              }
+              s_start[el] = ((uint32_t)(lane + 64 * rr) << 8) | (uint32_t)x;
+            }
+            off = __shfl(incl, 63);
+          }
+          if (O.map_obs && (P.w & 3) == 0) {  // bool map / 255 (lidar_localization2d.py:299), float4 stores
+            const float wall = 1.0f / 255.0f;
+            typedef float f4 __attribute__((ext_vector_type(4)));
+            float *mo = O.map_obs + (size_t)e * m * P.w;
+            const int q4 = P.w >> 2;
+            for (int k4 = lane; k4 < m * q4; k4 += 64) {
+              const int y = k4 / q4, x = (k4 - y * q4) * 4;
+              const uint32_t bits = (uint32_t)(mrow[y * 2 + (x >> 6)] >> (x & 63));
+              f4 v;
+              v.x = (bits & 1u) ? wall : 0.0f;
+              v.y = (bits & 2u) ? wall : 0.0f;
+              v.z = (bits & 4u) ? wall : 0.0f;
+              v.w = (bits & 8u) ? wall : 0.0f;
+              __builtin_nontemporal_store(v, reinterpret_cast<f4 *>(mo) + k4);
+            }
+          } else if (O.map_obs) {
+            float *mo = O.map_obs + (size_t)e * m * P.w;
+            for (int k = lane; k < m * P.w; k += 64) {
+              const int y = k / P.w, x = k - y * P.w;
+              mo[k] = ((mrow[y * 2 + (x >> 6)] >> (x & 63)) & 1ULL) ? 1.0f / 255.0f : 0.0f;
+            }
+          }
+        }
+        // R3: the env's lane finishes its reset (lidar_localization2d.py:293-315 tail)
+        if (pend) {
+          const uint32_t sc = s_start[my_el];
+          float px = 0.5f, py = 0.5f;
+          if (sc == ~0u) {
+            atomicOr(O.err, APG_ERR_MAPGEN);
+          } else {
+            px = __fadd_rn((float)(sc & 255u), 0.5f);
+            py = __fadd_rn((float)(sc >> 8), 0.5f);
+          }
+          S.pos[2 * my_e] = px;
+          S.pos[2 * my_e + 1] = py;
+          S.init_pos[2 * my_e] = px;
+          S.init_pos[2 * my_e + 1] = py;
+          S.elapsed[my_e] = 0;
+          S.flags[my_e] = (uint8_t)((f0 & F_AUTORESET) | F_JUST_RESET | F_FIRST);
+          *reinterpret_cast<Pcg64 *>(&S.rng[my_e]) = rng;
+          *reinterpret_cast<Pcg64 *>(&S.it_rng[my_e]) = it;
+          S.map_idx[my_e] = midx;
+          if (O.map_idx) O.map_idx[my_e] = midx;
+        }
+      } else {
+        // maze maps are carved straight into the env's occupancy rows; static maps only draw a start cell
+        if (pend) reset_one<GEN>(g, S, my_e, f0, false, 0, S.occ + (size_t)my_e * words, O.map_idx, O.err, bt);
+      }
+      __syncthreads();
+      if (own && (pf_f & F_AUTORESET)) {  // this env was reset above
+        pf_f = S.flags[oe];
+        pf_px = S.pos[2 * oe];
+        pf_py = S.pos[2 * oe + 1];
+        pf_ix = S.init_pos[2 * oe];
+        pf_iy = S.init_pos[2 * oe + 1];
+        pf_el = S.elapsed[oe];
       }
     }
   }
 
   // ---------------- phase 0: window origins from the pre-move positions; which envs reset
   if (P.beams <= MAX_STAGED_BEAMS && tid < 2 * P.beams) s_dirs[tid >> 1][tid & 1] = S.beam_dirs[tid];
-  if (tid < EPB) {
-    const int e = base + tid;
-    bool rs = false;
-    if (e < P.n) {
-      s_x0[tid] = (int)floorf(S.pos[2 * e]) - 15;
-      s_y0[tid] = (int)floorf(S.pos[2 * e + 1]) - 15;
-      rs = (S.flags[e] & F_JUST_RESET) != 0;
-    }
-    const unsigned long long m = __ballot(rs);
-    if (tid == 0) {
-      s_reset = m;
-      s_qn = 0;
-    }
+  constexpr bool kMapObsHere = !(FUSED && GEN == GEN_ROOMS);  // fused rooms resets wrote their map obs in R2
+  if (own) {
+    s_x0[tid] = (int)floorf(pf_px) - 15;
+    s_y0[tid] = (int)floorf(pf_py) - 15;
+    if (kMapObsHere && (pf_f & F_JUST_RESET)) s_rlist[atomicAdd(&s_cnt[0], 1)] = (uint16_t)tid;
   }
   __syncthreads();
   // map obs of the envs that reset this step: bool map / 255 (lidar_localization2d.py:299), written by
-  // the whole workgroup with float4 stores (only in reset steps; the maps came from k_lidar_reset)
-  if (s_reset != 0ULL && O.map_obs && !P.is_static) {
+  // the whole workgroup with float4 stores
+  if (kMapObsHere && s_cnt[0] != 0 && O.map_obs && !P.is_static) {
     const float wall = 1.0f / 255.0f;
-    const int cells = P.h * P.w;
-    unsigned long long m = s_reset;
-    while (m) {
-      const int j = __ffsll((long long)m) - 1;
-      m &= m - 1ULL;
+    const int cells = P.h * P.w, nr = s_cnt[0];
+    for (int r = 0; r < nr; r++) {
+      const int j = s_rlist[r];
       const uint64_t *rows = S.occ + (size_t)(base + j) * words;
       float *dst = O.map_obs + (size_t)(base + j) * cells;
       if ((P.w & 3) == 0) {  // 4 cells of one row per float4: one row-word load, non-temporal stores
         const int q = P.w >> 2;
-        for (int k4 = tid; k4 < cells / 4; k4 += STEP_THREADS) {
+        for (int k4 = tid; k4 < cells / 4; k4 += T) {
           const int y = k4 / q, x = (k4 - y * q) * 4;
           const uint32_t b = (uint32_t)(rows[y * P.wpr + (x >> 6)] >> (x & 63));
           typedef float f4 __attribute__((ext_vector_type(4)));
@@ -393,36 +585,50 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
           __builtin_nontemporal_store(v, reinterpret_cast<f4 *>(dst) + k4);
         }
       } else {
-        for (int k = tid; k < cells; k += STEP_THREADS) {
+        for (int k = tid; k < cells; k += T) {
           const int y = k / P.w, x = k - y * P.w;
           dst[k] = ((rows[y * P.wpr + (x >> 6)] >> (x & 63)) & 1ULL) ? wall : 0.0f;
         }
       }
     }
   }
-  for (int r = tid; r < EPB * P.wrows; r += STEP_THREADS) {
-    const int el = r / P.wrows, row = r - el * P.wrows;
-    const int e = base + el;
-    uint32_t v = 0;
-    if (e < P.n) {
-      const int y = s_y0[el] + row;
-      if ((unsigned)y < (unsigned)P.h)
-        v = extract_window_row(S.occ + (P.is_static ? 0 : e * words) + (size_t)y * P.wpr, P.wpr, s_x0[el]);
+  {  // window rows: all of a thread's row loads issued before any LDS store
+    constexpr int WIN_ITERS = EPB * MAX_WIN_ROWS / T;
+    uint32_t v[WIN_ITERS];
+#pragma unroll
+    for (int k = 0; k < WIN_ITERS; k++) {
+      const int r = tid + k * T;
+      const int el = r / MAX_WIN_ROWS, row = r - el * MAX_WIN_ROWS;
+      v[k] = 0;
+      if (base + el < P.n) {
+        const int y = s_y0[el] + row;
+        if ((unsigned)y < (unsigned)P.h)
+          v[k] = extract_window_row(S.occ + (P.is_static ? 0 : (size_t)(base + el) * words) + (size_t)y * P.wpr, P.wpr,
+                                    s_x0[el]);
+      }
     }
-    s_win[el * WIN_STRIDE + row] = v;
+#pragma unroll
+    for (int k = 0; k < WIN_ITERS; k++) {
+      const int r = tid + k * T;
+      const int el = r / MAX_WIN_ROWS, row = r - el * MAX_WIN_ROWS;
+      s_win[el * WIN_STRIDE + row] = v[k];
+    }
   }
   __syncthreads();
   STEP_MARK(1)
+  STEP_STOP(1)
 
-  // ---------------- phase 1: one lane per env
+  // ---------------- phase 1: lane = env (the prefetched inputs)
   if (tid < EPB) {
-    const int e = base + tid;
+    const int e = oe;
+    const int el = tid;
     uint32_t errbits = 0;
-    if (e < P.n) {
-      const RowsWindow rw{&s_win[tid * WIN_STRIDE], s_x0[tid], s_y0[tid], P.wrows};
-      uint8_t f = S.flags[e];
+    if (own) {
+      const RowsWindow rw{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
+      uint8_t f = pf_f;
       const bool was_reset = f & F_JUST_RESET;
-      float pos0 = S.pos[2 * e], pos1 = S.pos[2 * e + 1];
+      float pos0 = pf_px, pos1 = pf_py;
+      float ipx = pf_ix, ipy = pf_iy;
       const float mapw = (float)P.w, maph = (float)P.h;
       if (was_reset) {  // NEXT_STEP autoreset: this env returned reset obs, reward 0
         O.reward[e] = 0.0;
@@ -437,8 +643,8 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
         if (P.sparse) O.weight[e] = 0.0;
         f &= (uint8_t)~(F_JUST_RESET | F_AUTORESET);
       } else {
-        float ax = act[2 * e], ay = act[2 * e + 1];
-        const float prx = pred[2 * e], pry = pred[2 * e + 1];
+        float ax = pf_ax, ay = pf_ay;
+        const float prx = pf_prx, pry = pf_pry;
         if (isnan(ax) || isnan(ay)) errbits |= APG_ERR_NAN_ACTION;
         if (isnan(prx) || isnan(pry)) errbits |= APG_ERR_NAN_PREDICTION;
         if (errbits) {  // the reference raises ValueError before touching this env's state
@@ -496,6 +702,8 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
           if (f & F_FIRST) {  // initial_pos aliases pos until np.clip rebinds it (:305, :371)
             S.init_pos[2 * e] = pos0;
             S.init_pos[2 * e + 1] = pos1;
+            ipx = pos0;
+            ipy = pos1;
             f &= (uint8_t)~F_FIRST;
           }
           bool term = pos0 < 0.0f || pos1 < 0.0f || pos0 >= mapw || pos1 >= maph;
@@ -503,17 +711,18 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
           pos1 = fminf(fmaxf(pos1, 0.0f), maph);
           const float tgx = __fsub_rn(__fmul_rn(f32_div(lpx, mapw), 2.0f), 1.0f);
           const float tgy = __fsub_rn(__fmul_rn(f32_div(lpy, maph), 2.0f), 1.0f);
-          const int el = S.elapsed[e] + 1;
-          S.elapsed[e] = el;
-          if (el >= P.step_limit) term = true;  // TimeLimit(issue_termination=True)
+          const int el2 = pf_el + 1;
+          pf_el = el2;
+          S.elapsed[e] = el2;
+          if (el2 >= P.step_limit) term = true;  // TimeLimit(issue_termination=True)
           const float ex = __fsub_rn(prx, tgx), ey = __fsub_rn(pry, tgy);
           const float mse = f32_div(__fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey)), 2.0f);
           const float loss = __fadd_rn(__fmul_rn(mse, P.loss_scale), P.loss_offset);
           if (P.log_stats) {
             float *hist = S.stats_hist + (size_t)e * 2 * P.step_limit;
-            hist[el - 1] = norm_f32(ex, ey);  // |target - prediction|: the signs do not matter
-            hist[P.step_limit + el - 1] = mse;
-            if (term) log_episode_stats(P, O, e, hist, el);
+            hist[el2 - 1] = norm_f32(ex, ey);  // |target - prediction|: the signs do not matter
+            hist[P.step_limit + el2 - 1] = mse;
+            if (term) log_episode_stats(P, O, e, hist, el2);
             else O.stats_len[e] = 0;
           }
           O.base_reward[e] = br;
@@ -537,17 +746,18 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
       S.flags[e] = f;
       if (O.reset_mask) O.reset_mask[e] = was_reset;
       // odometry (:263-270) and TimeLimit time_step (time_limit.py:113-116)
-      const float ox = __fsub_rn(pos0, S.init_pos[2 * e]), oy = __fsub_rn(pos1, S.init_pos[2 * e + 1]);
+      const float ox = __fsub_rn(pos0, ipx), oy = __fsub_rn(pos1, ipy);
       O.odometry[2 * e] = __fsub_rn(__fmul_rn(f32_div(__fadd_rn(ox, mapw), __fadd_rn(mapw, mapw)), 2.0f), 1.0f);
       O.odometry[2 * e + 1] = __fsub_rn(__fmul_rn(f32_div(__fadd_rn(oy, maph), __fadd_rn(maph, maph)), 2.0f), 1.0f);
-      O.time_step[e] = (float)(2.0 * (double)S.elapsed[e] / (double)P.step_limit - 1.0);
-      s_pos[tid][0] = pos0;
-      s_pos[tid][1] = pos1;
+      O.time_step[e] = (float)(2.0 * (double)pf_el / (double)P.step_limit - 1.0);
+      s_pos[el][0] = pos0;
+      s_pos[el][1] = pos1;
     }
     if (errbits) atomicOr(O.err, errbits);  // rare: NaN inputs only
   }
   __syncthreads();
   STEP_MARK(2)
+  STEP_STOP(2)
 
   // ---------------- phase 2a: lane = env, wave = beam index (all 64 lanes of a wave cast the same
   // beam direction).  Beams whose bounding box holds no occupied cell are SCAN_EMPTY and finish
@@ -556,7 +766,7 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
   const bool staged = P.beams <= MAX_STAGED_BEAMS;
   const float px = s_pos[el][0], py = s_pos[el][1];
   const RowsWindow rw{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
-  for (int beam = tid / EPB; beam < P.beams; beam += STEP_THREADS / EPB) {
+  for (int beam = tid / EPB; beam < P.beams; beam += T / EPB) {
     bool walk = false;
     if (e < P.n) {
       const float dx = staged ? s_dirs[beam][0] : S.beam_dirs[2 * beam];
@@ -573,40 +783,56 @@ __global__ __launch_bounds__(STEP_THREADS, APG_STEP_MIN_WAVES) void k_lidar_step
       }
     }
     if (staged) {
-      const int lane = tid & 63;
       const unsigned long long m = __ballot(walk);
       int qbase = 0;
-      if (lane == 0 && m) qbase = atomicAdd(&s_qn, __popcll(m));
+      if (lane == 0 && m) qbase = atomicAdd(&s_cnt[1], __popcll(m));
       qbase = __shfl(qbase, 0);
-      if (walk) s_queue[qbase + __popcll(m & ((1ULL << lane) - 1ULL))] = (uint16_t)((beam << 6) | el);
+      if (walk) s_queue[qbase + __popcll(m & ((1ULL << lane) - 1ULL))] = (uint16_t)((beam << 8) | el);
     }
   }
   if (staged) {
     __syncthreads();
     STEP_MARK(3)
-    // ---------------- phase 2b: the queued scans, densely over all lanes of the workgroup
-    const int nq = s_qn;
-    for (int i = tid; i < nq; i += STEP_THREADS) {
-      const int ent = s_queue[i], qe = ent & (EPB - 1), beam = ent >> 6;
-      const float qpx = s_pos[qe][0], qpy = s_pos[qe][1];
-      const RowsWindow qrw{&s_win[qe * WIN_STRIDE], s_x0[qe], s_y0[qe], P.wrows};
-      const float qx = __fadd_rn(qpx, s_dirs[beam][0]), qy = __fadd_rn(qpy, s_dirs[beam][1]);
-      const float d = lidar_scan_walk(qrw, qpx, qpy, qx, qy).dist;
-      s_lid[qe * LS + beam] = fminf(fmaxf(f32_div(d, P.range), -1.0f), 1.0f);
+  STEP_STOP(3)
+    // ---------------- phase 2b: the queued scans, densely over the workgroup's waves; each wave takes
+    // the next 64 entries from a shared cursor, so waves with short walks take more of them
+    const int nq = s_cnt[1];
+    for (;;) {
+      int start = 0;
+      if (lane == 0) start = atomicAdd(&s_cnt[2], 64);
+      start = __shfl(start, 0);
+      if (start >= nq) break;
+      const int i = start + lane;
+      if (i < nq) {
+        const int ent = s_queue[i], qe = ent & 255, beam = ent >> 8;
+        const float qpx = s_pos[qe][0], qpy = s_pos[qe][1];
+        const RowsWindow qrw{&s_win[qe * WIN_STRIDE], s_x0[qe], s_y0[qe], P.wrows};
+        const float qx = __fadd_rn(qpx, s_dirs[beam][0]), qy = __fadd_rn(qpy, s_dirs[beam][1]);
+        const float d = lidar_scan_walk(qrw, qpx, qpy, qx, qy).dist;
+        s_lid[qe * LS + beam] = fminf(fmaxf(f32_div(d, P.range), -1.0f), 1.0f);
+      }
     }
     __syncthreads();
     STEP_MARK(4)
+  STEP_STOP(4)
     const int nenv = P.n - base < EPB ? P.n - base : EPB;
-    for (int i = tid; i < nenv * P.beams; i += STEP_THREADS) {
-      const int l = i / P.beams, beam = i - l * P.beams;
-      O.lidar[(size_t)base * P.beams + i] = s_lid[l * LS + beam];
+    const int B = P.beams, dl = T / B, db = T - dl * B;  // (env, beam) of element i advanced without divisions
+    int l = tid / B, beam = tid - l * B;
+    for (int i = tid; i < nenv * B; i += T) {
+      O.lidar[(size_t)base * B + i] = s_lid[l * LS + beam];
+      l += dl;
+      beam += db;
+      if (beam >= B) {
+        beam -= B;
+        l++;
+      }
     }
   }
 #ifdef APG_STEP_PROFILE
   __syncthreads();
   STEP_MARK(5)
   if (threadIdx.x == 0 && blockIdx.x < 16384) {
-    g_step_prof[blockIdx.x][6] = s_qn;
+    g_step_prof[blockIdx.x][6] = s_cnt[1];
     g_step_prof[blockIdx.x][7] = __builtin_amdgcn_s_memtime() - prof_clk0;
   }
 #endif
@@ -801,21 +1027,69 @@ int launch_map_generate_any(const Geo &g, const uint64_t *idx, int n, uint64_t *
   return launch_map_generate<GEN_ROOMS>(g, idx, n, occ, stack, err, s);
 }
 
-size_t step_lds_bytes(int beams) {
-  size_t b = (size_t)EPB * WIN_STRIDE * sizeof(uint32_t);
-  if (beams <= MAX_STAGED_BEAMS) b += (size_t)EPB * (beams + 1) * sizeof(float) + (size_t)EPB * beams * sizeof(uint16_t);
+// Dynamic LDS of a k_lidar_step instance: windows + staged lidar rows + walk queue; fused rooms resets
+// use the same bytes first for the primitives and each wave's map rows.
+size_t step_lds_bytes(int epb, int beams) {
+  size_t b = (size_t)epb * WIN_STRIDE * sizeof(uint32_t);
+  if (beams <= MAX_STAGED_BEAMS) b += (size_t)epb * (beams + 1) * sizeof(float) + (size_t)epb * beams * sizeof(uint16_t);
   return b;
 }
+size_t rooms_reset_lds_bytes(int epb) {
+  return (size_t)((epb * PRIM_STRIDE + 1) & ~1) * sizeof(uint32_t) + (size_t)(4 * epb / 64) * MAX_MAP_ROWS * 2 * sizeof(uint64_t);
+}
 
-// Rooms maps of a fused step workgroup live in its dynamic LDS during phase R: keep that within the
-// budget of four resident workgroups per CU (the step kernel's occupancy); larger rooms maps take
-// the two-launch path (k_lidar_reset, then the unfused step kernel).
-constexpr size_t FUSED_ROOMS_LDS_MAX = 36 * 1024;
-size_t fused_rooms_lds(const Geo &g) { return (size_t)EPB * g.h * g.wpr * sizeof(uint64_t); }
 int step_gen(const Geo &g) {
   if (g.is_static) return GEN_NONE;
-  if (g.kind == APG_MAP_MAZE) return GEN_MAZE;
-  return fused_rooms_lds(g) <= FUSED_ROOMS_LDS_MAX ? GEN_ROOMS : -1;  // -1: not fusable
+  return g.kind == APG_MAP_MAZE ? GEN_MAZE : GEN_ROOMS;
+}
+
+int cu_count() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+// Envs per step workgroup: 256 (1024 threads, one workgroup per CU: the CU's walks are balanced over
+// its 16 waves) when that still gives every CU a workgroup, else 64 (256 threads).  APG_STEP_EPB=64|256
+// overrides (tuning).
+int step_epb(int n) {
+  static int forced = -1;
+  if (forced < 0) {
+    const char *s = getenv("APG_STEP_EPB");
+    forced = s ? atoi(s) : 0;
+  }
+  if (forced == 64 || forced == 256) return forced;
+  return (int64_t)n >= (int64_t)256 * cu_count() ? 256 : 64;
+}
+
+template <int GEN, bool FUSED, int EPB>
+int launch_step_t(const StepParams &P, const Geo &g, const apg_lidar_state *st, const float *act, const float *pred,
+                  const apg_lidar_outputs *out, hipStream_t s, const BinomTable &bt) {
+  size_t lds = step_lds_bytes(EPB, P.beams);
+  if (FUSED && GEN == GEN_ROOMS && rooms_reset_lds_bytes(EPB) > lds) lds = rooms_reset_lds_bytes(EPB);
+  auto kern = k_lidar_step<GEN, FUSED, EPB>;
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return fail(APG_E_LAUNCH, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+  hipLaunchKernelGGL(kern, dim3(grid_for(P.n, EPB)), dim3(4 * EPB), lds, s, P, g, *st, act, pred, *out, bt);
+  return check_launch("k_lidar_step");
+}
+
+template <int EPB>
+int launch_step_epb(const StepParams &P, const Geo &g, const apg_lidar_state *st, const float *act, const float *pred,
+                    const apg_lidar_outputs *out, hipStream_t s, bool fused) {
+  const BinomTable bt = make_binom_table();
+  if (!fused) return launch_step_t<GEN_NONE, false, EPB>(P, g, st, act, pred, out, s, bt);
+  switch (step_gen(g)) {
+    case GEN_ROOMS: return launch_step_t<GEN_ROOMS, true, EPB>(P, g, st, act, pred, out, s, bt);
+    case GEN_MAZE: return launch_step_t<GEN_MAZE, true, EPB>(P, g, st, act, pred, out, s, bt);
+    default: return launch_step_t<GEN_NONE, true, EPB>(P, g, st, act, pred, out, s, bt);
+  }
 }
 
 int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *act,
@@ -836,25 +1110,8 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   P.loss_scale = cfg->loss_scale;
   P.loss_offset = cfg->loss_offset;
   const Geo g = make_geo(cfg);
-  const dim3 grid(grid_for(P.n, EPB)), block(STEP_THREADS);
-  const BinomTable bt = make_binom_table();
-  size_t lds = step_lds_bytes(P.beams);
-  const int gen = fused ? step_gen(g) : -1;
-  if (gen == GEN_ROOMS && fused_rooms_lds(g) > lds) lds = fused_rooms_lds(g);
-  switch (gen) {
-    case GEN_NONE:
-      hipLaunchKernelGGL((k_lidar_step<GEN_NONE, true>), grid, block, lds, s, P, g, *st, act, pred, *out, bt);
-      break;
-    case GEN_ROOMS:
-      hipLaunchKernelGGL((k_lidar_step<GEN_ROOMS, true>), grid, block, lds, s, P, g, *st, act, pred, *out, bt);
-      break;
-    case GEN_MAZE:
-      hipLaunchKernelGGL((k_lidar_step<GEN_MAZE, true>), grid, block, lds, s, P, g, *st, act, pred, *out, bt);
-      break;
-    default:
-      hipLaunchKernelGGL((k_lidar_step<GEN_NONE, false>), grid, block, lds, s, P, g, *st, act, pred, *out, bt);
-  }
-  return check_launch("k_lidar_step");
+  if (step_epb(P.n) == 256) return launch_step_epb<256>(P, g, st, act, pred, out, s, fused);
+  return launch_step_epb<64>(P, g, st, act, pred, out, s, fused);
 }
 
 }  // namespace
@@ -909,13 +1166,9 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
     return fail(APG_E_INVALID, "log_stats needs stats_hist, stats and stats_len buffers");
   if (cfg->sparse && !out->weight) return fail(APG_E_INVALID, "sparse needs the weight buffer");
   hipStream_t s = (hipStream_t)stream;
-  Geo g = make_geo(cfg);
-  // one launch per step: the fused step kernel performs the NEXT_STEP autoresets itself; only rooms
-  // maps beyond its LDS budget are generated by k_lidar_reset first
-  const bool fused = step_gen(g) >= 0;
-  if (!fused && (rc = launch_reset(g, st, 0, 0, 0, out, s))) return rc;
+  // one launch per step: the fused step kernel performs the NEXT_STEP autoresets itself
   if (ev_begin && hipEventRecord((hipEvent_t)ev_begin, s) != hipSuccess) return fail(APG_E_LAUNCH, "hipEventRecord");
-  rc = launch_step_kernel(cfg, st, action, prediction, out, s, fused);
+  rc = launch_step_kernel(cfg, st, action, prediction, out, s, true);
   if (rc == APG_OK && ev_end && hipEventRecord((hipEvent_t)ev_end, s) != hipSuccess)
     return fail(APG_E_LAUNCH, "hipEventRecord");
   return rc;

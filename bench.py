@@ -69,27 +69,44 @@ class HipEvents:
             self.hip.hipEventDestroy(e)
 
 
-def cpu_baseline(beams: int, size: int, num_envs: int, steps: int) -> dict:
-    """The C oracle (a 1-thread port of the reference path) on this host: reset + `steps` steps."""
+def cpu_threads() -> int:
+    """Host cores this process may use (the GPU box's share: OMP_NUM_THREADS, CPU affinity)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp)) if omp and omp.isdigit() else n)
+
+
+def cpu_baseline(beams: int, size: int, kind: str, num_envs: int | None, steps: int, threads: int | None) -> dict:
+    """The C oracle (a port of the reference path, bit-identical outputs) on this host: reset, then
+    `steps` steps (one autoreset burst in 101), once with `threads` OpenMP threads over the sub-envs
+    (the reported row) and once with 1 thread (`single_thread`, the reference's own single-core shape)."""
     import numpy as np
 
     from oracle import oracle
 
     oracle.build()
-    env = oracle.OracleLidarVectorEnv(num_envs, "rooms", size, False, 0, beams)
-    env.reset(0)
-    rng = np.random.default_rng(1)
-    acts = rng.uniform(-1, 1, (steps, num_envs, 2)).astype(np.float32)
-    preds = rng.uniform(-1, 1, (steps, num_envs, 2)).astype(np.float32)
-    t0 = time.perf_counter()
-    for t in range(steps):
-        env.step(acts[t], preds[t])
-    dt = time.perf_counter() - t0
-    env.close()
-    return {"value": num_envs * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/liboracle.so C port, 1 thread, LIDARLocRooms {size}x{size} {beams} beams, "
-                      f"{num_envs} envs x {steps} steps after reset(seed=0) incl. one autoreset burst "
-                      f"({dt:.1f} s)"}
+    threads = threads or cpu_threads()
+    per_env = 1.0 if kind == "rooms" else 4.0  # 127x127 mazes with 64 beams cost about 4x per env-step
+    rows = {}
+    for th, envs in ((threads, num_envs or int(8192 * min(threads, 16) / per_env)), (1, int(8192 / per_env))):
+        env = oracle.OracleLidarVectorEnv(envs, kind, size, False, 0, beams)
+        env.reset(0)
+        rng = np.random.default_rng(1)
+        acts = rng.uniform(-1, 1, (steps, envs, 2)).astype(np.float32)
+        preds = rng.uniform(-1, 1, (steps, envs, 2)).astype(np.float32)
+        t0 = time.perf_counter()
+        for t in range(steps):
+            env.step(acts[t], preds[t], threads=th)
+        dt = time.perf_counter() - t0
+        env.close()
+        rows[th] = {"value": envs * steps / dt, "unit": "env-steps/s", "cores": th, "kind": "port",
+                    "sample": f"oracle/liboracle.so C port ({'OpenMP, ' + str(th) + ' threads' if th > 1 else '1 thread'}), "
+                              f"LIDARLoc {kind} {size}x{size} {beams} beams, {envs} envs x {steps} steps after "
+                              f"reset(seed=0) incl. one autoreset burst ({dt:.1f} s)"}
+    out = dict(rows[threads])
+    if threads > 1:
+        out["single_thread"] = rows[1]
+    return out
 
 
 # image workloads (BASELINE.json configs 4, 5): per-GPU envs, pool, classes, sensor, kind
@@ -186,6 +203,13 @@ def run_image(args, world, rank, dev):
     if rank == 0:
         bpe = image_bytes_per_env_step(w["kind"], w["classes"], w["sensor"], c)
         achieved = bpe * n_local / (step_ms * 1e-3) / 1e9
+        tj, tpath = pmc_table(args.workload, "image",
+                              {"num_envs": n_local, "sensor": list(w["sensor"]), "classes": w["classes"]})
+        traffic = issue = None
+        if tj is not None:
+            traffic = tj["hbm_bytes_per_launch"]["step"]
+            issue = issue_fractions(tj["per_launch"]["step"], step_ms)
+            issue["source"] = tpath
         out = {
             "metric": "env-steps/sec (vectorized step) at 1/2/4/8 MI355X + achieved HBM GB/s",
             "value": n_total * args.steps / elapsed, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
@@ -197,9 +221,9 @@ def run_image(args, world, rank, dev):
                        "sensor": list(w["sensor"]), "classes": w["classes"], "step_limit": 16,
                        "reset_ms": reset_ms, "parallelism": f"env-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tpath,
                          "kernel": "image step (all kernels, HIP events around env.step)", "kernel_ms": step_ms,
-                         "bytes_per_launch": bpe * n_local},
+                         "bytes_per_launch": bpe * n_local, "issue": issue},
         }
         if world == 1 and not args.no_cpu_baseline:
             pool, labels = ds.device_pool()
@@ -211,27 +235,233 @@ def run_image(args, world, rank, dev):
         dist.destroy_process_group()
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=505)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", default="lidar", choices=["lidar", *IMAGE_WORKLOADS])
-    ap.add_argument("--num-envs", type=int, default=None, help="envs per GPU (default: the workload's)")
-    ap.add_argument("--pool-len", type=int, default=None, help="image pool size (image workloads)")
-    ap.add_argument("--beams", type=int, default=32)
-    ap.add_argument("--map-size", type=int, default=64)
-    ap.add_argument("--gather", action="store_true", help="all-gather step outputs across ranks (RCCL)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-envs", type=int, default=8192)
-    ap.add_argument("--cpu-steps", type=int, default=101)
-    args = ap.parse_args()
+# LIDAR workloads (BASELINE.json configs 2 and 3)
+LIDAR_WORKLOADS = {
+    "lidar": dict(env_id="LIDARLocRooms-v0", kind="rooms", map=64, beams=32, envs=65536, scaling="weak",
+                  note="BASELINE config 2: 65536 envs per GPU"),
+    "maze127": dict(env_id="LIDARLocMaze-v0", kind="maze", map=127, beams=64, envs_total=262144, scaling="strong",
+                    note="BASELINE config 3: 262144 envs in total, split over the GPUs (127x127: the reference "
+                         "maze needs odd sizes, SURVEY §0.6)"),
+}
+KERNEL_SOURCES = {
+    "lidar": ["apg_lidar.hip", "apg_scan.hpp", "apg_device.hpp", "apg_maps.hpp", "apg_rng.hpp", "apg_pairwise.hpp"],
+    "image": ["apg_image.hip", "apg_device.hpp", "apg_rng.hpp", "apg_pairwise.hpp"],
+}
+HIP_CLOCK_HZ = 2.4e9  # MI355X max engine clock (MI355X_MICROARCH.md); capacity of the issue fractions
+SIMDS, CUS = 1024, 256
+
+
+def kernel_source_sha(family: str) -> str:
+    """Hash of the kernel sources a PMC table was collected with (a stale table is never used)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES[family]:
+        with open(os.path.join(ROOT, "active-perception-gym_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_table(workload: str, family: str, shape: dict):
+    """The newest profiles/r*/pmc_<workload>.json collected (tools/collect_pmc.sh) from these kernel
+    sources at this run shape, or (None, None)."""
+    import glob
+
+    sha = kernel_source_sha(family)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{workload}.json")), reverse=True):
+        with open(path) as f:
+            tj = json.load(f)
+        if tj.get("source_sha") == sha and tj.get("shape") == shape:
+            return tj, os.path.relpath(path, ROOT)
+    return None, None
+
+
+def issue_fractions(per_launch: dict, kernel_ms: float) -> dict:
+    """Issue-rate roofline beside the HBM one: VALU wave-instructions x 2 cycles (wave64 on SIMD-32)
+    over the SIMDs' cycles, and LDS array cycles (2 per ds_read_b32 wave-instruction + the counted
+    bank-conflict cycles) over the CUs' LDS cycles, at the 2.4 GHz max clock."""
+    cyc = kernel_ms * 1e-3 * HIP_CLOCK_HZ
+    valu = per_launch.get("SQ_INSTS_VALU")
+    lds = per_launch.get("SQ_INSTS_LDS")
+    conf = per_launch.get("SQ_LDS_BANK_CONFLICT")
+    out = {"valu_insts": valu, "lds_insts": lds, "lds_bank_conflict_cycles": conf,
+           "valu_frac": 2.0 * valu / (SIMDS * cyc) if valu is not None else None,
+           "lds_frac": (2.0 * lds + (conf or 0.0)) / (CUS * cyc) if lds is not None else None}
+    if per_launch.get("SQ_WAIT_ANY") and per_launch.get("SQ_WAVE_CYCLES"):
+        out["wait_any_frac"] = per_launch["SQ_WAIT_ANY"] / per_launch["SQ_WAVE_CYCLES"]
+    if per_launch.get("SQ_THREAD_CYCLES_VALU") and per_launch.get("SQ_ACTIVE_INST_VALU"):
+        out["valu_lane_util"] = per_launch["SQ_THREAD_CYCLES_VALU"] / (64.0 * per_launch["SQ_ACTIVE_INST_VALU"])
+    return out
+
+
+def run_lidar(args, world, rank, dev):
+    import statistics
 
     import torch
     import torch.distributed as dist
 
     import ap_gym_amd as apg
     from ap_gym_amd.sharding import ShardedVectorEnv
+
+    w = LIDAR_WORKLOADS[args.workload]
+    beams = args.beams or w["beams"]
+    msize = args.map_size or w["map"]
+    if args.num_envs:
+        n_local = args.num_envs
+    elif "envs_total" in w:
+        n_local = w["envs_total"] // world
+    else:
+        n_local = w["envs"]
+    n_total = n_local * world
+    ds = (apg.FloorMapDatasetRooms(msize, msize) if w["kind"] == "rooms" else apg.FloorMapDatasetMaze(msize, msize))
+
+    def make_local(num_envs, env_offset):
+        return apg.make_vec(w["env_id"], num_envs=num_envs, lidar_beam_count=beams, dataset=ds, device=dev,
+                            array_backend="torch", env_offset=env_offset)
+
+    senv = ShardedVectorEnv(make_local, n_total, rank, world, beams, gather=args.gather and world > 1)
+    env = senv.env
+    ring = 128  # distinct synthetic action/prediction batches, cycled
+    g = torch.Generator(device=dev).manual_seed(1 + rank)
+    acts = torch.rand((ring, n_local, 2), generator=g, device=dev) * 2 - 1
+    preds = torch.rand((ring, n_local, 2), generator=g, device=dev) * 2 - 1
+    steps_done = 0
+
+    def step(ev=None):
+        nonlocal steps_done
+        if ev is not None:
+            env.set_kernel_timing_events(*ev)
+        k = steps_done % ring
+        senv.step({"action": acts[k], "prediction": preds[k]})
+        steps_done += 1
+
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    senv.reset(seed=0)
+    torch.cuda.synchronize(dev)
+    reset_ms = (time.perf_counter() - t0) * 1e3
+    for _ in range(args.warmup):
+        step()
+    ev = HipEvents(args.steps + EPISODE_PERIOD)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    first_timed = steps_done + 1
+    for t in range(args.steps):
+        step(ev.pair(t))
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    env.set_kernel_timing_events(None)
+    env.check_errors()
+    per_step = [ev.elapsed_ms(i) for i in range(args.steps)]
+    kernel_ms = sum(per_step) / args.steps
+    median_ms = statistics.median(per_step)
+    # reset steps (1-based step index t with t % 101 == 0: synchronized episodes) in the timed window
+    reset_steps = sum(1 for t in range(first_timed, first_timed + args.steps) if t % EPISODE_PERIOD == 0)
+
+    # one whole episode after the timed region (untimed for `value`): 100 steps + the autoreset step
+    episode = None
+    if not args.no_episode:
+        while steps_done % EPISODE_PERIOD:
+            step()
+        torch.cuda.synchronize(dev)
+        te = time.perf_counter()
+        for t in range(EPISODE_PERIOD):
+            step(ev.pair(args.steps + t))
+        torch.cuda.synchronize(dev)
+        ep_s = time.perf_counter() - te
+        env.set_kernel_timing_events(None)
+        env.check_errors()
+        ep = [ev.elapsed_ms(args.steps + t) for t in range(EPISODE_PERIOD)]
+        episode = [ep_s, ep[-1], statistics.median(ep[:-1]), sum(ep) / len(ep)]
+    ev.close()
+
+    if world > 1:
+        tt = torch.tensor([elapsed, kernel_ms, median_ms, reset_ms] + (episode or [0.0] * 4), dtype=torch.float64,
+                          device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        vals = [float(x) for x in tt]
+        elapsed, kernel_ms, median_ms, reset_ms = vals[:4]
+        episode = vals[4:] if episode else None
+
+    if rank == 0:
+        value = n_total * args.steps / elapsed
+        step_b = BYTES_PER_ENV_STEP(beams) * n_local
+        # a reset step also writes each env's map obs (f32) and its bit-packed occupancy rows
+        reset_b = step_b + (MAP_OBS_BYTES(msize) + msize * ((msize + 63) // 64) * 8) * n_local
+        bytes_per_launch = (step_b * (args.steps - reset_steps) + reset_b * reset_steps) / args.steps
+        achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+        shape = {"num_envs": n_local, "beams": beams, "map": msize}
+        tj, tpath = pmc_table(args.workload, "lidar", shape)
+        traffic = issue = None
+        if tj is not None:
+            hb = tj["hbm_bytes_per_launch"]
+            traffic = (hb["step"] * (args.steps - reset_steps) + hb["reset_step"] * reset_steps) / args.steps
+            issue = issue_fractions(tj["per_launch"]["step"], median_ms)
+            issue["source"] = tpath
+        out = {
+            "metric": "env-steps/sec (vectorized step) at 1/2/4/8 MI355X + achieved HBM GB/s",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": w["scaling"],
+            "vs_baseline": None,
+            "dtype": "f32 (f64 exact geometry predicates)",
+            "data": "synthetic (uniform(-1,1) actions/predictions generated on device; maps generated on device)",
+            "config": {"workload": w["env_id"], "num_envs_per_gpu": n_local, "num_envs_total": n_total,
+                       "beams": beams, "map": f"{msize}x{msize} {w['kind']}", "max_episode_steps": 100,
+                       "reset_ms": reset_ms, "note": w["note"],
+                       "parallelism": f"env-shard x{world}" + (" + all-gather" if args.gather and world > 1 else "")},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_lidar_step", "kernel_ms": kernel_ms, "median_kernel_ms": median_ms,
+                         "bytes_per_launch": bytes_per_launch, "reset_steps_timed": reset_steps,
+                         "traffic_source": tpath, "issue": issue},
+        }
+        if episode:
+            ep_s, reset_step_ms, ep_median, ep_mean = episode
+            out["episode"] = {
+                "steps": EPISODE_PERIOD, "env_steps_per_s": n_total * EPISODE_PERIOD / ep_s,
+                "ms_per_step": ep_s * 1e3 / EPISODE_PERIOD, "reset_step_kernel_ms": reset_step_ms,
+                "median_kernel_ms": ep_median, "mean_kernel_ms": ep_mean,
+                "note": "one synchronized episode after the timed steps: 100 steps + the NEXT_STEP autoreset step "
+                        "(map generation of every env + map obs), wall clock"}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(beams, msize, w["kind"], args.cpu_envs, args.cpu_steps,
+                                               args.cpu_threads)
+        print(json.dumps(out), flush=True)
+    senv.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=505)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workload", default="lidar", choices=[*LIDAR_WORKLOADS, *IMAGE_WORKLOADS])
+    ap.add_argument("--num-envs", type=int, default=None, help="envs per GPU (default: the workload's)")
+    ap.add_argument("--pool-len", type=int, default=None, help="image pool size (image workloads)")
+    ap.add_argument("--beams", type=int, default=None)
+    ap.add_argument("--map-size", type=int, default=None)
+    ap.add_argument("--gather", action="store_true", help="all-gather step outputs across ranks (RCCL)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-episode", action="store_true", help="skip the one-episode measurement after the timed steps")
+    ap.add_argument("--cpu-envs", type=int, default=None)
+    ap.add_argument("--cpu-steps", type=int, default=101)
+    ap.add_argument("--cpu-threads", type=int, default=None, help="OpenMP threads of the multi-thread CPU row")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -243,95 +473,9 @@ def main():
     dev = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    if args.workload != "lidar":
+    if args.workload in IMAGE_WORKLOADS:
         return run_image(args, world, rank, dev)
-
-    n_local = args.num_envs or 65536
-    n_total = n_local * world
-
-    def make_local(num_envs, env_offset):
-        return apg.make_vec("LIDARLocRooms-v0", num_envs=num_envs, lidar_beam_count=args.beams,
-                            dataset=apg.FloorMapDatasetRooms(args.map_size, args.map_size), device=dev,
-                            array_backend="torch", env_offset=env_offset)
-
-    senv = ShardedVectorEnv(make_local, n_total, rank, world, args.beams, gather=args.gather and world > 1)
-    env = senv.env
-    ring = 128  # distinct synthetic action/prediction batches, cycled
-    g = torch.Generator(device=dev).manual_seed(1 + rank)
-    acts = torch.rand((ring, n_local, 2), generator=g, device=dev) * 2 - 1
-    preds = torch.rand((ring, n_local, 2), generator=g, device=dev) * 2 - 1
-
-    senv.reset(seed=0)
-    for t in range(args.warmup):
-        senv.step({"action": acts[t % ring], "prediction": preds[t % ring]})
-    ev = HipEvents(args.steps)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for t in range(args.steps):
-        b, e = ev.pair(t)
-        env.set_kernel_timing_events(b, e)
-        k = (args.warmup + t) % ring
-        senv.step({"action": acts[k], "prediction": preds[k]})
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    env.set_kernel_timing_events(None)
-    env.check_errors()
-    kernel_ms = sum(ev.elapsed_ms(i) for i in range(args.steps)) / args.steps
-    ev.close()
-
-    if world > 1:
-        tt = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(tt[0]), float(tt[1])
-
-    if rank == 0:
-        value = n_total * args.steps / elapsed
-        # algorithmic bytes of the timed k_lidar_step launches: the per-env-step bytes every step, plus
-        # the map observation on the autoreset steps (all envs reset together: synchronized episodes)
-        reset_steps = sum(1 for t in range(args.steps) if (args.warmup + t + 1) % EPISODE_PERIOD == 0)
-        bytes_total = (BYTES_PER_ENV_STEP(args.beams) * n_local * args.steps
-                       + MAP_OBS_BYTES(args.map_size) * n_local * reset_steps)
-        bytes_per_launch = bytes_total / args.steps
-        achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-        traffic = None
-        tpath = os.path.join(ROOT, "profiles", "traffic_lidar_step.json")
-        if os.path.exists(tpath):
-            with open(tpath) as f:
-                tj = json.load(f)
-            if tj.get("num_envs") == n_local and tj.get("beams") == args.beams:
-                traffic = tj.get("hbm_bytes_per_launch")
-        out = {
-            "metric": "env-steps/sec (vectorized step) at 1/2/4/8 MI355X + achieved HBM GB/s",
-            "value": value,
-            "unit": "env-steps/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed * 1e3 / args.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32 (f64 exact geometry predicates)",
-            "data": "synthetic (uniform(-1,1) actions/predictions generated on device; maps generated on device)",
-            "config": {"workload": "LIDARLocRooms-v0", "num_envs_per_gpu": n_local, "num_envs_total": n_total,
-                       "beams": args.beams, "map": f"{args.map_size}x{args.map_size} rooms",
-                       "max_episode_steps": 100, "parallelism": f"env-shard x{world}" + (" + all-gather" if args.gather
-                                                                                         and world > 1 else "")},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_lidar_step", "kernel_ms": kernel_ms,
-                         "bytes_per_launch": bytes_per_launch, "reset_steps_timed": reset_steps},
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.beams, args.map_size, args.cpu_envs, args.cpu_steps)
-        print(json.dumps(out), flush=True)
-    senv.close()
-    if world > 1:
-        dist.destroy_process_group()
+    return run_lidar(args, world, rank, dev)
 
 
 if __name__ == "__main__":

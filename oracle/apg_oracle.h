@@ -69,6 +69,10 @@ int orc_lidar_step(orc_lidar_env *e, const float *action, const float *predictio
                    float *odometry, float *time_step, float *map_obs, double *reward,
                    uint8_t *terminated, uint8_t *truncated, float *base_reward, float *target,
                    float *loss, uint8_t *info_mask, uint64_t *map_idx);
+int orc_lidar_step_mt(orc_lidar_env *e, int threads, const float *action, const float *prediction,
+                      float *lidar, float *odometry, float *time_step, float *map_obs, double *reward,
+                      uint8_t *terminated, uint8_t *truncated, float *base_reward, float *target, float *loss,
+                      uint8_t *info_mask, uint64_t *map_idx);
 void orc_lidar_get_state(const orc_lidar_env *e, float *pos, float *init_pos, int32_t *elapsed,
                          uint8_t *autoreset);
 

@@ -463,12 +463,14 @@ void orc_lidar_reset(orc_lidar_env *e, uint64_t seed, float *lidar, float *odome
   }
 }
 
-int orc_lidar_step(orc_lidar_env *e, const float *action, const float *prediction, float *lidar,
-                   float *odometry, float *time_step, float *map_obs, double *reward,
-                   uint8_t *terminated, uint8_t *truncated, float *base_reward, float *target,
-                   float *loss, uint8_t *info_mask, uint64_t *map_idx) {
+/* One sub-env's SyncVectorEnv step (NEXT_STEP autoreset, TimeLimit, LIDARLocalization2DEnv.step);
+   sub-envs touch only their own state and output rows.  Returns the NaN error bits. */
+static int step_one(orc_lidar_env *e, int i, const float *action, const float *prediction, float *lidar,
+                    float *odometry, float *time_step, float *map_obs, double *reward, uint8_t *terminated,
+                    uint8_t *truncated, float *base_reward, float *target, float *loss, uint8_t *info_mask,
+                    uint64_t *map_idx) {
   int err = 0;
-  for (int i = 0; i < e->n; i++) {
+  {
     if (e->autoreset[i]) {
       env_reset_one(e, i);
       write_obs(e, i, lidar, odometry, time_step, map_obs);
@@ -480,7 +482,7 @@ int orc_lidar_step(orc_lidar_env *e, const float *action, const float *predictio
       info_mask[i] = 0;
       if (map_idx) map_idx[i] = e->map_idx[i];
       e->autoreset[i] = 0;
-      continue;
+      return 0;
     }
     const uint8_t *m = env_map(e, i);
     float ax = action[2 * i], ay = action[2 * i + 1];
@@ -561,6 +563,31 @@ int orc_lidar_step(orc_lidar_env *e, const float *action, const float *predictio
     if (map_idx) map_idx[i] = e->map_idx[i];
     e->autoreset[i] = (uint8_t)term;
   }
+  return err;
+}
+
+int orc_lidar_step(orc_lidar_env *e, const float *action, const float *prediction, float *lidar,
+                   float *odometry, float *time_step, float *map_obs, double *reward,
+                   uint8_t *terminated, uint8_t *truncated, float *base_reward, float *target,
+                   float *loss, uint8_t *info_mask, uint64_t *map_idx) {
+  int err = 0;
+  for (int i = 0; i < e->n; i++)
+    err |= step_one(e, i, action, prediction, lidar, odometry, time_step, map_obs, reward, terminated, truncated,
+                    base_reward, target, loss, info_mask, map_idx);
+  return err;
+}
+
+/* The same step with the sub-envs spread over `threads` OpenMP threads (bench.py's multi-core CPU
+   baseline row); outputs are identical to orc_lidar_step's. */
+int orc_lidar_step_mt(orc_lidar_env *e, int threads, const float *action, const float *prediction, float *lidar,
+                      float *odometry, float *time_step, float *map_obs, double *reward, uint8_t *terminated,
+                      uint8_t *truncated, float *base_reward, float *target, float *loss, uint8_t *info_mask,
+                      uint64_t *map_idx) {
+  int err = 0;
+#pragma omp parallel for num_threads(threads) reduction(| : err) schedule(dynamic, 64)
+  for (int i = 0; i < e->n; i++)
+    err |= step_one(e, i, action, prediction, lidar, odometry, time_step, map_obs, reward, terminated, truncated,
+                    base_reward, target, loss, info_mask, map_idx);
   return err;
 }
 

@@ -43,6 +43,8 @@ def lib():
         L.orc_lidar_reset.argtypes = [vp, u64, vp, vp, vp, vp, vp]
         L.orc_lidar_step.restype = i32
         L.orc_lidar_step.argtypes = [vp] + [vp] * 14
+        L.orc_lidar_step_mt.restype = i32
+        L.orc_lidar_step_mt.argtypes = [vp, i32] + [vp] * 14
         L.orc_lidar_get_state.argtypes = [vp, vp, vp, vp, vp]
         _lib = L
     return _lib
@@ -120,13 +122,17 @@ class OracleLidarVectorEnv:
         lib().orc_lidar_reset(self._e, seed, _p(self.lidar), _p(self.odometry), _p(self.time_step), _p(self.map),
                               _p(self.map_idx))
 
-    def step(self, action, prediction) -> int:
+    def step(self, action, prediction, threads: int = 1) -> int:
+        """threads > 1: the OpenMP variant (same outputs; bench.py's multi-core CPU baseline)."""
         a = np.ascontiguousarray(action, np.float32)
         p = np.ascontiguousarray(prediction, np.float32)
-        rc = lib().orc_lidar_step(self._e, _p(a), _p(p), _p(self.lidar), _p(self.odometry), _p(self.time_step),
-                                  _p(self.map), _p(self.reward), _p(self.terminated), _p(self.truncated),
-                                  _p(self.base_reward), _p(self.target), _p(self.loss), _p(self.info_mask),
-                                  _p(self.map_idx))
+        outs = (_p(self.lidar), _p(self.odometry), _p(self.time_step), _p(self.map), _p(self.reward),
+                _p(self.terminated), _p(self.truncated), _p(self.base_reward), _p(self.target), _p(self.loss),
+                _p(self.info_mask), _p(self.map_idx))
+        if threads > 1:
+            rc = lib().orc_lidar_step_mt(self._e, threads, _p(a), _p(p), *outs)
+        else:
+            rc = lib().orc_lidar_step(self._e, _p(a), _p(p), *outs)
         if self.sparse:
             # SparsifyWrapper.step per sub-env (sparsify_wrapper.py:137-151): weight = 1.0 if terminated
             # else 0.0 (SyncVectorEnv merges the floats into float64); reward = base_reward - loss * weight

@@ -36,11 +36,14 @@ for rep in range(3):
     a = torch.rand((n, 2), device="cuda", generator=g) * 2 - 1
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
-    env.step({"action": a, "prediction": a})
+    # through the ctypes C ABI of $APG_LIBRARY (the torch ops link the default library)
+    N.check(N.lib().apg_lidar_step(ctypes.byref(env._cfg), ctypes.byref(env._state), N.ptr(a), N.ptr(a),
+                                   ctypes.byref(env._out), N.stream_handle(a.device)), "apg_lidar_step")
     ev1.record()
     torch.cuda.synchronize()
     print(f"rep {rep}: events around env.step {ev0.elapsed_time(ev1) * 1000:.1f} us")
-    nwg = (n + 63) // 64
+    epb = int(os.environ.get("APG_STEP_EPB") or (256 if n >= 256 * 256 else 64))
+    nwg = (n + epb - 1) // epb
     buf = np.zeros((16384, 8), np.uint64)
     assert N.lib().apg_debug_step_profile(buf.ctypes.data, buf.nbytes) == 0
     b = buf[:nwg].astype(np.int64)
@@ -61,3 +64,7 @@ for rep in range(3):
     print(f"   shader clock / realtime x 100 MHz: {mhz:.0f} MHz")
     q = b[:, 6]
     print(f"   queued walks per WG: mean {q.mean():.0f} p90 {np.percentile(q, 90):.0f} max {q.max()}")
+    end = us(b[:, 5] - t0)
+    print(f"   WG end percentiles p10/p25/p50/p75/p90/p99/max: " +
+          "/".join(f"{np.percentile(end, p):.1f}" for p in (10, 25, 50, 75, 90, 99)) + f"/{end.max():.1f}")
+    print(f"   corr(queued walks, WG end) = {np.corrcoef(q, end)[0, 1]:.2f}")
