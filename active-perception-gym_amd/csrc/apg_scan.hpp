@@ -137,6 +137,12 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
   };
   const int ntot = nxl + nyl;
   int xi = 0, yi = 0;
+  // Every crossing's closure quad lies in rows cy and cy + sd (sd = sign(sy), -1 when sy == 0: the
+  // collinear-horizontal quads are rows ipy - 1 = cy - 1 and cy).  They are kept in registers and only
+  // shift when a y-crossing moves the walk to the next row; the row after them is read one crossing
+  // ahead, so the loop never waits on a just-issued LDS read.
+  const int sd = sy > 0 ? 1 : -1;
+  uint32_t r_c = rows.row(cy), r_o = rows.row(cy + sd), r_p = rows.row(cy + 2 * sd);
   while (xi + yi < ntot) {
     const int a = ax + sx * xi, b = by + sy * yi;
     const bool hx = xi < nxl, hy = yi < nyl;
@@ -149,8 +155,8 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
     const int j0 = takey ? b - 1 : (colh ? ipy - 1 : cy);
     const bool di = takex || colv, dj = takey || colh;
     const int sh = i0 - rows.x0;
-    const uint32_t r0 = rows.row(j0);
-    const uint32_t r1 = rows.row(dj ? j0 + 1 : j0);
+    const uint32_t r0 = takey ? (sy > 0 ? r_c : r_o) : (colh ? r_o : r_c);  // rows.row(j0)
+    const uint32_t r1 = (takey && sy > 0) ? r_o : r_c;                      // rows.row(j0 + dj)
     const unsigned q0 = (r0 >> sh) & 3u, q1 = (r1 >> sh) & 3u, m = di ? 3u : 1u;
     const bool onb = ((q0 | q1) & m) != 0u && ((q0 & q1 & m) != m);
     const int ncx = cx + (takex ? sx : 0), ncy = cy + (takey ? sy : 0);
@@ -192,6 +198,10 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
     xi += takex ? 1 : 0;
     yi += takey ? 1 : 0;
     cur_in = in_after;
+    const uint32_t r_next = rows.row(ncy + 2 * sd);  // unconditional: consumed a crossing later at the earliest
+    r_c = takey ? r_o : r_c;
+    r_o = takey ? r_p : r_o;
+    r_p = takey ? r_next : r_p;
   }
   // q: always a node
   const unsigned qst = quad_status(rows, qxi ? iqx - 1 : iqx, qxi ? 1 : 0, qyi ? iqy - 1 : iqy, qyi ? 1 : 0);
