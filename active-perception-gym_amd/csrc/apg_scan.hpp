@@ -103,8 +103,11 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
   const int ivdi = colv ? 1 : 0, ivdj = colh ? 1 : 0;  // interval cells [cx - ivdi, cx] x [cy - ivdj, cy]
 
   // node descriptors: type 0 = p, 1 = lattice (a, b), 2 = x-crossing on edge (a, b)-(a, b+1),
-  // 3 = y-crossing on edge (a, b)-(a+1, b), 4 = q
-  int pv_t = 0, pv_a = 0, pv_b = 0;
+  // 3 = y-crossing on edge (a, b)-(a+1, b), 4 = q; packed t | (a + 1024) << 3 | (b + 1024) << 17
+  auto pack_node = [](int t, int a, int b) -> uint32_t {
+    return (uint32_t)t | ((uint32_t)(a + 1024) << 3) | ((uint32_t)(b + 1024) << 17);
+  };
+  uint32_t pv = pack_node(0, 0, 0);
   bool pv_onb = quad_status(rows, pxi ? ipx - 1 : ipx, pxi ? 1 : 0, pyi ? ipy - 1 : ipy, pyi ? 1 : 0) == 1u;
   bool pv_left_in = false;
   bool cur_in = quad_status(rows, cx - ivdi, ivdi, cy - ivdj, ivdj) & 1u;
@@ -112,11 +115,12 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
   // the only ones the LineString/Point branches need); later ones (Multi* only) are rare and
   // folded into running f32 minima on the spot.
   int n_lines = 0, n_points = 0;
-  int l0_t = 0, l0_a = 0, l0_b = 0, p0_t = 0, p0_a = 0, p0_b = 0;
+  uint32_t l0 = pv, p0 = pv;
   float later_line = __builtin_inff(), later_point = __builtin_inff();
   float ll_x = 0.0f, ll_y = 0.0f, lp_x = 0.0f, lp_y = 0.0f;  // kContact: f32 nodes of those minima
 
-  auto node_coord = [&](int t, int a, int b, double &x, double &y) {
+  auto node_coord = [&](uint32_t node, double &x, double &y) {
+    const int t = (int)(node & 7u), a = (int)((node >> 3) & 16383u) - 1024, b = (int)(node >> 17) - 1024;
     if (t == 0) {
       x = px;
       y = py;
@@ -135,42 +139,14 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
   auto dist_f32 = [&](double x, double y) -> float {
     return norm_f32(__fsub_rn((float)x, fpx), __fsub_rn((float)y, fpy));
   };
-  const int ntot = nxl + nyl;
-  int xi = 0, yi = 0;
-  // Every crossing's closure quad lies in rows cy and cy + sd (sd = sign(sy), -1 when sy == 0: the
-  // collinear-horizontal quads are rows ipy - 1 = cy - 1 and cy).  They are kept in registers and only
-  // shift when a y-crossing moves the walk to the next row; the row after them is read one crossing
-  // ahead, so the loop never waits on a just-issued LDS read.
-  const int sd = sy > 0 ? 1 : -1;
-  uint32_t r_c = rows.row(cy), r_o = rows.row(cy + sd), r_p = rows.row(cy + 2 * sd);
-  while (xi + yi < ntot) {
-    const int a = ax + sx * xi, b = by + sy * yi;
-    const bool hx = xi < nxl, hy = yi < nyl;
-    // c < 0: x-crossing first, c > 0: y-crossing first, 0: both (lattice point)
-    const int o = orient_lattice(fpx, fpy, fqx, fqy, a, b);
-    const int c = (hx && hy) ? -o * sx * sy : (hx ? -1 : 1);
-    const bool takex = c <= 0, takey = c >= 0;
-    // closure quad of the crossing: cells [i0, i0+di] x [j0, j0+dj]
-    const int i0 = takex ? a - 1 : (colv ? ipx - 1 : cx);
-    const int j0 = takey ? b - 1 : (colh ? ipy - 1 : cy);
-    const bool di = takex || colv, dj = takey || colh;
-    const int sh = i0 - rows.x0;
-    const uint32_t r0 = takey ? (sy > 0 ? r_c : r_o) : (colh ? r_o : r_c);  // rows.row(j0)
-    const uint32_t r1 = (takey && sy > 0) ? r_o : r_c;                      // rows.row(j0 + dj)
-    const unsigned q0 = (r0 >> sh) & 3u, q1 = (r1 >> sh) & 3u, m = di ? 3u : 1u;
-    const bool onb = ((q0 | q1) & m) != 0u && ((q0 & q1 & m) != m);
-    const int ncx = cx + (takex ? sx : 0), ncy = cy + (takey ? sy : 0);
-    // status of the next open interval from the same quad: cell (ncx, ncy) (+ its collinear twin)
-    const unsigned u = (unsigned)(ncx - i0), v = (unsigned)(ncy - j0);
-    const unsigned rowv = v ? q1 : q0;
-    const bool in_after = colv ? (rowv & 3u) != 0u : (colh ? (((q0 | q1) >> u) & 1u) != 0u : ((rowv >> u) & 1u) != 0u);
-    // node bookkeeping, predicated (close the piece [previous node, this node])
+  // close the piece [previous node, this crossing] (is_line / is_point) and record the crossing as the
+  // previous node when it is on the boundary (onb)
+  auto close_piece = [&](bool onb, uint32_t node) {
     const bool is_line = onb && cur_in;
     const bool is_point = onb && !cur_in && pv_onb && !pv_left_in;
-    const bool first_line = is_line && n_lines == 0, first_point = is_point && n_points == 0;
     if ((is_line && n_lines > 0) || (is_point && n_points > 0)) {  // Multi* only: rare
       double x, y;
-      node_coord(pv_t, pv_a, pv_b, x, y);
+      node_coord(pv, x, y);
       const float d = dist_f32(x, y);
       if constexpr (kContact) {  // np.argmin: the first of equal minima
         if (is_line && d < later_line) ll_x = (float)x, ll_y = (float)y;
@@ -179,29 +155,99 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
       if (is_line) later_line = fminf(later_line, d);
       else later_point = fminf(later_point, d);
     }
-    l0_t = first_line ? pv_t : l0_t;
-    l0_a = first_line ? pv_a : l0_a;
-    l0_b = first_line ? pv_b : l0_b;
-    p0_t = first_point ? pv_t : p0_t;
-    p0_a = first_point ? pv_a : p0_a;
-    p0_b = first_point ? pv_b : p0_b;
+    l0 = (is_line && n_lines == 0) ? pv : l0;
+    p0 = (is_point && n_points == 0) ? pv : p0;
     n_lines += is_line ? 1 : 0;
     n_points += is_point ? 1 : 0;
     pv_left_in = onb ? cur_in : pv_left_in;
-    const bool lattice = (takex && takey) || (takex && colh) || (takey && colv);
-    pv_t = onb ? (lattice ? 1 : (takex ? 2 : 3)) : pv_t;
-    pv_a = onb ? (takex ? a : (colv ? ipx : cx)) : pv_a;
-    pv_b = onb ? (takey ? b : (colh ? ipy : cy)) : pv_b;
+    pv = onb ? node : pv;
     pv_onb = pv_onb || onb;
-    cx = ncx;
-    cy = ncy;
-    xi += takex ? 1 : 0;
-    yi += takey ? 1 : 0;
-    cur_in = in_after;
-    const uint32_t r_next = rows.row(ncy + 2 * sd);  // unconditional: consumed a crossing later at the earliest
-    r_c = takey ? r_o : r_c;
-    r_o = takey ? r_p : r_o;
-    r_p = takey ? r_next : r_p;
+  };
+  // Every crossing's closure quad lies in rows cy and cy + sd (sd = sign(sy), -1 when sy == 0: the
+  // collinear-horizontal quads are rows ipy - 1 = cy - 1 and cy).  They are kept in registers and only
+  // shift when a y-crossing moves the walk to the next row; the row after them is read one crossing
+  // ahead, so the loop never waits on a just-issued LDS read.
+  const int sd = sy > 0 ? 1 : -1;
+  uint32_t r_c = rows.row(cy), r_o = rows.row(cy + sd), r_p = rows.row(cy + 2 * sd);
+  if (!colv && !colh) {
+    // generic segment (not along a grid line): quads are [a-1, a] x cy (x-crossing), cx x [b-1, b]
+    // (y-crossing) or the 2 x 2 block at lattice point (a, b); the crossing order is the orientation
+    // of (a, b) against p -> q, folded with sign(sx * sy) into one f32 filter
+    const float sxy = (float)(sx * sy);
+    const unsigned ux = sx > 0 ? 1u : 0u, vy = sy > 0 ? 1u : 0u;  // next cell's offset in the quad
+    int a = ax, b = by, rx = nxl, ry = nyl;
+    while (rx + ry > 0) {
+      const bool hx = rx > 0, hy = ry > 0;
+      const float fa = (float)a, fb = (float)b;
+      const float dl = __fmul_rn(__fsub_rn(fpx, fa), __fsub_rn(fqy, fb));
+      const float dr = __fmul_rn(__fsub_rn(fpy, fb), __fsub_rn(fqx, fa));
+      const float dsx = __fmul_rn(__fsub_rn(dl, dr), sxy);  // orientation * sx * sy (exact sign flip)
+      const float bound = 1.7881398e-7f * __fadd_rn(fabsf(dl), fabsf(dr));
+      int c = dsx > bound ? -1 : (-dsx > bound ? 1 : 0);  // c < 0: x-crossing first, > 0: y first, 0: both
+      if (hx && hy && c == 0) c = -orient(fpx, fpy, fqx, fqy, (double)a, (double)b) * sx * sy;  // near-tie
+      c = (hx && hy) ? c : (hx ? -1 : 1);
+      const bool takex = c <= 0, takey = c >= 0;
+      const int i0 = takex ? a - 1 : cx;
+      const int sh = i0 - rows.x0;
+      const uint32_t r0 = (takey && sy < 0) ? r_o : r_c;  // rows.row(j0), j0 = takey ? b - 1 : cy
+      const uint32_t r1 = (takey && sy > 0) ? r_o : r_c;  // rows.row(j0 + dj)
+      const unsigned q0 = (r0 >> sh) & 3u, q1 = (r1 >> sh) & 3u, m = takex ? 3u : 1u;
+      const bool onb = ((q0 | q1) & m) != 0u && ((q0 & q1 & m) != m);
+      // status of the next open interval: cell (ncx, ncy) at offset (u, v) in the quad
+      const unsigned u = takex ? ux : 0u, v = takey ? vy : 0u;
+      const bool in_after = (((v ? q1 : q0) >> u) & 1u) != 0u;
+      close_piece(onb, pack_node((takex && takey) ? 1 : (takex ? 2 : 3), takex ? a : cx, takey ? b : cy));
+      cx += takex ? sx : 0;
+      cy += takey ? sy : 0;
+      a += takex ? sx : 0;
+      b += takey ? sy : 0;
+      rx -= takex ? 1 : 0;
+      ry -= takey ? 1 : 0;
+      cur_in = in_after;
+      const uint32_t r_next = rows.row(cy + 2 * sd);  // unconditional: consumed a crossing later at the earliest
+      r_c = takey ? r_o : r_c;
+      r_o = takey ? r_p : r_o;
+      r_p = takey ? r_next : r_p;
+    }
+  } else {
+    // along a grid line (colv / colh): every crossing is a lattice point, intervals touch two cells
+    const int ntot = nxl + nyl;
+    int xi = 0, yi = 0;
+    while (xi + yi < ntot) {
+      const int a = ax + sx * xi, b = by + sy * yi;
+      const bool hx = xi < nxl, hy = yi < nyl;
+      // c < 0: x-crossing first, c > 0: y-crossing first, 0: both (lattice point)
+      const int o = orient_lattice(fpx, fpy, fqx, fqy, a, b);
+      const int c = (hx && hy) ? -o * sx * sy : (hx ? -1 : 1);
+      const bool takex = c <= 0, takey = c >= 0;
+      // closure quad of the crossing: cells [i0, i0+di] x [j0, j0+dj]
+      const int i0 = takex ? a - 1 : (colv ? ipx - 1 : cx);
+      const int j0 = takey ? b - 1 : (colh ? ipy - 1 : cy);
+      const bool di = takex || colv;
+      const int sh = i0 - rows.x0;
+      const uint32_t r0 = takey ? (sy > 0 ? r_c : r_o) : (colh ? r_o : r_c);  // rows.row(j0)
+      const uint32_t r1 = (takey && sy > 0) ? r_o : r_c;                      // rows.row(j0 + dj)
+      const unsigned q0 = (r0 >> sh) & 3u, q1 = (r1 >> sh) & 3u, m = di ? 3u : 1u;
+      const bool onb = ((q0 | q1) & m) != 0u && ((q0 & q1 & m) != m);
+      const int ncx = cx + (takex ? sx : 0), ncy = cy + (takey ? sy : 0);
+      // status of the next open interval from the same quad: cell (ncx, ncy) (+ its collinear twin)
+      const unsigned u = (unsigned)(ncx - i0), v = (unsigned)(ncy - j0);
+      const unsigned rowv = v ? q1 : q0;
+      const bool in_after =
+          colv ? (rowv & 3u) != 0u : (colh ? (((q0 | q1) >> u) & 1u) != 0u : ((rowv >> u) & 1u) != 0u);
+      const bool lattice = (takex && takey) || (takex && colh) || (takey && colv);
+      close_piece(onb, pack_node(lattice ? 1 : (takex ? 2 : 3), takex ? a : (colv ? ipx : cx),
+                                 takey ? b : (colh ? ipy : cy)));
+      cx = ncx;
+      cy = ncy;
+      xi += takex ? 1 : 0;
+      yi += takey ? 1 : 0;
+      cur_in = in_after;
+      const uint32_t r_next = rows.row(ncy + 2 * sd);
+      r_c = takey ? r_o : r_c;
+      r_o = takey ? r_p : r_o;
+      r_p = takey ? r_next : r_p;
+    }
   }
   // q: always a node
   const unsigned qst = quad_status(rows, qxi ? iqx - 1 : iqx, qxi ? 1 : 0, qyi ? iqy - 1 : iqy, qyi ? 1 : 0);
@@ -209,7 +255,7 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
     const bool is_line = cur_in, is_point = !cur_in && pv_onb && !pv_left_in;
     if ((is_line && n_lines > 0) || (is_point && n_points > 0)) {
       double x, y;
-      node_coord(pv_t, pv_a, pv_b, x, y);
+      node_coord(pv, x, y);
       const float d = dist_f32(x, y);
       if constexpr (kContact) {
         if (is_line && d < later_line) ll_x = (float)x, ll_y = (float)y;
@@ -218,22 +264,16 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
       if (is_line) later_line = fminf(later_line, d);
       else later_point = fminf(later_point, d);
     }
-    const bool first_line = is_line && n_lines == 0, first_point = is_point && n_points == 0;
-    l0_t = first_line ? pv_t : l0_t;
-    l0_a = first_line ? pv_a : l0_a;
-    l0_b = first_line ? pv_b : l0_b;
-    p0_t = first_point ? pv_t : p0_t;
-    p0_a = first_point ? pv_a : p0_a;
-    p0_b = first_point ? pv_b : p0_b;
+    l0 = (is_line && n_lines == 0) ? pv : l0;
+    p0 = (is_point && n_points == 0) ? pv : p0;
     n_lines += is_line ? 1 : 0;
     n_points += is_point ? 1 : 0;
     pv_left_in = cur_in;
   }
-  pv_t = 4;
   pv_onb = qst == 1u;
   if (pv_onb && !pv_left_in) {
     if (n_points == 0) {
-      p0_t = 4;
+      p0 = pack_node(4, 0, 0);
     } else {
       const float d = dist_f32(qx, qy);
       if constexpr (kContact) {
@@ -252,7 +292,7 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
     o.kind = SCAN_COLLECTION;  // mixed points and lines: the reference's `else` branch (no hit)
   } else if (n_lines > 0) {
     double x, y;
-    node_coord(l0_t, l0_a, l0_b, x, y);
+    node_coord(l0, x, y);
     if (n_lines == 1) {
       o.kind = SCAN_LINE;
       const double dx = __dsub_rn(x, px), dy = __dsub_rn(y, py);
@@ -275,7 +315,7 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
     if constexpr (kContact) *contact = ScanContact{fpx, fpy, true};
   } else if (n_points > 1) {
     double x, y;
-    node_coord(p0_t, p0_a, p0_b, x, y);
+    node_coord(p0, x, y);
     o.kind = SCAN_MULTIPOINT;
     const float d0 = dist_f32(x, y);
     const float d = __fsub_rn(fminf(d0, later_point), 0.001f);
