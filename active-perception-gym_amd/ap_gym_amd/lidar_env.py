@@ -3,7 +3,7 @@
 Reference behaviour reproduced (ap_gym 0.5.0): `make_vec("LIDARLoc*-v0", N)` builds gymnasium's
 SyncVectorEnv over N copies of TimeLimit(100, issue_termination=True) ∘ LIDARLocalization2DEnv
 (ap_gym/envs/registration.py:319-356, :753-767).  This class is that whole composition as state in
-HBM plus three kernels per step (include/apgym_capi.h):
+HBM plus one fused kernel launch per step (include/apgym_capi.h):
 
   reset(seed=s)   sub-env i seeded with s+i (SyncVectorEnv.reset), map + start cell drawn on device
   step(action)    NEXT_STEP autoreset: envs done at the previous step return their reset obs with
@@ -167,8 +167,8 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             map_idx_out=t.zeros(n, dtype=t.int64, device=dev),
             reset_mask=t.zeros(n, dtype=t.bool, device=dev),
             err=t.zeros(1, dtype=t.int32, device=dev),
-            stats_hist=(t.zeros((n, 2, self.max_episode_steps), dtype=t.float32, device=dev) if self.log_stats
-                        else None),
+            stats_hist=(t.zeros((2, self.max_episode_steps, n), dtype=t.float32, device=dev) if self.log_stats
+                        else None),  # step-major: the per-step stores of the kernel are coalesced
             stats=t.zeros((4, n), dtype=t.float32, device=dev) if self.log_stats else None,
             stats_len=t.zeros(n, dtype=t.int32, device=dev) if self.log_stats else None,
             weight=t.zeros(n, dtype=t.float64, device=dev) if self.sparse else None,
@@ -472,8 +472,8 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             for j, name in enumerate(self.STAT_NAMES):
                 scalar[name] = T["stats"][j]
                 scalar["_" + name] = done
-            vector = {"euclidean_distance": T["stats_hist"][:, 0], "_euclidean_distance": done,
-                      "mse": T["stats_hist"][:, 1], "_mse": done, "length": T["stats_len"]}
+            vector = {"euclidean_distance": T["stats_hist"][0].T, "_euclidean_distance": done,
+                      "mse": T["stats_hist"][1].T, "_mse": done, "length": T["stats_len"]}  # [N, steps] views
             self._stats_view = {"stats": {"scalar": scalar, "_scalar": done, "vector": vector, "_vector": done},
                                 "_stats": done}
         if not self.copy:
@@ -494,7 +494,7 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             return
         st = T["stats"].cpu().numpy()
         idx = np.nonzero(done)[0]
-        hist = T["stats_hist"][torch_index(idx, self.device)].cpu().numpy()
+        hist = T["stats_hist"][:, :, torch_index(idx, self.device)].permute(2, 0, 1).cpu().numpy()  # [k, 2, steps]
         scalar: dict[str, Any] = {}
         for j, name in enumerate(self.STAT_NAMES):
             scalar[name] = np.where(done, st[j].astype(np.float64), 0.0)

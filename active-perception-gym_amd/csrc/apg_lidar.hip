@@ -258,14 +258,15 @@ struct StepParams {
 
 // ActiveRegressionLogWrapper (active_regression_env.py:131-159): per step |target - prediction| and
 // mean((target - prediction)^2) in float32; at the episode end avg = float(np.mean(list)) (numpy's
-// pairwise float32 mean) and final = the last value.  Stats for the steps of this episode live in
-// hist[0 .. len) (euclidean distance) and hist[step_limit ..) (mse).
+// pairwise float32 mean) and final = the last value.  The history is step-major,
+// stats_hist[metric][step][env] (metric 0 euclidean distance, 1 mse), so the per-step stores of a
+// wave are coalesced; the episode-end sums read an env's column with stride N.
 APG_DEV void log_episode_stats(const StepParams &P, const apg_lidar_outputs &O, int e, const float *hist, int len) {
   for (int m = 0; m < 2; m++) {
-    const float *h = hist + m * P.step_limit;
-    const float avg = f32_div(__fadd_rn(0.0f, pw_sum_ptr(h, len)), (float)len);
+    const float *h = hist + (size_t)m * P.step_limit * P.n + e;
+    const float avg = f32_div(__fadd_rn(0.0f, pw_sum_ptr(h, len, (size_t)P.n)), (float)len);
     O.stats[(size_t)m * P.n + e] = avg;
-    O.stats[(size_t)(2 + m) * P.n + e] = h[len - 1];
+    O.stats[(size_t)(2 + m) * P.n + e] = h[(size_t)(len - 1) * P.n];
   }
   O.stats_len[e] = len;
 }
@@ -301,7 +302,7 @@ __device__ unsigned long long g_step_prof[16384][8];
 template <int EPB>
 struct StepShape {
   static constexpr int T = 4 * EPB, W = T / 64, LPW = EPB / W;
-  static_assert(EPB == 64 || EPB == 256, "EPB: 64 (256 threads) or 256 (1024 threads)");
+  static_assert(EPB == 64 || EPB == 128 || EPB == 256, "EPB: 64, 128 or 256 (256 / 512 / 1024 threads)");
   static_assert(LPW == 16, "16 envs per wave in the env-major phases");
 };
 constexpr int PRIM_STRIDE = 33;  // LDS words per env of the rooms primitives: nw | nd << 8, 16 walls, 16 doors
@@ -672,11 +673,19 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           if (total > 0.0f) {
             dirx = f32_div(dirx, total);
             diry = f32_div(diry, total);
+#ifdef APG_X_NO_MOVE_SCAN  // tuning experiment only (wrong results)
+            const float d = total;
+#else
             const float d = lidar_scan(rw, pos0, pos1, tx, ty).dist;
+#endif
             pos0 = __fadd_rn(pos0, __fmul_rn(dirx, d));
             pos1 = __fadd_rn(pos1, __fmul_rn(diry, d));
             const float rem = __fsub_rn(total, d);
+#ifdef APG_X_NO_SLIDE  // tuning experiment only (wrong results)
+            if (false) {
+#else
             if (rem > 1e-5f) {  // slide along the wall (:345-364)
+#endif
               const float rvx = __fmul_rn(dirx, rem), rvy = __fmul_rn(diry, rem);
               const bool kx = rvx > 1e-5f, ky = rvy > 1e-5f;
               if (kx || ky) {
@@ -718,10 +727,14 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           const float ex = __fsub_rn(prx, tgx), ey = __fsub_rn(pry, tgy);
           const float mse = f32_div(__fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey)), 2.0f);
           const float loss = __fadd_rn(__fmul_rn(mse, P.loss_scale), P.loss_offset);
+#ifdef APG_X_NO_STATS  // tuning experiment only (wrong results)
+          if (false) {
+#else
           if (P.log_stats) {
-            float *hist = S.stats_hist + (size_t)e * 2 * P.step_limit;
-            hist[el2 - 1] = norm_f32(ex, ey);  // |target - prediction|: the signs do not matter
-            hist[P.step_limit + el2 - 1] = mse;
+#endif
+            float *hist = S.stats_hist;
+            hist[(size_t)(el2 - 1) * P.n + e] = norm_f32(ex, ey);  // |target - prediction|: the signs do not matter
+            hist[(size_t)(P.step_limit + el2 - 1) * P.n + e] = mse;
             if (term) log_episode_stats(P, O, e, hist, el2);
             else O.stats_len[e] = 0;
           }
@@ -774,7 +787,11 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       const float qx = __fadd_rn(px, dx), qy = __fadd_rn(py, dy);
       walk = scan_may_hit(rw, px, py, qx, qy);
       if (!walk || !staged) {
+#ifdef APG_X_NO_EMPTY_DIST  // tuning experiment only (wrong results)
+        const float d = walk ? lidar_scan_walk(rw, px, py, qx, qy).dist : P.range;
+#else
         const float d = walk ? lidar_scan_walk(rw, px, py, qx, qy).dist : scan_empty(px, py, qx, qy).dist;
+#endif
         const float v = fminf(fmaxf(f32_div(d, P.range), -1.0f), 1.0f);
         if (staged)
           s_lid[el * LS + beam] = v;
@@ -1063,7 +1080,7 @@ int step_epb(int n) {
     const char *s = getenv("APG_STEP_EPB");
     forced = s ? atoi(s) : 0;
   }
-  if (forced == 64 || forced == 256) return forced;
+  if (forced == 64 || forced == 128 || forced == 256) return forced;
   return (int64_t)n >= (int64_t)256 * cu_count() ? 256 : 64;
 }
 
@@ -1110,8 +1127,11 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   P.loss_scale = cfg->loss_scale;
   P.loss_offset = cfg->loss_offset;
   const Geo g = make_geo(cfg);
-  if (step_epb(P.n) == 256) return launch_step_epb<256>(P, g, st, act, pred, out, s, fused);
-  return launch_step_epb<64>(P, g, st, act, pred, out, s, fused);
+  switch (step_epb(P.n)) {
+    case 256: return launch_step_epb<256>(P, g, st, act, pred, out, s, fused);
+    case 128: return launch_step_epb<128>(P, g, st, act, pred, out, s, fused);
+    default: return launch_step_epb<64>(P, g, st, act, pred, out, s, fused);
+  }
 }
 
 }  // namespace

@@ -330,7 +330,7 @@ def run_lidar(args, world, rank, dev):
     def step(ev=None):
         nonlocal steps_done
         if ev is not None:
-            env.set_kernel_timing_events(*ev)
+            env.set_kernel_timing_events(*ev)  # (None, None): no events on this step
         k = steps_done % ring
         senv.step({"action": acts[k], "prediction": preds[k]})
         steps_done += 1
@@ -348,16 +348,17 @@ def run_lidar(args, world, rank, dev):
         dist.barrier()
     t0 = time.perf_counter()
     first_timed = steps_done + 1
+    timed = [t for t in range(args.steps) if t % args.event_every == 0]  # steps carrying kernel events
     for t in range(args.steps):
-        step(ev.pair(t))
+        step(ev.pair(t) if t % args.event_every == 0 else (None, None))
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     env.set_kernel_timing_events(None)
     env.check_errors()
-    per_step = [ev.elapsed_ms(i) for i in range(args.steps)]
-    kernel_ms = sum(per_step) / args.steps
+    per_step = [ev.elapsed_ms(i) for i in timed]
+    kernel_ms = sum(per_step) / len(per_step)
     median_ms = statistics.median(per_step)
     # reset steps (1-based step index t with t % 101 == 0: synchronized episodes) in the timed window
     reset_steps = sum(1 for t in range(first_timed, first_timed + args.steps) if t % EPISODE_PERIOD == 0)
@@ -392,14 +393,16 @@ def run_lidar(args, world, rank, dev):
         step_b = BYTES_PER_ENV_STEP(beams) * n_local
         # a reset step also writes each env's map obs (f32) and its bit-packed occupancy rows
         reset_b = step_b + (MAP_OBS_BYTES(msize) + msize * ((msize + 63) // 64) * 8) * n_local
-        bytes_per_launch = (step_b * (args.steps - reset_steps) + reset_b * reset_steps) / args.steps
+        # the launches the kernel time averages over: the timed steps that carried events
+        reset_ev = sum(1 for t in timed if (first_timed + t) % EPISODE_PERIOD == 0)
+        bytes_per_launch = (step_b * (len(timed) - reset_ev) + reset_b * reset_ev) / len(timed)
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
         shape = {"num_envs": n_local, "beams": beams, "map": msize}
         tj, tpath = pmc_table(args.workload, "lidar", shape)
         traffic = issue = None
         if tj is not None:
             hb = tj["hbm_bytes_per_launch"]
-            traffic = (hb["step"] * (args.steps - reset_steps) + hb["reset_step"] * reset_steps) / args.steps
+            traffic = (hb["step"] * (len(timed) - reset_ev) + hb["reset_step"] * reset_ev) / len(timed)
             issue = issue_fractions(tj["per_launch"]["step"], median_ms)
             issue["source"] = tpath
         out = {
@@ -423,6 +426,7 @@ def run_lidar(args, world, rank, dev):
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_lidar_step", "kernel_ms": kernel_ms, "median_kernel_ms": median_ms,
                          "bytes_per_launch": bytes_per_launch, "reset_steps_timed": reset_steps,
+                         "launches_timed": len(timed),
                          "traffic_source": tpath, "issue": issue},
         }
         if episode:
@@ -458,6 +462,9 @@ def main():
     ap.add_argument("--cpu-envs", type=int, default=None)
     ap.add_argument("--cpu-steps", type=int, default=101)
     ap.add_argument("--cpu-threads", type=int, default=None, help="OpenMP threads of the multi-thread CPU row")
+    ap.add_argument("--event-every", type=int, default=1,
+                    help="record the kernel's hipEvents on every N-th timed step (each event pair adds two "
+                         "stream packets between kernels)")
     args = ap.parse_args()
 
     import torch

@@ -119,7 +119,7 @@ typedef struct apg_lidar_state {
   uint16_t *stack;     /* [N][maze_frames] DFS frames, contiguous per env (dynamic maze only) */
   uint64_t *map_idx;   /* [N]   dataset index of the current map */
   const float *beam_dirs; /* [beams][2] lidar_directions (f32, computed by the host like the reference) */
-  float *stats_hist;   /* [N][2][step_limit] per-step euclidean_distance, mse of the episode (log_stats) */
+  float *stats_hist;   /* [2][step_limit][N] per-step euclidean_distance, mse of the episode (log_stats) */
 } apg_lidar_state;
 
 typedef struct apg_lidar_outputs {

@@ -13,8 +13,10 @@ print(sys.argv[2], '%.4g env-steps/s' % d['value'], 'wall %.1f us/step' % (d['ms
 " $1 $2; }
 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 200 --warmup 5 > gpurun_out/b_default.json 2> gpurun_out/b_default.err
 summ gpurun_out/b_default.json default
-APG_STEP_EPB=64 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 200 --warmup 5 > gpurun_out/b_epb64.json 2> gpurun_out/b_epb64.err
-summ gpurun_out/b_epb64.json epb64
+for e in ${EPBS:-64 128}; do
+  APG_STEP_EPB=$e timeout -k 10 200 python bench.py --no-cpu-baseline --steps 200 --warmup 5 > gpurun_out/b_epb$e.json 2> gpurun_out/b_epb$e.err
+  summ gpurun_out/b_epb$e.json epb$e
+done
 R=$PWD
 cd /tmp && export TMPDIR=/tmp
 rm -rf $R/gpurun_out/kt
