@@ -305,7 +305,6 @@ struct StepShape {
   static_assert(EPB == 64 || EPB == 128 || EPB == 256, "EPB: 64, 128 or 256 (256 / 512 / 1024 threads)");
   static_assert(LPW == 16, "16 envs per wave in the env-major phases");
 };
-constexpr int PRIM_STRIDE = 33;  // LDS words per env of the rooms primitives: nw | nd << 8, 16 walls, 16 doors
 constexpr int MAX_MAP_ROWS = 128;
 
 APG_DEV int wave_sum(int v) {
@@ -323,33 +322,57 @@ APG_DEV int wave_inclusive_scan(int v, int lane) {
   return v;
 }
 
-// position of the k-th set bit (k < popcount(m)) of m
+// position of the k-th set bit (k < popcount(m)) of m: binary search on popcounts
 APG_DEV int select_bit(uint64_t m, int k) {
-  for (int i = 0; i < k; i++) m &= m - 1ULL;
-  return __ffsll((long long)m) - 1;
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const int c = __popcll(m & ((1ULL << w) - 1ULL));
+    if (k >= c) {
+      k -= c;
+      m >>= w;
+      pos += w;
+    }
+  }
+  return pos;
 }
 
 // Row y of a rooms map painted from its primitives (rooms_paint's result, one row at a time): border
-// | walls & ~doors.  Word k covers columns [64k, 64k + 64).
-APG_DEV uint64_t rooms_row_word(const uint32_t *pr, int m, int y, int k) {
+// | walls & ~doors.  Word k covers columns [64k, 64k + 64); the primitives are pr[i * st].
+APG_DEV uint64_t rooms_row_word(const uint32_t *pr, int st, int m, int y, int k) {
   const int nw = (int)(pr[0] & 255u), nd = (int)(pr[0] >> 8);
   uint64_t v = (y == 0 || y == m - 1) ? span_mask(0, m, k) : (span_mask(0, 1, k) | span_mask(m - 1, 1, k));
   for (int i = 0; i < nw; i++) {
-    const uint32_t wl = pr[1 + i];
-    const int fixed = (int)((wl >> 16) & 255u), st = (int)((wl >> 8) & 255u), len = (int)(wl & 255u);
+    const uint32_t wl = pr[(1 + i) * st];
+    const int fixed = (int)((wl >> 16) & 255u), s0 = (int)((wl >> 8) & 255u), len = (int)(wl & 255u);
     if (wl >> 31) {
-      if (y >= st && y < st + len && (fixed >> 6) == k) v |= 1ULL << (fixed & 63);
+      if (y >= s0 && y < s0 + len && (fixed >> 6) == k) v |= 1ULL << (fixed & 63);
     } else if (fixed == y) {
-      v |= span_mask(st, len, k);
+      v |= span_mask(s0, len, k);
     }
   }
   for (int i = 0; i < nd; i++) {
-    const uint32_t d = pr[17 + i];
+    const uint32_t d = pr[(17 + i) * st];
     const int r0 = (int)(d >> 24), c0 = (int)((d >> 16) & 255u), hh = (int)((d >> 8) & 255u), ww = (int)(d & 255u);
     if (y >= r0 && y < r0 + hh) v &= ~span_mask(c0, ww, k);
   }
   return v;
 }
+
+// Phase-R LDS of the fused rooms autoresets (dynamic region, before the windows are staged), all
+// [index][EPB] so each thread's generator state is interleaved: primitives, task stack, split
+// capacities and sizes, cut points, then each wave's copy of the map being painted.
+constexpr int ROOMS_STACK = 20;  // pending tasks carry >= 1 room each: at most max_rooms <= 17
+template <int EPB>
+struct RoomsLds {
+  static constexpr size_t prim = 0;
+  static constexpr size_t stk = prim + (size_t)ROOMS_PRIM_WORDS * EPB * 4;
+  static constexpr size_t cap = stk + (size_t)ROOMS_STACK * EPB * 8;
+  static constexpr size_t size = cap + (size_t)17 * EPB * 2;
+  static constexpr size_t cut = size + (size_t)17 * EPB * 2;
+  static constexpr size_t mrow = (cut + (size_t)16 * EPB * 2 + 7) & ~(size_t)7;
+  static constexpr size_t bytes = mrow + (size_t)(4 * EPB / 64) * MAX_MAP_ROWS * 2 * 8;
+};
 
 // GEN / FUSED: FUSED instances start with phase R, the NEXT_STEP autoresets of the envs whose episode
 // ended at the previous step (map generation of kind GEN, start cell), so a step is one launch; the
@@ -422,36 +445,58 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   if constexpr (FUSED) {
     const uint8_t f0 = my_valid ? S.flags[my_e] : 0;
     const bool pend = my_valid && (f0 & F_AUTORESET);
+#ifdef APG_X_NO_SEED  // tuning experiment only: measure the map-index seeding
+#define APG_SEED_FN(x) Pcg64{x, x, x, x | 1, 0, 0}
+#else
+#define APG_SEED_FN(x) seed_pcg64(x)
+#endif
     if (__syncthreads_or(pend)) {
       if constexpr (GEN == GEN_ROOMS) {
-        // R1: the env's streams, its next map index and the map's primitives (into LDS)
-        uint32_t *s_prims = s_dyn;
-        uint64_t *s_mrow = reinterpret_cast<uint64_t *>(s_dyn + ((EPB * PRIM_STRIDE + 1) & ~1));
+        // R1: the env's streams, its next map index and the map's primitives, generated with the
+        // working storage interleaved in LDS (a private-array generator would live in scratch memory)
+        using L = RoomsLds<EPB>;
+        char *s_raw = reinterpret_cast<char *>(s_dyn);
+        uint32_t *s_prims = reinterpret_cast<uint32_t *>(s_raw + L::prim);
+        uint64_t *s_mrow = reinterpret_cast<uint64_t *>(s_raw + L::mrow);
         Pcg64 rng, it;
         uint64_t midx = 0;
         if (pend) {
           rng = *reinterpret_cast<const Pcg64 *>(&S.rng[my_e]);
           it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[my_e]);
           midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
-          Pcg64 map_rng = seed_pcg64(midx);  // FloorMapDatasetRooms.get_data_point: default_rng(idx)
-          RoomsPrims pr;
-          const int rc = rooms_primitives(map_rng, g.h, g.max_rooms, g.door_width, bt, pr);
+          Pcg64 map_rng = APG_SEED_FN(midx);  // FloorMapDatasetRooms.get_data_point: default_rng(idx)
+          const RoomsWork wk{reinterpret_cast<uint64_t *>(s_raw + L::stk) + my_el,
+                             reinterpret_cast<int16_t *>(s_raw + L::cap) + my_el,
+                             reinterpret_cast<int16_t *>(s_raw + L::size) + my_el,
+                             reinterpret_cast<int16_t *>(s_raw + L::cut) + my_el, s_prims + my_el, EPB, ROOMS_STACK};
+#ifdef APG_X_NO_R1  // tuning experiment only (wrong results): an empty rooms map
+          wk.P(0) = 0u;
+          const int rc = 0;
+#else
+          const int rc = rooms_primitives(map_rng, g.h, g.max_rooms, g.door_width, bt, wk);
+#endif
           if (rc != 0) atomicOr(O.err, APG_ERR_MAPGEN);
-          uint32_t *q = s_prims + my_el * PRIM_STRIDE;
-          q[0] = (uint32_t)pr.nw | ((uint32_t)pr.nd << 8);
-          for (int i = 0; i < pr.nw; i++) q[1 + i] = pr.wall[i];
-          for (int i = 0; i < pr.nd; i++) q[17 + i] = pr.door[i];
         }
-        __syncthreads();
+        // R2 reads only the primitives its own wave wrote in R1 (wave w owns the envs j * W + w): a wave
+        // barrier suffices, so waves that finish generating start their map stores while others still
+        // generate (the 4 * H * W-byte f32 map obs of every reset env is this step's dominant traffic)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // R2: each wave paints the maps of its own envs one after the other, lane = row: occupancy rows
         // out (coalesced), the f32 map obs from the wave's row copy in LDS, the free-cell count and the
         // start cell (place_start: the pick-th free cell in row-major order, drawn by the env's lane)
         uint64_t *mrow = s_mrow + (size_t)wave * MAX_MAP_ROWS * 2;
         const int m = P.h, wpr = P.wpr;
+#ifdef APG_X_NO_R2  // tuning experiment only (wrong results): no painting, start cell 0
+        if (pend) s_start[my_el] = 0;
+        for (int j = 0; j < 0; j++) {
+#else
         for (int j = 0; j < LPW; j++) {
+#endif
           if (!__shfl((int)pend, j)) continue;  // wave-uniform
           const int el = j * W + wave, e = base + el;
-          const uint32_t *pr = s_prims + el * PRIM_STRIDE;
+          const uint32_t *pr = s_prims + el;
           uint64_t *dst = S.occ + (size_t)e * words;
           int fr[2] = {0, 0};
           uint64_t rw[2][2] = {{0ULL, 0ULL}, {0ULL, 0ULL}};
@@ -461,7 +506,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
             if (y < m) {
               int occ = 0;
               for (int k = 0; k < wpr; k++) {
-                const uint64_t v = rooms_row_word(pr, m, y, k);
+                const uint64_t v = rooms_row_word(pr, EPB, m, y, k);
                 rw[rr][k] = v;
                 dst[y * wpr + k] = v;
                 mrow[y * 2 + k] = v;
@@ -1051,9 +1096,6 @@ size_t step_lds_bytes(int epb, int beams) {
   if (beams <= MAX_STAGED_BEAMS) b += (size_t)epb * (beams + 1) * sizeof(float) + (size_t)epb * beams * sizeof(uint16_t);
   return b;
 }
-size_t rooms_reset_lds_bytes(int epb) {
-  return (size_t)((epb * PRIM_STRIDE + 1) & ~1) * sizeof(uint32_t) + (size_t)(4 * epb / 64) * MAX_MAP_ROWS * 2 * sizeof(uint64_t);
-}
 
 int step_gen(const Geo &g) {
   if (g.is_static) return GEN_NONE;
@@ -1088,7 +1130,7 @@ template <int GEN, bool FUSED, int EPB>
 int launch_step_t(const StepParams &P, const Geo &g, const apg_lidar_state *st, const float *act, const float *pred,
                   const apg_lidar_outputs *out, hipStream_t s, const BinomTable &bt) {
   size_t lds = step_lds_bytes(EPB, P.beams);
-  if (FUSED && GEN == GEN_ROOMS && rooms_reset_lds_bytes(EPB) > lds) lds = rooms_reset_lds_bytes(EPB);
+  if (FUSED && GEN == GEN_ROOMS && RoomsLds<EPB>::bytes > lds) lds = RoomsLds<EPB>::bytes;
   auto kern = k_lidar_step<GEN, FUSED, EPB>;
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)

@@ -41,9 +41,27 @@ APG_DEV int64_t pyfloordiv(int64_t a, int64_t b) {
   return q;
 }
 
-// distribute_integers(n, k) (rooms.py:36-40) with k <= 17
-APG_DEV void distribute_integers(Pcg64 &r, int64_t n, int k, int64_t *out) {
-  int64_t cuts[16];
+// Working storage of the rooms generator, strided so that a workgroup can interleave its threads'
+// copies in LDS ([index][thread], conflict-free) or a thread can point it at private arrays (stride 1):
+// the task stack, the capacities and sizes of the current split, distribute_integers' cut points, and
+// the output primitives prim[0] = nw | nd << 8, prim[1 + i] walls, prim[17 + i] doors.
+struct RoomsWork {
+  uint64_t *stk;
+  int16_t *cap, *size, *cut;
+  uint32_t *prim;
+  int st;       // element stride
+  int stk_cap;  // stack capacity
+  APG_DEV uint64_t &S(int i) const { return stk[i * st]; }
+  APG_DEV int16_t &C(int i) const { return cap[i * st]; }
+  APG_DEV int16_t &Z(int i) const { return size[i * st]; }
+  APG_DEV int16_t &K(int i) const { return cut[i * st]; }
+  APG_DEV uint32_t &P(int i) const { return prim[i * st]; }
+};
+constexpr int ROOMS_PRIM_WORDS = 33;
+
+// distribute_integers(n, k) (rooms.py:36-40) with k <= 17, n < 2^15: out(i) for i < k
+template <class Out>
+APG_DEV void distribute_integers(Pcg64 &r, int64_t n, int k, const RoomsWork &W, Out out) {
   const int64_t nz = k > n ? k - n : 0;
   const int64_t pop = nz + (n > 1 ? n - 1 : 0);
   const int kk = k - 1;
@@ -52,31 +70,35 @@ APG_DEV void distribute_integers(Pcg64 &r, int64_t n, int k, int64_t *out) {
     int64_t val = (int64_t)bounded_u64(r, (uint64_t)j);
     int idx = (int)(j - (pop - kk));
     bool found = false;
-    for (int t = 0; t < idx; t++) found |= (cuts[t] == val);
-    cuts[idx] = found ? j : val;
+    for (int t = 0; t < idx; t++) found |= (W.K(t) == val);
+    W.K(idx) = (int16_t)(found ? j : val);
   }
   for (int i = kk - 1; i >= 1; i--) {
     int jj = (int)bounded_u64(r, (uint64_t)i);
-    int64_t t = cuts[jj];
-    cuts[jj] = cuts[i];
-    cuts[i] = t;
+    const int16_t t = W.K(jj);
+    W.K(jj) = W.K(i);
+    W.K(i) = t;
   }
-  for (int i = 0; i < kk; i++) cuts[i] = cuts[i] < nz ? 0 : cuts[i] - nz + 1;  // r[idx]
+  for (int i = 0; i < kk; i++) {  // r[idx], then sorted (insertion sort)
+    const int c = W.K(i);
+    W.K(i) = (int16_t)(c < nz ? 0 : c - nz + 1);
+  }
   for (int i = 1; i < kk; i++) {
-    int64_t v = cuts[i];
+    const int16_t v = W.K(i);
     int j = i - 1;
-    while (j >= 0 && cuts[j] > v) {
-      cuts[j + 1] = cuts[j];
+    while (j >= 0 && W.K(j) > v) {
+      W.K(j + 1) = W.K(j);
       j--;
     }
-    cuts[j + 1] = v;
+    W.K(j + 1) = v;
   }
   int64_t prev = 0;
   for (int i = 0; i < kk; i++) {
-    out[i] = cuts[i] - prev;
-    prev = cuts[i];
+    const int c = W.K(i);
+    out(i) = (int16_t)(c - prev);
+    prev = c;
   }
-  out[kk] = n - prev;
+  out(kk) = (int16_t)(n - prev);
 }
 
 struct Bits {  // bit-packed rows in global memory
@@ -98,23 +120,18 @@ APG_DEV uint64_t pack_task(int y0, int x0, int t, int n0, int n1, int mr) {
 // The reference paints walls (`room[wp] = where(room[wp] != -1, 1, -1)`) and doors (`= -1`) into an
 // int8 map in task order, then maps -1 to free.  A cell ends up a wall iff it is on the border or
 // covered by some wall segment, and covered by no door block: paint order never matters.  So the
-// generator only records the segments and blocks (in map coordinates) and paints rows at the end,
-// with the final 50% transpose applied to the primitives instead of the bitmap.
-struct RoomsPrims {
-  int nw, nd;
-  uint32_t wall[16];  // vertical << 31 | fixed << 16 | start << 8 | len   (len <= 255)
-  uint32_t door[16];  // r0 << 24 | c0 << 16 | h << 8 | w
-};
-
+// generator only records the segments and blocks (in map coordinates, W.P) and paints rows at the
+// end, with the final 50% transpose applied to the primitives instead of the bitmap.
+//   wall: vertical << 31 | fixed << 16 | start << 8 | len (len <= 255); door: r0 << 24 | c0 << 16 | h << 8 | w
 APG_DEV int rooms_primitives(Pcg64 &r, int m, int max_rooms, int door_width, const BinomTable &bt,
-                             RoomsPrims &P) {
+                             const RoomsWork &W) {
   const int min_size = door_width + 2;
-  P.nw = P.nd = 0;
-  uint64_t stack[64];
+  int nw = 0, nd = 0;
   int sp = 0;
-  stack[sp++] = pack_task(1, 1, 0, m - 2, m - 2, max_rooms);
+  W.P(0) = 0u;
+  W.S(sp++) = pack_task(1, 1, 0, m - 2, m - 2, max_rooms);
   while (sp > 0) {
-    const uint64_t tk = stack[--sp];
+    const uint64_t tk = W.S(--sp);
     const int y0 = (int)(tk & 255), x0 = (int)((tk >> 8) & 255), t = (int)((tk >> 16) & 1);
     const int n0 = (int)((tk >> 17) & 255), n1 = (int)((tk >> 25) & 255), mr = (int)((tk >> 33) & 255);
     int64_t mrl = pyfloordiv(n0 - min_size, min_size + 1) + 1;
@@ -122,51 +139,50 @@ APG_DEV int rooms_primitives(Pcg64 &r, int m, int max_rooms, int door_width, con
     if (mrl <= 1) continue;
     if (mrl > 17) return -2;  // max_rooms <= 17 (binomial table: mrl - 2 <= 15)
     const int k = (int)binomial_inv(r, mrl - 2, bt) + 2;
-    int64_t cap[17], sizes[17], starts[17], ends[17];
-    distribute_integers(r, mrl, k, cap);
-    distribute_integers(r, n0 - (int64_t)k * (1 + min_size) + 1, k, sizes);
-    int64_t acc = 0;
-    for (int i = 0; i < k; i++) {
-      sizes[i] += min_size;
-      acc += sizes[i] + 1;
-      ends[i] = acc - 1;
-    }
-    starts[0] = 0;
-    for (int i = 1; i < k; i++) starts[i] = ends[i - 1] + 2;
-    if (P.nw + k - 1 > 16) return -4;
+    distribute_integers(r, mrl, k, W, [&](int i) -> int16_t & { return W.C(i); });
+    distribute_integers(r, n0 - (int64_t)k * (1 + min_size) + 1, k, W, [&](int i) -> int16_t & { return W.Z(i); });
+    // sizes += min_size; room i spans view rows [starts[i], ends[i]] with ends[i] = acc_i - 1,
+    // starts[i] = acc_{i-1} + 1 (starts[0] = 0), acc_i = sum_{j <= i} (sizes[j] + 1)
+    for (int i = 0; i < k; i++) W.Z(i) = (int16_t)(W.Z(i) + min_size);
+    if (nw + k - 1 > 16) return -4;
+    int acc = (int)W.Z(0) + 1;
     for (int i = 1; i < k; i++) {
-      const int wp = (int)(starts[i] - 1);
+      const int wp = acc;  // starts[i] - 1
+      acc += (int)W.Z(i) + 1;
       const int dp = (int)integers(r, 0, n1 - door_width);
       if (wp - (door_width - 1) < 0 || wp + (door_width - 1) >= n0 || dp + door_width > n1) return -3;
       // wall: the whole view row wp; door: view rows wp-dw+1 .. wp+dw-1, columns dp .. dp+dw-1
       const int lo = wp - (door_width - 1), span = 2 * door_width - 1;
       if (t == 0) {
-        P.wall[P.nw++] = ((uint32_t)(y0 + wp) << 16) | ((uint32_t)x0 << 8) | (uint32_t)n1;
-        P.door[P.nd++] = ((uint32_t)(y0 + lo) << 24) | ((uint32_t)(x0 + dp) << 16) | ((uint32_t)span << 8) |
+        W.P(1 + nw++) = ((uint32_t)(y0 + wp) << 16) | ((uint32_t)x0 << 8) | (uint32_t)n1;
+        W.P(17 + nd++) = ((uint32_t)(y0 + lo) << 24) | ((uint32_t)(x0 + dp) << 16) | ((uint32_t)span << 8) |
                          (uint32_t)door_width;
       } else {
-        P.wall[P.nw++] = (1u << 31) | ((uint32_t)(x0 + wp) << 16) | ((uint32_t)y0 << 8) | (uint32_t)n1;
-        P.door[P.nd++] = ((uint32_t)(y0 + dp) << 24) | ((uint32_t)(x0 + lo) << 16) | ((uint32_t)door_width << 8) |
+        W.P(1 + nw++) = (1u << 31) | ((uint32_t)(x0 + wp) << 16) | ((uint32_t)y0 << 8) | (uint32_t)n1;
+        W.P(17 + nd++) = ((uint32_t)(y0 + dp) << 24) | ((uint32_t)(x0 + lo) << 16) | ((uint32_t)door_width << 8) |
                          (uint32_t)span;
       }
     }
-    // children room[s:e+1].T, depth-first in order => push in reverse
-    if (sp + k > 64) return -4;
+    // children room[s:e+1].T, depth-first in order => push in reverse (acc = acc_{k-1} here)
+    if (sp + k > W.stk_cap) return -4;
     for (int i = k - 1; i >= 0; i--) {
-      int64_t s = starts[i], e = ends[i] + 1;
+      const int acc_prev = acc - ((int)W.Z(i) + 1);
+      int64_t s = i == 0 ? 0 : acc_prev + 1, e = acc;  // starts[i], ends[i] + 1
+      acc = acc_prev;
       if (e > n0) e = n0;
       if (s > n0) s = n0;
       const int cy0 = t ? y0 : y0 + (int)s, cx0 = t ? x0 + (int)s : x0;
-      stack[sp++] = pack_task(cy0, cx0, 1 - t, n1, (int)(e - s), (int)cap[i]);
+      W.S(sp++) = pack_task(cy0, cx0, 1 - t, n1, (int)(e - s), (int)W.C(i));
     }
   }
   if (integers(r, 0, 2) == 0) {  // map_int = map_int.T: transpose the primitives
-    for (int i = 0; i < P.nw; i++) P.wall[i] ^= 1u << 31;
-    for (int i = 0; i < P.nd; i++) {
-      const uint32_t d = P.door[i];
-      P.door[i] = (((d >> 16) & 255u) << 24) | (((d >> 24) & 255u) << 16) | ((d & 255u) << 8) | ((d >> 8) & 255u);
+    for (int i = 0; i < nw; i++) W.P(1 + i) ^= 1u << 31;
+    for (int i = 0; i < nd; i++) {
+      const uint32_t d = W.P(17 + i);
+      W.P(17 + i) = (((d >> 16) & 255u) << 24) | (((d >> 24) & 255u) << 16) | ((d & 255u) << 8) | ((d >> 8) & 255u);
     }
   }
+  W.P(0) = (uint32_t)nw | ((uint32_t)nd << 8);
   return 0;
 }
 
@@ -180,12 +196,13 @@ APG_DEV uint64_t span_mask(int s, int l, int k) {
 
 // Paint rows [m][wpr] = border | walls & ~doors, one primitive at a time (each primitive is read
 // once; the row words are read-modify-written, so `rows` should be LDS: see k_lidar_reset).
-APG_DEV void rooms_paint(const RoomsPrims &P, int m, int wpr, uint64_t *rows) {
+APG_DEV void rooms_paint(const RoomsWork &W, int m, int wpr, uint64_t *rows) {
+  const int nw = (int)(W.P(0) & 255u), nd = (int)(W.P(0) >> 8);
   for (int y = 0; y < m; y++)
     for (int k = 0; k < wpr; k++)
       rows[y * wpr + k] = (y == 0 || y == m - 1) ? span_mask(0, m, k) : (span_mask(0, 1, k) | span_mask(m - 1, 1, k));
-  for (int i = 0; i < P.nw; i++) {
-    const uint32_t wl = P.wall[i];
+  for (int i = 0; i < nw; i++) {
+    const uint32_t wl = W.P(1 + i);
     const int fixed = (int)((wl >> 16) & 255u), st = (int)((wl >> 8) & 255u), len = (int)(wl & 255u);
     if (wl >> 31) {  // vertical: column `fixed`, rows [st, st + len)
       const uint64_t bit = 1ULL << (fixed & 63);
@@ -194,20 +211,23 @@ APG_DEV void rooms_paint(const RoomsPrims &P, int m, int wpr, uint64_t *rows) {
       for (int k = 0; k < wpr; k++) rows[fixed * wpr + k] |= span_mask(st, len, k);
     }
   }
-  for (int i = 0; i < P.nd; i++) {
-    const uint32_t d = P.door[i];
+  for (int i = 0; i < nd; i++) {
+    const uint32_t d = W.P(17 + i);
     const int r0 = (int)(d >> 24), c0 = (int)((d >> 16) & 255u), hh = (int)((d >> 8) & 255u), ww = (int)(d & 255u);
     for (int y = r0; y < r0 + hh; y++)
       for (int k = 0; k < wpr; k++) rows[y * wpr + k] &= ~span_mask(c0, ww, k);
   }
 }
 
-// generate + paint: occ rows [m][wpr]
+// generate + paint: occ rows [m][wpr]; working storage in this thread's private arrays
 APG_DEV int rooms_generate(Pcg64 &r, uint64_t *occ, int wpr, int m, int max_rooms, int door_width,
                            const BinomTable &bt) {
-  RoomsPrims P;
-  const int rc = rooms_primitives(r, m, max_rooms, door_width, bt, P);
-  rooms_paint(P, m, wpr, occ);
+  uint64_t stk[24];
+  int16_t cap[17], size[17], cut[16];
+  uint32_t prim[ROOMS_PRIM_WORDS];
+  const RoomsWork W{stk, cap, size, cut, prim, 1, 24};
+  const int rc = rooms_primitives(r, m, max_rooms, door_width, bt, W);
+  rooms_paint(W, m, wpr, occ);
   return rc;
 }
 

@@ -12,6 +12,6 @@ for lib in default $(ls $R/active-perception-gym_amd/ap_gym_amd/_lib/variants/*.
 import csv, glob, sys, numpy as np
 f = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
 d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in csv.DictReader(open(f)) if "k_lidar_step" in r["Kernel_Name"] and "true" in r["Kernel_Name"]]
-print(f"{sys.argv[1].split('/')[-1]:24s} n={len(d)} median {np.median(d):.1f} us")
+print(f"{sys.argv[1].split('/')[-1]:24s} n={len(d)} median {np.median(d):.1f} max {max(d):.1f} us")
 PY
 done
