@@ -313,22 +313,36 @@ def test_nan_action_raises(gpu):
         et.step({"action": torch.zeros((4, 2), device=gpu), "prediction": torch.from_numpy(p).to(gpu)})
 
 
-def test_full_size_properties(gpu, oracle_mod):
-    """BASELINE cfg 2 size (N=65536, 32 beams, 64x64): size-independent invariants + sampled oracle checks."""
+@pytest.mark.parametrize("kind,size,beams,n", [("rooms", 64, 32, 65536), ("maze", 127, 64, 262144)],
+                         ids=["cfg2_rooms64_b32_n65536", "cfg3_maze127_b64_n262144"])
+def test_full_size_properties(gpu, oracle_mod, kind, size, beams, n):
+    """BASELINE configs 2 and 3 at full size on one GPU (cfg 3 is the whole 262144-env batch the 8-GPU
+    run shards): size-independent invariants over 203 steps (two synchronized autoreset bursts), the
+    reset maps of sampled envs against the oracle's generator, and the complete step trace (lidar,
+    odometry, reward, termination) of sampled envs against a one-env oracle seeded with seed + e."""
     import torch
 
     import ap_gym_amd as ap
 
-    n = 65536
-    env = ap.make_vec("LIDARLocRooms-v0", num_envs=n, lidar_beam_count=32, dataset=ap.FloorMapDatasetRooms(64, 64),
-                      device=gpu, array_backend="torch")
+    env_id = "LIDARLocRooms-v0" if kind == "rooms" else "LIDARLocMaze-v0"
+    env = ap.make_vec(env_id, num_envs=n, lidar_beam_count=beams, dataset=_ds(ap, kind, size), device=gpu,
+                      array_backend="torch")
     obs, info = env.reset(seed=0)
     g = torch.Generator(device=gpu).manual_seed(0)
-    sample = np.random.default_rng(0).choice(n, 24, replace=False)
+    sample = np.sort(np.random.default_rng(0).choice(n, 8, replace=False))
+    sample[-1] = n - 1  # the last env of the last workgroup
     idx0 = info["map_idx"].cpu().numpy().astype(np.uint64)
-    maps = obs["map"][sample, ..., 0].cpu().numpy()
+    maps = obs["map"][torch.as_tensor(sample, device=gpu), ..., 0].cpu().numpy()
+    refs = []
     for j, e in enumerate(sample):
-        assert np.array_equal(maps[j] > 0, oracle_mod.rooms_map(int(idx0[e]), 64).astype(bool))
+        want = (oracle_mod.rooms_map(int(idx0[e]), size) if kind == "rooms"
+                else oracle_mod.maze_map(int(idx0[e]), size)).astype(bool)
+        assert np.array_equal(maps[j] > 0, want), f"reset map of env {e}"
+        ref = oracle_mod.OracleLidarVectorEnv(1, kind, size, False, 0, beams)
+        ref.reset(int(e))  # sub-env 0 seeded with seed + e, like env e of the batch
+        assert np.array_equal(obs["lidar"][int(e)].cpu().numpy(), ref.lidar[0]), f"reset lidar of env {e}"
+        refs.append(ref)
+    sel = torch.as_tensor(sample, device=gpu)
     resets = 0
     for t in range(1, 203):
         a = torch.rand((n, 2), device=gpu, generator=g) * 2 - 1
@@ -343,8 +357,20 @@ def test_full_size_properties(gpu, oracle_mod):
             resets += 1
             reset_now = ~info["_base_reward"]
             assert int(reset_now.sum()) >= 0.99 * n and bool((rew[reset_now] == 0).all())
+        a_s, p_s = a[sel].cpu().numpy(), p[sel].cpu().numpy()
+        got = {k: v[sel].cpu().numpy() for k, v in (("lidar", lid), ("odometry", obs["odometry"]), ("reward", rew),
+                                                      ("terminated", term))}
+        for j, ref in enumerate(refs):
+            ref.step(a_s[j:j + 1], p_s[j:j + 1])
+            e = int(sample[j])
+            assert np.array_equal(got["lidar"][j], ref.lidar[0]), f"step {t} env {e}: lidar"
+            assert np.array_equal(got["odometry"][j], ref.odometry[0]), f"step {t} env {e}: odometry"
+            assert got["reward"][j] == ref.reward[0], f"step {t} env {e}: reward"
+            assert bool(got["terminated"][j]) == bool(ref.terminated[0]), f"step {t} env {e}: terminated"
     env.check_errors()
     assert resets == 2
+    for ref in refs:
+        ref.close()
 
 
 @pytest.mark.parametrize("kind,size,beams", [("rooms", 64, 32), ("maze", 21, 8)])
