@@ -1,13 +1,21 @@
 """Env sharding across GPUs (one process per GPU, torch.distributed).
 
-Sub-envs are independent (SyncVectorEnv seeds sub-env i with seed+i and every later draw comes
-from that sub-env's own streams), so rank r simply owns the contiguous block
-[r*N/W, (r+1)*N/W) and seeds it with an env offset: no data-path collective is needed and the
-union of the shards is bit-identical to one unsharded env.
+Sub-envs are independent, so rank r owns the contiguous block [r*N/W, (r+1)*N/W):
+  * LIDAR ids: SyncVectorEnv seeds sub-env i with seed+i and every later draw comes from that
+    sub-env's own streams, so the shard simply resets with env_offset = r*N/W;
+  * image ids: the vector env draws each batch from one stream, so every shard draws the whole
+    batch of num_envs_total (a few microseconds on device) and keeps its slice (env_offset).
+Either way the union of the shards is bit-identical to one unsharded env and no data-path
+collective is needed (weak scaling).
 
-`ShardedVectorEnv(..., gather=True)` additionally reassembles the batched step outputs (everything
-except the per-reset map observation) on every rank with one all-gather over a packed byte row per
-env — RCCL over xGMI on MI355X, gloo on CPU — for consumers that need the full batch.
+`ShardedVectorEnv(..., gather=True)` additionally reassembles the batched step outputs on every rank
+with one all-gather over a packed byte row per env — RCCL over xGMI on MI355X, gloo on CPU — for
+consumers that need the full batch (the north star's obs/reward reassembly):
+  LIDAR  lidar, odometry, time_step, reward, base_reward, target, loss, terminated, truncated,
+         info mask (the per-reset map observation stays sharded)
+  image  glimpse_pos, time_step, reward, base_reward, target, loss, index, terminated, truncated
+         (+ glimpse and target_glimpse with gather_glimpse=True)
+(image_classification.py:117-151 and image_localization.py:131-181 are the outputs gathered).
 """
 
 from __future__ import annotations
@@ -22,23 +30,61 @@ def shard_bounds(num_envs_total: int, rank: int, world: int) -> tuple[int, int]:
     return rank * n, n
 
 
-# packed per-env row: (name, bytes per env) in order; lidar width depends on the beam count
-def _row_layout(beams: int):
-    return [("lidar", 4 * beams), ("odometry", 8), ("time_step", 4), ("reward", 8), ("base_reward", 4),
-            ("target", 8), ("loss", 4), ("terminated", 1), ("truncated", 1), ("info_mask", 1)]
+def _is_lidar(env, beams) -> bool:
+    return beams is not None or hasattr(env, "lidar_beam_count")
+
+
+def _row_spec(env, beams, gather_glimpse: bool):
+    """(name, dtype, per-env shape) of the gathered fields of `env`'s torch step outputs."""
+    import torch
+
+    f32, f64, b8, i32, i64 = torch.float32, torch.float64, torch.bool, torch.int32, torch.int64
+    if _is_lidar(env, beams):
+        b = env.lidar_beam_count if beams is None else beams
+        return [("lidar", f32, (b,)), ("odometry", f32, (2,)), ("time_step", f32, ()), ("reward", f64, ()),
+                ("base_reward", f32, ()), ("target", f32, (2,)), ("loss", f32, ()), ("terminated", b8, ()),
+                ("truncated", b8, ()), ("info_mask", b8, ())]
+    from . import _native as N
+
+    loc = env.kind == N.APG_IMAGE_LOCALIZE
+    spec = [("glimpse_pos", f32, (2,)), ("time_step", f32, ()), ("reward", f64, ()), ("base_reward", f32, ()),
+            ("target", f32, (2,)) if loc else ("target", i32, ()), ("loss", f32 if loc else f64, ()),
+            ("index", i64, ()), ("terminated", b8, ()), ("truncated", b8, ())]
+    if gather_glimpse:
+        g = tuple(env.single_observation_space["glimpse"].shape)
+        spec.append(("glimpse", f32, g))
+        if loc:
+            spec.append(("target_glimpse", f32, g))
+    return spec
+
+
+def _nbytes(dtype, shape) -> int:
+    import torch
+
+    n = torch.empty((), dtype=dtype).element_size()
+    for s in shape:
+        n *= int(s)
+    return n
 
 
 class ShardedVectorEnv:
+    """One rank's shard of a vector env (`make_local(num_envs=, env_offset=)` builds it; image envs also
+    take num_envs_total=) plus the optional packed all-gather of the step outputs."""
+
     def __init__(self, make_local: Callable[..., object], num_envs_total: int, rank: int, world: int,
-                 beams: int, gather: bool = False, group=None):
+                 beams: int | None = None, gather: bool = False, group=None, gather_glimpse: bool = False,
+                 time_gather: bool = False):
         self.rank, self.world, self.gather, self.group = rank, world, gather, group
         self.offset, self.local_num_envs = shard_bounds(num_envs_total, rank, world)
         self.num_envs = num_envs_total
         self.env = make_local(num_envs=self.local_num_envs, env_offset=self.offset)
-        self._layout = _row_layout(beams)
-        self._row = sum(b for _, b in self._layout)
+        self._lidar = _is_lidar(self.env, beams)
+        self._spec = _row_spec(self.env, beams, gather_glimpse)
+        self._row = sum(_nbytes(dt, sh) for _, dt, sh in self._spec)
         self._row += (-self._row) % 8
         self._send = self._recv = None
+        self.time_gather = time_gather
+        self.gather_events: list = []  # (begin, end) torch.cuda.Event pairs around each all-gather
 
     def reset(self, *, seed=None, options=None):
         return self.env.reset(seed=seed, options=options)
@@ -48,48 +94,81 @@ class ShardedVectorEnv:
 
         n = self.local_num_envs
         if self._send is None:
-            dev = fields["lidar"].device
+            dev = fields[self._spec[0][0]].device
             self._send = torch.zeros((n, self._row), dtype=torch.uint8, device=dev)
             self._recv = torch.zeros((self.world * n, self._row), dtype=torch.uint8, device=dev)
         o = 0
-        for name, nb in self._layout:
-            self._send[:, o:o + nb] = fields[name].contiguous().view(torch.uint8).reshape(n, nb)
+        for name, dt, sh in self._spec:
+            nb = _nbytes(dt, sh)
+            self._send[:, o:o + nb] = fields[name].to(dt).contiguous().view(torch.uint8).reshape(n, nb)
             o += nb
         return self._send
 
     def _unpack(self, buf):
-        import torch
-
-        dtypes = {"reward": torch.float64, "terminated": torch.bool, "truncated": torch.bool,
-                  "info_mask": torch.bool}
         out, o = {}, 0
-        for name, nb in self._layout:
-            dt = dtypes.get(name, torch.float32)
-            v = buf[:, o:o + nb].contiguous().view(dt)
-            out[name] = v.reshape(buf.shape[0], -1) if name in ("lidar", "odometry", "target") else v.reshape(-1)
+        rows = buf.shape[0]
+        for name, dt, sh in self._spec:
+            nb = _nbytes(dt, sh)
+            out[name] = buf[:, o:o + nb].contiguous().view(dt).reshape(rows, *sh)
             o += nb
         return out
 
     def all_gather(self, fields: dict) -> dict:
+        import torch
         import torch.distributed as dist
 
         send = self._pack(fields)
+        ev = None
+        if self.time_gather and send.is_cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         if dist.get_backend(self.group) == "nccl":
             dist.all_gather_into_tensor(self._recv, send, group=self.group)
-        else:
-            dist.all_gather(list(self._recv.chunk(self.world)), send, group=self.group)
+        else:  # gloo (CPU tests, or several ranks sharing one GPU): through host buffers
+            recv = [torch.empty_like(send, device="cpu") for _ in range(self.world)]
+            dist.all_gather(recv, send.cpu(), group=self.group)
+            self._recv.copy_(torch.cat(recv))
+        if ev is not None:
+            ev[1].record()
+            self.gather_events.append(ev)
         return self._unpack(self._recv)
+
+    def gather_ms(self) -> float | None:
+        """Mean time of the timed all-gathers so far (synchronizes), then forgets them."""
+        import torch
+
+        if not self.gather_events:
+            return None
+        torch.cuda.synchronize()
+        ms = sum(a.elapsed_time(b) for a, b in self.gather_events) / len(self.gather_events)
+        self.gather_events.clear()
+        return ms
 
     def step(self, action):
         obs, rew, term, trunc, info = self.env.step(action)
         if not self.gather:
             return obs, rew, term, trunc, info
-        full = self.all_gather({"lidar": obs["lidar"], "odometry": obs["odometry"], "time_step": obs["time_step"],
-                                "reward": rew, "base_reward": info["base_reward"],
-                                "target": info["prediction"]["target"], "loss": info["prediction"]["loss"],
-                                "terminated": term, "truncated": trunc, "info_mask": info["_base_reward"]})
-        gobs = {"lidar": full["lidar"], "odometry": full["odometry"], "time_step": full["time_step"]}
-        ginfo = {"base_reward": full["base_reward"], "_base_reward": full["info_mask"],
+        if self._lidar:
+            full = self.all_gather({"lidar": obs["lidar"], "odometry": obs["odometry"], "time_step": obs["time_step"],
+                                    "reward": rew, "base_reward": info["base_reward"],
+                                    "target": info["prediction"]["target"], "loss": info["prediction"]["loss"],
+                                    "terminated": term, "truncated": trunc, "info_mask": info["_base_reward"]})
+            gobs = {"lidar": full["lidar"], "odometry": full["odometry"], "time_step": full["time_step"]}
+            ginfo = {"base_reward": full["base_reward"], "_base_reward": full["info_mask"],
+                     "prediction": {"target": full["target"], "loss": full["loss"]}, "local_obs": obs}
+            return gobs, full["reward"], full["terminated"], full["truncated"], ginfo
+        target = info["prediction"]["target"]
+        if isinstance(target, dict):  # -sparse ids: {"target", "weight"}
+            target = target["target"]
+        fields = {"glimpse_pos": obs["glimpse_pos"], "time_step": obs["time_step"], "reward": rew,
+                  "base_reward": info["base_reward"], "target": target, "loss": info["prediction"]["loss"],
+                  "index": info["index"], "terminated": term, "truncated": trunc}
+        for k in ("glimpse", "target_glimpse"):
+            if k in obs:
+                fields[k] = obs[k]
+        full = self.all_gather(fields)
+        gobs = {k: full[k] for k in ("glimpse", "glimpse_pos", "time_step", "target_glimpse") if k in full}
+        ginfo = {"index": full["index"], "base_reward": full["base_reward"],
                  "prediction": {"target": full["target"], "loss": full["loss"]}, "local_obs": obs}
         return gobs, full["reward"], full["terminated"], full["truncated"], ginfo
 

@@ -161,7 +161,12 @@ def run_image(args, world, rank, dev):
     ds = apg.SyntheticImageClassificationDataset(pool_len, w["shape"], w["classes"], c, seed=0)
     cfg = apg.ImagePerceptionConfig(dataset=ds, sensor_size=w["sensor"], step_limit=16)
     cls = apg.ImageClassificationVectorEnv if w["kind"] == "cls" else apg.ImageLocalizationVectorEnv
-    env = cls(n_local, cfg, device=dev, array_backend="torch", num_envs_total=n_total, env_offset=rank * n_local)
+    from ap_gym_amd.sharding import ShardedVectorEnv
+
+    senv = ShardedVectorEnv(lambda num_envs, env_offset: cls(num_envs, cfg, device=dev, array_backend="torch",
+                                                             num_envs_total=n_total, env_offset=env_offset),
+                            n_total, rank, world, gather=args.gather and world > 1, time_gather=True)
+    env = senv.env
     ring = 17
     g = torch.Generator(device=dev).manual_seed(1 + rank)
     acts = torch.rand((ring, n_local, 2), generator=g, device=dev) * 2 - 1
@@ -175,7 +180,8 @@ def run_image(args, world, rank, dev):
     torch.cuda.synchronize(dev)
     reset_ms = (time.perf_counter() - t0) * 1e3
     for t in range(args.warmup):
-        env.step({"action": acts[t % ring], "prediction": preds[t % ring]})
+        senv.step({"action": acts[t % ring], "prediction": preds[t % ring]})
+    senv.gather_ms()
     ev = HipEvents(args.steps)
     stream = torch.cuda.current_stream(dev).cuda_stream
     ev.hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
@@ -187,7 +193,8 @@ def run_image(args, world, rank, dev):
         b, e = ev.pair(t)
         k = (args.warmup + t) % ring
         ev.hip.hipEventRecord(b, stream)
-        env.step({"action": acts[k], "prediction": preds[k]})
+        env.step({"action": acts[k], "prediction": preds[k]}) if not senv.gather else \
+            senv.step({"action": acts[k], "prediction": preds[k]})
         ev.hip.hipEventRecord(e, stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -195,11 +202,12 @@ def run_image(args, world, rank, dev):
     elapsed = time.perf_counter() - t0
     env.check_errors()
     step_ms = sum(ev.elapsed_ms(i) for i in range(args.steps)) / args.steps
+    gather_ms = senv.gather_ms() or 0.0
     ev.close()
     if world > 1:
-        tt = torch.tensor([elapsed, step_ms, reset_ms], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed, step_ms, reset_ms, gather_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, step_ms, reset_ms = (float(x) for x in tt)
+        elapsed, step_ms, reset_ms, gather_ms = (float(x) for x in tt)
     if rank == 0:
         bpe = image_bytes_per_env_step(w["kind"], w["classes"], w["sensor"], c)
         achieved = bpe * n_local / (step_ms * 1e-3) / 1e9
@@ -219,7 +227,9 @@ def run_image(args, world, rank, dev):
                     "uniform actions, normal logits / uniform predictions generated on device",
             "config": {"workload": w["name"], "num_envs_per_gpu": n_local, "num_envs_total": n_total,
                        "sensor": list(w["sensor"]), "classes": w["classes"], "step_limit": 16,
-                       "reset_ms": reset_ms, "parallelism": f"env-shard x{world}"},
+                       "reset_ms": reset_ms, "parallelism": f"env-shard x{world}" + (" + all-gather" if senv.gather
+                                                                                        else ""),
+                       "gather_ms": gather_ms if senv.gather else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tpath,
                          "kernel": "image step (all kernels, HIP events around env.step)", "kernel_ms": step_ms,
@@ -319,7 +329,8 @@ def run_lidar(args, world, rank, dev):
         return apg.make_vec(w["env_id"], num_envs=num_envs, lidar_beam_count=beams, dataset=ds, device=dev,
                             array_backend="torch", env_offset=env_offset)
 
-    senv = ShardedVectorEnv(make_local, n_total, rank, world, beams, gather=args.gather and world > 1)
+    senv = ShardedVectorEnv(make_local, n_total, rank, world, beams, gather=args.gather and world > 1,
+                            time_gather=True)
     env = senv.env
     ring = 128  # distinct synthetic action/prediction batches, cycled
     g = torch.Generator(device=dev).manual_seed(1 + rank)
@@ -342,6 +353,7 @@ def run_lidar(args, world, rank, dev):
     reset_ms = (time.perf_counter() - t0) * 1e3
     for _ in range(args.warmup):
         step()
+    senv.gather_ms()
     ev = HipEvents(args.steps + EPISODE_PERIOD)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -358,6 +370,7 @@ def run_lidar(args, world, rank, dev):
     env.set_kernel_timing_events(None)
     env.check_errors()
     per_step = [ev.elapsed_ms(i) for i in timed]
+    gather_ms = senv.gather_ms() or 0.0
     kernel_ms = sum(per_step) / len(per_step)
     median_ms = statistics.median(per_step)
     # reset steps (1-based step index t with t % 101 == 0: synchronized episodes) in the timed window
@@ -381,12 +394,12 @@ def run_lidar(args, world, rank, dev):
     ev.close()
 
     if world > 1:
-        tt = torch.tensor([elapsed, kernel_ms, median_ms, reset_ms] + (episode or [0.0] * 4), dtype=torch.float64,
-                          device=dev)
+        tt = torch.tensor([elapsed, kernel_ms, median_ms, reset_ms, gather_ms] + (episode or [0.0] * 4),
+                          dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         vals = [float(x) for x in tt]
-        elapsed, kernel_ms, median_ms, reset_ms = vals[:4]
-        episode = vals[4:] if episode else None
+        elapsed, kernel_ms, median_ms, reset_ms, gather_ms = vals[:5]
+        episode = vals[5:] if episode else None
 
     if rank == 0:
         value = n_total * args.steps / elapsed
@@ -420,7 +433,7 @@ def run_lidar(args, world, rank, dev):
             "data": "synthetic (uniform(-1,1) actions/predictions generated on device; maps generated on device)",
             "config": {"workload": w["env_id"], "num_envs_per_gpu": n_local, "num_envs_total": n_total,
                        "beams": beams, "map": f"{msize}x{msize} {w['kind']}", "max_episode_steps": 100,
-                       "reset_ms": reset_ms, "note": w["note"],
+                       "reset_ms": reset_ms, "note": w["note"], "gather_ms": gather_ms if senv.gather else None,
                        "parallelism": f"env-shard x{world}" + (" + all-gather" if args.gather and world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -417,9 +417,9 @@ def test_image_env_nan_errors(gpu):
         env.close()
 
 
-def test_image_env_full_size_properties(gpu):
-    """MNIST-shaped classification at N = 65536 (BASELINE config 4) and localization at N = 4096:
-    bounded glimpses, clipped positions, reset cadence, label targets from the pool."""
+def test_image_cls_full_size_properties(gpu):
+    """BASELINE config 4 (MNIST-shaped classification, N = 65536, 5x5 glimpse): bounded glimpses,
+    clipped positions, reset cadence, label targets from the pool."""
     import torch
 
     import ap_gym_amd as ap
@@ -437,5 +437,59 @@ def test_image_env_full_size_properties(gpu):
         assert bool((obs["glimpse_pos"].abs() <= 1).all())
         assert bool((info["prediction"]["target"] == pool_labels[info["index"]]).all())
         assert bool(term.all()) == (t % 17 == 15)
+    env.check_errors()
+    env.close()
+
+
+def test_image_loc_full_size_cfg5(gpu):
+    """BASELINE config 5 itself (TinyImageNetLoc shape: N = 32768, 64x64x3 pool of 100000, 12x12 glimpse,
+    MSE) including the unique-sampler reset: reset targets in [-1, 1], glimpses in [0, 1]; for sampled
+    envs the uniqueness ranking equals image_oracle.unique_top_k on their images, and their complete
+    first episode (glimpse, glimpse_pos, target glimpse, reward, loss) equals an ImageVectorEnvOracle
+    started from their reset state."""
+    import torch
+
+    import ap_gym_amd as ap
+    from oracle import image_oracle as io
+
+    n, sensor = 32768, (12, 12)
+    ds = ap.SyntheticImageClassificationDataset(100000, (64, 64, 3), 200, 3, seed=0)
+    cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=sensor, step_limit=16)
+    env = ap.ImageLocalizationVectorEnv(n, cfg, array_backend="torch")
+    obs, info = env.reset(seed=0)
+    T = env._t
+    tgt = T["target"]
+    assert bool(((tgt >= -1) & (tgt <= 1)).all())
+    assert bool(((obs["glimpse"] >= 0) & (obs["glimpse"] <= 1)).all())
+    assert bool(((obs["target_glimpse"] >= 0) & (obs["target_glimpse"] <= 1)).all())
+    sample = np.sort(np.random.default_rng(5).choice(n, 6, replace=False))
+    sel = torch.as_tensor(sample, device=gpu)
+    pool, labels = ds.device_pool()
+    idx = info["index"][sel].cpu().numpy()
+    ref = io.ImageVectorEnvOracle("loc", pool, labels, 200, 3, len(sample), sensor, step_limit=16)
+    ref.seed(0)  # the per-env state below replaces everything the batch-level streams would draw
+    top_ref, _, _, _ = io.unique_top_k(ref.pool[idx], sensor, 1.0, int(cfg.unique_sampling_top_k))
+    assert np.array_equal(T["top_k"][sel].cpu().numpy(), top_ref)
+    ref.idx, ref.images, ref.cur_labels = idx, ref.pool[idx], ref.labels_pool[idx]
+    ref.pos = T["pos"][sel].cpu().numpy().astype(np.float64)
+    ref.target = tgt[sel].cpu().numpy().astype(np.float32)
+    ref.t, ref.prev_done, ref.env_prev_done = 0, np.zeros(len(sample), bool), np.zeros(len(sample), bool)
+    ref.hist, ref.log_prev_done = [[] for _ in sample], np.zeros(len(sample), bool)
+    assert np.array_equal(obs["glimpse"][sel].cpu().numpy(), io.glimpse(ref.images, ref.pos, sensor, 1.0))
+    g = torch.Generator(device=gpu).manual_seed(1)
+    for t in range(1, 21):
+        a = torch.rand((n, 2), generator=g, device=gpu) * 2 - 1
+        p = torch.rand((n, 2), generator=g, device=gpu) * 2 - 1
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        assert bool(((obs["glimpse"] >= 0) & (obs["glimpse"] <= 1)).all())
+        assert bool((obs["glimpse_pos"].abs() <= 1).all())
+        assert bool(term.all()) == (t == 16)
+        if t <= 16:  # the first episode of the sampled envs, step by step
+            ro, rr, rt, _, ri = ref.step(a[sel].cpu().numpy(), p[sel].cpu().numpy())
+            assert np.array_equal(obs["glimpse"][sel].cpu().numpy(), ro["glimpse"]), t
+            assert np.array_equal(obs["glimpse_pos"][sel].cpu().numpy(), ro["glimpse_pos"]), t
+            assert np.array_equal(obs["target_glimpse"][sel].cpu().numpy(), ro["target_glimpse"]), t
+            assert np.array_equal(rew[sel].cpu().numpy(), np.asarray(rr, np.float64)), t
+            assert np.array_equal(info["prediction"]["loss"][sel].cpu().numpy(), ri["prediction"]["loss"]), t
     env.check_errors()
     env.close()

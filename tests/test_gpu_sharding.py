@@ -1,0 +1,140 @@
+"""GPU sharding: the device envs split into shards (env_offset / num_envs_total) reproduce the unsharded
+env bit for bit, and ShardedVectorEnv's packed all-gather reassembles that batch on every rank.
+
+* single process: two shard envs on cuda:0 stepped side by side, concatenated, vs one unsharded env;
+* two processes (torch.multiprocessing, gloo — RCCL refuses two ranks on one device) sharing cuda:0,
+  ShardedVectorEnv(gather=True) on each: the gathered batch of every rank vs the unsharded env.
+Both for the LIDAR path (LIDARLocRooms) and the image path (ImageLocalizationVectorEnv with the
+unique-sampler reset), across autoresets.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N_TOTAL = 256
+
+
+def _make(kind, num_envs, env_offset=0, num_envs_total=None):
+    import ap_gym_amd as ap
+
+    if kind == "lidar":
+        return ap.make_vec("LIDARLocRooms-v0", num_envs=num_envs, lidar_beam_count=16,
+                           dataset=ap.FloorMapDatasetRooms(32, 32), device="cuda:0", array_backend="torch",
+                           env_offset=env_offset)
+    ds = ap.SyntheticImageClassificationDataset(64, (32, 32, 3), 10, 3, seed=3)
+    cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=(8, 8), step_limit=8)
+    return ap.ImageLocalizationVectorEnv(num_envs, cfg, device="cuda:0", array_backend="torch",
+                                         num_envs_total=num_envs_total or num_envs, env_offset=env_offset)
+
+
+def _steps(kind):
+    return 110 if kind == "lidar" else 30  # both cross autoresets (TimeLimit 100 / step_limit 8)
+
+
+def _actions(kind, t, n):
+    import torch
+
+    g = torch.Generator(device="cuda:0").manual_seed(1000 + t)
+    return (torch.rand((n, 2), device="cuda:0", generator=g) * 2 - 1,
+            torch.rand((n, 2), device="cuda:0", generator=g) * 2 - 1)
+
+
+def _flat(kind, obs, rew, term, info):
+    """The gathered fields of one step as numpy arrays (the same set ShardedVectorEnv packs)."""
+    if kind == "lidar":
+        d = {"lidar": obs["lidar"], "odometry": obs["odometry"], "time_step": obs["time_step"], "reward": rew,
+             "base_reward": info["base_reward"], "target": info["prediction"]["target"],
+             "loss": info["prediction"]["loss"], "terminated": term}
+    else:
+        d = {"glimpse_pos": obs["glimpse_pos"], "time_step": obs["time_step"], "reward": rew,
+             "base_reward": info["base_reward"], "target": info["prediction"]["target"],
+             "loss": info["prediction"]["loss"], "index": info["index"], "terminated": term}
+        if "glimpse" in obs:
+            d["glimpse"] = obs["glimpse"]
+            d["target_glimpse"] = obs["target_glimpse"]
+    return {k: v.detach().cpu().numpy().copy() for k, v in d.items()}
+
+
+def _reference(kind):
+    env = _make(kind, N_TOTAL)
+    env.reset(seed=5)
+    out = []
+    for t in range(_steps(kind)):
+        a, p = _actions(kind, t, N_TOTAL)
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        out.append(_flat(kind, obs, rew, term, info))
+    env.check_errors()
+    env.close()
+    return out
+
+
+@pytest.mark.parametrize("kind", ["lidar", "image"])
+def test_shards_union_equals_unsharded(gpu, kind):
+    import torch
+
+    half = N_TOTAL // 2
+    shards = [_make(kind, half, r * half, N_TOTAL) for r in range(2)]
+    for s in shards:
+        s.reset(seed=5)
+    ref = _reference(kind)
+    for t in range(_steps(kind)):
+        a, p = _actions(kind, t, N_TOTAL)
+        parts = []
+        for r, s in enumerate(shards):
+            obs, rew, term, trunc, info = s.step({"action": a[r * half:(r + 1) * half],
+                                                  "prediction": p[r * half:(r + 1) * half]})
+            parts.append(_flat(kind, obs, rew, term, info))
+        for k, want in ref[t].items():
+            got = np.concatenate([parts[0][k], parts[1][k]])
+            assert np.array_equal(got, want), f"step {t}: {k}"
+    torch.cuda.synchronize()
+
+
+def _worker(rank, world, port, kind, outdir):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ap_gym_amd  # noqa: F401
+    from ap_gym_amd.sharding import ShardedVectorEnv
+
+    senv = ShardedVectorEnv(lambda num_envs, env_offset: _make(kind, num_envs, env_offset, N_TOTAL), N_TOTAL, rank,
+                            world, gather=True, gather_glimpse=True)
+    lo, n = senv.offset, senv.local_num_envs
+    senv.reset(seed=5)
+    rows = []
+    for t in range(_steps(kind)):
+        a, p = _actions(kind, t, N_TOTAL)
+        obs, rew, term, trunc, info = senv.step({"action": a[lo:lo + n], "prediction": p[lo:lo + n]})
+        rows.append(_flat(kind, obs, rew, term, info))
+    torch.cuda.synchronize()
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"),
+             **{f"{t}_{k}": v for t, r in enumerate(rows) for k, v in r.items()})
+    senv.close()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("kind", ["lidar", "image"])
+def test_two_rank_gather_on_gpu_equals_unsharded(gpu, kind, tmp_path):
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_worker, args=(2, _free_port(), kind, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    ref = _reference(kind)
+    got = [np.load(tmp_path / f"rank{r}.npz") for r in range(2)]
+    for t, want in enumerate(ref):
+        for k, v in want.items():
+            for r in range(2):
+                assert np.array_equal(got[r][f"{t}_{k}"], v), f"rank {r} step {t}: {k}"
