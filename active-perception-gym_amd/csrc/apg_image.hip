@@ -348,24 +348,19 @@ struct Axis {  // one sampling coordinate: grid interval, fractional weight, 1 -
   double w, nw;
 };
 
-template <class PosT>
-__global__ __launch_bounds__(GS_THREADS) void k_glimpse_sep(GlimpseGeo g, const void *pool, const int64_t *index,
-                                                            const PosT *pos, int npos, int units, int upb,
-                                                            FastDiv per_div, FastDiv s1_div, FastDiv side_div,
-                                                            float *out, uint32_t *err) {
-  __shared__ float s_lut[256];
-  extern __shared__ Axis s_ax[];  // [unit][rows s0 | columns s1]
-  __shared__ int64_t s_base[GS_MAX_UNITS];
-  const int tid = threadIdx.x;
-  for (int v = tid; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
-  const int u0 = blockIdx.x * upb, nu = units - u0 < upb ? units - u0 : upb;
+// Separable glimpse of `nu` units (env x position) starting at unit u0, in two passes over a workgroup:
+// gs_axes computes every unit's row and column grid intervals / weights once (into LDS s_ax, plus the
+// pool offset of its image), gs_pixels then evaluates one pixel per thread from them.
+template <class PosAt>
+APG_DEV uint32_t gs_axes(const GlimpseGeo &g, const int64_t *index, PosAt pos_at, int u0, int nu, int npos,
+                         FastDiv side_div, Axis *s_ax, int64_t *s_base) {
   const int side = g.s0 + g.s1;
   uint32_t bad = 0;
-  for (int q = tid; q < nu * side; q += GS_THREADS) {
+  for (int q = threadIdx.x; q < nu * side; q += GS_THREADS) {
     const int u = (int)side_div.div((uint32_t)q), k = q - u * side;
     const bool row = k < g.s0;
     const int t = row ? k : k - g.s0;
-    const double p = (double)pos[2 * (u0 + u) + (row ? 1 : 0)];
+    const double p = pos_at(u, row ? 1 : 0);
     // flip(denormalize(pos)) + offsets (glimpse_pixel): rows use pos[1], columns pos[0]
     const double off = __dmul_rn(__dsub_rn((double)t, ((double)(row ? g.s0 : g.s1) - 1.0) / 2.0), g.scale);
     const double c = __dadd_rn(__dmul_rn(p, row ? g.lim_y : g.lim_x), off);
@@ -377,9 +372,14 @@ __global__ __launch_bounds__(GS_THREADS) void k_glimpse_sep(GlimpseGeo g, const 
     s_ax[q] = ax;
     if (k == 0) s_base[u] = index[(u0 + u) / npos] * g.img_elems;
   }
-  __syncthreads();
+  return bad;
+}
+
+APG_DEV void gs_pixels(const GlimpseGeo &g, const void *pool, int u0, int nu, FastDiv per_div, FastDiv s1_div,
+                       const Axis *s_ax, const int64_t *s_base, const float *s_lut, float *out) {
+  const int side = g.s0 + g.s1;
   const int per = g.s0 * g.s1;
-  for (int q = tid; q < nu * per; q += GS_THREADS) {
+  for (int q = threadIdx.x; q < nu * per; q += GS_THREADS) {
     const int u = (int)per_div.div((uint32_t)q), pix = q - u * per;
     const int i = (int)s1_div.div((uint32_t)pix), j = pix - i * g.s1;
     const Axis ay = s_ax[u * side + i], axx = s_ax[u * side + g.s0 + j];
@@ -442,6 +442,22 @@ __global__ __launch_bounds__(GS_THREADS) void k_glimpse_sep(GlimpseGeo g, const 
       for (int ch = 0; ch < g.c; ch++) dst[ch] = res[ch];
     }
   }
+}
+
+template <class PosT>
+__global__ __launch_bounds__(GS_THREADS) void k_glimpse_sep(GlimpseGeo g, const void *pool, const int64_t *index,
+                                                            const PosT *pos, int npos, int units, int upb,
+                                                            FastDiv per_div, FastDiv s1_div, FastDiv side_div,
+                                                            float *out, uint32_t *err) {
+  __shared__ float s_lut[256];
+  extern __shared__ Axis s_ax[];  // [unit][rows s0 | columns s1]
+  __shared__ int64_t s_base[GS_MAX_UNITS];
+  for (int v = threadIdx.x; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
+  const int u0 = blockIdx.x * upb, nu = units - u0 < upb ? units - u0 : upb;
+  const uint32_t bad = gs_axes(g, index, [&](int u, int c) { return (double)pos[2 * (u0 + u) + c]; }, u0, nu, npos,
+                               side_div, s_ax, s_base);
+  __syncthreads();
+  gs_pixels(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out);
   if (bad) atomicOr(err, bad);
 }
 
@@ -515,6 +531,22 @@ APG_DEV void log_classification(const EnvArgs &a, int e, const apg_image_outputs
   out.stats_idx[(size_t)a.n + e] = last_incorrect;
 }
 
+// ImagePerceptionModule.step's move (:197-213): project_sphere (util.py:94-97) in f32, then
+// max_step_length (f64) * step, clip(-1, 1); returns |action| (f32) for the base reward.
+APG_DEV float move_pos(const EnvArgs &a, float a0, float a1, double &px, double &py) {
+  const float mag = norm_f32(a0, a1);
+  float s0 = a0, s1 = a1;
+  if (mag > 1.0f) {
+    s0 = __fmul_rn(f32_div(a0, mag), 1.0f);
+    s1 = __fmul_rn(f32_div(a1, mag), 1.0f);
+  }
+  px = __dadd_rn(px, __dmul_rn(a.msl[0], (double)s0));
+  py = __dadd_rn(py, __dmul_rn(a.msl[1], (double)s1));
+  px = px < -1.0 ? -1.0 : (px > 1.0 ? 1.0 : px);
+  py = py < -1.0 ? -1.0 : (py > 1.0 ? 1.0 : py);
+  return mag;
+}
+
 // The per-env tail of ImagePerceptionModule.step (:197-213) + ActivePerceptionVectorEnv.step
 // (reward = base_reward - loss): move (or not, on the autoreset step), rewards, glimpse_pos, time.
 APG_DEV uint32_t env_tail(const EnvArgs &a, int e, const float *__restrict__ act, double *pos,
@@ -533,17 +565,7 @@ APG_DEV uint32_t env_tail(const EnvArgs &a, int e, const float *__restrict__ act
   } else {
     const float a0 = act[2 * e], a1 = act[2 * e + 1];
     if (a0 != a0 || a1 != a1) err |= APG_ERR_NAN_ACTION;
-    // project_sphere (util.py:94-97) in f32, then max_step_length (f64) * step, clip(-1, 1)
-    const float mag = norm_f32(a0, a1);
-    float s0 = a0, s1 = a1;
-    if (mag > 1.0f) {
-      s0 = __fmul_rn(f32_div(a0, mag), 1.0f);
-      s1 = __fmul_rn(f32_div(a1, mag), 1.0f);
-    }
-    px = __dadd_rn(px, __dmul_rn(a.msl[0], (double)s0));
-    py = __dadd_rn(py, __dmul_rn(a.msl[1], (double)s1));
-    px = px < -1.0 ? -1.0 : (px > 1.0 ? 1.0 : px);
-    py = py < -1.0 ? -1.0 : (py > 1.0 ? 1.0 : py);
+    const float mag = move_pos(a, a0, a1, px, py);
     pos[2 * e] = px;
     pos[2 * e + 1] = py;
     const float base = __fmul_rn(-mag, 1e-3f);  // -norm(action) * 1e-3 (f32, weak Python scalar)
@@ -557,12 +579,9 @@ APG_DEV uint32_t env_tail(const EnvArgs &a, int e, const float *__restrict__ act
   return err;
 }
 
-// Localization: one thread per env; MSE against the target before the autoreset update.
-__global__ __launch_bounds__(256) void k_image_env_loc(EnvArgs a, const float *__restrict__ act,
-                                                       const float *__restrict__ pred, double *pos,
-                                                       apg_image_outputs out, float *hist) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= a.n) return;
+// Localization step of env e: MSE against the target before the autoreset update.
+APG_DEV void loc_env(const EnvArgs &a, int e, const float *__restrict__ act, const float *__restrict__ pred,
+                     double *pos, const apg_image_outputs &out, float *hist) {
   uint32_t err = 0;
   const float p0 = pred[2 * e], p1 = pred[2 * e + 1];
   if (p0 != p0 || p1 != p1) err |= APG_ERR_NAN_PREDICTION;  // 1 - |pred - target| / 2 is NaN
@@ -580,6 +599,14 @@ __global__ __launch_bounds__(256) void k_image_env_loc(EnvArgs a, const float *_
   log_regression(a, e, out, hist, norm_f32(d0, d1), mse);  // |target - prediction|: signs do not matter
   err |= env_tail(a, e, act, pos, out, (double)loss_f, loss_f);
   if (err) atomicOr(out.err, err);
+}
+
+// Localization: one thread per env.
+__global__ __launch_bounds__(256) void k_image_env_loc(EnvArgs a, const float *__restrict__ act,
+                                                       const float *__restrict__ pred, double *pos,
+                                                       apg_image_outputs out, float *hist) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < a.n) loc_env(a, e, act, pred, pos, out, hist);
 }
 
 // numpy pairwise sum of x[off .. off+n) by the 8 lanes of a group (lane j owns accumulator j of
@@ -680,11 +707,16 @@ __global__ __launch_bounds__(256) void k_image_env_cls(EnvArgs a, int envs_per_b
 // then the tail — the order pw_leaf8 distributes over 8 lanes), log, with the same device libm calls.
 constexpr int CLS1_ENVS = 128;
 constexpr int CLS1_MAX_K = 16;
+APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const float *__restrict__ act, const int32_t *label,
+                      double *pos, const apg_image_outputs &out, float *hist);
+// LDS row stride of a K-logit row: odd, so lanes = envs hit distinct banks (k + 1 is even for odd K)
+APG_DEV int cls1_stride(int k) { return k + 1 + (k & 1); }
+
 __global__ __launch_bounds__(CLS1_ENVS) void k_image_env_cls1(EnvArgs a, const float *__restrict__ act,
                                                              const float *__restrict__ pred, const int32_t *label,
                                                              double *pos, apg_image_outputs out, float *hist) {
-  extern __shared__ float s_logit[];  // [CLS1_ENVS][k + 1]
-  const int k = a.k, stride = k + 1;
+  extern __shared__ float s_logit[];  // [CLS1_ENVS][cls1_stride(k)]
+  const int k = a.k, stride = cls1_stride(k);
   const int e0 = blockIdx.x * CLS1_ENVS;
   const int ne = a.n - e0 < CLS1_ENVS ? a.n - e0 : CLS1_ENVS;
   for (int q = threadIdx.x; q < ne * k; q += CLS1_ENVS) {
@@ -693,7 +725,13 @@ __global__ __launch_bounds__(CLS1_ENVS) void k_image_env_cls1(EnvArgs a, const f
   }
   __syncthreads();
   if ((int)threadIdx.x >= ne) return;
-  float *row = s_logit + threadIdx.x * stride;
+  cls1_env(a, e0 + threadIdx.x, s_logit + threadIdx.x * stride, act, label, pos, out, hist);
+}
+
+// Classification step of env e for K <= CLS1_MAX_K from its logit row (in LDS; overwritten with the exps).
+APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const float *__restrict__ act, const int32_t *label,
+                      double *pos, const apg_image_outputs &out, float *hist) {
+  const int k = a.k;
   float m = -INFINITY;
   bool nan = false, pos_inf = false, all_neg_inf = true;
   for (int i = 0; i < k; i++) {
@@ -704,7 +742,6 @@ __global__ __launch_bounds__(CLS1_ENVS) void k_image_env_cls1(EnvArgs a, const f
     m = v > m ? v : m;
   }
   if (nan || isinf(m)) m = 0.0f;  // x_max[~isfinite(x_max)] = 0
-  const int e = e0 + threadIdx.x;
   const int32_t l = label[e];
   const int lc = l < 0 ? 0 : (l >= k ? k - 1 : l);
   const float xt = row[lc];
@@ -733,6 +770,51 @@ __global__ __launch_bounds__(CLS1_ENVS) void k_image_env_cls1(EnvArgs a, const f
   log_classification(a, e, out, hist, f32_div(row[lc], sum));
   err |= env_tail(a, e, act, pos, out, loss_d, 0.0f);
   if (err) atomicOr(out.err, err);
+}
+
+// One launch per ordinary (non-reset) step: a glimpse workgroup computes the glimpses of its `nu` envs at
+// their new positions (gs_axes / gs_pixels; every axis thread recomputes its env's move with move_pos,
+// so no barrier separates the env step from the glimpse) and runs their env steps (loc_env / cls1_env:
+// loss, stats, move).  KIND: APG_IMAGE_LOCALIZE, or APG_IMAGE_CLASSIFY with K <= CLS1_MAX_K (logits
+// staged in LDS with coalesced loads, one thread per env as k_image_env_cls1).
+#ifndef APG_FUSED_MIN_WAVES
+#define APG_FUSED_MIN_WAVES 8  // <= 64 VGPRs: every workgroup of the grid resident at once
+#endif
+template <int KIND>
+__global__ __launch_bounds__(GS_THREADS, APG_FUSED_MIN_WAVES) void k_image_step_fused(
+    EnvArgs a, GlimpseGeo g, const void *pool, const int64_t *index, const float *__restrict__ act,
+    const float *__restrict__ pred, const int32_t *label, double *pos, apg_image_outputs out, float *hist, int upb,
+    FastDiv per_div, FastDiv s1_div, FastDiv side_div) {
+  __shared__ float s_lut[256];
+  __shared__ int64_t s_base[GS_MAX_UNITS];
+  extern __shared__ Axis s_ax[];  // [unit][rows s0 | columns s1], then (classify) the logits [unit][stride]
+  const int tid = threadIdx.x;
+  for (int v = tid; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
+  const int u0 = blockIdx.x * upb, nu = a.n - u0 < upb ? a.n - u0 : upb;
+  float *s_logit = reinterpret_cast<float *>(s_ax + (size_t)upb * (g.s0 + g.s1));
+  if constexpr (KIND == APG_IMAGE_CLASSIFY) {
+    const int k = a.k, stride = cls1_stride(k);
+    for (int q = tid; q < nu * k; q += GS_THREADS) {
+      const int r = q / k;
+      s_logit[r * stride + (q - r * k)] = pred[(size_t)u0 * k + q];
+    }
+  }
+  const uint32_t bad = gs_axes(g, index, [&](int u, int c) {
+    const int e = u0 + u;
+    double px = pos[2 * e], py = pos[2 * e + 1];
+    move_pos(a, act[2 * e], act[2 * e + 1], px, py);
+    return c ? py : px;
+  }, u0, nu, 1, side_div, s_ax, s_base);
+  __syncthreads();
+  gs_pixels(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
+  if (tid < nu) {
+    const int e = u0 + tid;
+    if constexpr (KIND == APG_IMAGE_CLASSIFY)
+      cls1_env(a, e, s_logit + tid * cls1_stride(a.k), act, label, pos, out, hist);
+    else
+      loc_env(a, e, act, pred, pos, out, hist);
+  }
+  if (bad) atomicOr(out.err, bad);
 }
 
 // ------------------------------------------------------------------ k_unique
@@ -1182,16 +1264,23 @@ int launch_uniform(apg_pcg64 *state, int64_t n, int cols, const double *low, con
   return check_launch("k_fill_uniform");
 }
 
+// Glimpse units (env x position) per k_glimpse_sep / k_image_step_fused workgroup: about APG_GLIMPSE_PPT
+// (default 4, clamped to [1, 16]: the Axis LDS stays far below 64 KiB) pixels per thread.  The output
+// does not depend on it.
+int glimpse_units_per_block(int per) {
+  static const int ppt = getenv("APG_GLIMPSE_PPT") ? std::max(1, std::min(16, atoi(getenv("APG_GLIMPSE_PPT")))) : 4;
+  return std::max(1, std::min(GS_MAX_UNITS, (ppt * GS_THREADS + per - 1) / per));
+}
+
 template <class PosT>
 int launch_glimpse(const GlimpseGeo &g, const void *pool, const int64_t *index, const PosT *pos, int n, int npos,
                    float *out, uint32_t *err, hipStream_t s) {
   const int64_t total = (int64_t)n * npos * g.s0 * g.s1;
   if (total >= (int64_t)1 << 31) return fail(APG_E_INVALID, "glimpse batch too large (>= 2**31 pixels)");
-  if (g.s0 <= GS_MAX_SIDE && g.s1 <= GS_MAX_SIDE && !getenv("APG_GLIMPSE_GENERIC")) {
+  static const bool generic = getenv("APG_GLIMPSE_GENERIC") != nullptr;
+  if (g.s0 <= GS_MAX_SIDE && g.s1 <= GS_MAX_SIDE && !generic) {
     const int per = g.s0 * g.s1, units = n * npos;
-    // pixels per thread of a workgroup (tuning knob APG_GLIMPSE_PPT; output does not depend on it)
-    static const int ppt = getenv("APG_GLIMPSE_PPT") ? std::max(1, atoi(getenv("APG_GLIMPSE_PPT"))) : 4;
-    const int upb = std::max(1, std::min(GS_MAX_UNITS, (ppt * GS_THREADS + per - 1) / per));
+    const int upb = glimpse_units_per_block(per);
     const size_t dyn = (size_t)upb * (g.s0 + g.s1) * sizeof(Axis);
     hipLaunchKernelGGL(k_glimpse_sep<PosT>, dim3(grid_for(units, upb)), dim3(GS_THREADS), dyn, s, g, pool, index, pos,
                        npos, units, upb, make_fastdiv((uint32_t)per), make_fastdiv((uint32_t)g.s1),
@@ -1438,8 +1527,30 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
   a.time_value = (float)(((double)t_new / (double)c->step_limit) * 2.0 - 1.0);
   a.loss_weight = !c->sparse ? 1.0f : (!prev_done && t_new >= c->step_limit ? 1.0f : 0.0f);
   a.copy_target = c->kind == APG_IMAGE_LOCALIZE && !prev_done ? st->target : nullptr;
-  if (c->kind == APG_IMAGE_CLASSIFY && c->num_classes <= CLS1_MAX_K && !getenv("APG_CLS_LANES8")) {
-    const size_t lds = (size_t)CLS1_ENVS * (c->num_classes + 1) * sizeof(float);
+  // tuning knobs, read once: APG_IMAGE_UNFUSED (two launches per step), APG_GLIMPSE_GENERIC, APG_CLS_LANES8
+  static const bool unfused = getenv("APG_IMAGE_UNFUSED") != nullptr, generic = getenv("APG_GLIMPSE_GENERIC") != nullptr,
+                    lanes8 = getenv("APG_CLS_LANES8") != nullptr;
+  const GlimpseGeo g = make_geo(c);
+  const bool fusable = !prev_done && !unfused && !generic && !lanes8 && g.s0 <= GS_MAX_SIDE && g.s1 <= GS_MAX_SIDE &&
+                       (c->kind == APG_IMAGE_LOCALIZE || c->num_classes <= CLS1_MAX_K);
+  if (fusable) {
+    const int per = g.s0 * g.s1;
+    const int upb = glimpse_units_per_block(per);
+    size_t dyn = (size_t)upb * (g.s0 + g.s1) * sizeof(Axis);
+    if (c->kind == APG_IMAGE_CLASSIFY) dyn += (size_t)upb * (c->num_classes + 2) * sizeof(float);
+    const dim3 grid(grid_for(n, upb)), block(GS_THREADS);
+    const FastDiv pd = make_fastdiv((uint32_t)per), sd = make_fastdiv((uint32_t)g.s1),
+                  sid = make_fastdiv((uint32_t)(g.s0 + g.s1));
+    if (c->kind == APG_IMAGE_LOCALIZE)
+      hipLaunchKernelGGL(k_image_step_fused<APG_IMAGE_LOCALIZE>, grid, block, dyn, s, a, g, st->pool, st->index, action,
+                         prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, sd, sid);
+    else
+      hipLaunchKernelGGL(k_image_step_fused<APG_IMAGE_CLASSIFY>, grid, block, dyn, s, a, g, st->pool, st->index, action,
+                         prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, sd, sid);
+    return check_launch("k_image_step_fused");  // the target glimpse only changes on the autoreset step
+  }
+  if (c->kind == APG_IMAGE_CLASSIFY && c->num_classes <= CLS1_MAX_K && !lanes8) {
+    const size_t lds = (size_t)CLS1_ENVS * (c->num_classes + 2) * sizeof(float);
     hipLaunchKernelGGL(k_image_env_cls1, dim3(grid_for(n, CLS1_ENVS)), dim3(CLS1_ENVS), lds, s, a, action, prediction,
                        st->label, st->pos, *out, st->stats_hist);
   } else if (c->kind == APG_IMAGE_CLASSIFY) {
