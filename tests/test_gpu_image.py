@@ -296,7 +296,16 @@ def test_image_env_matches_reference_trace(gpu, name):
 
 @pytest.mark.parametrize("kind,n,shape,sensor,k,steps", [("cls", 2048, (28, 28), (5, 5), 10, 40),
                                                          ("cls", 256, (64, 64, 3), (10, 10), 200, 20),
-                                                         ("loc", 48, (28, 28), (5, 5), 10, 36)])
+                                                         ("loc", 48, (28, 28), (5, 5), 10, 36),
+                                                         # k_image_env_cls1 / the fused step for K <= 16:
+                                                         # the < 8 sequential sum, k % 8 == 0 without a
+                                                         # tail, odd K (odd LDS stride), the K = 16 edge,
+                                                         # and a partial last workgroup (n % 128 != 0)
+                                                         ("cls", 2000, (28, 28), (5, 5), 2, 20),
+                                                         ("cls", 2000, (28, 28), (5, 5), 3, 20),
+                                                         ("cls", 2000, (28, 28), (5, 5), 8, 20),
+                                                         ("cls", 2000, (28, 28), (5, 5), 13, 20),
+                                                         ("cls", 2000, (28, 28), (5, 5), 16, 20)])
 def test_image_env_matches_oracle_at_scale(gpu, kind, n, shape, sensor, k, steps):
     import ap_gym_amd as ap
     from oracle import image_oracle as io
@@ -493,3 +502,30 @@ def test_image_loc_full_size_cfg5(gpu):
             assert np.array_equal(info["prediction"]["loss"][sel].cpu().numpy(), ri["prediction"]["loss"]), t
     env.check_errors()
     env.close()
+
+
+@pytest.mark.parametrize("knobs", [{"APG_GLIMPSE_PPT": "9"}, {"APG_CLS_LANES8": "1"}, {"APG_IMAGE_UNFUSED": "1"},
+                                   {"APG_GLIMPSE_PPT": "16", "APG_IMAGE_UNFUSED": "1"}])
+def test_tuning_knobs_do_not_change_results(gpu, tmp_path, knobs):
+    """The library reads its tuning knobs once per process, so each setting runs in a child process
+    (tests/knob_child.py) and must reproduce the default-knob child bit for bit: another glimpse
+    workgroup size, the 8-lane classification kernel for K <= 16, and the two-launch step."""
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+
+    def run(env_extra, name):
+        env = {k: v for k, v in os.environ.items() if not k.startswith("APG_")}
+        env.update(env_extra)
+        out = tmp_path / name
+        subprocess.run([sys.executable, os.path.join(here, "knob_child.py"), str(out)], env=env, check=True,
+                       timeout=300)
+        return np.load(out)
+
+    base = run({}, "base.npz")
+    got = run(knobs, "knob.npz")
+    assert set(base.files) == set(got.files)
+    for key in base.files:
+        assert np.array_equal(base[key], got[key]), key
