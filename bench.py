@@ -281,7 +281,8 @@ def pmc_table(workload: str, family: str, shape: dict):
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{workload}.json")), reverse=True):
         with open(path) as f:
             tj = json.load(f)
-        if tj.get("source_sha") == sha and tj.get("shape") == shape:
+        if (tj.get("source_sha") == sha and tj.get("shape") == shape and "step" in tj.get("per_launch", {})
+                and tj.get("hbm_bytes_per_launch", {}).get("step") is not None):
             return tj, os.path.relpath(path, ROOT)
     return None, None
 
@@ -415,7 +416,8 @@ def run_lidar(args, world, rank, dev):
         traffic = issue = None
         if tj is not None:
             hb = tj["hbm_bytes_per_launch"]
-            traffic = (hb["step"] * (len(timed) - reset_ev) + hb["reset_step"] * reset_ev) / len(timed)
+            reset_b_pmc = hb.get("reset_step") or hb["step"]  # a table without a reset step: no reset in the window
+            traffic = (hb["step"] * (len(timed) - reset_ev) + reset_b_pmc * reset_ev) / len(timed)
             issue = issue_fractions(tj["per_launch"]["step"], median_ms)
             issue["source"] = tpath
         out = {

@@ -20,6 +20,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -67,7 +68,7 @@ def main():
         for did in sorted(rows):
             kname, vals = rows[did]
             if wl in bench.LIDAR_WORKLOADS:
-                fused = "true>" in kname.replace(" ", "")
+                fused = re.search(r"k_lidar_step<\s*\d+\s*,\s*true", kname) is not None
                 cls = lidar_class(kname, ordinal if fused else None)
                 ordinal += 1 if fused else 0
             else:
