@@ -68,11 +68,122 @@ APG_DEV ScanOut scan_empty(float fpx, float fpy, float fqx, float fqy) {
   return o;
 }
 
+// Fast path of the walk when no crossing passes through a lattice point and the segment does not run
+// along a grid line.  Then every crossing is an edge crossing between the two cells before and after
+// it, so a crossing is a boundary node iff those cells differ, and the pieces are decided by the
+// sequence of visited cells: its runs of occupied cells are the line pieces, and the only possible
+// Point pieces are p and q themselves (an endpoint on the boundary whose adjacent interval is
+// outside; only endpoints on a grid line can be on the boundary).  Lines and points: the reference's
+// mixed-collection branch (|q - p|); one run: SCAN_LINE from its start; two or more: SCAN_MULTILINE,
+// whose minimum over the runs' f32 start distances is the first run's (any later run start lies >= 1
+// further along the ray: between two run starts lie an exit and so three distinct grid lines, two of
+// them parallel and one cell apart, which dwarfs the < 1e-4 rounding of the f32 distances); points
+// only: SCAN_POINT / SCAN_MULTIPOINT at distance 0 (the first point is p when p is one).  Returns false
+// (the caller runs the general walk) when a crossing turns out to be a lattice point or the segment is
+// collinear with a grid line; the exact orientation decides near-ties as in the general walk.
+template <class Rows>
+APG_DEV bool lidar_scan_fast(const Rows &rows, float fpx, float fpy, float fqx, float fqy, ScanOut &o) {
+  const int sx = (fqx > fpx) - (fqx < fpx), sy = (fqy > fpy) - (fqy < fpy);
+  const float flpx = floorf(fpx), flpy = floorf(fpy), flqx = floorf(fqx), flqy = floorf(fqy);
+  const bool pxi = flpx == fpx, pyi = flpy == fpy, qxi = flqx == fqx, qyi = flqy == fqy;
+  if ((sx == 0 && pxi) || (sy == 0 && pyi)) return false;
+  const int ipx = (int)flpx, ipy = (int)flpy, iqx = (int)flqx, iqy = (int)flqy;
+  // first interval's cell (cx, cy); the next x-line to cross is a = cx + ux (likewise b = cy + vy) and
+  // the lines strictly inside the segment number nxl / nyl (q's own grid line is not crossed)
+  const int ux = sx > 0 ? 1 : 0, vy = sy > 0 ? 1 : 0;
+  const int cx = (sx < 0 && pxi) ? ipx - 1 : ipx;
+  int cy = (sy < 0 && pyi) ? ipy - 1 : ipy;
+  int a = cx + ux, b = cy + vy;
+  int nxl = sx > 0 ? (qxi ? iqx - 1 : iqx) - a + 1 : (sx < 0 ? a - iqx : 0);
+  int nyl = sy > 0 ? (qyi ? iqy - 1 : iqy) - b + 1 : (sy < 0 ? b - iqy : 0);
+  nxl = nxl < 0 ? 0 : nxl;
+  nyl = nyl < 0 ? 0 : nyl;
+  const int a_end = a + sx * nxl, b_end = b + sy * nyl;  // no x-crossing left once a == a_end
+  const int sd = sy > 0 ? 1 : -1;
+  int sh = cx - rows.x0;  // bit of the current column in a window row
+  uint32_t r_c = rows.row(cy), r_o = rows.row(cy + sd), r_p = rows.row(cy + 2 * sd);
+  const bool cur0 = (r_c >> sh) & 1u;
+  bool cur = cur0;
+  int n_runs = cur ? 1 : 0;
+  // start node of the first run: x-crossing (true) or y-crossing on the edge from lattice point (na, nb)
+  bool n_x = false;
+  int na = 0, nb = 0;
+  const float sxy = (float)(sx * sy);
+  for (int left = nxl + nyl; left > 0; left--) {
+    const bool hx = a != a_end, hy = b != b_end;
+    const float fa = (float)a, fb = (float)b;
+    const float dl = __fmul_rn(__fsub_rn(fpx, fa), __fsub_rn(fqy, fb));
+    const float dr = __fmul_rn(__fsub_rn(fpy, fb), __fsub_rn(fqx, fa));
+    const float dsx = __fmul_rn(__fsub_rn(dl, dr), sxy);
+    const float bound = 1.7881398e-7f * __fadd_rn(fabsf(dl), fabsf(dr));
+    int c = dsx > bound ? -1 : (-dsx > bound ? 1 : 0);
+    if (hx && hy && c == 0) {
+      c = -orient(fpx, fpy, fqx, fqy, (double)a, (double)b) * sx * sy;
+      if (c == 0) return false;  // through a lattice point
+    }
+    const bool takex = (hx && hy) ? c < 0 : hx;
+    const int ea = takex ? a : a - ux, eb = takex ? b - vy : b;  // crossed edge's lower-left lattice point
+    const int dx = takex ? sx : 0, dy = takex ? 0 : sy;  // selects, not branches: the lanes diverge here
+    a += dx;
+    sh += dx;
+    b += dy;
+    cy += dy;
+    r_c = takex ? r_c : r_o;
+    r_o = takex ? r_o : r_p;
+    r_p = rows.row(cy + 2 * sd);  // unchanged row after an x-crossing; consumed a crossing later at the earliest
+    const bool in = (r_c >> sh) & 1u;
+    const bool first = in && !cur && n_runs == 0;
+    n_x = first ? takex : n_x;
+    na = first ? ea : na;
+    nb = first ? eb : nb;
+    n_runs += (in && !cur) ? 1 : 0;
+    cur = in;
+  }
+  // endpoints on the boundary next to an outside interval are Point pieces
+  int n_points = 0;
+  if ((pxi || pyi) && !cur0 && quad_status(rows, pxi ? ipx - 1 : ipx, pxi ? 1 : 0, pyi ? ipy - 1 : ipy, pyi ? 1 : 0) == 1u)
+    n_points++;
+  if ((qxi || qyi) && !cur && quad_status(rows, qxi ? iqx - 1 : iqx, qxi ? 1 : 0, qyi ? iqy - 1 : iqy, qyi ? 1 : 0) == 1u)
+    n_points++;
+  o.kind = SCAN_EMPTY;
+  if (n_runs == 0 || n_points > 0) {
+    o.dist = norm_f32(__fsub_rn(fqx, fpx), __fsub_rn(fqy, fpy));
+    if (n_runs > 0) {
+      o.kind = SCAN_COLLECTION;
+    } else if (n_points > 0) {
+      o.kind = n_points == 1 ? SCAN_POINT : SCAN_MULTIPOINT;
+      o.dist = 0.0f;  // POINT: 0; MULTIPOINT: max(min(|p - p|, ...) - 1e-3, 0) with p the first point
+    }
+    return true;
+  }
+  double x = fpx, y = fpy;
+  if (!cur0)
+    geos_intersection((double)fpx, (double)fpy, (double)fqx, (double)fqy, (double)na, (double)nb,
+                      (double)(n_x ? na : na + 1), (double)(n_x ? nb + 1 : nb), x, y);
+  if (n_runs == 1) {
+    o.kind = SCAN_LINE;
+    const double dx = __dsub_rn(x, (double)fpx), dy = __dsub_rn(y, (double)fpy);
+    const double d = __dsub_rn(__dsqrt_rn(__fma_rn(dy, dy, __dmul_rn(dx, dx))), 1e-3);
+    o.dist = (float)(d > 0.0 ? d : 0.0);
+  } else {
+    o.kind = SCAN_MULTILINE;
+    const float d = __fsub_rn(norm_f32(__fsub_rn((float)x, fpx), __fsub_rn((float)y, fpy)), 0.001f);
+    o.dist = d > 0.0f ? d : 0.0f;
+  }
+  return true;
+}
+
 // kContact (render path): also report the reference's contact point in *contact; the hot path
 // instantiates kContact = false, which compiles to the distance-only walk.
 template <class Rows, bool kContact = false>
 APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fqx, float fqy,
                                 ScanContact *contact = nullptr) {
+#ifndef APG_X_NO_FAST_WALK  // tuning / test builds: general walk only
+  if constexpr (!kContact) {
+    ScanOut fo;
+    if (lidar_scan_fast(rows, fpx, fpy, fqx, fqy, fo)) return fo;
+  }
+#endif
   const double px = fpx, py = fpy, qx = fqx, qy = fqy;
   const int sx = (fqx > fpx) - (fqx < fpx), sy = (fqy > fpy) - (fqy < fpy);
   const float flpx = floorf(fpx), flpy = floorf(fpy), flqx = floorf(fqx), flqy = floorf(fqy);
@@ -204,10 +315,9 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
       rx -= takex ? 1 : 0;
       ry -= takey ? 1 : 0;
       cur_in = in_after;
-      const uint32_t r_next = rows.row(cy + 2 * sd);  // unconditional: consumed a crossing later at the earliest
       r_c = takey ? r_o : r_c;
       r_o = takey ? r_p : r_o;
-      r_p = takey ? r_next : r_p;
+      r_p = rows.row(cy + 2 * sd);  // the same row after an x-crossing: no select on the fresh read
     }
   } else {
     // along a grid line (colv / colh): every crossing is a lattice point, intervals touch two cells
@@ -243,10 +353,9 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
       xi += takex ? 1 : 0;
       yi += takey ? 1 : 0;
       cur_in = in_after;
-      const uint32_t r_next = rows.row(ncy + 2 * sd);
       r_c = takey ? r_o : r_c;
       r_o = takey ? r_p : r_o;
-      r_p = takey ? r_next : r_p;
+      r_p = rows.row(ncy + 2 * sd);
     }
   }
   // q: always a node

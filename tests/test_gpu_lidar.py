@@ -140,6 +140,53 @@ def test_device_scan_matches_oracle_degenerate_sweep(gpu, oracle_mod):
             assert od == dist[i] and ok == kinds[i], (kind, i, segs[i], od, dist[i], ok, kinds[i])
 
 
+def test_device_scan_matches_oracle_generic_and_near_grid(gpu, oracle_mod):
+    """The walk's fast path (p, q off the grid lines, no lattice crossing: runs of occupied cells decide
+    LINE / MULTILINE / EMPTY) and its hand-over to the general walk: uniform segments up to 12 cells
+    long on rooms, mazes and 35 %-noise maps (many runs: MULTILINE), endpoints one ulp off a grid line,
+    directions one ulp off an axis or a diagonal, and segments through lattice points."""
+    rng = np.random.default_rng(11)
+    size = 64
+    noise = [rng.random((size, size)) < 0.35 for _ in range(2)]
+    maps = np.stack([oracle_mod.rooms_map(0, size), oracle_mod.rooms_map(1, size),
+                     np.pad(oracle_mod.maze_map(2, size - 1), ((0, 1), (0, 1))), *noise]).astype(bool)
+    n = 60000
+    mi = rng.integers(0, len(maps), n).astype(np.int32)
+    p = rng.uniform(14, size - 14, (n, 2)).astype(np.float32)
+    ang = rng.uniform(0, 2 * np.pi, n)
+    ln = rng.uniform(0.05, 12, n)
+    d = np.stack([np.cos(ang) * ln, np.sin(ang) * ln], 1).astype(np.float32)
+    k = np.arange(n) % 8
+    # endpoints one ulp beside a grid line (either side), and exactly on one (general walk)
+    up = np.nextafter(np.floor(p), np.float32(np.inf)).astype(np.float32)
+    dn = np.nextafter(np.floor(p), np.float32(-np.inf)).astype(np.float32)
+    p = np.where((k == 1)[:, None], up, p)
+    p = np.where((k == 2)[:, None], dn, p)
+    p = np.where((k == 3)[:, None], np.floor(p), p)
+    # directions one ulp off an axis / the diagonal, and exact diagonals from lattice-aligned p
+    tiny = np.float32(1e-7)
+    d = np.where((k == 4)[:, None], np.stack([d[:, 0], np.full(n, tiny, np.float32)], 1), d)
+    d = np.where((k == 5)[:, None], np.stack([ln.astype(np.float32), np.nextafter(ln.astype(np.float32), 0)], 1), d)
+    p = np.where((k == 6)[:, None], (np.floor(p) + np.float32(0.5)), p)
+    d = np.where((k == 6)[:, None], np.float32(3.0) * np.sign(d).astype(np.float32), d)
+    q = (p + d).astype(np.float32)
+    # q on a grid line (x, or both coordinates), and p on a grid line with a generic direction
+    q = np.where((k == 7)[:, None], np.stack([np.floor(q[:, 0]), np.where(np.arange(n) % 16 == 7,
+                                                                          np.floor(q[:, 1]), q[:, 1])], 1), q)
+    segs = np.concatenate([p, q], axis=1).astype(np.float32)
+    dist, kinds = _scan_gpu(gpu, maps, mi, segs)
+    bad = []
+    counts = np.zeros(6, int)
+    for i in range(n):
+        od, ok = oracle_mod.lidar_scan(maps[mi[i]], segs[i, :2], segs[i, 2:])
+        counts[ok] += 1
+        if not (od == dist[i] and ok == kinds[i]):
+            bad.append((i, segs[i], od, dist[i], ok, kinds[i]))
+    assert not bad, (len(bad), bad[:5])
+    assert counts[1] > 1000 and counts[2] > 1000 and counts[0] > 1000, counts  # LINE, MULTILINE, EMPTY
+    assert counts[3] > 0 and counts[5] > 0, counts  # POINT, COLLECTION (endpoints on the boundary)
+
+
 @pytest.mark.parametrize("name", sorted(ENV_CASES))
 def test_vector_env_matches_reference_trace(gpu, name):
     import ap_gym_amd as ap
