@@ -251,6 +251,13 @@ APG_DEV void geos_intersection(double p1x_, double p1y_, double p2x_, double p2y
 APG_DEV float f32_div(float a, float b) { return (float)__ddiv_rn((double)a, (double)b); }
 APG_DEV float f32_sqrt(float a) { return (float)__dsqrt_rn((double)a); }
 
+// a / b for a divisor fixed per launch, from inv = 1.0 / (double)b (correctly rounded f64): the f64
+// product is within 2^-52 (relative) of a / b, while a quotient of two f32 values is never an f32
+// rounding midpoint (odd 25-bit x 24-bit significands need >= 25 bits) and, when not one, lies >= 2^-49
+// (relative) from it -- so rounding the product to f32 gives the correctly rounded quotient, as
+// f32_div does (normal f32 results; the callers' quotients are 0 or >= 2^-30).
+APG_DEV float f32_div_inv(float a, double inv) { return (float)__dmul_rn((double)a, inv); }
+
 // numpy norm of a float32 2-vector (OpenBLAS sdot: f32 products, f32 sum) then f32 sqrt.
 APG_DEV float norm_f32(float dx, float dy) {
   float s = __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));

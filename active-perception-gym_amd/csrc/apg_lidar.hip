@@ -763,14 +763,14 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           bool term = pos0 < 0.0f || pos1 < 0.0f || pos0 >= mapw || pos1 >= maph;
           pos0 = fminf(fmaxf(pos0, 0.0f), mapw);
           pos1 = fminf(fmaxf(pos1, 0.0f), maph);
-          const float tgx = __fsub_rn(__fmul_rn(f32_div(lpx, mapw), 2.0f), 1.0f);
-          const float tgy = __fsub_rn(__fmul_rn(f32_div(lpy, maph), 2.0f), 1.0f);
+          const float tgx = __fsub_rn(__fmul_rn(f32_div_inv(lpx, 1.0 / (double)mapw), 2.0f), 1.0f);
+          const float tgy = __fsub_rn(__fmul_rn(f32_div_inv(lpy, 1.0 / (double)maph), 2.0f), 1.0f);
           const int el2 = pf_el + 1;
           pf_el = el2;
           S.elapsed[e] = el2;
           if (el2 >= P.step_limit) term = true;  // TimeLimit(issue_termination=True)
           const float ex = __fsub_rn(prx, tgx), ey = __fsub_rn(pry, tgy);
-          const float mse = f32_div(__fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey)), 2.0f);
+          const float mse = __fmul_rn(__fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey)), 0.5f);  // exact / 2
           const float loss = __fadd_rn(__fmul_rn(mse, P.loss_scale), P.loss_offset);
 #ifdef APG_X_NO_STATS  // tuning experiment only (wrong results)
           if (false) {
@@ -805,8 +805,10 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       if (O.reset_mask) O.reset_mask[e] = was_reset;
       // odometry (:263-270) and TimeLimit time_step (time_limit.py:113-116)
       const float ox = __fsub_rn(pos0, ipx), oy = __fsub_rn(pos1, ipy);
-      O.odometry[2 * e] = __fsub_rn(__fmul_rn(f32_div(__fadd_rn(ox, mapw), __fadd_rn(mapw, mapw)), 2.0f), 1.0f);
-      O.odometry[2 * e + 1] = __fsub_rn(__fmul_rn(f32_div(__fadd_rn(oy, maph), __fadd_rn(maph, maph)), 2.0f), 1.0f);
+      O.odometry[2 * e] =
+          __fsub_rn(__fmul_rn(f32_div_inv(__fadd_rn(ox, mapw), 1.0 / (double)__fadd_rn(mapw, mapw)), 2.0f), 1.0f);
+      O.odometry[2 * e + 1] =
+          __fsub_rn(__fmul_rn(f32_div_inv(__fadd_rn(oy, maph), 1.0 / (double)__fadd_rn(maph, maph)), 2.0f), 1.0f);
       O.time_step[e] = (float)(2.0 * (double)pf_el / (double)P.step_limit - 1.0);
       s_pos[el][0] = pos0;
       s_pos[el][1] = pos1;
@@ -819,75 +821,73 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
 
   // ---------------- phase 2a: lane = env, wave = beam index (all 64 lanes of a wave cast the same
   // beam direction).  Beams whose bounding box holds no occupied cell are SCAN_EMPTY and finish
-  // here; the others are queued (env, beam) in LDS, grouped by beam, for 2b.
+  // here; the others are queued (env, beam) in LDS, grouped by beam, for 2b.  Up to MAX_STAGED_BEAMS
+  // beams (every configuration of the reference) the lidar rows are staged in LDS; the instance for more
+  // beams walks in place and stores straight to HBM.
   const int el = tid & (EPB - 1), e = base + el;
-  const bool staged = P.beams <= MAX_STAGED_BEAMS;
   const float px = s_pos[el][0], py = s_pos[el][1];
   const RowsWindow rw{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
+  const double inv_range = 1.0 / (double)P.range;
+  auto beam_value = [&](float d) { return fminf(fmaxf(f32_div_inv(d, inv_range), -1.0f), 1.0f); };
+  if (P.beams > MAX_STAGED_BEAMS) {
+    for (int beam = tid / EPB; beam < P.beams; beam += T / EPB) {
+      if (e < P.n) {
+        const float qx = __fadd_rn(px, S.beam_dirs[2 * beam]), qy = __fadd_rn(py, S.beam_dirs[2 * beam + 1]);
+        O.lidar[(size_t)e * P.beams + beam] = beam_value(lidar_scan(rw, px, py, qx, qy).dist);
+      }
+    }
+    return;
+  }
   for (int beam = tid / EPB; beam < P.beams; beam += T / EPB) {
     bool walk = false;
     if (e < P.n) {
-      const float dx = staged ? s_dirs[beam][0] : S.beam_dirs[2 * beam];
-      const float dy = staged ? s_dirs[beam][1] : S.beam_dirs[2 * beam + 1];
-      const float qx = __fadd_rn(px, dx), qy = __fadd_rn(py, dy);
+      const float qx = __fadd_rn(px, s_dirs[beam][0]), qy = __fadd_rn(py, s_dirs[beam][1]);
       walk = scan_may_hit(rw, px, py, qx, qy);
-      if (!walk || !staged) {
 #ifdef APG_X_NO_EMPTY_DIST  // tuning experiment only (wrong results)
-        const float d = walk ? lidar_scan_walk(rw, px, py, qx, qy).dist : P.range;
+      if (!walk) s_lid[el * LS + beam] = 1.0f;
 #else
-        const float d = walk ? lidar_scan_walk(rw, px, py, qx, qy).dist : scan_empty(px, py, qx, qy).dist;
+      if (!walk) s_lid[el * LS + beam] = beam_value(scan_empty(px, py, qx, qy).dist);
 #endif
-        const float v = fminf(fmaxf(f32_div(d, P.range), -1.0f), 1.0f);
-        if (staged)
-          s_lid[el * LS + beam] = v;
-        else
-          O.lidar[(size_t)e * P.beams + beam] = v;
-      }
     }
-    if (staged) {
-      const unsigned long long m = __ballot(walk);
-      int qbase = 0;
-      if (lane == 0 && m) qbase = atomicAdd(&s_cnt[1], __popcll(m));
-      qbase = __shfl(qbase, 0);
-      if (walk) s_queue[qbase + __popcll(m & ((1ULL << lane) - 1ULL))] = (uint16_t)((beam << 8) | el);
+    const unsigned long long m = __ballot(walk);
+    int qbase = 0;
+    if (lane == 0 && m) qbase = atomicAdd(&s_cnt[1], __popcll(m));
+    qbase = __shfl(qbase, 0);
+    if (walk) s_queue[qbase + __popcll(m & ((1ULL << lane) - 1ULL))] = (uint16_t)((beam << 8) | el);
+  }
+  __syncthreads();
+  STEP_MARK(3)
+  STEP_STOP(3)
+  // ---------------- phase 2b: the queued scans, densely over the workgroup's waves; each wave takes
+  // the next 64 entries from a shared cursor, so waves with short walks take more of them
+  const int nq = s_cnt[1];
+  for (;;) {
+    int start = 0;
+    if (lane == 0) start = atomicAdd(&s_cnt[2], 64);
+    start = __shfl(start, 0);
+    if (start >= nq) break;
+    const int i = start + lane;
+    if (i < nq) {
+      const int ent = s_queue[i], qe = ent & 255, beam = ent >> 8;
+      const float qpx = s_pos[qe][0], qpy = s_pos[qe][1];
+      const RowsWindow qrw{&s_win[qe * WIN_STRIDE], s_x0[qe], s_y0[qe], P.wrows};
+      const float qx = __fadd_rn(qpx, s_dirs[beam][0]), qy = __fadd_rn(qpy, s_dirs[beam][1]);
+      s_lid[qe * LS + beam] = beam_value(lidar_scan_walk(qrw, qpx, qpy, qx, qy).dist);
     }
   }
-  if (staged) {
-    __syncthreads();
-    STEP_MARK(3)
-  STEP_STOP(3)
-    // ---------------- phase 2b: the queued scans, densely over the workgroup's waves; each wave takes
-    // the next 64 entries from a shared cursor, so waves with short walks take more of them
-    const int nq = s_cnt[1];
-    for (;;) {
-      int start = 0;
-      if (lane == 0) start = atomicAdd(&s_cnt[2], 64);
-      start = __shfl(start, 0);
-      if (start >= nq) break;
-      const int i = start + lane;
-      if (i < nq) {
-        const int ent = s_queue[i], qe = ent & 255, beam = ent >> 8;
-        const float qpx = s_pos[qe][0], qpy = s_pos[qe][1];
-        const RowsWindow qrw{&s_win[qe * WIN_STRIDE], s_x0[qe], s_y0[qe], P.wrows};
-        const float qx = __fadd_rn(qpx, s_dirs[beam][0]), qy = __fadd_rn(qpy, s_dirs[beam][1]);
-        const float d = lidar_scan_walk(qrw, qpx, qpy, qx, qy).dist;
-        s_lid[qe * LS + beam] = fminf(fmaxf(f32_div(d, P.range), -1.0f), 1.0f);
-      }
-    }
-    __syncthreads();
-    STEP_MARK(4)
+  __syncthreads();
+  STEP_MARK(4)
   STEP_STOP(4)
-    const int nenv = P.n - base < EPB ? P.n - base : EPB;
-    const int B = P.beams, dl = T / B, db = T - dl * B;  // (env, beam) of element i advanced without divisions
-    int l = tid / B, beam = tid - l * B;
-    for (int i = tid; i < nenv * B; i += T) {
-      O.lidar[(size_t)base * B + i] = s_lid[l * LS + beam];
-      l += dl;
-      beam += db;
-      if (beam >= B) {
-        beam -= B;
-        l++;
-      }
+  const int nenv = P.n - base < EPB ? P.n - base : EPB;
+  const int B = P.beams, dl = T / B, db = T - dl * B;  // (env, beam) of element i advanced without divisions
+  int l = tid / B, beam = tid - l * B;
+  for (int i = tid; i < nenv * B; i += T) {
+    O.lidar[(size_t)base * B + i] = s_lid[l * LS + beam];
+    l += dl;
+    beam += db;
+    if (beam >= B) {
+      beam -= B;
+      l++;
     }
   }
 #ifdef APG_STEP_PROFILE

@@ -5,7 +5,7 @@ R=$PWD
 V=$R/active-perception-gym_amd/ap_gym_amd/_lib/variants
 O=$R/gpurun_out/phase2
 rm -rf $O; mkdir -p $O
-for lib in prof prof_nofast; do
+for lib in prof; do
   APG_LIBRARY=$V/lib$lib.so timeout -k 10 120 python tools/step_phase_profile.py > $O/$lib.log 2>&1
   echo "$lib ok"
 done
