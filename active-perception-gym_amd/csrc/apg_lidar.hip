@@ -1092,7 +1092,7 @@ int launch_map_generate_any(const Geo &g, const uint64_t *idx, int n, uint64_t *
 // Dynamic LDS of a k_lidar_step instance: windows + staged lidar rows + walk queue; fused rooms resets
 // use the same bytes first for the primitives and each wave's map rows.
 size_t step_lds_bytes(int epb, int beams) {
-  size_t b = (size_t)epb * WIN_STRIDE * sizeof(uint32_t);
+  size_t b = ((size_t)epb * WIN_STRIDE + 8) * sizeof(uint32_t);  // + RowsWindow::or_rows's over-read
   if (beams <= MAX_STAGED_BEAMS) b += (size_t)epb * (beams + 1) * sizeof(float) + (size_t)epb * beams * sizeof(uint16_t);
   return b;
 }

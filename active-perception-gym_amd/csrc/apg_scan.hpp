@@ -56,9 +56,7 @@ APG_DEV bool scan_may_hit(const Rows &rows, float fpx, float fpy, float fqx, flo
   const int j0 = (int)ceilf(fminf(fpy, fqy)) - 1, j1 = (int)floorf(fmaxf(fpy, fqy));
   const int wdt = i1 - i0 + 1;  // <= lidar range + 2 < 32
   const uint32_t mask = ((1u << wdt) - 1u) << (i0 - rows.x0);
-  uint32_t acc = 0u;
-  for (int j = j0; j <= j1; j++) acc |= rows.row(j);
-  return (acc & mask) != 0u;
+  return (rows.or_rows(j0, j1) & mask) != 0u;
 }
 
 APG_DEV ScanOut scan_empty(float fpx, float fpy, float fqx, float fqy) {
@@ -460,6 +458,21 @@ struct RowsWindow {  // 32-row x 32-column window staged in LDS (rows [y0, y0+32
   const uint32_t *win;  // every access inside the window (see k_lidar_step), so no bounds test
   int x0, y0, nrows;
   APG_DEV uint32_t row(int y) const { return win[(unsigned)(y - y0) & 31u]; }
+  // OR of rows [j0, j1] (inside the window): eight loads at immediate offsets from row j0, masked past j1
+  // (they may read up to 7 words beyond the window: the LDS layout pads the last one), a loop only for
+  // boxes taller than 8 rows
+  APG_DEV uint32_t or_rows(int j0, int j1) const {
+    const uint32_t *w = win + (j0 - y0);
+    const int h = j1 - j0 + 1;
+    uint32_t acc = 0u;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+      const uint32_t v = w[t];
+      acc |= t < h ? v : 0u;
+    }
+    for (int t = 8; t < h; t++) acc |= w[t];
+    return acc;
+  }
 };
 
 struct RowsGlobal {  // bit rows in global memory, read through a 32-column window at x0
@@ -468,6 +481,11 @@ struct RowsGlobal {  // bit rows in global memory, read through a 32-column wind
   APG_DEV uint32_t row(int y) const {
     if ((unsigned)y >= (unsigned)h) return 0u;
     return extract_window_row(occ + (size_t)y * wpr, wpr, x0);
+  }
+  APG_DEV uint32_t or_rows(int j0, int j1) const {
+    uint32_t acc = 0u;
+    for (int j = j0; j <= j1; j++) acc |= row(j);
+    return acc;
   }
 };
 
