@@ -66,6 +66,62 @@ APG_DEV ScanOut scan_empty(float fpx, float fpy, float fqx, float fqy) {
   return o;
 }
 
+// Result of a walk without lattice crossings from its runs of occupied cells (see lidar_scan_fast):
+// n_runs runs, whether the first / last visited cell is occupied, and the crossed edge (from lattice
+// point (na, nb), vertical when n_x) where the first run starts unless it starts at p.  Endpoints on a
+// grid line can be Point pieces.  One f64 square root serves every outcome.
+template <class Rows>
+APG_DEV ScanOut scan_runs_result(const Rows &rows, float fpx, float fpy, float fqx, float fqy, int n_runs, bool cur0,
+                                 bool cur_last, bool n_x, int na, int nb) {
+  const float flpx = floorf(fpx), flpy = floorf(fpy), flqx = floorf(fqx), flqy = floorf(fqy);
+  const bool pxi = flpx == fpx, pyi = flpy == fpy, qxi = flqx == fqx, qyi = flqy == fqy;
+  // endpoints on the boundary next to an outside interval are Point pieces
+  int n_points = 0;
+  if ((pxi || pyi) && !cur0 &&
+      quad_status(rows, (int)flpx - (pxi ? 1 : 0), pxi ? 1 : 0, (int)flpy - (pyi ? 1 : 0), pyi ? 1 : 0) == 1u)
+    n_points++;
+  if ((qxi || qyi) && !cur_last &&
+      quad_status(rows, (int)flqx - (qxi ? 1 : 0), qxi ? 1 : 0, (int)flqy - (qyi ? 1 : 0), qyi ? 1 : 0) == 1u)
+    n_points++;
+  const bool hit = n_runs > 0 && n_points == 0;  // LINE / MULTILINE
+  double x = fpx, y = fpy;
+  if (hit && !cur0)
+    geos_intersection((double)fpx, (double)fpy, (double)fqx, (double)fqy, (double)na, (double)nb,
+                      (double)(n_x ? na : na + 1), (double)(n_x ? nb + 1 : nb), x, y);
+  // LINE: |c - p| in f64; MULTILINE: |f32(c) - p| in f32; EMPTY / COLLECTION: |q - p| in f32
+  const bool line = hit && n_runs == 1;
+  double arg;
+  if (line) {
+    const double dx = __dsub_rn(x, (double)fpx), dy = __dsub_rn(y, (double)fpy);
+    arg = __fma_rn(dy, dy, __dmul_rn(dx, dx));
+  } else {
+    const float ex = hit ? __fsub_rn((float)x, fpx) : __fsub_rn(fqx, fpx);
+    const float ey = hit ? __fsub_rn((float)y, fpy) : __fsub_rn(fqy, fpy);
+    arg = (double)__fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey));
+  }
+  const double r = __dsqrt_rn(arg);
+  ScanOut o;
+  if (line) {
+    o.kind = SCAN_LINE;
+    const double d = __dsub_rn(r, 1e-3);
+    o.dist = (float)(d > 0.0 ? d : 0.0);
+  } else if (hit) {
+    o.kind = SCAN_MULTILINE;
+    const float d = __fsub_rn((float)r, 0.001f);
+    o.dist = d > 0.0f ? d : 0.0f;
+  } else if (n_runs > 0) {
+    o.kind = SCAN_COLLECTION;  // lines and points: the reference's `else` branch (no hit)
+    o.dist = (float)r;
+  } else if (n_points > 0) {
+    o.kind = n_points == 1 ? SCAN_POINT : SCAN_MULTIPOINT;
+    o.dist = 0.0f;  // POINT: 0; MULTIPOINT: max(min(|p - p|, ...) - 1e-3, 0), p being the first point
+  } else {
+    o.kind = SCAN_EMPTY;
+    o.dist = (float)r;
+  }
+  return o;
+}
+
 // Fast path of the walk when no crossing passes through a lattice point and the segment does not run
 // along a grid line.  Then every crossing is an edge crossing between the two cells before and after
 // it, so a crossing is a boundary node iff those cells differ, and the pieces are decided by the
@@ -137,37 +193,7 @@ APG_DEV bool lidar_scan_fast(const Rows &rows, float fpx, float fpy, float fqx, 
     n_runs += (in && !cur) ? 1 : 0;
     cur = in;
   }
-  // endpoints on the boundary next to an outside interval are Point pieces
-  int n_points = 0;
-  if ((pxi || pyi) && !cur0 && quad_status(rows, pxi ? ipx - 1 : ipx, pxi ? 1 : 0, pyi ? ipy - 1 : ipy, pyi ? 1 : 0) == 1u)
-    n_points++;
-  if ((qxi || qyi) && !cur && quad_status(rows, qxi ? iqx - 1 : iqx, qxi ? 1 : 0, qyi ? iqy - 1 : iqy, qyi ? 1 : 0) == 1u)
-    n_points++;
-  o.kind = SCAN_EMPTY;
-  if (n_runs == 0 || n_points > 0) {
-    o.dist = norm_f32(__fsub_rn(fqx, fpx), __fsub_rn(fqy, fpy));
-    if (n_runs > 0) {
-      o.kind = SCAN_COLLECTION;
-    } else if (n_points > 0) {
-      o.kind = n_points == 1 ? SCAN_POINT : SCAN_MULTIPOINT;
-      o.dist = 0.0f;  // POINT: 0; MULTIPOINT: max(min(|p - p|, ...) - 1e-3, 0) with p the first point
-    }
-    return true;
-  }
-  double x = fpx, y = fpy;
-  if (!cur0)
-    geos_intersection((double)fpx, (double)fpy, (double)fqx, (double)fqy, (double)na, (double)nb,
-                      (double)(n_x ? na : na + 1), (double)(n_x ? nb + 1 : nb), x, y);
-  if (n_runs == 1) {
-    o.kind = SCAN_LINE;
-    const double dx = __dsub_rn(x, (double)fpx), dy = __dsub_rn(y, (double)fpy);
-    const double d = __dsub_rn(__dsqrt_rn(__fma_rn(dy, dy, __dmul_rn(dx, dx))), 1e-3);
-    o.dist = (float)(d > 0.0 ? d : 0.0);
-  } else {
-    o.kind = SCAN_MULTILINE;
-    const float d = __fsub_rn(norm_f32(__fsub_rn((float)x, fpx), __fsub_rn((float)y, fpy)), 0.001f);
-    o.dist = d > 0.0f ? d : 0.0f;
-  }
+  o = scan_runs_result(rows, fpx, fpy, fqx, fqy, n_runs, cur0, cur, n_x, na, nb);
   return true;
 }
 

@@ -169,6 +169,16 @@ def test_device_scan_matches_oracle_generic_and_near_grid(gpu, oracle_mod):
     d = np.where((k == 5)[:, None], np.stack([ln.astype(np.float32), np.nextafter(ln.astype(np.float32), 0)], 1), d)
     p = np.where((k == 6)[:, None], (np.floor(p) + np.float32(0.5)), p)
     d = np.where((k == 6)[:, None], np.float32(3.0) * np.sign(d).astype(np.float32), d)
+    # axis-parallel segments (the slide scans' shape): vertical / horizontal, from generic points, from
+    # points with the travel coordinate on a grid line, and along a grid line (general walk)
+    i = np.arange(n)
+    sgn = np.where(rng.random(n) < 0.5, -1, 1).astype(np.float32)
+    lf = (ln * sgn).astype(np.float32)
+    zero = np.zeros(n, np.float32)
+    d = np.where((i % 16 == 0)[:, None], np.stack([zero, lf], 1), d)
+    d = np.where((i % 16 == 8)[:, None], np.stack([lf, zero], 1), d)
+    p = np.where((i % 64 == 24)[:, None], np.stack([np.floor(p[:, 0]), p[:, 1]], 1), p)
+    p = np.where((i % 64 == 48)[:, None], np.floor(p), p)
     q = (p + d).astype(np.float32)
     # q on a grid line (x, or both coordinates), and p on a grid line with a generic direction
     q = np.where((k == 7)[:, None], np.stack([np.floor(q[:, 0]), np.where(np.arange(n) % 16 == 7,

@@ -7,7 +7,7 @@ rm -rf $O; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 for lib in default $(ls $R/active-perception-gym_amd/ap_gym_amd/_lib/variants/*.so); do
   if [ $lib = default ]; then unset APG_LIBRARY; name=default; else export APG_LIBRARY=$lib; name=$(basename $lib .so); fi
-  timeout -s KILL 90 rocprofv3 --kernel-trace --output-format csv -d $O/$name -o run -- python3 $R/tools/phase_pmc.py > $O/$name.log 2>&1
+  STEPS=80 timeout -s KILL 90 rocprofv3 --kernel-trace --output-format csv -d $O/$name -o run -- python3 $R/tools/phase_pmc.py > $O/$name.log 2>&1
   python3 - $O/$name <<'PY'
 import csv, glob, sys, numpy as np
 f = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
