@@ -146,54 +146,57 @@ APG_DEV bool lidar_scan_fast(const Rows &rows, float fpx, float fpy, float fqx, 
   // the lines strictly inside the segment number nxl / nyl (q's own grid line is not crossed)
   const int ux = sx > 0 ? 1 : 0, vy = sy > 0 ? 1 : 0;
   const int cx = (sx < 0 && pxi) ? ipx - 1 : ipx;
-  int cy = (sy < 0 && pyi) ? ipy - 1 : ipy;
+  const int cy = (sy < 0 && pyi) ? ipy - 1 : ipy;
   int a = cx + ux, b = cy + vy;
   int nxl = sx > 0 ? (qxi ? iqx - 1 : iqx) - a + 1 : (sx < 0 ? a - iqx : 0);
   int nyl = sy > 0 ? (qyi ? iqy - 1 : iqy) - b + 1 : (sy < 0 ? b - iqy : 0);
   nxl = nxl < 0 ? 0 : nxl;
   nyl = nyl < 0 ? 0 : nyl;
-  const int a_end = a + sx * nxl, b_end = b + sy * nyl;  // no x-crossing left once a == a_end
+  // Which line comes next is the orientation of lattice point (a, b) against the ray p -> q extended
+  // past q: once one family is used up, its next line is crossed at or beyond q, after every line of
+  // the other family still ahead, so the order test needs no "lines left" bookkeeping (and never ties
+  // there: those two crossings are distinct points).  Rays along an axis cross one family only.
+  const int force = sx == 0 ? 1 : (sy == 0 ? -1 : 0);  // > 0: y-lines only, < 0: x-lines only
   const int sd = sy > 0 ? 1 : -1;
-  int sh = cx - rows.x0;  // bit of the current column in a window row
+  const int xoff = ux + rows.x0;  // the current column is a - ux: its bit in a window row is a - xoff
   uint32_t r_c = rows.row(cy), r_o = rows.row(cy + sd), r_p = rows.row(cy + 2 * sd);
-  const bool cur0 = (r_c >> sh) & 1u;
+  const bool cur0 = (r_c >> (cx - rows.x0)) & 1u;
   bool cur = cur0;
   int n_runs = cur ? 1 : 0;
-  // start node of the first run: x-crossing (true) or y-crossing on the edge from lattice point (na, nb)
-  bool n_x = false;
-  int na = 0, nb = 0;
+  // the first run's entry crossing: lines (na, nb) ahead of it and whether it crossed the x-line
+  int n_x = 0, na = 0, nb = 0;
+  bool bail = false;  // a crossing through a lattice point: the general walk takes over after the loop
   const float sxy = (float)(sx * sy);
   for (int left = nxl + nyl; left > 0; left--) {
-    const bool hx = a != a_end, hy = b != b_end;
     const float fa = (float)a, fb = (float)b;
     const float dl = __fmul_rn(__fsub_rn(fpx, fa), __fsub_rn(fqy, fb));
     const float dr = __fmul_rn(__fsub_rn(fpy, fb), __fsub_rn(fqx, fa));
     const float dsx = __fmul_rn(__fsub_rn(dl, dr), sxy);
     const float bound = 1.7881398e-7f * __fadd_rn(fabsf(dl), fabsf(dr));
     int c = dsx > bound ? -1 : (-dsx > bound ? 1 : 0);
-    if (hx && hy && c == 0) {
+    if (force == 0 && c == 0) {
       c = -orient(fpx, fpy, fqx, fqy, (double)a, (double)b) * sx * sy;
-      if (c == 0) return false;  // through a lattice point
+      bail = bail || c == 0;  // single-exit loop: no early return here
     }
-    const bool takex = (hx && hy) ? c < 0 : hx;
-    const int ea = takex ? a : a - ux, eb = takex ? b - vy : b;  // crossed edge's lower-left lattice point
-    const int dx = takex ? sx : 0, dy = takex ? 0 : sy;  // selects, not branches: the lanes diverge here
-    a += dx;
-    sh += dx;
-    b += dy;
-    cy += dy;
+    const bool takex = force != 0 ? force < 0 : c < 0;
+    const int pa = a, pb = b;
+    a += takex ? sx : 0;
+    b += takex ? 0 : sy;
     r_c = takex ? r_c : r_o;
     r_o = takex ? r_o : r_p;
-    r_p = rows.row(cy + 2 * sd);  // unchanged row after an x-crossing; consumed a crossing later at the earliest
-    const bool in = (r_c >> sh) & 1u;
-    const bool first = in && !cur && n_runs == 0;
-    n_x = first ? takex : n_x;
-    na = first ? ea : na;
-    nb = first ? eb : nb;
-    n_runs += (in && !cur) ? 1 : 0;
+    r_p = rows.row_nw(b - vy + 2 * sd);  // unchanged row after an x-crossing; consumed a crossing later at the earliest
+    const bool in = __builtin_amdgcn_ubfe(r_c, (unsigned)(a - xoff), 1u) != 0u;
+    const bool rise = in && !cur;
+    const bool first = rise && n_runs == 0;
+    n_x = first ? (int)takex : n_x;
+    na = first ? pa : na;
+    nb = first ? pb : nb;
+    n_runs += rise ? 1 : 0;
     cur = in;
   }
-  o = scan_runs_result(rows, fpx, fpy, fqx, fqy, n_runs, cur0, cur, n_x, na, nb);
+  if (bail) return false;
+  // the crossed edge's lower-left lattice point: x-line na in row nb - vy, or y-line nb in column na - ux
+  o = scan_runs_result(rows, fpx, fpy, fqx, fqy, n_runs, cur0, cur, n_x, n_x ? na : na - ux, n_x ? nb - vy : nb);
   return true;
 }
 
@@ -484,6 +487,7 @@ struct RowsWindow {  // 32-row x 32-column window staged in LDS (rows [y0, y0+32
   const uint32_t *win;  // every access inside the window (see k_lidar_step), so no bounds test
   int x0, y0, nrows;
   APG_DEV uint32_t row(int y) const { return win[(unsigned)(y - y0) & 31u]; }
+  APG_DEV uint32_t row_nw(int y) const { return win[y - y0]; }  // y known to lie in the window
   // OR of rows [j0, j1] (inside the window): eight loads at immediate offsets from row j0, masked past j1
   // (they may read up to 7 words beyond the window: the LDS layout pads the last one), a loop only for
   // boxes taller than 8 rows
@@ -508,6 +512,7 @@ struct RowsGlobal {  // bit rows in global memory, read through a 32-column wind
     if ((unsigned)y >= (unsigned)h) return 0u;
     return extract_window_row(occ + (size_t)y * wpr, wpr, x0);
   }
+  APG_DEV uint32_t row_nw(int y) const { return row(y); }
   APG_DEV uint32_t or_rows(int j0, int j1) const {
     uint32_t acc = 0u;
     for (int j = j0; j <= j1; j++) acc |= row(j);
