@@ -53,6 +53,9 @@ constexpr uint8_t F_AUTORESET = 1, F_JUST_RESET = 2, F_FIRST = 4;
 constexpr int MAX_WIN_ROWS = 32;
 constexpr int WIN_STRIDE = MAX_WIN_ROWS + 1;  // LDS words per env window (+1: lanes = envs hit distinct banks)
 constexpr int MAX_STAGED_BEAMS = 64;          // lidar rows staged in LDS for coalesced stores
+// SCAN_EMPTY beam values by the bit pattern of |q - p|^2 (f32) around range^2: a beam of length range
+// from p lands within ~1e-4 of it (f32 rounding of p + dir), i.e. within a few hundred f32 steps
+constexpr int EMPTY_TAB = 1024;
 
 BinomTable make_binom_table() {
   BinomTable t;
@@ -398,6 +401,9 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   const int LS = P.beams + 1;  // odd row stride: lanes = envs hit distinct banks
   float *s_lid = reinterpret_cast<float *>(s_dyn + EPB * WIN_STRIDE);
   uint16_t *s_queue = reinterpret_cast<uint16_t *>(s_lid + EPB * LS);
+  float *s_tab = reinterpret_cast<float *>(s_queue + EPB * P.beams);  // EMPTY_TAB entries (staged instances)
+  // first table entry's bit pattern (recomputed where used: nothing stays live across the phases)
+  auto tab_base = [&]() { return __float_as_uint(__fmul_rn(P.range, P.range)) - (uint32_t)(EMPTY_TAB / 2); };
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int base = blockIdx.x * EPB;
   const size_t words = (size_t)P.h * P.wpr;
@@ -438,6 +444,29 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       pf_pry = pred[2 * oe + 1];
     }
   }
+  // The occupancy windows (32 x 32 cells from the pre-move position, see above): each thread's rows of
+  // up to WIN_ITERS envs, loaded first thing from the envs' positions in HBM, so their latency overlaps
+  // the input loads (a workgroup with autoresets reloads them after phase R).  Beam directions likewise.
+  constexpr int WIN_ITERS = EPB * MAX_WIN_ROWS / T;
+  uint32_t wv[WIN_ITERS];
+  auto load_windows = [&]() {
+#pragma unroll
+    for (int k = 0; k < WIN_ITERS; k++) {
+      const int r = tid + k * T;
+      const int el = r / MAX_WIN_ROWS, row = r - el * MAX_WIN_ROWS;
+      wv[k] = 0;
+      if (base + el < P.n) {
+        const float wpx = S.pos[2 * (base + el)], wpy = S.pos[2 * (base + el) + 1];
+        const int y = (int)floorf(wpy) - 15 + row;
+        if ((unsigned)y < (unsigned)P.h)
+          wv[k] = extract_window_row(S.occ + (P.is_static ? 0 : (size_t)(base + el) * words) + (size_t)y * P.wpr,
+                                     P.wpr, (int)floorf(wpx) - 15);
+      }
+    }
+  };
+  load_windows();
+  const bool dir_thread = P.beams <= MAX_STAGED_BEAMS && tid < 2 * P.beams;
+  const float dir_v = dir_thread ? S.beam_dirs[tid] : 0.0f;
   if constexpr (!FUSED) __syncthreads();
 
   // ---------------- phase R: NEXT_STEP autoresets (fused instances), env-major.  The barrier of
@@ -596,18 +625,19 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         pf_iy = S.init_pos[2 * oe + 1];
         pf_el = S.elapsed[oe];
       }
+      load_windows();  // the reset envs' new maps and positions
     }
   }
 
   // ---------------- phase 0: window origins from the pre-move positions; which envs reset
-  if (P.beams <= MAX_STAGED_BEAMS && tid < 2 * P.beams) s_dirs[tid >> 1][tid & 1] = S.beam_dirs[tid];
+  if (dir_thread) s_dirs[tid >> 1][tid & 1] = dir_v;
   constexpr bool kMapObsHere = !(FUSED && GEN == GEN_ROOMS);  // fused rooms resets wrote their map obs in R2
   if (own) {
     s_x0[tid] = (int)floorf(pf_px) - 15;
     s_y0[tid] = (int)floorf(pf_py) - 15;
     if (kMapObsHere && (pf_f & F_JUST_RESET)) s_rlist[atomicAdd(&s_cnt[0], 1)] = (uint16_t)tid;
   }
-  __syncthreads();
+  if constexpr (kMapObsHere) __syncthreads();
   // map obs of the envs that reset this step: bool map / 255 (lidar_localization2d.py:299), written by
   // the whole workgroup with float4 stores
   if (kMapObsHere && s_cnt[0] != 0 && O.map_obs && !P.is_static) {
@@ -638,26 +668,20 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       }
     }
   }
-  {  // window rows: all of a thread's row loads issued before any LDS store
-    constexpr int WIN_ITERS = EPB * MAX_WIN_ROWS / T;
-    uint32_t v[WIN_ITERS];
-#pragma unroll
-    for (int k = 0; k < WIN_ITERS; k++) {
-      const int r = tid + k * T;
-      const int el = r / MAX_WIN_ROWS, row = r - el * MAX_WIN_ROWS;
-      v[k] = 0;
-      if (base + el < P.n) {
-        const int y = s_y0[el] + row;
-        if ((unsigned)y < (unsigned)P.h)
-          v[k] = extract_window_row(S.occ + (P.is_static ? 0 : (size_t)(base + el) * words) + (size_t)y * P.wpr, P.wpr,
-                                    s_x0[el]);
+  {
+    // while the rows are in flight: the SCAN_EMPTY value table, v(s) = clip(f32 sqrt(s) / range, -1, 1)
+    if (P.beams <= MAX_STAGED_BEAMS) {
+      const double inv_range = 1.0 / (double)P.range;
+      for (int k = tid; k < EMPTY_TAB; k += T) {
+        const float d = f32_sqrt(__uint_as_float(tab_base() + (uint32_t)k));
+        s_tab[k] = fminf(fmaxf(f32_div_inv(d, inv_range), -1.0f), 1.0f);
       }
     }
 #pragma unroll
     for (int k = 0; k < WIN_ITERS; k++) {
       const int r = tid + k * T;
       const int el = r / MAX_WIN_ROWS, row = r - el * MAX_WIN_ROWS;
-      s_win[el * WIN_STRIDE + row] = v[k];
+      s_win[el * WIN_STRIDE + row] = wv[k];
     }
   }
   __syncthreads();
@@ -841,13 +865,18 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   for (int beam = tid / EPB; beam < P.beams; beam += T / EPB) {
     bool walk = false;
     if (e < P.n) {
-      const float qx = __fadd_rn(px, s_dirs[beam][0]), qy = __fadd_rn(py, s_dirs[beam][1]);
-      walk = scan_may_hit(rw, px, py, qx, qy);
-#ifdef APG_X_NO_EMPTY_DIST  // tuning experiment only (wrong results)
-      if (!walk) s_lid[el * LS + beam] = 1.0f;
-#else
-      if (!walk) s_lid[el * LS + beam] = beam_value(scan_empty(px, py, qx, qy).dist);
-#endif
+      const float dy = s_dirs[beam][1];
+      const float qx = __fadd_rn(px, s_dirs[beam][0]), qy = __fadd_rn(py, dy);
+      // the box spans <= floor(|qy - py|) + 2 <= floor(|dy| + 1e-4) + 2 rows (positions < 1024): a bound
+      // uniform per wave
+      const int hmax = __builtin_amdgcn_readfirstlane((int)floorf(fabsf(dy) + 1e-4f) + 2);
+      walk = scan_may_hit(rw, px, py, qx, qy, hmax);
+      if (!walk) {  // SCAN_EMPTY: |q - p| (f32 norm), its value from the table
+        const float ex = __fsub_rn(qx, px), ey = __fsub_rn(qy, py);
+        const float s2 = __fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey));
+        const uint32_t k = __float_as_uint(s2) - tab_base();
+        s_lid[el * LS + beam] = k < (uint32_t)EMPTY_TAB ? s_tab[k] : beam_value(f32_sqrt(s2));
+      }
     }
     const unsigned long long m = __ballot(walk);
     int qbase = 0;
@@ -1093,7 +1122,8 @@ int launch_map_generate_any(const Geo &g, const uint64_t *idx, int n, uint64_t *
 // use the same bytes first for the primitives and each wave's map rows.
 size_t step_lds_bytes(int epb, int beams) {
   size_t b = ((size_t)epb * WIN_STRIDE + 8) * sizeof(uint32_t);  // + RowsWindow::or_rows's over-read
-  if (beams <= MAX_STAGED_BEAMS) b += (size_t)epb * (beams + 1) * sizeof(float) + (size_t)epb * beams * sizeof(uint16_t);
+  if (beams <= MAX_STAGED_BEAMS)
+    b += (size_t)epb * (beams + 1) * sizeof(float) + (size_t)epb * beams * sizeof(uint16_t) + EMPTY_TAB * sizeof(float);
   return b;
 }
 

@@ -50,13 +50,15 @@ APG_DEV unsigned quad_status(const Rows &rows, int i0, int di, int j0, int dj) {
 // i in [ceil(min x) - 1, floor(max x)] and j in [ceil(min y) - 1, floor(max y)].  When none of those
 // cells is occupied the intersection is empty and the scan is SCAN_EMPTY with |q - p| (exactly what
 // the walk below returns for it).  Rows/columns are read through the same window as the walk.
+// hmax: an upper bound of the box height j1 - j0 + 1 that is uniform across the wave (beams of one
+// direction), so row reads past every lane's box are skipped
 template <class Rows>
-APG_DEV bool scan_may_hit(const Rows &rows, float fpx, float fpy, float fqx, float fqy) {
+APG_DEV bool scan_may_hit(const Rows &rows, float fpx, float fpy, float fqx, float fqy, int hmax = 8) {
   const int i0 = (int)ceilf(fminf(fpx, fqx)) - 1, i1 = (int)floorf(fmaxf(fpx, fqx));
   const int j0 = (int)ceilf(fminf(fpy, fqy)) - 1, j1 = (int)floorf(fmaxf(fpy, fqy));
   const int wdt = i1 - i0 + 1;  // <= lidar range + 2 < 32
   const uint32_t mask = ((1u << wdt) - 1u) << (i0 - rows.x0);
-  return (rows.or_rows(j0, j1) & mask) != 0u;
+  return (rows.or_rows(j0, j1, hmax) & mask) != 0u;
 }
 
 APG_DEV ScanOut scan_empty(float fpx, float fpy, float fqx, float fqy) {
@@ -491,12 +493,13 @@ struct RowsWindow {  // 32-row x 32-column window staged in LDS (rows [y0, y0+32
   // OR of rows [j0, j1] (inside the window): eight loads at immediate offsets from row j0, masked past j1
   // (they may read up to 7 words beyond the window: the LDS layout pads the last one), a loop only for
   // boxes taller than 8 rows
-  APG_DEV uint32_t or_rows(int j0, int j1) const {
+  APG_DEV uint32_t or_rows(int j0, int j1, int hmax) const {
     const uint32_t *w = win + (j0 - y0);
     const int h = j1 - j0 + 1;
     uint32_t acc = 0u;
 #pragma unroll
     for (int t = 0; t < 8; t++) {
+      if (t >= hmax) break;  // wave-uniform
       const uint32_t v = w[t];
       acc |= t < h ? v : 0u;
     }
@@ -513,7 +516,7 @@ struct RowsGlobal {  // bit rows in global memory, read through a 32-column wind
     return extract_window_row(occ + (size_t)y * wpr, wpr, x0);
   }
   APG_DEV uint32_t row_nw(int y) const { return row(y); }
-  APG_DEV uint32_t or_rows(int j0, int j1) const {
+  APG_DEV uint32_t or_rows(int j0, int j1, int) const {
     uint32_t acc = 0u;
     for (int j = j0; j <= j1; j++) acc |= row(j);
     return acc;
