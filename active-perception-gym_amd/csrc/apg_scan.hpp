@@ -137,82 +137,116 @@ APG_DEV ScanOut scan_runs_result(const Rows &rows, float fpx, float fpy, float f
 // only: SCAN_POINT / SCAN_MULTIPOINT at distance 0 (the first point is p when p is one).  Returns false
 // (the caller runs the general walk) when a crossing turns out to be a lattice point or the segment is
 // collinear with a grid line; the exact orientation decides near-ties as in the general walk.
-template <class Rows>
-APG_DEV bool lidar_scan_fast(const Rows &rows, float fpx, float fpy, float fqx, float fqy, ScanOut &o) {
-  const int sx = (fqx > fpx) - (fqx < fpx), sy = (fqy > fpy) - (fqy < fpy);
-  const float flpx = floorf(fpx), flpy = floorf(fpy), flqx = floorf(fqx), flqy = floorf(fqy);
-  const bool pxi = flpx == fpx, pyi = flpy == fpy, qxi = flqx == fqx, qyi = flqy == fqy;
-  if ((sx == 0 && pxi) || (sy == 0 && pyi)) return false;
-  const int ipx = (int)flpx, ipy = (int)flpy, iqx = (int)flqx, iqy = (int)flqy;
-  // first interval's cell (cx, cy); the next x-line to cross is a = cx + ux (likewise b = cy + vy) and
-  // the lines strictly inside the segment number nxl / nyl (q's own grid line is not crossed)
-  const int ux = sx > 0 ? 1 : 0, vy = sy > 0 ? 1 : 0;
-  const int cx = (sx < 0 && pxi) ? ipx - 1 : ipx;
-  const int cy = (sy < 0 && pyi) ? ipy - 1 : ipy;
-  int a = cx + ux, b = cy + vy;
-  int nxl = sx > 0 ? (qxi ? iqx - 1 : iqx) - a + 1 : (sx < 0 ? a - iqx : 0);
-  int nyl = sy > 0 ? (qyi ? iqy - 1 : iqy) - b + 1 : (sy < 0 ? b - iqy : 0);
-  nxl = nxl < 0 ? 0 : nxl;
-  nyl = nyl < 0 ? 0 : nyl;
-  // Which line comes next is the orientation of lattice point (a, b) against the ray p -> q extended
-  // past q: once one family is used up, its next line is crossed at or beyond q, after every line of
-  // the other family still ahead, so the order test needs no "lines left" bookkeeping (and never ties
-  // there: those two crossings are distinct points).  Rays along an axis cross one family only.
-  const int force = sx == 0 ? 1 : (sy == 0 ? -1 : 0);  // > 0: y-lines only, < 0: x-lines only
-  const int sd = sy > 0 ? 1 : -1;
-  const int xoff = ux + rows.x0;  // the current column is a - ux: its bit in a window row is a - xoff
-  uint32_t r_c = rows.row(cy), r_o = rows.row(cy + sd), r_p = rows.row(cy + 2 * sd);
-  const bool cur0 = (r_c >> (cx - rows.x0)) & 1u;
-  bool cur = cur0;
-  int n_runs = cur ? 1 : 0;
-  // the first run's entry crossing: lines (na, nb) ahead of it and whether it crossed the x-line
-  int n_x = 0, na = 0, nb = 0;
-  bool bail = false;  // a crossing through a lattice point: the general walk takes over after the loop
-  const float sxy = (float)(sx * sy);
-  for (int left = nxl + nyl; left > 0; left--) {
+struct FastWalk {
+  float px, py, qx, qy, sxy;
+  int sx, sy, ux, vy, sd, force, a, b, xoff, left;
+  uint32_t r_c, r_o, r_p;
+  bool cur0, cur, bail;
+  int n_runs, n_x, na, nb;
+
+  // false when the segment runs along a grid line (the general walk's case)
+  template <class Rows>
+  APG_DEV bool init(const Rows &rows, float fpx, float fpy, float fqx, float fqy) {
+    px = fpx, py = fpy, qx = fqx, qy = fqy;
+    sx = (fqx > fpx) - (fqx < fpx), sy = (fqy > fpy) - (fqy < fpy);
+    const float flpx = floorf(fpx), flpy = floorf(fpy), flqx = floorf(fqx), flqy = floorf(fqy);
+    const bool pxi = flpx == fpx, pyi = flpy == fpy, qxi = flqx == fqx, qyi = flqy == fqy;
+    left = 0;
+    bail = (sx == 0 && pxi) || (sy == 0 && pyi);
+    const int ipx = (int)flpx, ipy = (int)flpy, iqx = (int)flqx, iqy = (int)flqy;
+    // first interval's cell (cx, cy); the next x-line to cross is a = cx + ux (likewise b = cy + vy) and
+    // the lines strictly inside the segment number nxl / nyl (q's own grid line is not crossed)
+    ux = sx > 0 ? 1 : 0, vy = sy > 0 ? 1 : 0;
+    const int cx = (sx < 0 && pxi) ? ipx - 1 : ipx;
+    const int cy = (sy < 0 && pyi) ? ipy - 1 : ipy;
+    a = cx + ux, b = cy + vy;
+    int nxl = sx > 0 ? (qxi ? iqx - 1 : iqx) - a + 1 : (sx < 0 ? a - iqx : 0);
+    int nyl = sy > 0 ? (qyi ? iqy - 1 : iqy) - b + 1 : (sy < 0 ? b - iqy : 0);
+    nxl = nxl < 0 ? 0 : nxl;
+    nyl = nyl < 0 ? 0 : nyl;
+    // Which line comes next is the orientation of lattice point (a, b) against the ray p -> q extended
+    // past q: once one family is used up, its next line is crossed at or beyond q, after every line of
+    // the other family still ahead, so the order test needs no "lines left" bookkeeping (and never ties
+    // there: those two crossings are distinct points).  Rays along an axis cross one family only.
+    force = sx == 0 ? 1 : (sy == 0 ? -1 : 0);  // > 0: y-lines only, < 0: x-lines only
+    sd = sy > 0 ? 1 : -1;
+    xoff = ux + rows.x0;  // the current column is a - ux: its bit in a window row is a - xoff
+    r_c = rows.row(cy), r_o = rows.row(cy + sd), r_p = rows.row(cy + 2 * sd);
+    cur0 = (r_c >> (cx - rows.x0)) & 1u;
+    cur = cur0;
+    n_runs = cur ? 1 : 0;
+    n_x = 0, na = 0, nb = 0;  // the first run's entry crossing: lines (na, nb) ahead of it, x-line or not
+    sxy = (float)(sx * sy);
+    left = bail ? 0 : nxl + nyl;
+    return !bail;
+  }
+
+  // f32 filter of the crossing order at (a, b): < 0 x-line first, > 0 y-line first, 0 undecided
+  APG_DEV int order() const {
     const float fa = (float)a, fb = (float)b;
-    const float dl = __fmul_rn(__fsub_rn(fpx, fa), __fsub_rn(fqy, fb));
-    const float dr = __fmul_rn(__fsub_rn(fpy, fb), __fsub_rn(fqx, fa));
+    const float dl = __fmul_rn(__fsub_rn(px, fa), __fsub_rn(qy, fb));
+    const float dr = __fmul_rn(__fsub_rn(py, fb), __fsub_rn(qx, fa));
     const float dsx = __fmul_rn(__fsub_rn(dl, dr), sxy);
     const float bound = 1.7881398e-7f * __fadd_rn(fabsf(dl), fabsf(dr));
-    int c = dsx > bound ? -1 : (-dsx > bound ? 1 : 0);
-    if (force == 0 && c == 0) {
-      c = -orient(fpx, fpy, fqx, fqy, (double)a, (double)b) * sx * sy;
-      bail = bail || c == 0;  // single-exit loop: no early return here
-    }
+    return dsx > bound ? -1 : (-dsx > bound ? 1 : 0);
+  }
+  APG_DEV bool undecided(int c) const { return force == 0 && c == 0; }
+  // exact order for an undecided filter; 0 (a crossing through a lattice point) hands the segment over
+  // to the general walk
+  APG_DEV int order_exact() {
+    const int c = -orient(px, py, qx, qy, (double)a, (double)b) * sx * sy;
+    bail = bail || c == 0;
+    return c;
+  }
+
+  // one crossing; act = false leaves the result state alone (the pair walk's shorter segment, whose
+  // position then runs past q: kWrap keeps its row reads inside the window)
+  template <bool kWrap, class Rows>
+  APG_DEV void step(const Rows &rows, int c, bool act) {
     const bool takex = force != 0 ? force < 0 : c < 0;
     const int pa = a, pb = b;
     a += takex ? sx : 0;
     b += takex ? 0 : sy;
     r_c = takex ? r_c : r_o;
     r_o = takex ? r_o : r_p;
-    r_p = rows.row_nw(b - vy + 2 * sd);  // unchanged row after an x-crossing; consumed a crossing later at the earliest
+    const int ry = b - vy + 2 * sd;  // unchanged after an x-crossing; consumed a crossing later at the earliest
+    r_p = kWrap ? rows.row(ry) : rows.row_nw(ry);
     const bool in = __builtin_amdgcn_ubfe(r_c, (unsigned)(a - xoff), 1u) != 0u;
-    const bool rise = in && !cur;
+    const bool rise = act && in && !cur;
     const bool first = rise && n_runs == 0;
     n_x = first ? (int)takex : n_x;
     na = first ? pa : na;
     nb = first ? pb : nb;
     n_runs += rise ? 1 : 0;
-    cur = in;
+    cur = act ? in : cur;
   }
-  if (bail) return false;
-  // the crossed edge's lower-left lattice point: x-line na in row nb - vy, or y-line nb in column na - ux
-  o = scan_runs_result(rows, fpx, fpy, fqx, fqy, n_runs, cur0, cur, n_x, n_x ? na : na - ux, n_x ? nb - vy : nb);
+
+  template <class Rows>
+  APG_DEV ScanOut result(const Rows &rows) const {
+    // the crossed edge's lower-left lattice point: x-line na in row nb - vy, or y-line nb in column na - ux
+    return scan_runs_result(rows, px, py, qx, qy, n_runs, cur0, cur, n_x, n_x ? na : na - ux, n_x ? nb - vy : nb);
+  }
+};
+
+template <class Rows>
+APG_DEV bool lidar_scan_fast(const Rows &rows, float fpx, float fpy, float fqx, float fqy, ScanOut &o) {
+  FastWalk w;
+  if (!w.init(rows, fpx, fpy, fqx, fqy)) return false;
+  for (int left = w.left; left > 0; left--) {  // single exit: a lattice crossing is checked after the loop
+    int c = w.order();
+    if (w.undecided(c)) c = w.order_exact();
+    w.step<false>(rows, c, true);
+  }
+  if (w.bail) return false;
+  o = w.result(rows);
   return true;
 }
 
 // kContact (render path): also report the reference's contact point in *contact; the hot path
 // instantiates kContact = false, which compiles to the distance-only walk.
 template <class Rows, bool kContact = false>
-APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fqx, float fqy,
-                                ScanContact *contact = nullptr) {
-#ifndef APG_X_NO_FAST_WALK  // tuning / test builds: general walk only
-  if constexpr (!kContact) {
-    ScanOut fo;
-    if (lidar_scan_fast(rows, fpx, fpy, fqx, fqy, fo)) return fo;
-  }
-#endif
+APG_DEV ScanOut lidar_scan_general(const Rows &rows, float fpx, float fpy, float fqx, float fqy,
+                                   ScanContact *contact = nullptr) {
   const double px = fpx, py = fpy, qx = fqx, qy = fqy;
   const int sx = (fqx > fpx) - (fqx < fpx), sy = (fqy > fpy) - (fqy < fpy);
   const float flpx = floorf(fpx), flpy = floorf(fpy), flqx = floorf(fqx), flqy = floorf(fqy);
@@ -464,6 +498,18 @@ APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fq
     }
   }
   return o;
+}
+
+template <class Rows, bool kContact = false>
+APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fqx, float fqy,
+                                ScanContact *contact = nullptr) {
+#ifndef APG_X_NO_FAST_WALK  // tuning / test builds: general walk only
+  if constexpr (!kContact) {
+    ScanOut fo;
+    if (lidar_scan_fast(rows, fpx, fpy, fqx, fqy, fo)) return fo;
+  }
+#endif
+  return lidar_scan_general<Rows, kContact>(rows, fpx, fpy, fqx, fqy, contact);
 }
 
 template <class Rows>
