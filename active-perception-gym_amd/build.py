@@ -33,6 +33,9 @@ FLAGS = [
     "-ffp-contract=off",
     "-fno-fast-math",
     "-fno-gpu-flush-denormals-to-zero",
+    # every build (tuning variants included) answers to libapgym_hip.so: a variant loaded first through
+    # APG_LIBRARY then also serves libapgym_torch.so's dependency, so the torch ops run it too
+    "-Wl,-soname,libapgym_hip.so",
 ]
 
 

@@ -343,8 +343,8 @@ FastDiv make_fastdiv(uint32_t d) {
   return f;
 }
 
-struct Axis {  // one sampling coordinate: grid interval, fractional weight, 1 - weight
-  int idx;
+struct Axis {  // one sampling coordinate: pool offset of its grid interval (rows: idx * w * pc, columns:
+  int off;      // idx * pc), fractional weight, 1 - weight
   double w, nw;
 };
 
@@ -367,7 +367,7 @@ APG_DEV uint32_t gs_axes(const GlimpseGeo &g, const int64_t *index, PosAt pos_at
     const double lim = row ? g.cy : g.cx;
     if (!(c >= -lim && c <= lim)) bad |= row ? APG_ERR_OOB_Y : APG_ERR_OOB_X;
     Axis ax;
-    ax.idx = grid_interval(c, lim, row ? g.h : g.w, ax.w);
+    ax.off = grid_interval(c, lim, row ? g.h : g.w, ax.w) * (row ? g.w * g.pc : g.pc);
     ax.nw = __dsub_rn(1.0, ax.w);
     s_ax[q] = ax;
     if (k == 0) s_base[u] = index[(u0 + u) / npos] * g.img_elems;
@@ -375,10 +375,14 @@ APG_DEV uint32_t gs_axes(const GlimpseGeo &g, const int64_t *index, PosAt pos_at
   return bad;
 }
 
-APG_DEV void gs_pixels(const GlimpseGeo &g, const void *pool, int u0, int nu, FastDiv per_div, FastDiv s1_div,
-                       const Axis *s_ax, const int64_t *s_base, const float *s_lut, float *out) {
+// one instantiation per pool format (u8 / f32), pool channels PC and output channels C (validate() admits
+// (1, 1), (1, 3), (3, 3)), so the channel loops unroll and the u8 table reads stay LDS reads
+template <bool F32, int PC, int C>
+APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, FastDiv per_div, FastDiv s1_div,
+                         const Axis *s_ax, const int64_t *s_base, const float *s_lut, float *out) {
   const int side = g.s0 + g.s1;
   const int per = g.s0 * g.s1;
+  const int row_elems = g.w * PC;
   for (int q = threadIdx.x; q < nu * per; q += GS_THREADS) {
     const int u = (int)per_div.div((uint32_t)q), pix = q - u * per;
     const int i = (int)s1_div.div((uint32_t)pix), j = pix - i * g.s1;
@@ -386,62 +390,75 @@ APG_DEV void gs_pixels(const GlimpseGeo &g, const void *pool, int u0, int nu, Fa
     // hypercube order of _evaluate_linear: (i0, j0), (i0, j0+1), (i0+1, j0), (i0+1, j0+1); w = (1*wy)*wx
     const double w00 = __dmul_rn(ay.nw, axx.nw), w01 = __dmul_rn(ay.nw, axx.w), w10 = __dmul_rn(ay.w, axx.nw),
                  w11 = __dmul_rn(ay.w, axx.w);
-    const int64_t r0 = s_base[u] + ((int64_t)ay.idx * g.w + axx.idx) * g.pc, r1 = r0 + (int64_t)g.w * g.pc;
-    float *dst = out + ((size_t)u0 * per + q) * g.c;
-    // u8 pools: the 2 * pc tap bytes of each row are contiguous; read them with aligned dword loads
-    // (at most three per row, only the ones they occupy) instead of one byte load per tap
-    uint32_t rw0[3] = {0, 0, 0}, rw1[3] = {0, 0, 0};
-    int o0 = 0, o1 = 0;
-    if (!g.pool_f32) {
-      const uint8_t *im = static_cast<const uint8_t *>(pool);
-      const uintptr_t a0 = reinterpret_cast<uintptr_t>(im + r0), a1 = reinterpret_cast<uintptr_t>(im + r1);
-      o0 = (int)(a0 & 3u);
-      o1 = (int)(a1 & 3u);
-      const uint32_t *d0 = reinterpret_cast<const uint32_t *>(a0 - o0), *d1 = reinterpret_cast<const uint32_t *>(a1 - o1);
-      const int span = 2 * g.pc;
-      rw0[0] = d0[0];
-      rw1[0] = d1[0];
-      if (o0 + span > 4) rw0[1] = d0[1];
-      if (o1 + span > 4) rw1[1] = d1[1];
-      if (o0 + span > 8) rw0[2] = d0[2];
-      if (o1 + span > 8) rw1[2] = d1[2];
-    }
-    auto tap = [&](const uint32_t *w, int k) {  // byte k of the loaded dwords
-      const uint32_t word = k < 4 ? w[0] : (k < 8 ? w[1] : w[2]);
-      return s_lut[(word >> (8 * (k & 3))) & 0xffu];
-    };
-    float res[3];
-    for (int ch = 0; ch < g.c; ch++) {
-      const int cc = g.pc == 1 ? 0 : ch;
-      float t00, t01, t10, t11;
-      if (g.pool_f32) {
-        const float *im = static_cast<const float *>(pool);
-        t00 = im[r0 + cc];
-        t01 = im[r0 + g.pc + cc];
-        t10 = im[r1 + cc];
-        t11 = im[r1 + g.pc + cc];
-      } else {
-        t00 = tap(rw0, o0 + cc);
-        t01 = tap(rw0, o0 + g.pc + cc);
-        t10 = tap(rw1, o1 + cc);
-        t11 = tap(rw1, o1 + g.pc + cc);
+    const int64_t r0 = s_base[u] + (ay.off + axx.off), r1 = r0 + row_elems;
+    float *dst = out + ((size_t)u0 * per + q) * C;
+    float res[C];
+    if constexpr (F32) {
+      const float *im = static_cast<const float *>(pool);
+#pragma unroll
+      for (int ch = 0; ch < C; ch++) {
+        const int cc = PC == 1 ? 0 : ch;
+        double v = __dadd_rn(0.0, __dmul_rn((double)im[r0 + cc], w00));
+        v = __dadd_rn(v, __dmul_rn((double)im[r0 + PC + cc], w01));
+        v = __dadd_rn(v, __dmul_rn((double)im[r1 + cc], w10));
+        v = __dadd_rn(v, __dmul_rn((double)im[r1 + PC + cc], w11));
+        res[ch] = (float)(v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v));  // np.clip(0, 1)
       }
-      double v = __dadd_rn(0.0, __dmul_rn((double)t00, w00));
-      v = __dadd_rn(v, __dmul_rn((double)t01, w01));
-      v = __dadd_rn(v, __dmul_rn((double)t10, w10));
-      v = __dadd_rn(v, __dmul_rn((double)t11, w11));
-      v = v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);  // np.clip(0, 1)
-      res[ch] = (float)v;
+    } else {
+      // the 2 * PC tap bytes of each row are contiguous: aligned dword loads, only the ones they occupy
+      const uint8_t *im = static_cast<const uint8_t *>(pool);
+      const int o0 = (int)(reinterpret_cast<uintptr_t>(im + r0) & 3u), o1 = (int)(reinterpret_cast<uintptr_t>(im + r1) & 3u);
+      // pointer arithmetic (not integer round trips) keeps the loads global rather than flat
+      const uint32_t *d0 = reinterpret_cast<const uint32_t *>(im + (r0 - o0)),
+                     *d1 = reinterpret_cast<const uint32_t *>(im + (r1 - o1));
+      constexpr int span = 2 * PC;
+      const uint32_t a00 = d0[0], a10 = d1[0];
+      const uint32_t a01 = o0 + span > 4 ? d0[1] : 0u, a11 = o1 + span > 4 ? d1[1] : 0u;
+      uint32_t a02 = 0u, a12 = 0u;
+      if constexpr (span > 4) {
+        a02 = o0 + span > 8 ? d0[2] : 0u;
+        a12 = o1 + span > 8 ? d1[2] : 0u;
+      }
+      // the span bytes realigned to byte 0 (funnel shifts by the runtime offset), so every tap below sits
+      // at a compile-time byte position
+      const uint32_t b0[2] = {__builtin_amdgcn_alignbit(a01, a00, 8u * o0), __builtin_amdgcn_alignbit(a02, a01, 8u * o0)};
+      const uint32_t b1[2] = {__builtin_amdgcn_alignbit(a11, a10, 8u * o1), __builtin_amdgcn_alignbit(a12, a11, 8u * o1)};
+      auto tap = [&](const uint32_t *b, int t) { return s_lut[(b[t >> 2] >> (8 * (t & 3))) & 0xffu]; };
+#pragma unroll
+      for (int ch = 0; ch < C; ch++) {
+        const int cc = PC == 1 ? 0 : ch;
+        // u8 taps and the weights are >= +0: 0.0 + t00 * w00 is t00 * w00 and only the upper clip applies
+        double v = __dmul_rn((double)tap(b0, cc), w00);
+        v = __dadd_rn(v, __dmul_rn((double)tap(b0, PC + cc), w01));
+        v = __dadd_rn(v, __dmul_rn((double)tap(b1, cc), w10));
+        v = __dadd_rn(v, __dmul_rn((double)tap(b1, PC + cc), w11));
+        res[ch] = (float)fmin(v, 1.0);
+      }
     }
-    if (g.c == 3) {
+    if constexpr (C == 3) {
       struct F3 {
         float x, y, z;
       };
       *reinterpret_cast<F3 *>(dst) = F3{res[0], res[1], res[2]};  // one 12-byte store per pixel
     } else {
-      for (int ch = 0; ch < g.c; ch++) dst[ch] = res[ch];
+      dst[0] = res[0];
     }
   }
+}
+
+APG_DEV void gs_pixels(const GlimpseGeo &g, const void *pool, int u0, int nu, FastDiv per_div, FastDiv s1_div,
+                       const Axis *s_ax, const int64_t *s_base, const float *s_lut, float *out) {
+#define APG_GS_PIXELS(F, P, C) gs_pixels_t<F, P, C>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out)
+  if (g.pool_f32) {
+    if (g.pc == 3) APG_GS_PIXELS(true, 3, 3);
+    else if (g.c == 3) APG_GS_PIXELS(true, 1, 3);
+    else APG_GS_PIXELS(true, 1, 1);
+  } else {
+    if (g.pc == 3) APG_GS_PIXELS(false, 3, 3);
+    else if (g.c == 3) APG_GS_PIXELS(false, 1, 3);
+    else APG_GS_PIXELS(false, 1, 1);
+  }
+#undef APG_GS_PIXELS
 }
 
 template <class PosT>
@@ -780,13 +797,14 @@ APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const float *__restri
 #ifndef APG_FUSED_MIN_WAVES
 #define APG_FUSED_MIN_WAVES 8  // <= 64 VGPRs: every workgroup of the grid resident at once
 #endif
-template <int KIND>
+template <int KIND, bool F32, int PC, int C>
 __global__ __launch_bounds__(GS_THREADS, APG_FUSED_MIN_WAVES) void k_image_step_fused(
     EnvArgs a, GlimpseGeo g, const void *pool, const int64_t *index, const float *__restrict__ act,
     const float *__restrict__ pred, const int32_t *label, double *pos, apg_image_outputs out, float *hist, int upb,
-    FastDiv per_div, FastDiv s1_div, FastDiv side_div) {
+    FastDiv per_div, FastDiv s1_div, FastDiv side_div, FastDiv k_div) {
   __shared__ float s_lut[256];
   __shared__ int64_t s_base[GS_MAX_UNITS];
+  __shared__ double s_npos[GS_MAX_UNITS][2];  // the units' positions after this step's move
   extern __shared__ Axis s_ax[];  // [unit][rows s0 | columns s1], then (classify) the logits [unit][stride]
   const int tid = threadIdx.x;
   for (int v = tid; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
@@ -795,19 +813,36 @@ __global__ __launch_bounds__(GS_THREADS, APG_FUSED_MIN_WAVES) void k_image_step_
   if constexpr (KIND == APG_IMAGE_CLASSIFY) {
     const int k = a.k, stride = cls1_stride(k);
     for (int q = tid; q < nu * k; q += GS_THREADS) {
-      const int r = q / k;
+      const int r = (int)k_div.div((uint32_t)q);
       s_logit[r * stride + (q - r * k)] = pred[(size_t)u0 * k + q];
     }
   }
+#ifdef APG_X_MOVE_EACH  // tuning builds: every axis thread recomputes its unit's move (no extra barrier)
   const uint32_t bad = gs_axes(g, index, [&](int u, int c) {
     const int e = u0 + u;
     double px = pos[2 * e], py = pos[2 * e + 1];
     move_pos(a, act[2 * e], act[2 * e + 1], px, py);
     return c ? py : px;
   }, u0, nu, 1, side_div, s_ax, s_base);
-  __syncthreads();
-  gs_pixels(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
+#else
+  // each unit's move once (the env step below repeats it for its outputs), shared with its axis threads
   if (tid < nu) {
+    const int e = u0 + tid;
+    double px = pos[2 * e], py = pos[2 * e + 1];
+    move_pos(a, act[2 * e], act[2 * e + 1], px, py);
+    s_npos[tid][0] = px;
+    s_npos[tid][1] = py;
+  }
+  __syncthreads();
+  const uint32_t bad = gs_axes(g, index, [&](int u, int c) { return s_npos[u][c]; }, u0, nu, 1, side_div, s_ax, s_base);
+#endif
+  __syncthreads();
+  gs_pixels_t<F32, PC, C>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
+#ifdef APG_X_IMG_NOENV  // tuning experiment only (wrong results): no env step
+  if (false) {
+#else
+  if (tid < nu) {
+#endif
     const int e = u0 + tid;
     if constexpr (KIND == APG_IMAGE_CLASSIFY)
       cls1_env(a, e, s_logit + tid * cls1_stride(a.k), act, label, pos, out, hist);
@@ -1540,13 +1575,27 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
     if (c->kind == APG_IMAGE_CLASSIFY) dyn += (size_t)upb * (c->num_classes + 2) * sizeof(float);
     const dim3 grid(grid_for(n, upb)), block(GS_THREADS);
     const FastDiv pd = make_fastdiv((uint32_t)per), sd = make_fastdiv((uint32_t)g.s1),
-                  sid = make_fastdiv((uint32_t)(g.s0 + g.s1));
-    if (c->kind == APG_IMAGE_LOCALIZE)
-      hipLaunchKernelGGL(k_image_step_fused<APG_IMAGE_LOCALIZE>, grid, block, dyn, s, a, g, st->pool, st->index, action,
-                         prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, sd, sid);
-    else
-      hipLaunchKernelGGL(k_image_step_fused<APG_IMAGE_CLASSIFY>, grid, block, dyn, s, a, g, st->pool, st->index, action,
-                         prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, sd, sid);
+                  sid = make_fastdiv((uint32_t)(g.s0 + g.s1)), kd = make_fastdiv((uint32_t)std::max(1, c->num_classes));
+    // one instance per env kind and pool format (u8 / f32, pool channels, glimpse channels)
+#define APG_FUSED(K, F, P, C)                                                                                  \
+  hipLaunchKernelGGL((k_image_step_fused<K, F, P, C>), grid, block, dyn, s, a, g, st->pool, st->index, action, \
+                     prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, sd, sid, kd)
+#define APG_FUSED_KIND(K)                                   \
+  do {                                                      \
+    if (g.pool_f32) {                                       \
+      if (g.pc == 3) APG_FUSED(K, true, 3, 3);              \
+      else if (g.c == 3) APG_FUSED(K, true, 1, 3);          \
+      else APG_FUSED(K, true, 1, 1);                        \
+    } else {                                                \
+      if (g.pc == 3) APG_FUSED(K, false, 3, 3);             \
+      else if (g.c == 3) APG_FUSED(K, false, 1, 3);         \
+      else APG_FUSED(K, false, 1, 1);                       \
+    }                                                       \
+  } while (0)
+    if (c->kind == APG_IMAGE_LOCALIZE) APG_FUSED_KIND(APG_IMAGE_LOCALIZE);
+    else APG_FUSED_KIND(APG_IMAGE_CLASSIFY);
+#undef APG_FUSED_KIND
+#undef APG_FUSED
     return check_launch("k_image_step_fused");  // the target glimpse only changes on the autoreset step
   }
   if (c->kind == APG_IMAGE_CLASSIFY && c->num_classes <= CLS1_MAX_K && !lanes8) {

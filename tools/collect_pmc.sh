@@ -13,7 +13,7 @@ rm -rf "$O"
 mkdir -p "$O"
 case $WL in
   lidar | maze127) REGEX=k_lidar_step ;;
-  *) REGEX='k_glimpse|k_image_env|k_fill' ;;
+  *) REGEX='k_glimpse|k_image_env|k_image_step|k_fill|k_unique|k_loc_target' ;;
 esac
 # 110 steps from reset(seed=0): step 101 is the synchronized autoreset step
 ARGS=(--workload "$WL" --no-cpu-baseline --steps 110 --warmup 0 --no-episode "$@")

@@ -72,7 +72,7 @@ def main():
                 cls = lidar_class(kname, ordinal if fused else None)
                 ordinal += 1 if fused else 0
             else:
-                cls = kname.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+                cls = kname.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
             for c, v in vals.items():
                 acc[cls][c].append(v)
     per = {cls: {c: sum(v) / len(v) for c, v in cs.items()} for cls, cs in acc.items()}
