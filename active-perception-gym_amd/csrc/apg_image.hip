@@ -370,31 +370,58 @@ APG_DEV uint32_t gs_axes(const GlimpseGeo &g, const int64_t *index, PosAt pos_at
     ax.off = grid_interval(c, lim, row ? g.h : g.w, ax.w) * (row ? g.w * g.pc : g.pc);
     ax.nw = __dsub_rn(1.0, ax.w);
     s_ax[q] = ax;
-    if (k == 0) s_base[u] = index[(u0 + u) / npos] * g.img_elems;
+    if (k == 0 && index) s_base[u] = index[(u0 + u) / npos] * g.img_elems;  // index == nullptr: s_base is set
   }
   return bad;
 }
 
 // one instantiation per pool format (u8 / f32), pool channels PC and output channels C (validate() admits
 // (1, 1), (1, 3), (3, 3)), so the channel loops unroll and the u8 table reads stay LDS reads
+// u8 taps of one glimpse pixel: the dwords holding its two rows' 2 * PC tap bytes, and their byte offsets
+struct U8Taps {
+  uint32_t a00, a01, a02, a10, a11, a12;
+  int o0, o1;
+};
+
 template <bool F32, int PC, int C>
 APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, FastDiv per_div, FastDiv s1_div,
                          const Axis *s_ax, const int64_t *s_base, const float *s_lut, float *out) {
   const int side = g.s0 + g.s1;
   const int per = g.s0 * g.s1;
   const int row_elems = g.w * PC;
-  for (int q = threadIdx.x; q < nu * per; q += GS_THREADS) {
-    const int u = (int)per_div.div((uint32_t)q), pix = q - u * per;
-    const int i = (int)s1_div.div((uint32_t)pix), j = pix - i * g.s1;
-    const Axis ay = s_ax[u * side + i], axx = s_ax[u * side + g.s0 + j];
-    // hypercube order of _evaluate_linear: (i0, j0), (i0, j0+1), (i0+1, j0), (i0+1, j0+1); w = (1*wy)*wx
-    const double w00 = __dmul_rn(ay.nw, axx.nw), w01 = __dmul_rn(ay.nw, axx.w), w10 = __dmul_rn(ay.w, axx.nw),
-                 w11 = __dmul_rn(ay.w, axx.w);
-    const int64_t r0 = s_base[u] + (ay.off + axx.off), r1 = r0 + row_elems;
+  const int total = nu * per;
+  auto coords = [&](int q, int &u, int &i, int &j) {
+    u = (int)per_div.div((uint32_t)q);
+    const int pix = q - u * per;
+    i = (int)s1_div.div((uint32_t)pix);
+    j = pix - i * g.s1;
+  };
+  // weights in the hypercube order of _evaluate_linear: (i0, j0), (i0, j0+1), (i0+1, j0), (i0+1, j0+1); (1*wy)*wx
+  auto weights = [&](const Axis &ay, const Axis &axx, double &w00, double &w01, double &w10, double &w11) {
+    w00 = __dmul_rn(ay.nw, axx.nw), w01 = __dmul_rn(ay.nw, axx.w), w10 = __dmul_rn(ay.w, axx.nw),
+    w11 = __dmul_rn(ay.w, axx.w);
+  };
+  auto store = [&](int q, const float *res) {
     float *dst = out + ((size_t)u0 * per + q) * C;
-    float res[C];
-    if constexpr (F32) {
-      const float *im = static_cast<const float *>(pool);
+    if constexpr (C == 3) {
+      struct F3 {
+        float x, y, z;
+      };
+      *reinterpret_cast<F3 *>(dst) = F3{res[0], res[1], res[2]};  // one 12-byte store per pixel
+    } else {
+      dst[0] = res[0];
+    }
+  };
+  if constexpr (F32) {
+    const float *im = static_cast<const float *>(pool);
+    for (int q = threadIdx.x; q < total; q += GS_THREADS) {
+      int u, i, j;
+      coords(q, u, i, j);
+      const Axis ay = s_ax[u * side + i], axx = s_ax[u * side + g.s0 + j];
+      double w00, w01, w10, w11;
+      weights(ay, axx, w00, w01, w10, w11);
+      const int64_t r0 = s_base[u] + (ay.off + axx.off), r1 = r0 + row_elems;
+      float res[C];
 #pragma unroll
       for (int ch = 0; ch < C; ch++) {
         const int cc = PC == 1 ? 0 : ch;
@@ -404,26 +431,49 @@ APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, 
         v = __dadd_rn(v, __dmul_rn((double)im[r1 + PC + cc], w11));
         res[ch] = (float)(v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v));  // np.clip(0, 1)
       }
-    } else {
-      // the 2 * PC tap bytes of each row are contiguous: aligned dword loads, only the ones they occupy
-      const uint8_t *im = static_cast<const uint8_t *>(pool);
-      const int o0 = (int)(reinterpret_cast<uintptr_t>(im + r0) & 3u), o1 = (int)(reinterpret_cast<uintptr_t>(im + r1) & 3u);
+      store(q, res);
+    }
+  } else {
+    // the 2 * PC tap bytes of each row are contiguous: aligned dword loads, only the ones they occupy (issuing
+    // the next pixel's loads ahead of this pixel's arithmetic measured slower: register pressure)
+    const uint8_t *im = static_cast<const uint8_t *>(pool);
+    constexpr int span = 2 * PC;
+    auto fetch = [&](int q) {
+      int u, i, j;
+      coords(q, u, i, j);
+      const int64_t r0 = s_base[u] + (s_ax[u * side + i].off + s_ax[u * side + g.s0 + j].off), r1 = r0 + row_elems;
+      U8Taps t;
+      t.o0 = (int)(reinterpret_cast<uintptr_t>(im + r0) & 3u);
+      t.o1 = (int)(reinterpret_cast<uintptr_t>(im + r1) & 3u);
       // pointer arithmetic (not integer round trips) keeps the loads global rather than flat
-      const uint32_t *d0 = reinterpret_cast<const uint32_t *>(im + (r0 - o0)),
-                     *d1 = reinterpret_cast<const uint32_t *>(im + (r1 - o1));
-      constexpr int span = 2 * PC;
-      const uint32_t a00 = d0[0], a10 = d1[0];
-      const uint32_t a01 = o0 + span > 4 ? d0[1] : 0u, a11 = o1 + span > 4 ? d1[1] : 0u;
-      uint32_t a02 = 0u, a12 = 0u;
+      const uint32_t *d0 = reinterpret_cast<const uint32_t *>(im + (r0 - t.o0)),
+                     *d1 = reinterpret_cast<const uint32_t *>(im + (r1 - t.o1));
+      t.a00 = d0[0];
+      t.a10 = d1[0];
+      t.a01 = t.o0 + span > 4 ? d0[1] : 0u;
+      t.a11 = t.o1 + span > 4 ? d1[1] : 0u;
+      t.a02 = t.a12 = 0u;
       if constexpr (span > 4) {
-        a02 = o0 + span > 8 ? d0[2] : 0u;
-        a12 = o1 + span > 8 ? d1[2] : 0u;
+        t.a02 = t.o0 + span > 8 ? d0[2] : 0u;
+        t.a12 = t.o1 + span > 8 ? d1[2] : 0u;
       }
-      // the span bytes realigned to byte 0 (funnel shifts by the runtime offset), so every tap below sits
-      // at a compile-time byte position
-      const uint32_t b0[2] = {__builtin_amdgcn_alignbit(a01, a00, 8u * o0), __builtin_amdgcn_alignbit(a02, a01, 8u * o0)};
-      const uint32_t b1[2] = {__builtin_amdgcn_alignbit(a11, a10, 8u * o1), __builtin_amdgcn_alignbit(a12, a11, 8u * o1)};
+      return t;
+    };
+    for (int q = threadIdx.x; q < total; q += GS_THREADS) {
+      const U8Taps cur = fetch(q);
+      int u, i, j;
+      coords(q, u, i, j);
+      const Axis ay = s_ax[u * side + i], axx = s_ax[u * side + g.s0 + j];
+      double w00, w01, w10, w11;
+      weights(ay, axx, w00, w01, w10, w11);
+      // the span bytes realigned to byte 0 (funnel shifts by the runtime offset), so every tap sits at a
+      // compile-time byte position
+      const uint32_t b0[2] = {__builtin_amdgcn_alignbit(cur.a01, cur.a00, 8u * cur.o0),
+                              __builtin_amdgcn_alignbit(cur.a02, cur.a01, 8u * cur.o0)};
+      const uint32_t b1[2] = {__builtin_amdgcn_alignbit(cur.a11, cur.a10, 8u * cur.o1),
+                              __builtin_amdgcn_alignbit(cur.a12, cur.a11, 8u * cur.o1)};
       auto tap = [&](const uint32_t *b, int t) { return s_lut[(b[t >> 2] >> (8 * (t & 3))) & 0xffu]; };
+      float res[C];
 #pragma unroll
       for (int ch = 0; ch < C; ch++) {
         const int cc = PC == 1 ? 0 : ch;
@@ -434,14 +484,7 @@ APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, 
         v = __dadd_rn(v, __dmul_rn((double)tap(b1, PC + cc), w11));
         res[ch] = (float)fmin(v, 1.0);
       }
-    }
-    if constexpr (C == 3) {
-      struct F3 {
-        float x, y, z;
-      };
-      *reinterpret_cast<F3 *>(dst) = F3{res[0], res[1], res[2]};  // one 12-byte store per pixel
-    } else {
-      dst[0] = res[0];
+      store(q, res);
     }
   }
 }
@@ -564,12 +607,42 @@ APG_DEV float move_pos(const EnvArgs &a, float a0, float a1, double &px, double 
   return mag;
 }
 
+// Per-env inputs of the env step, loaded up front (the fused kernel loads them before its glimpse
+// passes, so their latency hides behind the glimpse).
+struct EnvIn {
+  float a0, a1;          // action (not read on the autoreset step)
+  double px, py;         // position before this step's move
+  float p0, p1, t0, t1;  // localization: prediction, target before the autoreset update
+  int32_t label;         // classification
+};
+template <int KIND>
+APG_DEV EnvIn load_env_in(const EnvArgs &a, int e, const float *__restrict__ act, const float *__restrict__ pred,
+                          const int32_t *label, const double *pos, const apg_image_outputs &out) {
+  EnvIn in{};
+  if (!a.resetting) {
+    in.a0 = act[2 * e];
+    in.a1 = act[2 * e + 1];
+  }
+  in.px = pos[2 * e];
+  in.py = pos[2 * e + 1];
+  if constexpr (KIND == APG_IMAGE_LOCALIZE) {
+    in.p0 = pred[2 * e];
+    in.p1 = pred[2 * e + 1];
+    const float *tg = a.copy_target ? a.copy_target : out.target;
+    in.t0 = tg[2 * e];
+    in.t1 = tg[2 * e + 1];
+  } else {
+    in.label = label[e];
+  }
+  return in;
+}
+
 // The per-env tail of ImagePerceptionModule.step (:197-213) + ActivePerceptionVectorEnv.step
 // (reward = base_reward - loss): move (or not, on the autoreset step), rewards, glimpse_pos, time.
-APG_DEV uint32_t env_tail(const EnvArgs &a, int e, const float *__restrict__ act, double *pos,
-                          const apg_image_outputs &out, double loss_d, float loss_f) {
+APG_DEV uint32_t env_tail(const EnvArgs &a, int e, const EnvIn &in, double *pos, const apg_image_outputs &out,
+                          double loss_d, float loss_f) {
   uint32_t err = 0;
-  double px = pos[2 * e], py = pos[2 * e + 1];
+  double px = in.px, py = in.py;
   // WeightedLossFn (loss_fn.py:307-316): loss * weight; f64 * f32 -> f64 (classify), f32 * f32 (localize).
   // weight 1 leaves the loss bit-identical (including inf / NaN), so the dense ids share this path.
   loss_d = __dmul_rn(loss_d, (double)a.loss_weight);
@@ -580,7 +653,7 @@ APG_DEV uint32_t env_tail(const EnvArgs &a, int e, const float *__restrict__ act
     out.base_reward[e] = 0.0f;
     out.reward[e] = __dsub_rn(0.0, loss_d);
   } else {
-    const float a0 = act[2 * e], a1 = act[2 * e + 1];
+    const float a0 = in.a0, a1 = in.a1;
     if (a0 != a0 || a1 != a1) err |= APG_ERR_NAN_ACTION;
     const float mag = move_pos(a, a0, a1, px, py);
     pos[2 * e] = px;
@@ -597,24 +670,23 @@ APG_DEV uint32_t env_tail(const EnvArgs &a, int e, const float *__restrict__ act
 }
 
 // Localization step of env e: MSE against the target before the autoreset update.
-APG_DEV void loc_env(const EnvArgs &a, int e, const float *__restrict__ act, const float *__restrict__ pred,
-                     double *pos, const apg_image_outputs &out, float *hist) {
+APG_DEV void loc_env(const EnvArgs &a, int e, const EnvIn &in, double *pos, const apg_image_outputs &out,
+                     float *hist) {
   uint32_t err = 0;
-  const float p0 = pred[2 * e], p1 = pred[2 * e + 1];
+  const float p0 = in.p0, p1 = in.p1;
   if (p0 != p0 || p1 != p1) err |= APG_ERR_NAN_PREDICTION;  // 1 - |pred - target| / 2 is NaN
+  const float t0 = in.t0, t1 = in.t1;
   if (a.copy_target) {  // k_loc_target folded in (no refresh this step)
-    out.target[2 * e] = a.copy_target[2 * e];
-    out.target[2 * e + 1] = a.copy_target[2 * e + 1];
+    out.target[2 * e] = t0;
+    out.target[2 * e + 1] = t1;
   }
-  const float t0 = a.copy_target ? a.copy_target[2 * e] : out.target[2 * e];
-  const float t1 = a.copy_target ? a.copy_target[2 * e + 1] : out.target[2 * e + 1];
   const float d0 = __fsub_rn(p0, t0), d1 = __fsub_rn(p1, t1);
   // np.mean(f32 [2]): (0 + d0^2 + d1^2) / 2, then * scale + offset in f32
   const float mse = f32_div(__fadd_rn(__fadd_rn(0.0f, __fmul_rn(d0, d0)), __fmul_rn(d1, d1)), 2.0f);
   const float loss_f = __fadd_rn(__fmul_rn(mse, a.mse_scale), a.mse_offset);
   out.loss_f32[e] = loss_f;
   log_regression(a, e, out, hist, norm_f32(d0, d1), mse);  // |target - prediction|: signs do not matter
-  err |= env_tail(a, e, act, pos, out, (double)loss_f, loss_f);
+  err |= env_tail(a, e, in, pos, out, (double)loss_f, loss_f);
   if (err) atomicOr(out.err, err);
 }
 
@@ -623,7 +695,7 @@ __global__ __launch_bounds__(256) void k_image_env_loc(EnvArgs a, const float *_
                                                        const float *__restrict__ pred, double *pos,
                                                        apg_image_outputs out, float *hist) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < a.n) loc_env(a, e, act, pred, pos, out, hist);
+  if (e < a.n) loc_env(a, e, load_env_in<APG_IMAGE_LOCALIZE>(a, e, act, pred, nullptr, pos, out), pos, out, hist);
 }
 
 // numpy pairwise sum of x[off .. off+n) by the 8 lanes of a group (lane j owns accumulator j of
@@ -713,7 +785,7 @@ __global__ __launch_bounds__(256) void k_image_env_cls(EnvArgs a, int envs_per_b
   out.label_target[e] = l;
   // scipy.special.softmax(prediction)[label] = exp(x_l - max) / sum(exp(x - max)) (finite logits)
   log_classification(a, e, out, hist, f32_div(row[lc], sum));
-  err |= env_tail(a, e, act, pos, out, loss_d, 0.0f);
+  err |= env_tail(a, e, load_env_in<APG_IMAGE_CLASSIFY>(a, e, act, pred, label, pos, out), pos, out, loss_d, 0.0f);
   if (err) atomicOr(out.err, err);
 }
 
@@ -724,8 +796,8 @@ __global__ __launch_bounds__(256) void k_image_env_cls(EnvArgs a, int envs_per_b
 // then the tail — the order pw_leaf8 distributes over 8 lanes), log, with the same device libm calls.
 constexpr int CLS1_ENVS = 128;
 constexpr int CLS1_MAX_K = 16;
-APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const float *__restrict__ act, const int32_t *label,
-                      double *pos, const apg_image_outputs &out, float *hist);
+APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const EnvIn &in, double *pos, const apg_image_outputs &out,
+                      float *hist);
 // LDS row stride of a K-logit row: odd, so lanes = envs hit distinct banks (k + 1 is even for odd K)
 APG_DEV int cls1_stride(int k) { return k + 1 + (k & 1); }
 
@@ -742,12 +814,14 @@ __global__ __launch_bounds__(CLS1_ENVS) void k_image_env_cls1(EnvArgs a, const f
   }
   __syncthreads();
   if ((int)threadIdx.x >= ne) return;
-  cls1_env(a, e0 + threadIdx.x, s_logit + threadIdx.x * stride, act, label, pos, out, hist);
+  const int e = e0 + threadIdx.x;
+  cls1_env(a, e, s_logit + threadIdx.x * stride, load_env_in<APG_IMAGE_CLASSIFY>(a, e, act, pred, label, pos, out), pos,
+           out, hist);
 }
 
 // Classification step of env e for K <= CLS1_MAX_K from its logit row (in LDS; overwritten with the exps).
-APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const float *__restrict__ act, const int32_t *label,
-                      double *pos, const apg_image_outputs &out, float *hist) {
+APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const EnvIn &in, double *pos, const apg_image_outputs &out,
+                      float *hist) {
   const int k = a.k;
   float m = -INFINITY;
   bool nan = false, pos_inf = false, all_neg_inf = true;
@@ -759,7 +833,7 @@ APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const float *__restri
     m = v > m ? v : m;
   }
   if (nan || isinf(m)) m = 0.0f;  // x_max[~isfinite(x_max)] = 0
-  const int32_t l = label[e];
+  const int32_t l = in.label;
   const int lc = l < 0 ? 0 : (l >= k ? k - 1 : l);
   const float xt = row[lc];
   for (int i = 0; i < k; i++) row[i] = expf(__fsub_rn(row[i], m));
@@ -785,7 +859,7 @@ APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const float *__restri
   out.loss_f64[e] = loss_d;
   out.label_target[e] = l;
   log_classification(a, e, out, hist, f32_div(row[lc], sum));
-  err |= env_tail(a, e, act, pos, out, loss_d, 0.0f);
+  err |= env_tail(a, e, in, pos, out, loss_d, 0.0f);
   if (err) atomicOr(out.err, err);
 }
 
@@ -817,25 +891,20 @@ __global__ __launch_bounds__(GS_THREADS, APG_FUSED_MIN_WAVES) void k_image_step_
       s_logit[r * stride + (q - r * k)] = pred[(size_t)u0 * k + q];
     }
   }
-#ifdef APG_X_MOVE_EACH  // tuning builds: every axis thread recomputes its unit's move (no extra barrier)
-  const uint32_t bad = gs_axes(g, index, [&](int u, int c) {
-    const int e = u0 + u;
-    double px = pos[2 * e], py = pos[2 * e + 1];
-    move_pos(a, act[2 * e], act[2 * e + 1], px, py);
-    return c ? py : px;
-  }, u0, nu, 1, side_div, s_ax, s_base);
-#else
-  // each unit's move once (the env step below repeats it for its outputs), shared with its axis threads
+  // each unit's env inputs and image offset, loaded first; its move once (the env step below repeats it
+  // for its outputs), shared with its axis threads
+  EnvIn in{};
   if (tid < nu) {
     const int e = u0 + tid;
-    double px = pos[2 * e], py = pos[2 * e + 1];
-    move_pos(a, act[2 * e], act[2 * e + 1], px, py);
+    in = load_env_in<KIND>(a, e, act, pred, label, pos, out);
+    s_base[tid] = index[e] * g.img_elems;
+    double px = in.px, py = in.py;
+    move_pos(a, in.a0, in.a1, px, py);
     s_npos[tid][0] = px;
     s_npos[tid][1] = py;
   }
   __syncthreads();
-  const uint32_t bad = gs_axes(g, index, [&](int u, int c) { return s_npos[u][c]; }, u0, nu, 1, side_div, s_ax, s_base);
-#endif
+  const uint32_t bad = gs_axes(g, nullptr, [&](int u, int c) { return s_npos[u][c]; }, u0, nu, 1, side_div, s_ax, s_base);
   __syncthreads();
   gs_pixels_t<F32, PC, C>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
 #ifdef APG_X_IMG_NOENV  // tuning experiment only (wrong results): no env step
@@ -845,9 +914,9 @@ __global__ __launch_bounds__(GS_THREADS, APG_FUSED_MIN_WAVES) void k_image_step_
 #endif
     const int e = u0 + tid;
     if constexpr (KIND == APG_IMAGE_CLASSIFY)
-      cls1_env(a, e, s_logit + tid * cls1_stride(a.k), act, label, pos, out, hist);
+      cls1_env(a, e, s_logit + tid * cls1_stride(a.k), in, pos, out, hist);
     else
-      loc_env(a, e, act, pred, pos, out, hist);
+      loc_env(a, e, in, pos, out, hist);
   }
   if (bad) atomicOr(out.err, bad);
 }

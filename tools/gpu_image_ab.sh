@@ -11,8 +11,11 @@ one() {
   env "$@" timeout -k 10 200 python bench.py --workload $w --no-cpu-baseline --steps 200 > $O/${tag}_$w.json 2> $O/${tag}_$w.err
   python3 -c "import json;d=json.loads(open('$O/${tag}_$w.json').read().strip().splitlines()[-1]);print('%-22s %-18s %6.1f us/step  kernel %6.1f us  median %6.1f us' % ('$tag', '$w', d['ms_per_step']*1e3, d['roofline']['kernel_ms']*1e3, (d['roofline'].get('median_kernel_ms') or 0)*1e3))"
 }
-for w in mnist tinyimagenet-loc; do
-  one default $w A=1
-  for p in ${PPTS:-}; do one ppt$p $w APG_GLIMPSE_PPT=$p; done
-  for lib in $V/*.so; do one $(basename $lib .so) $w APG_LIBRARY=$lib; done
+# two interleaved rounds: box-to-box and run-order drift shows up as round-to-round differences
+for round in 1 2; do
+  for w in mnist tinyimagenet-loc; do
+    one default $w A=1
+    for p in ${PPTS:-}; do one ppt$p $w APG_GLIMPSE_PPT=$p; done
+    for lib in $V/*.so; do one $(basename $lib .so) $w APG_LIBRARY=$lib; done
+  done
 done
