@@ -2,6 +2,7 @@
 # Image step A/B (tuning aid): bench kernel time of every library in _lib/variants (loaded through
 # APG_LIBRARY; the torch ops follow it by SONAME) and of the default one with glimpse knob settings.
 set -e
+shopt -s nullglob
 R=$PWD
 V=$R/active-perception-gym_amd/ap_gym_amd/_lib/variants
 O=$R/gpurun_out/image_ab

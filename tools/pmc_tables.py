@@ -6,7 +6,8 @@ LIDAR workloads: every k_lidar_step dispatch is classified by the bench's step o
 unfused instance is reset(seed)'s observation pass; fused dispatch k is env step t = k + 1, and
 t % 101 == 0 is the synchronized autoreset step), and each counter is averaged per class:
 "step" (ordinary steps), "reset_step" and "reset_pass".  Image workloads: per kernel name, and
-"step" = the sum over the kernels launched on every step.
+"step" = the ordinary step's k_image_step_fused launch (else the sum over the kernels launched on
+every step).
 
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch; hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE in
 bytes (MI355X_MICROARCH.md, HBM: gfx950's FETCH_SIZE tallies 128-B read requests at 64 B).  The table
@@ -91,13 +92,15 @@ def main():
         family = "image"
         shape = {"num_envs": cfg["num_envs_per_gpu"], "sensor": cfg["sensor"], "classes": cfg["classes"]}
         steps = b["steps"]
-        every = [cls for cls, n in counts.items() if n >= steps]
+        fused = [cls for cls in counts if cls.startswith("k_image_step_fused")]
+        # an ordinary step is one k_image_step_fused launch; otherwise the kernels launched on every step
+        every = fused if fused else [cls for cls, n in counts.items() if n >= steps]
         step = collections.defaultdict(float)
         for cls in every:
             for c, v in per[cls].items():
                 step[c] += v
         per["step"] = dict(step)
-        counts["step"] = steps
+        counts["step"] = counts[fused[0]] if fused else steps
         hbm_b = {cls: hbm(p) for cls, p in per.items()}
     print(json.dumps({"workload": wl, "kernel_family": family, "source_sha": bench.kernel_source_sha(family),
                       "shape": shape, "launches": counts, "per_launch": per, "hbm_bytes_per_launch": hbm_b,
