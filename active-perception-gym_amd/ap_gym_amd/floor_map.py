@@ -93,7 +93,7 @@ def generate_maps(ds: FloorMapDataset, idx: np.ndarray, device="cuda") -> np.nda
     dev = torch.device(device)
     idx_t = torch.as_tensor(idx.astype(np.int64), device=dev)
     occ = torch.zeros((n, h, wpr), dtype=torch.int64, device=dev)
-    scratch = torch.zeros_like(occ) if ds.map_kind == N.APG_MAP_ROOMS else None
+    scratch = None  # reserved ABI slot, unused
     frames = ((h + 1) // 2) * ((w + 1) // 2) + 4
     stack = torch.zeros((n, frames), dtype=torch.int16, device=dev) if ds.map_kind == N.APG_MAP_MAZE else None
     err = torch.zeros(1, dtype=torch.int32, device=dev)

@@ -149,8 +149,9 @@ APG_DEV int place_start(Pcg64 &rng, const uint64_t *rows, int h, int w, int wpr,
 enum : int { GEN_NONE = 0, GEN_ROOMS = 1, GEN_MAZE = 2 };
 
 template <int GEN>
-APG_DEV int generate_one(const Geo &g, Pcg64 &r, uint64_t *occ, uint16_t *stack, const BinomTable &bt) {
-  if constexpr (GEN == GEN_MAZE) return maze_generate(r, Bits{occ, g.wpr}, g.h, g.w, g.bp, stack, 1, g.frames);
+APG_DEV int generate_one(const Geo &g, Pcg64 &r, uint64_t *occ, uint16_t *stack, const BinomTable &bt,
+                         const MazeLds &ml) {
+  if constexpr (GEN == GEN_MAZE) return maze_generate(r, Bits{occ, g.wpr}, g.h, g.w, g.bp, stack, g.frames, ml);
   else return rooms_generate(r, occ, g.wpr, g.h, g.max_rooms, g.door_width, bt);
 }
 
@@ -167,7 +168,7 @@ APG_DEV void copy_out_maps(const uint64_t *s_maps, unsigned long long done, size
 template <int GEN>
 __global__ __launch_bounds__(64) void k_map_generate(Geo g, const uint64_t *idx, int n, uint64_t *occ,
                                                      uint16_t *stack, uint32_t *err, BinomTable bt, int lanes) {
-  extern __shared__ uint64_t s_rows[];  // rooms: [lanes][h * wpr]
+  extern __shared__ uint64_t s_rows[];  // rooms: [lanes][h * wpr]; maze: maze_lds_at's layout
   const int lane = threadIdx.x;
   const int i = blockIdx.x * lanes + lane;
   const bool active = lane < lanes && i < n;
@@ -178,7 +179,8 @@ __global__ __launch_bounds__(64) void k_map_generate(Geo g, const uint64_t *idx,
     if constexpr (GEN == GEN_ROOMS)
       rc = rooms_generate(r, s_rows + lane * words, g.wpr, g.h, g.max_rooms, g.door_width, bt);
     else
-      rc = generate_one<GEN>(g, r, occ + (size_t)i * words, stack ? stack + (size_t)i * g.frames : nullptr, bt);
+      rc = generate_one<GEN>(g, r, occ + (size_t)i * words, stack + (size_t)i * g.frames, bt,
+                             maze_lds_at(s_rows, g.h, lanes, lane));
   }
   if constexpr (GEN == GEN_ROOMS) copy_out_maps(s_rows, __ballot(active), words, occ + (size_t)blockIdx.x * lanes * words, lane);
   if (rc != 0 && err) atomicOr(err, APG_ERR_MAPGEN);
@@ -190,7 +192,8 @@ __global__ __launch_bounds__(64) void k_map_generate(Geo g, const uint64_t *idx,
 // cell draw.  Returns the env's new flags.
 template <int GEN>
 APG_DEV uint8_t reset_one(const Geo &g, const apg_lidar_state &S, int e, uint8_t f, bool use_seed, uint64_t seed,
-                          uint64_t *own, uint64_t *out_map_idx, uint32_t *err, const BinomTable &bt) {
+                          uint64_t *own, uint64_t *out_map_idx, uint32_t *err, const BinomTable &bt,
+                          const MazeLds &ml) {
   Pcg64 rng;
   Pcg64 it;
   if (use_seed) {
@@ -209,7 +212,10 @@ APG_DEV uint8_t reset_one(const Geo &g, const apg_lidar_state &S, int e, uint8_t
     if constexpr (GEN == GEN_ROOMS)
       rc = rooms_generate(map_rng, own, g.wpr, g.h, g.max_rooms, g.door_width, bt);
     else
-      rc = generate_one<GEN>(g, map_rng, own, S.stack + (size_t)e * g.frames, bt);
+    {
+      rc = generate_one<GEN>(g, map_rng, own, S.stack + (size_t)e * g.frames, bt, ml);
+      maze_publish();
+    }
     if (place_start(rng, own, g.h, g.w, g.wpr, px, py) != 0) rc = -6;
     if (rc != 0) atomicOr(err, APG_ERR_MAPGEN);
     *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
@@ -238,7 +244,7 @@ template <int GEN>
 __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, uint64_t seed, int use_seed,
                                                     int all, uint64_t *out_map_idx, uint32_t *err, BinomTable bt,
                                                     int lanes) {
-  extern __shared__ uint64_t s_rows[];  // rooms: [lanes][h * wpr]
+  extern __shared__ uint64_t s_rows[];  // rooms: [lanes][h * wpr]; maze: maze_lds_at's layout
   const int lane = threadIdx.x;
   const int e = blockIdx.x * lanes + lane;
   const bool mine = lane < lanes && e < g.n;
@@ -249,7 +255,7 @@ __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, ui
   const size_t words = (size_t)g.h * g.wpr;
   if (active) {
     uint64_t *own = GEN == GEN_ROOMS ? s_rows + lane * words : S.occ + (size_t)e * words;
-    reset_one<GEN>(g, S, e, f, use_seed != 0, seed, own, out_map_idx, err, bt);
+    reset_one<GEN>(g, S, e, f, use_seed != 0, seed, own, out_map_idx, err, bt, maze_lds_at(s_rows, g.h, lanes, lane));
   }
   if constexpr (GEN == GEN_ROOMS) copy_out_maps(s_rows, todo, words, S.occ + (size_t)blockIdx.x * lanes * words, lane);
 }
@@ -612,9 +618,17 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           S.map_idx[my_e] = midx;
           if (O.map_idx) O.map_idx[my_e] = midx;
         }
+      } else if constexpr (GEN == GEN_MAZE) {
+        // maze maps: one serial, divergent DFS per env, run lane-dense (env base + tid on the first EPB / 64
+        // waves) rather than env-major: a quarter of the wave instructions, which is what bounds the carving
+        // (reset step of 262 144 127 x 127 mazes: 155 -> 109 ms).  The DFS state lives in the dynamic LDS
+        // (maze_lds_at's layout over the EPB env slots), the map in the env's occupancy rows.
+        if (own && (pf_f & F_AUTORESET))
+          reset_one<GEN>(g, S, oe, pf_f, false, 0, S.occ + (size_t)oe * words, O.map_idx, O.err, bt,
+                         maze_lds_at(s_dyn, P.h, EPB, tid));
       } else {
-        // maze maps are carved straight into the env's occupancy rows; static maps only draw a start cell
-        if (pend) reset_one<GEN>(g, S, my_e, f0, false, 0, S.occ + (size_t)my_e * words, O.map_idx, O.err, bt);
+        // static maps only draw a start cell
+        if (pend) reset_one<GEN>(g, S, my_e, f0, false, 0, nullptr, O.map_idx, O.err, bt, MazeLds{});
       }
       __syncthreads();
       if (own && (pf_f & F_AUTORESET)) {  // this env was reset above
@@ -1076,7 +1090,9 @@ int gen_lanes(int n) {
 // Dynamic LDS of a map-generation launch: rooms bitmaps [lanes][h * wpr] (opted in above 64 KiB).
 template <class K>
 int gen_lds(K kernel, int gen, const Geo &g, int lanes, size_t &dyn) {
-  dyn = gen == GEN_ROOMS ? (size_t)lanes * g.h * g.wpr * sizeof(uint64_t) : 0;
+  dyn = gen == GEN_ROOMS  ? (size_t)lanes * g.h * g.wpr * sizeof(uint64_t)
+        : gen == GEN_MAZE ? maze_lds_bytes(g.h, lanes)
+                          : 0;
   if (dyn > 64 * 1024 &&
       hipFuncSetAttribute((const void *)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) != hipSuccess)
     return fail(APG_E_LAUNCH, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
@@ -1161,6 +1177,7 @@ int launch_step_t(const StepParams &P, const Geo &g, const apg_lidar_state *st, 
                   const apg_lidar_outputs *out, hipStream_t s, const BinomTable &bt) {
   size_t lds = step_lds_bytes(EPB, P.beams);
   if (FUSED && GEN == GEN_ROOMS && RoomsLds<EPB>::bytes > lds) lds = RoomsLds<EPB>::bytes;
+  if (FUSED && GEN == GEN_MAZE && maze_lds_bytes(P.h, EPB) > lds) lds = maze_lds_bytes(P.h, EPB);
   auto kern = k_lidar_step<GEN, FUSED, EPB>;
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)

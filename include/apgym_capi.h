@@ -115,7 +115,7 @@ typedef struct apg_lidar_state {
   apg_pcg64 *rng;      /* [N]   env np_random */
   apg_pcg64 *it_rng;   /* [N]   DatasetIterator rng (dynamic maps) */
   uint64_t *occ;       /* [N or 1][H][wpr] bit-packed occupancy, wpr = ceil(W/64) */
-  uint64_t *scratch;   /* [N][H][wpr] rooms door plane (dynamic rooms only) */
+  uint64_t *scratch;   /* reserved, unused (may be NULL; query_sizes reports scratch_bytes = 0) */
   uint16_t *stack;     /* [N][maze_frames] DFS frames, contiguous per env (dynamic maze only) */
   uint64_t *map_idx;   /* [N]   dataset index of the current map */
   const float *beam_dirs; /* [beams][2] lidar_directions (f32, computed by the host like the reference) */
@@ -144,7 +144,7 @@ typedef struct apg_lidar_outputs {
 } apg_lidar_outputs;
 
 typedef struct apg_lidar_state_sizes {
-  size_t occ_bytes, scratch_bytes, stack_bytes; /* bytes of the variable-size buffers */
+  size_t occ_bytes, scratch_bytes, stack_bytes; /* bytes of the variable-size buffers (scratch_bytes: reserved, 0) */
   int32_t wpr, maze_frames;
 } apg_lidar_state_sizes;
 
@@ -173,7 +173,8 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
                             const float *prediction, const apg_lidar_outputs *out, apg_stream_t stream,
                             void *ev_begin, void *ev_end);
 
-/* n maps from dataset indices idx[n] into occ[n][h][wpr]; scratch/stack as in apg_lidar_state. */
+/* n maps from dataset indices idx[n] into occ[n][h][wpr]; stack [n][maze_frames] (mazes only);
+ * scratch is reserved and unused (may be NULL). */
 int apg_map_generate(int map_kind, const uint64_t *idx, int n, int h, int w, int max_rooms,
                      int door_width, double branching_prob, uint64_t *occ, uint64_t *scratch,
                      uint16_t *stack, uint32_t *err, apg_stream_t stream);

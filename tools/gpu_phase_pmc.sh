@@ -6,7 +6,7 @@ O=$R/gpurun_out/phase_pmc
 rm -rf $O; mkdir -p $O
 V=$R/active-perception-gym_amd/ap_gym_amd/_lib/variants
 cd /tmp && export TMPDIR=/tmp
-for epb in 256 64; do
+for epb in ${EPBS:-256 64}; do
   for v in stop1 stop2 stop3 stop4 full; do
     if [ $v = full ]; then unset APG_LIBRARY; else export APG_LIBRARY=$V/lib$v.so; fi
     export APG_STEP_EPB=$epb
