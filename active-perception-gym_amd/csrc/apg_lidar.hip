@@ -300,6 +300,9 @@ __device__ unsigned long long g_step_prof[16384][8];
 #else
 #define STEP_MARK(k)
 #endif
+#ifndef APG_SLIDE_SPLIT
+#define APG_SLIDE_SPLIT 1  // phase 1: second slide scan on the idle waves (0: both on the env's lane; A/B 36.4 -> 35.8 us)
+#endif
 #ifndef APG_STEP_MIN_WAVES
 #define APG_STEP_MIN_WAVES 4  // keep k_lidar_step at <= 128 VGPRs: 4 waves per SIMD
 #endif
@@ -399,6 +402,9 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   __shared__ uint32_t s_start[EPB];  // rooms autoreset: start cell y << 8 | x, or ~0u (no free cell)
   __shared__ int s_cnt[4];           // 0: reset-list length, 1: queued walks, 2: walk cursor
   __shared__ float s_dirs[MAX_STAGED_BEAMS][2];  // beam_dirs, read inside the beam loops (LDS, not HBM latency)
+#if APG_SLIDE_SPLIT
+  __shared__ float s_slide[EPB];  // phase 1: the second slide candidate's length, then its scan distance
+#endif
   // dynamic LDS (step_lds_bytes): occupancy windows, then (beams <= MAX_STAGED_BEAMS) the lidar rows
   // staged for coalesced stores and the phase-2b work list of (beam << 8) | env entries.  Phase R
   // (rooms) uses the same bytes first for the primitives and each wave's map rows.
@@ -702,19 +708,99 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   STEP_MARK(1)
   STEP_STOP(1)
 
-  // ---------------- phase 1: lane = env (the prefetched inputs)
+  // ---------------- phase 1: lane = env (the prefetched inputs).  1a: NaN checks, base reward, the move up
+  // to the first wall (:318-344); slides (:345-364) need two more scans from the stopped position, which
+  // are independent of each other: with APG_SLIDE_SPLIT the second runs on the next EPB threads (waves
+  // that are idle in this phase) between two barriers.  1b: slide, clip, loss, TimeLimit, stats, obs.
+  {
+  const int e = oe, el = tid;
+  uint32_t errbits = 0;
+  bool was_reset = false, moved = false, slide = false;
+  uint8_t f = pf_f;
+  float pos0 = pf_px, pos1 = pf_py, ipx = pf_ix, ipy = pf_iy;
+  const float prx = pf_prx, pry = pf_pry;
+  float br = 0.0f, c0x = 0.0f, c1y = 0.0f;
+  const float lpx = pf_px, lpy = pf_py;
+  if (tid < EPB && own) {
+    was_reset = f & F_JUST_RESET;
+    if (!was_reset) {
+      float ax = pf_ax, ay = pf_ay;
+      if (isnan(ax) || isnan(ay)) errbits |= APG_ERR_NAN_ACTION;
+      if (isnan(prx) || isnan(pry)) errbits |= APG_ERR_NAN_PREDICTION;
+      if (!errbits) {  // else the reference raises ValueError before touching this env's state
+        moved = true;
+        const RowsWindow rw{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
+        br = __fsub_rn(0.1f, __fmul_rn(0.001f, __fadd_rn(__fmul_rn(ax, ax), __fmul_rn(ay, ay))));
+        const float mag = norm_f32(ax, ay);
+        if (mag > 1.0f) {
+          ax = f32_div(ax, mag);
+          ay = f32_div(ay, mag);
+        }
+        const float tx = __fadd_rn(pos0, ax), ty = __fadd_rn(pos1, ay);
+        float dirx = __fsub_rn(tx, pos0), diry = __fsub_rn(ty, pos1);
+        const float total = norm_f32(dirx, diry);
+        if (total > 0.0f) {
+          dirx = f32_div(dirx, total);
+          diry = f32_div(diry, total);
+#ifdef APG_X_NO_MOVE_SCAN  // tuning experiment only (wrong results)
+          const float d = total;
+#else
+          const float d = lidar_scan(rw, pos0, pos1, tx, ty).dist;
+#endif
+          pos0 = __fadd_rn(pos0, __fmul_rn(dirx, d));
+          pos1 = __fadd_rn(pos1, __fmul_rn(diry, d));
+          const float rem = __fsub_rn(total, d);
+#ifdef APG_X_NO_SLIDE  // tuning experiment only (wrong results)
+          if (false) {
+#else
+          if (rem > 1e-5f) {  // slide along the wall (:345-364)
+#endif
+            const float rvx = __fmul_rn(dirx, rem), rvy = __fmul_rn(diry, rem);
+            const bool kx = rvx > 1e-5f, ky = rvy > 1e-5f;
+            if (kx || ky) {
+              slide = true;
+              c0x = kx ? rvx : rvy;  // eye(2) * kept
+              c1y = ky ? rvy : rvx;  // > 1e-5: 0 marks "no slide" below
+            }
+          }
+        }
+      }
+    }
+  }
+  float d0 = 0.0f, d1 = 0.0f;
+#if APG_SLIDE_SPLIT
   if (tid < EPB) {
-    const int e = oe;
-    const int el = tid;
-    uint32_t errbits = 0;
+    s_pos[tid][0] = pos0;
+    s_pos[tid][1] = pos1;
+    s_slide[tid] = slide ? c1y : 0.0f;
+  }
+  __syncthreads();
+  if (tid >= EPB && tid < 2 * EPB) {  // the second slide candidate of env tid - EPB
+    const int j = tid - EPB;
+    const float cy = s_slide[j];
+    if (cy > 0.0f) {
+      const RowsWindow rwj{&s_win[j * WIN_STRIDE], s_x0[j], s_y0[j], P.wrows};
+      const float q0 = s_pos[j][0], q1 = s_pos[j][1];
+      s_slide[j] = lidar_scan(rwj, q0, q1, __fadd_rn(q0, 0.0f), __fadd_rn(q1, cy)).dist;
+    }
+  }
+  if (slide) {
+    const RowsWindow rw{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
+    d0 = lidar_scan(rw, pos0, pos1, __fadd_rn(pos0, c0x), __fadd_rn(pos1, 0.0f)).dist;
+  }
+  __syncthreads();
+  if (slide) d1 = s_slide[tid];
+#else
+  if (slide) {
+    const RowsWindow rw{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
+    d0 = lidar_scan(rw, pos0, pos1, __fadd_rn(pos0, c0x), __fadd_rn(pos1, 0.0f)).dist;
+    d1 = lidar_scan(rw, pos0, pos1, __fadd_rn(pos0, 0.0f), __fadd_rn(pos1, c1y)).dist;
+  }
+#endif
+  if (tid < EPB) {
     if (own) {
-      const RowsWindow rw{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
-      uint8_t f = pf_f;
-      const bool was_reset = f & F_JUST_RESET;
-      float pos0 = pf_px, pos1 = pf_py;
-      float ipx = pf_ix, ipy = pf_iy;
       const float mapw = (float)P.w, maph = (float)P.h;
-      if (was_reset) {  // NEXT_STEP autoreset: this env returned reset obs, reward 0
+      if (was_reset || errbits) {  // NEXT_STEP autoreset (this env returned reset obs, reward 0) or NaN inputs
         O.reward[e] = 0.0;
         O.terminated[e] = 0;
         O.truncated[e] = 0;
@@ -725,119 +811,70 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         O.info_mask[e] = 0;
         if (P.log_stats) O.stats_len[e] = 0;
         if (P.sparse) O.weight[e] = 0.0;
-        f &= (uint8_t)~(F_JUST_RESET | F_AUTORESET);
-      } else {
-        float ax = pf_ax, ay = pf_ay;
-        const float prx = pf_prx, pry = pf_pry;
-        if (isnan(ax) || isnan(ay)) errbits |= APG_ERR_NAN_ACTION;
-        if (isnan(prx) || isnan(pry)) errbits |= APG_ERR_NAN_PREDICTION;
-        if (errbits) {  // the reference raises ValueError before touching this env's state
-          O.reward[e] = 0.0;
-          O.terminated[e] = 0;
-          O.truncated[e] = 0;
-          O.base_reward[e] = 0.0f;
-          O.target[2 * e] = 0.0f;
-          O.target[2 * e + 1] = 0.0f;
-          O.loss[e] = 0.0f;
-          O.info_mask[e] = 0;
-          if (P.log_stats) O.stats_len[e] = 0;
-          if (P.sparse) O.weight[e] = 0.0;
-        } else {
-          const float lpx = pos0, lpy = pos1;
-          const float br = __fsub_rn(0.1f, __fmul_rn(0.001f, __fadd_rn(__fmul_rn(ax, ax), __fmul_rn(ay, ay))));
-          const float mag = norm_f32(ax, ay);
-          if (mag > 1.0f) {
-            ax = f32_div(ax, mag);
-            ay = f32_div(ay, mag);
-          }
-          const float tx = __fadd_rn(pos0, ax), ty = __fadd_rn(pos1, ay);
-          float dirx = __fsub_rn(tx, pos0), diry = __fsub_rn(ty, pos1);
-          const float total = norm_f32(dirx, diry);
-          if (total > 0.0f) {
-            dirx = f32_div(dirx, total);
-            diry = f32_div(diry, total);
-#ifdef APG_X_NO_MOVE_SCAN  // tuning experiment only (wrong results)
-            const float d = total;
-#else
-            const float d = lidar_scan(rw, pos0, pos1, tx, ty).dist;
-#endif
-            pos0 = __fadd_rn(pos0, __fmul_rn(dirx, d));
-            pos1 = __fadd_rn(pos1, __fmul_rn(diry, d));
-            const float rem = __fsub_rn(total, d);
-#ifdef APG_X_NO_SLIDE  // tuning experiment only (wrong results)
-            if (false) {
-#else
-            if (rem > 1e-5f) {  // slide along the wall (:345-364)
-#endif
-              const float rvx = __fmul_rn(dirx, rem), rvy = __fmul_rn(diry, rem);
-              const bool kx = rvx > 1e-5f, ky = rvy > 1e-5f;
-              if (kx || ky) {
-                const float c0x = kx ? rvx : rvy, c1y = ky ? rvy : rvx;  // eye(2) * kept
-                const float d0 = lidar_scan(rw, pos0, pos1, __fadd_rn(pos0, c0x), __fadd_rn(pos1, 0.0f)).dist;
-                const float d1 = lidar_scan(rw, pos0, pos1, __fadd_rn(pos0, 0.0f), __fadd_rn(pos1, c1y)).dist;
-                float cx, cy, dd;
-                if (d0 > 0.0f) {
-                  cx = c0x;
-                  cy = 0.0f;
-                  dd = d0;
-                } else {
-                  cx = 0.0f;
-                  cy = c1y;
-                  dd = d1;
-                }
-                const float nrm = norm_f32(cx, cy);
-                pos0 = __fadd_rn(pos0, __fmul_rn(f32_div(cx, nrm), dd));
-                pos1 = __fadd_rn(pos1, __fmul_rn(f32_div(cy, nrm), dd));
-              }
-            }
-          }
-          if (f & F_FIRST) {  // initial_pos aliases pos until np.clip rebinds it (:305, :371)
-            S.init_pos[2 * e] = pos0;
-            S.init_pos[2 * e + 1] = pos1;
-            ipx = pos0;
-            ipy = pos1;
-            f &= (uint8_t)~F_FIRST;
-          }
-          bool term = pos0 < 0.0f || pos1 < 0.0f || pos0 >= mapw || pos1 >= maph;
-          pos0 = fminf(fmaxf(pos0, 0.0f), mapw);
-          pos1 = fminf(fmaxf(pos1, 0.0f), maph);
-          const float tgx = __fsub_rn(__fmul_rn(f32_div_inv(lpx, 1.0 / (double)mapw), 2.0f), 1.0f);
-          const float tgy = __fsub_rn(__fmul_rn(f32_div_inv(lpy, 1.0 / (double)maph), 2.0f), 1.0f);
-          const int el2 = pf_el + 1;
-          pf_el = el2;
-          S.elapsed[e] = el2;
-          if (el2 >= P.step_limit) term = true;  // TimeLimit(issue_termination=True)
-          const float ex = __fsub_rn(prx, tgx), ey = __fsub_rn(pry, tgy);
-          const float mse = __fmul_rn(__fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey)), 0.5f);  // exact / 2
-          const float loss = __fadd_rn(__fmul_rn(mse, P.loss_scale), P.loss_offset);
-#ifdef APG_X_NO_STATS  // tuning experiment only (wrong results)
-          if (false) {
-#else
-          if (P.log_stats) {
-#endif
-            float *hist = S.stats_hist;
-            hist[(size_t)(el2 - 1) * P.n + e] = norm_f32(ex, ey);  // |target - prediction|: the signs do not matter
-            hist[(size_t)(P.step_limit + el2 - 1) * P.n + e] = mse;
-            if (term) log_episode_stats(P, O, e, hist, el2);
-            else O.stats_len[e] = 0;
-          }
-          O.base_reward[e] = br;
-          O.target[2 * e] = tgx;
-          O.target[2 * e + 1] = tgy;
-          O.loss[e] = loss;
-          if (P.sparse) {  // SparsifyWrapper: base_reward - loss * (1.0 if terminated else 0.0), in f32
-            O.weight[e] = term ? 1.0 : 0.0;
-            O.reward[e] = (double)__fsub_rn(br, __fmul_rn(loss, term ? 1.0f : 0.0f));
+        if (was_reset) f &= (uint8_t)~(F_JUST_RESET | F_AUTORESET);
+      }
+      if (moved) {
+        if (slide) {
+          float cx, cy, dd;
+          if (d0 > 0.0f) {
+            cx = c0x;
+            cy = 0.0f;
+            dd = d0;
           } else {
-            O.reward[e] = (double)__fsub_rn(br, loss);
+            cx = 0.0f;
+            cy = c1y;
+            dd = d1;
           }
-          O.terminated[e] = term;
-          O.truncated[e] = 0;
-          O.info_mask[e] = 1;
-          if (term) f |= F_AUTORESET;
-          S.pos[2 * e] = pos0;
-          S.pos[2 * e + 1] = pos1;
+          const float nrm = norm_f32(cx, cy);
+          pos0 = __fadd_rn(pos0, __fmul_rn(f32_div(cx, nrm), dd));
+          pos1 = __fadd_rn(pos1, __fmul_rn(f32_div(cy, nrm), dd));
         }
+        if (f & F_FIRST) {  // initial_pos aliases pos until np.clip rebinds it (:305, :371)
+          S.init_pos[2 * e] = pos0;
+          S.init_pos[2 * e + 1] = pos1;
+          ipx = pos0;
+          ipy = pos1;
+          f &= (uint8_t)~F_FIRST;
+        }
+        bool term = pos0 < 0.0f || pos1 < 0.0f || pos0 >= mapw || pos1 >= maph;
+        pos0 = fminf(fmaxf(pos0, 0.0f), mapw);
+        pos1 = fminf(fmaxf(pos1, 0.0f), maph);
+        const float tgx = __fsub_rn(__fmul_rn(f32_div_inv(lpx, 1.0 / (double)mapw), 2.0f), 1.0f);
+        const float tgy = __fsub_rn(__fmul_rn(f32_div_inv(lpy, 1.0 / (double)maph), 2.0f), 1.0f);
+        const int el2 = pf_el + 1;
+        pf_el = el2;
+        S.elapsed[e] = el2;
+        if (el2 >= P.step_limit) term = true;  // TimeLimit(issue_termination=True)
+        const float ex = __fsub_rn(prx, tgx), ey = __fsub_rn(pry, tgy);
+        const float mse = __fmul_rn(__fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey)), 0.5f);  // exact / 2
+        const float loss = __fadd_rn(__fmul_rn(mse, P.loss_scale), P.loss_offset);
+#ifdef APG_X_NO_STATS  // tuning experiment only (wrong results)
+        if (false) {
+#else
+        if (P.log_stats) {
+#endif
+          float *hist = S.stats_hist;
+          hist[(size_t)(el2 - 1) * P.n + e] = norm_f32(ex, ey);  // |target - prediction|: the signs do not matter
+          hist[(size_t)(P.step_limit + el2 - 1) * P.n + e] = mse;
+          if (term) log_episode_stats(P, O, e, hist, el2);
+          else O.stats_len[e] = 0;
+        }
+        O.base_reward[e] = br;
+        O.target[2 * e] = tgx;
+        O.target[2 * e + 1] = tgy;
+        O.loss[e] = loss;
+        if (P.sparse) {  // SparsifyWrapper: base_reward - loss * (1.0 if terminated else 0.0), in f32
+          O.weight[e] = term ? 1.0 : 0.0;
+          O.reward[e] = (double)__fsub_rn(br, __fmul_rn(loss, term ? 1.0f : 0.0f));
+        } else {
+          O.reward[e] = (double)__fsub_rn(br, loss);
+        }
+        O.terminated[e] = term;
+        O.truncated[e] = 0;
+        O.info_mask[e] = 1;
+        if (term) f |= F_AUTORESET;
+        S.pos[2 * e] = pos0;
+        S.pos[2 * e + 1] = pos1;
       }
       S.flags[e] = f;
       if (O.reset_mask) O.reset_mask[e] = was_reset;
@@ -852,6 +889,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       s_pos[el][1] = pos1;
     }
     if (errbits) atomicOr(O.err, errbits);  // rare: NaN inputs only
+  }
   }
   __syncthreads();
   STEP_MARK(2)
