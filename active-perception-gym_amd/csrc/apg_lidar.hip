@@ -1217,9 +1217,12 @@ int launch_step_t(const StepParams &P, const Geo &g, const apg_lidar_state *st, 
   if (FUSED && GEN == GEN_ROOMS && RoomsLds<EPB>::bytes > lds) lds = RoomsLds<EPB>::bytes;
   if (FUSED && GEN == GEN_MAZE && maze_lds_bytes(P.h, EPB) > lds) lds = maze_lds_bytes(P.h, EPB);
   auto kern = k_lidar_step<GEN, FUSED, EPB>;
-  if (lds > 64 * 1024 &&
-      hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return fail(APG_E_LAUNCH, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+  static size_t lds_opted_in = 64 * 1024;  // per instance: the attribute call costs host time on every step
+  if (lds > lds_opted_in) {
+    if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return fail(APG_E_LAUNCH, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+    lds_opted_in = lds;
+  }
   hipLaunchKernelGGL(kern, dim3(grid_for(P.n, EPB)), dim3(4 * EPB), lds, s, P, g, *st, act, pred, *out, bt);
   return check_launch("k_lidar_step");
 }
