@@ -226,6 +226,27 @@ def torch_ops():
     return _torch_ops
 
 
+def exact_device(device):
+    """`device` with its index filled in (tensors report cuda:0, never a bare cuda)."""
+    import torch
+
+    if device.type == "cuda" and device.index is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    return device
+
+
+def as_device_f32(x, dev, numel: int, shape=None):
+    """`x` as a contiguous float32 tensor on `dev` (an exact_device): `x` itself when it already is one
+    with `numel` elements (the step hot path: no tensor constructions), else converted."""
+    import torch
+
+    if (type(x) is torch.Tensor and x.dtype is torch.float32 and x.device == dev and x.is_contiguous()
+            and x.numel() == numel):
+        return x
+    t = torch.as_tensor(x, dtype=torch.float32, device=dev)
+    return (t if shape is None else t.reshape(shape)).contiguous()
+
+
 def op_buffers(tensors, device):
     """Buffer list for an env handle: None -> a 0-element tensor (NULL in the C struct)."""
     import torch

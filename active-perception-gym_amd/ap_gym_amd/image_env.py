@@ -221,6 +221,8 @@ class _ImageVectorEnv(VectorEnv):
                                                               "loss_f64", "loss_f32", "err", "stats", "stats_idx")])
         c = self._cfg
         self._ops = N.torch_ops()  # torch.ops.apgym: the reset/step hot path
+        self._step_op = self._ops.image_step.default  # the overload itself: no per-call overload resolution
+        self._dev = N.exact_device(self.device)
         self._h = t.classes.apgym.ImageEnv(
             [c.num_envs, c.kind, c.height, c.width, c.pool_channels, c.channels, c.pool_dtype, c.sensor_h,
              c.sensor_w, c.step_limit, c.num_classes, c.invert_labels, c.top_k, c.unique_points, c.num_envs_total,
@@ -367,11 +369,11 @@ class _ImageVectorEnv(VectorEnv):
             p_t = torch.from_numpy(p_np).to(self.device, non_blocking=True)
         else:
             self.check_errors(block=False)
-            a_t = torch.as_tensor(a, dtype=torch.float32, device=self.device).reshape(n, 2).contiguous()
-            p_t = torch.as_tensor(p, dtype=torch.float32, device=self.device).reshape(n, pdim).contiguous()
+            a_t = N.as_device_f32(a, self._dev, 2 * n, (n, 2))
+            p_t = N.as_device_f32(p, self._dev, pdim * n, (n, pdim))
         resetting = self._prev_done
         self._track_render(p_np if numpy_mode else p_t, resetting)
-        self._ops.image_step(self._h, a_t, p_t, int(self._t_step), bool(resetting))
+        self._step_op(self._h, a_t, p_t, int(self._t_step), bool(resetting))
         if resetting:
             self._t_step = 0
             terminated = False

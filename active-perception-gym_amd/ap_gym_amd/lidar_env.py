@@ -185,6 +185,8 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
                                    N.ptr(T["stats_len"]), N.ptr(T["weight"]))
         c = self._cfg
         self._ops = N.torch_ops()  # torch.ops.apgym: the reset/step hot path
+        self._step_op = self._ops.lidar_step.default  # the overload itself: no per-call overload resolution
+        self._dev = N.exact_device(self.device)
         self._h = t.classes.apgym.LidarEnv(
             [c.num_envs, c.height, c.width, c.map_kind, c.is_static, c.static_map_index, c.beams, c.step_limit,
              c.max_rooms, c.door_width, c.log_stats, c.sparse],
@@ -428,15 +430,15 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             p_t = torch.from_numpy(p_np).to(self.device, non_blocking=True)
         else:
             self.check_errors(block=False)
-            a_t = torch.as_tensor(a, dtype=torch.float32, device=self.device).contiguous()
-            p_t = torch.as_tensor(p, dtype=torch.float32, device=self.device).contiguous()
+            a_t = N.as_device_f32(a, self._dev, 2 * self.num_envs)
+            p_t = N.as_device_f32(p, self._dev, 2 * self.num_envs)
         if self._kernel_events is None:
-            self._ops.lidar_step(self._h, a_t, p_t)
+            self._step_op(self._h, a_t, p_t)
         else:  # bench timing: hipEvents on the op's stream around the step launch(es)
             ev_b, ev_e = self._kernel_events
             s = self._stream()
             N.event_record(ev_b, s)
-            self._ops.lidar_step(self._h, a_t, p_t)
+            self._step_op(self._h, a_t, p_t)
             N.event_record(ev_e, s)
         self._track_render(p_t)
         if numpy_mode:

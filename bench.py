@@ -189,15 +189,15 @@ def run_image(args, world, rank, dev):
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    timed = [t for t in range(args.steps) if t % args.event_every == 0]  # steps carrying hipEvents
+    timed = [t for t in range(args.steps) if t % args.event_every == args.event_every - 1]  # steps with hipEvents
     for t in range(args.steps):
         b, e = ev.pair(t)
         k = (args.warmup + t) % ring
-        if t % args.event_every == 0:
+        if t % args.event_every == args.event_every - 1:
             ev.hip.hipEventRecord(b, stream)
         env.step({"action": acts[k], "prediction": preds[k]}) if not senv.gather else \
             senv.step({"action": acts[k], "prediction": preds[k]})
-        if t % args.event_every == 0:
+        if t % args.event_every == args.event_every - 1:
             ev.hip.hipEventRecord(e, stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -365,9 +365,9 @@ def run_lidar(args, world, rank, dev):
         dist.barrier()
     t0 = time.perf_counter()
     first_timed = steps_done + 1
-    timed = [t for t in range(args.steps) if t % args.event_every == 0]  # steps carrying kernel events
+    timed = [t for t in range(args.steps) if t % args.event_every == args.event_every - 1]  # steps with hipEvents
     for t in range(args.steps):
-        step(ev.pair(t) if t % args.event_every == 0 else (None, None))
+        step(ev.pair(t) if t % args.event_every == args.event_every - 1 else (None, None))
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -389,7 +389,8 @@ def run_lidar(args, world, rank, dev):
         torch.cuda.synchronize(dev)
         te = time.perf_counter()
         # events on every event_every-th step and on the autoreset step (the last)
-        ep_t = [t for t in range(EPISODE_PERIOD) if t % args.event_every == 0 or t == EPISODE_PERIOD - 1]
+        ep_t = [t for t in range(EPISODE_PERIOD)
+                if t % args.event_every == args.event_every - 1 or t == EPISODE_PERIOD - 1]
         for t in range(EPISODE_PERIOD):
             step(ev.pair(args.steps + t) if t in ep_t else (None, None))
         torch.cuda.synchronize(dev)
@@ -486,10 +487,12 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=101)
     ap.add_argument("--cpu-threads", type=int, default=None, help="OpenMP threads of the multi-thread CPU row")
     ap.add_argument("--event-every", type=int, default=4,
-                    help="record the kernel's hipEvents on every N-th timed step: each event pair adds two stream "
-                         "packets between kernels, measured +6..9 us of wall per step on MI355X "
-                         "(tools/host_overhead.py), so sampling keeps `value` unperturbed")
+                    help="record the kernel's hipEvents on every N-th timed step (steps N-1, 2N-1, ...: not the "
+                         "first launch after the synchronize): each event pair adds two stream packets between "
+                         "kernels, measured +6..9 us of wall per step on MI355X (tools/host_overhead.py), so "
+                         "sampling keeps `value` unperturbed")
     args = ap.parse_args()
+    args.event_every = max(1, min(args.event_every, args.steps))  # at least one timed launch carries events
 
     import torch
     import torch.distributed as dist
