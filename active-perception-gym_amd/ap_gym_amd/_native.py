@@ -235,16 +235,35 @@ def exact_device(device):
     return device
 
 
-def as_device_f32(x, dev, numel: int, shape=None):
+def as_device_f32(x, dev, numel: int, shape=None, name: str = "input"):
     """`x` as a contiguous float32 tensor on `dev` (an exact_device): `x` itself when it already is one
-    with `numel` elements (the step hot path: no tensor constructions), else converted."""
+    with `numel` elements (the step hot path: no tensor constructions), else converted.  The size is
+    checked here because the C ABI takes raw pointers (the torch ops check it in check_io)."""
     import torch
 
     if (type(x) is torch.Tensor and x.dtype is torch.float32 and x.device == dev and x.is_contiguous()
             and x.numel() == numel):
         return x
     t = torch.as_tensor(x, dtype=torch.float32, device=dev)
-    return (t if shape is None else t.reshape(shape)).contiguous()
+    t = (t if shape is None or t.numel() != numel else t.reshape(shape)).contiguous()
+    if t.numel() != numel:
+        raise RuntimeError(f"{name} must have {numel} elements, got {t.numel()}")
+    return t
+
+
+def wrong_current_device(dev) -> bool:
+    """True when HIP's current device is not `dev` (an exact_device): direct C-ABI launches run on the
+    current device."""
+    import torch
+
+    return torch._C._cuda_getDevice() != dev.index
+
+
+def current_stream_ptr(dev) -> int:
+    """Raw HIP stream of torch's current stream on `dev` (an exact_device), the stream the torch ops use."""
+    import torch
+
+    return torch._C._cuda_getCurrentRawStream(dev.index)
 
 
 def op_buffers(tensors, device):

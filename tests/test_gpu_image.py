@@ -342,8 +342,11 @@ def test_image_env_matches_oracle_at_scale(gpu, kind, n, shape, sensor, k, steps
     env.close()
 
 
+@pytest.mark.parametrize("via_op", [False, True], ids=["c_abi", "torch_op"])
 @pytest.mark.parametrize("kind,sparse", [("cls", False), ("loc", False), ("cls", True), ("loc", True)])
-def test_image_env_torch_backend_matches_numpy(gpu, kind, sparse):
+def test_image_env_torch_backend_matches_numpy(gpu, kind, sparse, via_op):
+    """The torch backend equals the numpy backend, with eager steps through the C ABI (default) and
+    through torch.ops.apgym.image_step (use_torch_op)."""
     import torch
 
     import ap_gym_amd as ap
@@ -353,6 +356,7 @@ def test_image_env_torch_backend_matches_numpy(gpu, kind, sparse):
     else:
         g = golden("image_cls_mnist.npz" if kind == "cls" else "image_loc_mnist.npz")
     e_np, e_t = _make_env(ap, g, sparse=sparse), _make_env(ap, g, backend="torch", copy=True, sparse=sparse)
+    e_t.use_torch_op = via_op
     o1, _ = e_np.reset(seed=5)
     o2, _ = e_t.reset(seed=5)
     for k in o1:
