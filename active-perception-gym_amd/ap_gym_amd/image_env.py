@@ -228,6 +228,7 @@ class _ImageVectorEnv(VectorEnv):
         # them through torch.ops.apgym.image_step instead.
         self.use_torch_op = False
         self._c_args = None
+        self._kernel_events = None
         self._h = t.classes.apgym.ImageEnv(
             [c.num_envs, c.kind, c.height, c.width, c.pool_channels, c.channels, c.pool_dtype, c.sensor_h,
              c.sensor_w, c.step_limit, c.num_classes, c.invert_labels, c.top_k, c.unique_points, c.num_envs_total,
@@ -378,6 +379,9 @@ class _ImageVectorEnv(VectorEnv):
             p_t = N.as_device_f32(p, self._dev, pdim * n, (n, pdim), name="prediction")
         resetting = self._prev_done
         self._track_render(p_np if numpy_mode else p_t, resetting)
+        ev = self._kernel_events
+        if ev is not None:  # bench timing: hipEvents on the launch stream right around the step's launches
+            N.event_record(ev[0], N.current_stream_ptr(self._dev))
         if self.use_torch_op:
             self._step_op(self._h, a_t, p_t, int(self._t_step), bool(resetting))
         elif N.wrong_current_device(self._dev):  # the op's DeviceGuard, for the direct call
@@ -385,6 +389,8 @@ class _ImageVectorEnv(VectorEnv):
                 self._c_step(a_t, p_t, resetting)
         else:
             self._c_step(a_t, p_t, resetting)
+        if ev is not None:
+            N.event_record(ev[1], N.current_stream_ptr(self._dev))
         if resetting:
             self._t_step = 0
             terminated = False
@@ -396,6 +402,11 @@ class _ImageVectorEnv(VectorEnv):
             return self._numpy_step(resetting, terminated)
         self._post_launch_error_copy()
         return self._torch_step(resetting, terminated)
+
+    def set_kernel_timing_events(self, begin=None, end=None):
+        """Record hipEvent_t handles `begin`/`end` around the next steps' kernel launches (not around the
+        Python step), on their stream (bench.py's live timing).  None disables."""
+        self._kernel_events = None if begin is None else (begin, end)
 
     def _c_step(self, a_t, p_t, resetting):
         if self._c_args is None:

@@ -183,22 +183,18 @@ def run_image(args, world, rank, dev):
         senv.step({"action": acts[t % ring], "prediction": preds[t % ring]})
     senv.gather_ms()
     ev = HipEvents(args.steps)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    ev.hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     timed = [t for t in range(args.steps) if t % args.event_every == args.event_every - 1]  # steps with hipEvents
     for t in range(args.steps):
-        b, e = ev.pair(t)
         k = (args.warmup + t) % ring
-        if t % args.event_every == args.event_every - 1:
-            ev.hip.hipEventRecord(b, stream)
+        # hipEvents right around the step's kernel launches (inside env.step), on sampled steps
+        env.set_kernel_timing_events(*(ev.pair(t) if t % args.event_every == args.event_every - 1 else (None, None)))
         env.step({"action": acts[k], "prediction": preds[k]}) if not senv.gather else \
             senv.step({"action": acts[k], "prediction": preds[k]})
-        if t % args.event_every == args.event_every - 1:
-            ev.hip.hipEventRecord(e, stream)
+    env.set_kernel_timing_events(None)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -235,7 +231,7 @@ def run_image(args, world, rank, dev):
                        "gather_ms": gather_ms if senv.gather else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tpath,
-                         "kernel": "image step (all kernels, HIP events around env.step)", "kernel_ms": step_ms,
+                         "kernel": "image step (all kernels, HIP events around the step's launches)", "kernel_ms": step_ms,
                          "launches_timed": len(timed), "event_every": args.event_every,
                          "bytes_per_launch": bpe * n_local, "issue": issue},
         }
