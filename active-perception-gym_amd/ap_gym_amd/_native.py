@@ -59,7 +59,7 @@ class LidarConfig(ctypes.Structure):
                 ("beams", ctypes.c_int32), ("step_limit", ctypes.c_int32), ("max_rooms", ctypes.c_int32),
                 ("door_width", ctypes.c_int32), ("lidar_range", ctypes.c_float), ("loss_scale", ctypes.c_float),
                 ("loss_offset", ctypes.c_float), ("branching_prob", ctypes.c_double), ("log_stats", ctypes.c_int32),
-                ("sparse", ctypes.c_int32)]
+                ("sparse", ctypes.c_int32), ("out_row_bytes", ctypes.c_int32)]
 
 
 class LidarState(ctypes.Structure):
@@ -147,6 +147,7 @@ SYMBOLS = [
                                       ctypes.POINTER(LidarOutputs), _vp]),
     ("apg_lidar_step_profiled", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(LidarState), _vp, _vp,
                                                ctypes.POINTER(LidarOutputs), _vp, _vp, _vp]),
+    ("apg_maze_frames", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("apg_map_generate", ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp]),
     ("apg_lidar_scan_batch", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp,

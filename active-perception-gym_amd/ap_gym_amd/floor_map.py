@@ -94,7 +94,7 @@ def generate_maps(ds: FloorMapDataset, idx: np.ndarray, device="cuda") -> np.nda
     idx_t = torch.as_tensor(idx.astype(np.int64), device=dev)
     occ = torch.zeros((n, h, wpr), dtype=torch.int64, device=dev)
     scratch = None  # reserved ABI slot, unused
-    frames = ((h + 1) // 2) * ((w + 1) // 2) + 4
+    frames = int(N.lib().apg_maze_frames(h, w))
     stack = torch.zeros((n, frames), dtype=torch.int16, device=dev) if ds.map_kind == N.APG_MAP_MAZE else None
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     rc = N.lib().apg_map_generate(ds.map_kind, N.ptr(idx_t), n, h, w, p["max_rooms"], p["door_width"],

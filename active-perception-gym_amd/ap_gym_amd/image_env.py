@@ -685,6 +685,8 @@ class _ImageVectorEnv(VectorEnv):
             self._closed = True
             self.closed = True
             self._t = {}
+            self._h = None  # the op handle keeps every state/output buffer alive
+            self._c_args = None
 
 
 class ImageClassificationVectorEnv(_ImageVectorEnv):

@@ -57,6 +57,54 @@ def lidar_beam_directions(beams: int, lidar_range: float) -> np.ndarray:
     return np.ascontiguousarray(unscaled * lidar_range, dtype=np.float32)
 
 
+# Packed output rows (apg_lidar_config.out_row_bytes): every per-env output of a step in one row per env,
+# 8-byte fields first, so ShardedVectorEnv all-gathers the [N, row] buffer as is (no packing copies) and
+# the gathered fields are strided views of the receive buffer.
+def lidar_output_row_layout(beams: int, log_stats: bool = False, sparse: bool = False):
+    """[(name, torch dtype, per-env shape, byte offset)] of the packed output row, and the row size."""
+    import torch
+
+    f64, i64, f32, i32, b8 = torch.float64, torch.int64, torch.float32, torch.int32, torch.bool
+    fields = [("reward", f64, ()), ("map_idx_out", i64, ())] + ([("weight", f64, ())] if sparse else []) + [
+        ("lidar", f32, (beams,)), ("odometry", f32, (2,)), ("target", f32, (2,)), ("time_step", f32, ()),
+        ("base_reward", f32, ()), ("loss", f32, ())] + (
+        [("stats", f32, (4,)), ("stats_len", i32, ())] if log_stats else []) + [
+        ("terminated", b8, ()), ("truncated", b8, ()), ("info_mask", b8, ()), ("reset_mask", b8, ())]
+    out, off = [], 0
+    for name, dt, sh in fields:
+        out.append((name, dt, sh, off))
+        off += torch.empty((), dtype=dt).element_size() * int(np.prod(sh, dtype=np.int64))
+    return out, off + (-off) % 8
+
+
+def row_views(buf, layout) -> dict:
+    """Field views of a packed [rows, row_bytes] uint8 buffer (stats as [4, rows] like the dense layout)."""
+    import torch
+
+    v = {}
+    for name, dt, sh, off in layout:
+        nb = torch.empty((), dtype=dt).element_size() * int(np.prod(sh, dtype=np.int64))
+        t = buf[:, off:off + nb].view(dt)
+        if not sh:
+            t = t[:, 0]
+        v[name] = t.T if name == "stats" else t
+    return v
+
+
+def row_views_np(buf: np.ndarray, layout) -> dict:
+    """numpy field views of a packed [rows, row_bytes] uint8 host buffer (stats as [4, rows])."""
+    import torch
+
+    v = {}
+    for name, dt, sh, off in layout:
+        npdt = torch.empty((), dtype=dt).numpy().dtype
+        nb = npdt.itemsize * int(np.prod(sh, dtype=np.int64))
+        a = buf[:, off:off + nb].view(npdt)
+        a = a[:, 0] if not sh else a.reshape(buf.shape[0], *sh)
+        v[name] = a.T if name == "stats" else a
+    return v
+
+
 def torch_index(idx: np.ndarray, device):
     import torch
 
@@ -92,7 +140,7 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
                  static_map_index: int = 0, prefetch: bool = True, prefetch_buffer_size: int = 128,
                  max_episode_steps: int = 100, device=None, env_offset: int = 0, copy: bool = False,
                  strict_errors: bool = False, array_backend: str = "numpy", log_stats: bool = False,
-                 sparse: bool = False, render_envs=None, sparse_reset_info: bool = False):
+                 sparse: bool = False, render_envs=None, sparse_reset_info: bool = False, packed_outputs: bool = False):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -128,13 +176,17 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         # ---- native configuration
         p = dataset.native_params()
         scale, offset = affine_f32(inner_loss)
+        self.output_layout, row_bytes = lidar_output_row_layout(self.lidar_beam_count, self.log_stats, self.sparse)
+        # the numpy backend always uses the packed rows: one D2H copy per step for every per-env output
+        if not (packed_outputs or array_backend == "numpy"):
+            self.output_layout, row_bytes = None, 0
         self._cfg = N.LidarConfig(num_envs=self.num_envs, height=h, width=w, map_kind=dataset.map_kind,
                                   is_static=int(self.static_map), static_map_index=int(static_map_index),
                                   beams=self.lidar_beam_count, step_limit=self.max_episode_steps,
                                   max_rooms=p["max_rooms"], door_width=p["door_width"],
                                   lidar_range=float(np.float32(lidar_range)), loss_scale=scale, loss_offset=offset,
                                   branching_prob=p["branching_prob"], log_stats=int(self.log_stats),
-                                  sparse=int(self.sparse))
+                                  sparse=int(self.sparse), out_row_bytes=row_bytes)
         L = N.lib()
         sizes = N.LidarSizes()
         N.check(L.apg_lidar_query_sizes(ctypes.byref(self._cfg), ctypes.byref(sizes)), "apg_lidar_query_sizes")
@@ -173,6 +225,11 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             stats_len=t.zeros(n, dtype=t.int32, device=dev) if self.log_stats else None,
             weight=t.zeros(n, dtype=t.float64, device=dev) if self.sparse else None,
         )
+        # packed_outputs: the per-env outputs are field views of one [n, row] buffer (ShardedVectorEnv's send)
+        self.output_rows = None
+        if row_bytes:
+            self.output_rows = t.zeros((n, row_bytes), dtype=t.uint8, device=dev)
+            self._t.update(row_views(self.output_rows, self.output_layout))
         T = self._t
         self._state = N.LidarState(*[N.ptr(T[k]) for k in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng",
                                                             "occ", "scratch", "stack", "map_idx", "beam_dirs",
@@ -194,7 +251,7 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         self._c_args = None
         self._h = t.classes.apgym.LidarEnv(
             [c.num_envs, c.height, c.width, c.map_kind, c.is_static, c.static_map_index, c.beams, c.step_limit,
-             c.max_rooms, c.door_width, c.log_stats, c.sparse],
+             c.max_rooms, c.door_width, c.log_stats, c.sparse, c.out_row_bytes],
             [c.lidar_range, c.loss_scale, c.loss_offset, c.branching_prob],
             N.op_buffers([T[k] for k in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng", "occ", "scratch",
                                          "stack", "map_idx", "beam_dirs", "stats_hist")], dev),
@@ -205,6 +262,7 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         self._err_event = t.cuda.Event()
         self._err_pending = False
         self._autoreset_host = np.zeros(n, dtype=bool)
+        self._rows_host = self._rows_np = self._map_host = None  # numpy backend: pinned host mirrors
         self._seeded = False
         self._closed = False
         self._kernel_events = None
@@ -422,8 +480,9 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         T = self._t
         if self.array_backend == "numpy":
             self.check_errors(block=True)
-            return self._to_numpy_obs(), {"map_idx": T["map_idx_out"].cpu().numpy().astype(np.int64),
-                                          "_map_idx": np.ones(self.num_envs, dtype=bool)}
+            R = self._host_rows()
+            return self._to_numpy_obs(R, None), {"map_idx": R["map_idx_out"].astype(np.int64),
+                                                 "_map_idx": np.ones(self.num_envs, dtype=bool)}
         self._post_launch_error_copy()
         return self._obs_out(), {"map_idx": T["map_idx_out"], "_map_idx": T["reset_mask"]}
 
@@ -507,15 +566,15 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
 
         return clone(self._stats_view)
 
-    def _numpy_stats(self, info: dict):
+    def _numpy_stats(self, info: dict, R: dict):
         """SyncVectorEnv's merge of the sub-envs' ActiveRegressionLogWrapper stats (util.py:18-37):
         python-float scalars -> float64 arrays, lists -> object arrays, `_key` masks."""
         T = self._t
-        lens = T["stats_len"].cpu().numpy()
+        lens = R["stats_len"].copy()
         done = lens > 0
         if not done.any():
             return
-        st = T["stats"].cpu().numpy()
+        st = R["stats"]
         idx = np.nonzero(done)[0]
         hist = T["stats_hist"][:, :, torch_index(idx, self.device)].permute(2, 0, 1).cpu().numpy()  # [k, 2, steps]
         scalar: dict[str, Any] = {}
@@ -542,44 +601,75 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         obs["time_step"] = c(T["time_step"])
         return obs
 
-    def _to_numpy_obs(self):
+    def _host_rows(self) -> dict:
+        """numpy backend: the packed output rows and the error word copied D2H into pinned host memory in one
+        go, then one synchronize; returns numpy field views of the host rows (valid until the next call)."""
+        import torch
+
+        if self._rows_host is None:
+            self._rows_host = torch.empty(tuple(self.output_rows.shape), dtype=torch.uint8).pin_memory()
+            self._rows_np = row_views_np(self._rows_host.numpy(), self.output_layout)
+        self._rows_host.copy_(self.output_rows, non_blocking=True)
+        self._err_host.copy_(self._t["err"], non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        self._err_pending = False
+        return self._rows_np
+
+    def _map_refresh(self, reset_mask: np.ndarray | None):
+        """The host mirror of the map observation, refreshed only for the sub-envs that reset (the map obs
+        changes only then); None refreshes every sub-env.  Returned as is (copy=False) or copied."""
+        import torch
+
+        if self.static_map:
+            return None
         T = self._t
-        obs = {"lidar": T["lidar"].cpu().numpy(), "odometry": T["odometry"].cpu().numpy()}
+        if self._map_host is None:
+            self._map_host = torch.empty(tuple(T["map_obs"].shape), dtype=torch.float32).pin_memory()
+            reset_mask = None
+        if reset_mask is None or reset_mask.all():
+            self._map_host.copy_(T["map_obs"])
+        elif reset_mask.any():
+            idx = np.nonzero(reset_mask)[0]
+            self._map_host.numpy()[idx] = T["map_obs"][torch_index(idx, self.device)].cpu().numpy()
+        m = self._map_host.numpy()
+        return m.copy() if self.copy else m
+
+    def _to_numpy_obs(self, R: dict | None = None, reset_mask: np.ndarray | None = None):
+        if R is None:
+            R = self._host_rows()
+        obs = {"lidar": R["lidar"].copy(), "odometry": R["odometry"].copy()}
         if not self.static_map:
-            obs["map"] = T["map_obs"].cpu().numpy()
-        obs["time_step"] = T["time_step"].cpu().numpy()
+            obs["map"] = self._map_refresh(reset_mask)
+        obs["time_step"] = R["time_step"].copy()
         return obs
 
     def _numpy_step_result(self):
-        import torch
-
-        torch.cuda.synchronize(self.device)
-        T = self._t
-        bits = int(T["err"].item())
+        R = self._host_rows()  # every per-env output in one D2H copy + one synchronize
+        bits = int(self._err_host[0])
         if bits:
-            T["err"].zero_()
+            self._t["err"].zero_()
             self._raise_error_bits(bits)
-        obs = self._to_numpy_obs()
-        reward = T["reward"].cpu().numpy()
-        term = T["terminated"].cpu().numpy()
-        trunc = T["truncated"].cpu().numpy()
-        mask = T["info_mask"].cpu().numpy()
+        reset_mask = R["reset_mask"].copy()
+        obs = self._to_numpy_obs(R, reset_mask)
+        reward = R["reward"].copy()
+        term = R["terminated"].copy()
+        trunc = R["truncated"].copy()
+        mask = R["info_mask"].copy()
         info: dict[str, Any] = {}
         if mask.any():
-            info["base_reward"] = np.where(mask, T["base_reward"].cpu().numpy(), np.float32(0))
+            info["base_reward"] = np.where(mask, R["base_reward"], np.float32(0))
             info["_base_reward"] = mask.copy()
-            tgt = np.where(mask[:, None], T["target"].cpu().numpy(), np.float32(0))
-            loss = np.where(mask, T["loss"].cpu().numpy(), np.float32(0))
+            tgt = np.where(mask[:, None], R["target"], np.float32(0))
+            loss = np.where(mask, R["loss"], np.float32(0))
             if self.sparse:
                 tgt = {"target": tgt, "_target": mask.copy(),
-                       "weight": np.where(mask, T["weight"].cpu().numpy(), 0.0), "_weight": mask.copy()}
+                       "weight": np.where(mask, R["weight"], 0.0), "_weight": mask.copy()}
             info["prediction"] = {"target": tgt, "_target": mask.copy(), "loss": loss, "_loss": mask.copy()}
             info["_prediction"] = mask.copy()
         if self.log_stats:
-            self._numpy_stats(info)
-        reset_mask = T["reset_mask"].cpu().numpy()
+            self._numpy_stats(info, R)
         if reset_mask.any():
-            info["map_idx"] = np.where(reset_mask, T["map_idx_out"].cpu().numpy(), 0).astype(np.int64)
+            info["map_idx"] = np.where(reset_mask, R["map_idx_out"], 0).astype(np.int64)
             info["_map_idx"] = reset_mask
         self._autoreset_host = term | trunc
         return obs, reward, term, trunc, info
@@ -589,6 +679,9 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             self._closed = True
             self.closed = True
             self._t = {}
+            self._h = None  # the op handle keeps every state/output buffer alive
+            self._c_args = None
+            self.output_rows = None
 
     def __repr__(self):
         kind = "maze" if isinstance(self.dataset, FloorMapDatasetMaze) else "rooms"

@@ -8,18 +8,25 @@ Sub-envs are independent, so rank r owns the contiguous block [r*N/W, (r+1)*N/W)
 Either way the union of the shards is bit-identical to one unsharded env and no data-path
 collective is needed (weak scaling).
 
-`ShardedVectorEnv(..., gather=True)` additionally reassembles the batched step outputs on every rank
-with one all-gather over a packed byte row per env — RCCL over xGMI on MI355X, gloo on CPU — for
-consumers that need the full batch (the north star's obs/reward reassembly):
-  LIDAR  lidar, odometry, time_step, reward, base_reward, target, loss, terminated, truncated,
-         info mask (the per-reset map observation stays sharded)
+`ShardedVectorEnv(..., gather=True)` additionally reassembles the batched outputs on every rank (after
+reset and after every step) with one all-gather over a row of bytes per env — RCCL over xGMI on MI355X,
+gloo on CPU — for consumers that need the full batch (the north star's obs/reward reassembly):
+  LIDAR  the local env is built with packed_outputs=True: its step kernel writes every per-env output
+         (lidar, odometry, time_step, reward, terminated, truncated, base_reward, target, loss, info mask,
+         map_idx, reset mask, and stats / weight when logged / sparse) straight into one [N, row] buffer
+         (lidar_env.lidar_output_row_layout), which is the all-gather's send buffer as is, and the gathered
+         fields are strided views of the receive buffer: no packing or unpacking copies.  The per-reset map
+         observation (4*H*W bytes per env) and the per-step stats history stay sharded: they are returned
+         as info["local_obs"] / the local env's buffers.
   image  glimpse_pos, time_step, reward, base_reward, target, loss, index, terminated, truncated
-         (+ glimpse and target_glimpse with gather_glimpse=True)
+         (+ glimpse and target_glimpse with gather_glimpse=True), packed per step by copies
 (image_classification.py:117-151 and image_localization.py:131-181 are the outputs gathered).
+Envs without packed rows (e.g. test doubles) take the copying path for LIDAR too.
 """
 
 from __future__ import annotations
 
+import inspect
 from typing import Callable
 
 
@@ -34,8 +41,16 @@ def _is_lidar(env, beams) -> bool:
     return beams is not None or hasattr(env, "lidar_beam_count")
 
 
+def _accepts(fn, name: str) -> bool:
+    try:
+        ps = inspect.signature(fn).parameters.values()
+    except (TypeError, ValueError):
+        return False
+    return any(p.name == name or p.kind == inspect.Parameter.VAR_KEYWORD for p in ps)
+
+
 def _row_spec(env, beams, gather_glimpse: bool):
-    """(name, dtype, per-env shape) of the gathered fields of `env`'s torch step outputs."""
+    """(name, dtype, per-env shape) of the gathered fields of `env`'s torch step outputs (copying path)."""
     import torch
 
     f32, f64, b8, i32, i64 = torch.float32, torch.float64, torch.bool, torch.int32, torch.int64
@@ -69,7 +84,8 @@ def _nbytes(dtype, shape) -> int:
 
 class ShardedVectorEnv:
     """One rank's shard of a vector env (`make_local(num_envs=, env_offset=)` builds it; image envs also
-    take num_envs_total=) plus the optional packed all-gather of the step outputs."""
+    take num_envs_total=; LIDAR envs get packed_outputs=True when gathering and make_local accepts it) plus
+    the optional all-gather of the outputs."""
 
     def __init__(self, make_local: Callable[..., object], num_envs_total: int, rank: int, world: int,
                  beams: int | None = None, gather: bool = False, group=None, gather_glimpse: bool = False,
@@ -77,17 +93,50 @@ class ShardedVectorEnv:
         self.rank, self.world, self.gather, self.group = rank, world, gather, group
         self.offset, self.local_num_envs = shard_bounds(num_envs_total, rank, world)
         self.num_envs = num_envs_total
-        self.env = make_local(num_envs=self.local_num_envs, env_offset=self.offset)
+        kw = {"packed_outputs": True} if gather and beams is not None and _accepts(make_local, "packed_outputs") else {}
+        self.env = make_local(num_envs=self.local_num_envs, env_offset=self.offset, **kw)
         self._lidar = _is_lidar(self.env, beams)
+        self._packed = gather and getattr(self.env, "output_rows", None) is not None
         self._spec = _row_spec(self.env, beams, gather_glimpse)
         self._row = sum(_nbytes(dt, sh) for _, dt, sh in self._spec)
         self._row += (-self._row) % 8
         self._send = self._recv = None
+        self._views = None
         self.time_gather = time_gather
         self.gather_events: list = []  # (begin, end) torch.cuda.Event pairs around each all-gather
 
-    def reset(self, *, seed=None, options=None):
-        return self.env.reset(seed=seed, options=options)
+    # ------------------------------------------------------------------ collectives
+    def _all_gather_rows(self, send):
+        """All-gather of a [n, row] uint8 buffer into self._recv [world * n, row] (allocated once)."""
+        import torch
+        import torch.distributed as dist
+
+        if self._recv is None:
+            self._recv = torch.zeros((self.world * send.shape[0], send.shape[1]), dtype=torch.uint8,
+                                     device=send.device)
+        ev = None
+        if self.time_gather and send.is_cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(self._recv, send, group=self.group)
+        else:  # gloo (CPU tests, or several ranks sharing one GPU): through host buffers
+            recv = [torch.empty_like(send, device="cpu") for _ in range(self.world)]
+            dist.all_gather(recv, send.cpu(), group=self.group)
+            self._recv.copy_(torch.cat(recv))
+        if ev is not None:
+            ev[1].record()
+            self.gather_events.append(ev)
+        return self._recv
+
+    def _gathered_rows(self) -> dict:
+        """The packed path: gather the local env's output rows; field views of the receive buffer."""
+        from .lidar_env import row_views
+
+        recv = self._all_gather_rows(self.env.output_rows)
+        if self._views is None:
+            self._views = row_views(recv, self.env.output_layout)
+        return self._views
 
     def _pack(self, fields: dict):
         import torch
@@ -96,7 +145,6 @@ class ShardedVectorEnv:
         if self._send is None:
             dev = fields[self._spec[0][0]].device
             self._send = torch.zeros((n, self._row), dtype=torch.uint8, device=dev)
-            self._recv = torch.zeros((self.world * n, self._row), dtype=torch.uint8, device=dev)
         o = 0
         for name, dt, sh in self._spec:
             nb = _nbytes(dt, sh)
@@ -114,24 +162,8 @@ class ShardedVectorEnv:
         return out
 
     def all_gather(self, fields: dict) -> dict:
-        import torch
-        import torch.distributed as dist
-
-        send = self._pack(fields)
-        ev = None
-        if self.time_gather and send.is_cuda:
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record()
-        if dist.get_backend(self.group) == "nccl":
-            dist.all_gather_into_tensor(self._recv, send, group=self.group)
-        else:  # gloo (CPU tests, or several ranks sharing one GPU): through host buffers
-            recv = [torch.empty_like(send, device="cpu") for _ in range(self.world)]
-            dist.all_gather(recv, send.cpu(), group=self.group)
-            self._recv.copy_(torch.cat(recv))
-        if ev is not None:
-            ev[1].record()
-            self.gather_events.append(ev)
-        return self._unpack(self._recv)
+        """The copying path: pack `fields` (the spec's), all-gather, unpack."""
+        return self._unpack(self._all_gather_rows(self._pack(fields)))
 
     def gather_ms(self) -> float | None:
         """Mean time of the timed all-gathers so far (synchronizes), then forgets them."""
@@ -144,10 +176,44 @@ class ShardedVectorEnv:
         self.gather_events.clear()
         return ms
 
+    # ------------------------------------------------------------------ API
+    def reset(self, *, seed=None, options=None):
+        obs, info = self.env.reset(seed=seed, options=options)
+        if not (self.gather and self._packed):
+            # the copying path gathers step outputs only (a reset has no reward / prediction fields)
+            return obs, info
+        v = self._gathered_rows()
+        gobs = {"lidar": v["lidar"], "odometry": v["odometry"], "time_step": v["time_step"]}
+        return gobs, {"map_idx": v["map_idx_out"], "_map_idx": v["reset_mask"], "local_obs": obs,
+                      "local_info": info}
+
+    def _packed_step_info(self, v: dict, obs: dict) -> dict:
+        mask = v["info_mask"]
+        target = v["target"]
+        if "weight" in v:  # -sparse ids
+            target = {"target": target, "_target": mask, "weight": v["weight"], "_weight": mask}
+        info = {"base_reward": v["base_reward"], "_base_reward": mask,
+                "prediction": {"target": target, "_target": mask, "loss": v["loss"], "_loss": mask},
+                "_prediction": mask, "map_idx": v["map_idx_out"], "_map_idx": v["reset_mask"], "local_obs": obs}
+        if "stats" in v:  # scalar episode statistics (the per-step history stays in the local env)
+            done = v["terminated"]
+            names = ("avg_euclidean_distance", "avg_mse", "final_euclidean_distance", "final_mse")
+            scalar = {}
+            for j, name in enumerate(names):
+                scalar[name] = v["stats"][j]
+                scalar["_" + name] = done
+            info["stats"] = {"scalar": scalar, "_scalar": done, "length": v["stats_len"]}
+            info["_stats"] = done
+        return info
+
     def step(self, action):
         obs, rew, term, trunc, info = self.env.step(action)
         if not self.gather:
             return obs, rew, term, trunc, info
+        if self._packed:
+            v = self._gathered_rows()
+            gobs = {"lidar": v["lidar"], "odometry": v["odometry"], "time_step": v["time_step"]}
+            return gobs, v["reward"], v["terminated"], v["truncated"], self._packed_step_info(v, obs)
         if self._lidar:
             full = self.all_gather({"lidar": obs["lidar"], "odometry": obs["odometry"], "time_step": obs["time_step"],
                                     "reward": rew, "base_reward": info["base_reward"],

@@ -18,10 +18,13 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 
 #include "../../include/apgym_capi.h"
 #include "apg_host.hpp"
 #include "apg_maps.hpp"
+#include "apg_maze.hpp"
 #include "apg_pairwise.hpp"
 #include "apg_scan.hpp"
 
@@ -72,9 +75,17 @@ BinomTable make_binom_table() {
 }
 
 struct Geo {
-  int n, h, w, wpr, is_static, kind, max_rooms, door_width, frames;
+  int n, h, w, wpr, is_static, kind, max_rooms, door_width, frames, row;
   double bp;
 };
+
+// Output element j of env e: a dense [N][k] array, or (row > 0: apg_lidar_config.out_row_bytes) a field of env
+// e's packed output row, the layout ShardedVectorEnv all-gathers without a packing copy.
+template <class T>
+APG_DEV T &oat(T *p, int row, int e, int k, int j = 0) {
+  return row ? *reinterpret_cast<T *>(reinterpret_cast<char *>(p) + (size_t)e * (size_t)row + (size_t)j * sizeof(T))
+             : p[(size_t)e * k + j];
+}
 
 Geo make_geo(const apg_lidar_config *c) {
   Geo g;
@@ -86,8 +97,9 @@ Geo make_geo(const apg_lidar_config *c) {
   g.kind = c->map_kind;
   g.max_rooms = c->max_rooms;
   g.door_width = c->door_width;
-  g.frames = ((c->height + 1) / 2) * ((c->width + 1) / 2) + 4;
+  g.frames = (int)(maze_scratch_bytes(c->height, c->width) / 2);  // maze scratch, in u16 units
   g.bp = c->branching_prob;
+  g.row = c->out_row_bytes;
   return g;
 }
 
@@ -111,6 +123,7 @@ int validate(const apg_lidar_config *c) {
     return fail(APG_E_INVALID, "lidar_range must be in (0, 10] (occupancy window of the fused step kernel)");
   if (c->step_limit <= 0) return fail(APG_E_INVALID, "step_limit must be positive");
   if (c->log_stats && c->step_limit > PW_PTR_MAX_N) return fail(APG_E_INVALID, "log_stats needs step_limit <= 968");
+  if (c->out_row_bytes < 0 || (c->out_row_bytes & 7)) return fail(APG_E_INVALID, "out_row_bytes must be a multiple of 8");
   return APG_OK;
 }
 
@@ -146,14 +159,7 @@ APG_DEV int place_start(Pcg64 &rng, const uint64_t *rows, int h, int w, int wpr,
 // ------------------------------------------------------------------ kernels
 // Map generator of a kernel instance (template parameter GEN): static maps are generated once by
 // apg_lidar_init, so the reset kernel for them only draws start cells.
-enum : int { GEN_NONE = 0, GEN_ROOMS = 1, GEN_MAZE = 2 };
-
-template <int GEN>
-APG_DEV int generate_one(const Geo &g, Pcg64 &r, uint64_t *occ, uint16_t *stack, const BinomTable &bt,
-                         const MazeLds &ml) {
-  if constexpr (GEN == GEN_MAZE) return maze_generate(r, Bits{occ, g.wpr}, g.h, g.w, g.bp, stack, g.frames, ml);
-  else return rooms_generate(r, occ, g.wpr, g.h, g.max_rooms, g.door_width, bt);
-}
+enum : int { GEN_NONE = 0, GEN_ROOMS = 1 };  // mazes: k_maze
 
 // Rooms maps are painted into the lane's LDS bitmap (row words are read-modify-written once per
 // primitive), then the wave copies its bitmaps out with coalesced stores.
@@ -165,10 +171,9 @@ APG_DEV void copy_out_maps(const uint64_t *s_maps, unsigned long long done, size
   }
 }
 
-template <int GEN>
-__global__ __launch_bounds__(64) void k_map_generate(Geo g, const uint64_t *idx, int n, uint64_t *occ,
-                                                     uint16_t *stack, uint32_t *err, BinomTable bt, int lanes) {
-  extern __shared__ uint64_t s_rows[];  // rooms: [lanes][h * wpr]; maze: maze_lds_at's layout
+__global__ __launch_bounds__(64) void k_map_generate_rooms(Geo g, const uint64_t *idx, int n, uint64_t *occ,
+                                                           uint32_t *err, BinomTable bt, int lanes) {
+  extern __shared__ uint64_t s_rows[];  // [lanes][h * wpr]
   const int lane = threadIdx.x;
   const int i = blockIdx.x * lanes + lane;
   const bool active = lane < lanes && i < n;
@@ -176,24 +181,50 @@ __global__ __launch_bounds__(64) void k_map_generate(Geo g, const uint64_t *idx,
   int rc = 0;
   if (active) {
     Pcg64 r = seed_pcg64(idx[i]);
-    if constexpr (GEN == GEN_ROOMS)
-      rc = rooms_generate(r, s_rows + lane * words, g.wpr, g.h, g.max_rooms, g.door_width, bt);
-    else
-      rc = generate_one<GEN>(g, r, occ + (size_t)i * words, stack + (size_t)i * g.frames, bt,
-                             maze_lds_at(s_rows, g.h, lanes, lane));
+    rc = rooms_generate(r, s_rows + lane * words, g.wpr, g.h, g.max_rooms, g.door_width, bt);
   }
-  if constexpr (GEN == GEN_ROOMS) copy_out_maps(s_rows, __ballot(active), words, occ + (size_t)blockIdx.x * lanes * words, lane);
+  copy_out_maps(s_rows, __ballot(active), words, occ + (size_t)blockIdx.x * lanes * words, lane);
   if (rc != 0 && err) atomicOr(err, APG_ERR_MAPGEN);
+}
+
+APG_DEV int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+APG_DEV int wave_inclusive_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// position of the k-th set bit (k < popcount(m)) of m: binary search on popcounts
+APG_DEV int select_bit(uint64_t m, int k) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const int c = __popcll(m & ((1ULL << w) - 1ULL));
+    if (k >= c) {
+      k -= c;
+      m >>= w;
+      pos += w;
+    }
+  }
+  return pos;
 }
 
 // reset of env e (lidar_localization2d.py:293-315 with the _np_random setter :547-557 on reset(seed)):
 // reseed (use_seed) or continue the env's streams, next map index from the DatasetIterator stream,
-// map generation into `own` (rooms: the caller's LDS bitmap; maze: the env's occupancy rows), start
-// cell draw.  Returns the env's new flags.
+// rooms map generation into `own` (the caller's LDS bitmap), start cell draw.  Mazes: k_maze.
+// Returns the env's new flags.
 template <int GEN>
 APG_DEV uint8_t reset_one(const Geo &g, const apg_lidar_state &S, int e, uint8_t f, bool use_seed, uint64_t seed,
-                          uint64_t *own, uint64_t *out_map_idx, uint32_t *err, const BinomTable &bt,
-                          const MazeLds &ml) {
+                          uint64_t *own, uint64_t *out_map_idx, uint32_t *err, const BinomTable &bt) {
+  static_assert(GEN == GEN_NONE || GEN == GEN_ROOMS, "mazes reset in k_maze");
   Pcg64 rng;
   Pcg64 it;
   if (use_seed) {
@@ -208,14 +239,7 @@ APG_DEV uint8_t reset_one(const Geo &g, const apg_lidar_state &S, int e, uint8_t
   if constexpr (GEN != GEN_NONE) {
     midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
     Pcg64 map_rng = seed_pcg64(midx);  // FloorMapDataset*.get_data_point: default_rng(idx)
-    int rc;
-    if constexpr (GEN == GEN_ROOMS)
-      rc = rooms_generate(map_rng, own, g.wpr, g.h, g.max_rooms, g.door_width, bt);
-    else
-    {
-      rc = generate_one<GEN>(g, map_rng, own, S.stack + (size_t)e * g.frames, bt, ml);
-      maze_publish();
-    }
+    int rc = rooms_generate(map_rng, own, g.wpr, g.h, g.max_rooms, g.door_width, bt);
     if (place_start(rng, own, g.h, g.w, g.wpr, px, py) != 0) rc = -6;
     if (rc != 0) atomicOr(err, APG_ERR_MAPGEN);
     *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
@@ -232,19 +256,19 @@ APG_DEV uint8_t reset_one(const Geo &g, const apg_lidar_state &S, int e, uint8_t
   const uint8_t nf = (uint8_t)((f & F_AUTORESET) | F_JUST_RESET | F_FIRST);
   S.flags[e] = nf;
   *reinterpret_cast<Pcg64 *>(&S.rng[e]) = rng;
-  if (out_map_idx) out_map_idx[e] = midx;
+  if (out_map_idx) oat(out_map_idx, g.row, e, 1) = midx;
   return nf;
 }
 
-// reset(seed) of all envs (and, for maps too large for the fused step kernel's LDS, the autoresets):
-// one wave per `lanes` (<= 64) envs.  Map generation is a long serial, divergent chain per env whose
-// speed is set by instruction latency, not by lanes, so the host spreads the envs over as many waves
-// as fit on the chip at once (gen_lanes).  Waves with nothing to reset exit after one flag load.
+// reset(seed) of all envs (static maps and rooms; mazes: k_maze): one wave per `lanes` (<= 64) envs.
+// Map generation is a long serial, divergent chain per env whose speed is set by instruction latency,
+// not by lanes, so the host spreads the envs over as many waves as fit on the chip at once (gen_lanes).
+// Waves with nothing to reset exit after one flag load.
 template <int GEN>
 __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, uint64_t seed, int use_seed,
                                                     int all, uint64_t *out_map_idx, uint32_t *err, BinomTable bt,
                                                     int lanes) {
-  extern __shared__ uint64_t s_rows[];  // rooms: [lanes][h * wpr]; maze: maze_lds_at's layout
+  extern __shared__ uint64_t s_rows[];  // rooms: [lanes][h * wpr]
   const int lane = threadIdx.x;
   const int e = blockIdx.x * lanes + lane;
   const bool mine = lane < lanes && e < g.n;
@@ -253,15 +277,155 @@ __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, ui
   const unsigned long long todo = __ballot(active);
   if (todo == 0ULL) return;
   const size_t words = (size_t)g.h * g.wpr;
-  if (active) {
-    uint64_t *own = GEN == GEN_ROOMS ? s_rows + lane * words : S.occ + (size_t)e * words;
-    reset_one<GEN>(g, S, e, f, use_seed != 0, seed, own, out_map_idx, err, bt, maze_lds_at(s_rows, g.h, lanes, lane));
-  }
+  if (active) reset_one<GEN>(g, S, e, f, use_seed != 0, seed, s_rows + lane * words, out_map_idx, err, bt);
   if constexpr (GEN == GEN_ROOMS) copy_out_maps(s_rows, todo, words, S.occ + (size_t)blockIdx.x * lanes * words, lane);
 }
 
+// Mazes (FloorMapDatasetMaze.get_data_point, floor_map_dataset_maze.py:24-55, see apg_maze.hpp), one lane
+// per maze, `lanes` (<= 64) mazes per one-wave workgroup:
+//   MZ_MAPS   maps of dataset indices idx[0, n) into occ (static map, dataset access);
+//   MZ_RESET  reset_one for mazes: the envs of the workgroup that reset (all, or those with an autoreset
+//             pending), their streams, map index, maze into S.occ, its f32 map obs (bool map / 255,
+//             lidar_localization2d.py:299: the step kernel launched after it is given no map obs), start
+//             cell (place_start), state.
+// After the DFS of its mazes the wave paints each one's occupancy rows from its carve log in LDS, writes
+// them out coalesced (lane = row), counts free cells per row and draws the start cell like place_start.
+enum : int { MZ_MAPS = 0, MZ_RESET = 1 };
+
+template <bool ONEW>
+__global__ __launch_bounds__(64) void k_maze(Geo g, apg_lidar_state S, const uint64_t *idx, int n, uint64_t *occ,
+                                             uint8_t *scratch, int mode, uint64_t seed, int use_seed, int all,
+                                             uint64_t *out_map_idx, float *map_obs, uint32_t *err, int lanes) {
+  extern __shared__ uint64_t s_mz[];  // maze_lane_at's layout, then (after the DFS) the paint bitmap
+  const int lane = threadIdx.x;
+  const int i = blockIdx.x * lanes + lane;
+  const bool mine = lane < lanes && i < n;
+  const MazeGeom m = maze_geom(g.h, g.w);
+  const size_t words = (size_t)g.h * g.wpr;
+  const size_t sb = maze_scratch_bytes(g.h, g.w), lb = maze_log_bytes(g.h, g.w);
+  uint8_t f = 0;
+  bool active = mine;
+  uint64_t midx = 0;
+  if (mode == MZ_RESET) {
+    f = mine ? S.flags[i] : 0;
+    active = mine && (all || (f & F_AUTORESET));
+  } else if (mine) {
+    midx = idx[i];
+  }
+  if (__ballot(active) == 0ULL) return;
+  Pcg64 rng, it, mr;
+  if (active) {
+    if (mode == MZ_RESET) {
+      if (use_seed) {
+        rng = seed_pcg64(seed + (uint64_t)i);
+        it = seed_pcg64(bounded_u64(rng, 0x100000000ULL));  // integers(0, 2**32, endpoint=True)
+      } else {
+        rng = *reinterpret_cast<const Pcg64 *>(&S.rng[i]);
+        it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[i]);
+      }
+      midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
+    }
+    mr = seed_pcg64(midx);  // get_data_point: default_rng(idx)
+  }
+  uint8_t *mine_scr = scratch + (size_t)(active ? i : 0) * sb;
+  const int nlog = maze_dfs<ONEW>(mr, active, m, g.bp, maze_lane_at(s_mz, m, lanes, lane), mine_scr + lb,
+                                  reinterpret_cast<uint32_t *>(mine_scr));
+  __syncthreads();  // the DFS state is dead: the LDS now holds one maze's bitmap at a time
+  uint64_t *bm = s_mz;
+  uint64_t *dst_base = mode == MZ_RESET ? S.occ : occ;
+  int sx = -1, sy = -1;
+  unsigned long long todo = __ballot(active);
+  while (todo) {
+    const int j = __ffsll((long long)todo) - 1;
+    todo &= todo - 1ULL;
+    const int e = blockIdx.x * lanes + j;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous maze's reads of the bitmap are done
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    maze_paint(m, g.wpr, reinterpret_cast<const uint32_t *>(scratch + (size_t)e * sb), __shfl(nlog, j), bm, lane);
+    uint64_t *dst = dst_base + (size_t)e * words;
+    // rows out, lane = row (passes of 64 rows); free cells per row for the start draw
+    int off = 0, nfree = 0;
+    for (int y0 = 0; y0 < g.h; y0 += 64) {
+      const int y = y0 + lane;
+      int fr = 0;
+      if (y < g.h) {
+        int oc = 0;
+        for (int k = 0; k < g.wpr; k++) {
+          const uint64_t v = bm[y * g.wpr + k];
+          dst[y * g.wpr + k] = v;
+          oc += __popcll(v);
+        }
+        fr = g.w - oc;
+      }
+      nfree += wave_sum(fr);
+    }
+    if (mode != MZ_RESET) continue;
+    if (map_obs) {  // the f32 map obs from the bitmap, lane = column (coalesced row stores)
+      float *mo = map_obs + (size_t)e * g.h * g.w;
+      for (int y = 0; y < g.h; y++)
+        for (int x = lane; x < g.w; x += 64)
+          __builtin_nontemporal_store(((bm[y * g.wpr + (x >> 6)] >> (x & 63)) & 1ULL) ? 1.0f / 255.0f : 0.0f,
+                                      mo + (size_t)y * g.w + x);
+    }
+    // place_start (reset :304): the pick-th free cell in row-major order, pick = integers(0, nfree)
+    long long pick = -1;
+    if (lane == j && nfree > 0) pick = (long long)integers(rng, 0, nfree);
+    pick = __shfl(pick, j);
+    int hx = -1, hy = -1;
+    for (int y0 = 0; y0 < g.h; y0 += 64) {
+      const int y = y0 + lane;
+      int fr = 0;
+      if (y < g.h) {
+        int oc = 0;
+        for (int k = 0; k < g.wpr; k++) oc += __popcll(bm[y * g.wpr + k]);
+        fr = g.w - oc;
+      }
+      const int incl = wave_inclusive_scan(fr, lane) + off, excl = incl - fr;
+      if (y < g.h && pick >= excl && pick < incl) {
+        int k2 = (int)(pick - excl);
+        for (int k = 0; k < g.wpr && hx < 0; k++) {
+          const int lo = 64 * k;
+          const uint64_t valid = g.w - lo >= 64 ? ~0ULL : ((1ULL << (g.w - lo)) - 1ULL);
+          const uint64_t fm = ~bm[y * g.wpr + k] & valid;
+          const int c = __popcll(fm);
+          if (k2 < c) hx = lo + select_bit(fm, k2);
+          else k2 -= c;
+        }
+        hy = y;
+      }
+      off = __shfl(incl, 63);
+    }
+    const unsigned long long hit = __ballot(hx >= 0);
+    const int src = hit ? __ffsll((long long)hit) - 1 : 0;
+    const int bx = __shfl(hx, src), by = __shfl(hy, src);
+    if (lane == j && hit) {
+      sx = bx;
+      sy = by;
+    }
+  }
+  if (mode != MZ_RESET || !active) return;
+  float px = 0.5f, py = 0.5f;
+  if (sx < 0) {
+    atomicOr(err, APG_ERR_MAPGEN);
+  } else {
+    px = __fadd_rn((float)sx, 0.5f);
+    py = __fadd_rn((float)sy, 0.5f);
+  }
+  S.pos[2 * i] = px;
+  S.pos[2 * i + 1] = py;
+  S.init_pos[2 * i] = px;
+  S.init_pos[2 * i + 1] = py;
+  S.elapsed[i] = 0;
+  S.flags[i] = (uint8_t)((f & F_AUTORESET) | F_JUST_RESET | F_FIRST);
+  *reinterpret_cast<Pcg64 *>(&S.rng[i]) = rng;
+  *reinterpret_cast<Pcg64 *>(&S.it_rng[i]) = it;
+  S.map_idx[i] = midx;
+  if (out_map_idx) oat(out_map_idx, g.row, i, 1) = midx;
+}
+
 struct StepParams {
-  int n, h, w, wpr, beams, step_limit, is_static, R, wrows, log_stats, sparse;
+  int n, h, w, wpr, beams, step_limit, is_static, R, wrows, log_stats, sparse, row;
   float range, loss_scale, loss_offset;
 };
 
@@ -274,10 +438,16 @@ APG_DEV void log_episode_stats(const StepParams &P, const apg_lidar_outputs &O, 
   for (int m = 0; m < 2; m++) {
     const float *h = hist + (size_t)m * P.step_limit * P.n + e;
     const float avg = f32_div(__fadd_rn(0.0f, pw_sum_ptr(h, len, (size_t)P.n)), (float)len);
-    O.stats[(size_t)m * P.n + e] = avg;
-    O.stats[(size_t)(2 + m) * P.n + e] = h[(size_t)(len - 1) * P.n];
+    const float fin = h[(size_t)(len - 1) * P.n];
+    if (P.row) {
+      oat(O.stats, P.row, e, 4, m) = avg;
+      oat(O.stats, P.row, e, 4, 2 + m) = fin;
+    } else {
+      O.stats[(size_t)m * P.n + e] = avg;
+      O.stats[(size_t)(2 + m) * P.n + e] = fin;
+    }
   }
-  O.stats_len[e] = len;
+  oat(O.stats_len, P.row, e, 1) = len;
 }
 
 // Occupancy window per env, staged in LDS from the PRE-move position p0: the 32 x 32 cells
@@ -318,36 +488,6 @@ struct StepShape {
   static_assert(LPW == 16, "16 envs per wave in the env-major phases");
 };
 constexpr int MAX_MAP_ROWS = 128;
-
-APG_DEV int wave_sum(int v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-
-APG_DEV int wave_inclusive_scan(int v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(v, o);
-    if (lane >= o) v += u;
-  }
-  return v;
-}
-
-// position of the k-th set bit (k < popcount(m)) of m: binary search on popcounts
-APG_DEV int select_bit(uint64_t m, int k) {
-  int pos = 0;
-#pragma unroll
-  for (int w = 32; w >= 1; w >>= 1) {
-    const int c = __popcll(m & ((1ULL << w) - 1ULL));
-    if (k >= c) {
-      k -= c;
-      m >>= w;
-      pos += w;
-    }
-  }
-  return pos;
-}
 
 // Row y of a rooms map painted from its primitives (rooms_paint's result, one row at a time): border
 // | walls & ~doors.  Word k covers columns [64k, 64k + 64); the primitives are pr[i * st].
@@ -486,11 +626,6 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   if constexpr (FUSED) {
     const uint8_t f0 = my_valid ? S.flags[my_e] : 0;
     const bool pend = my_valid && (f0 & F_AUTORESET);
-#ifdef APG_X_NO_SEED  // tuning experiment only: measure the map-index seeding
-#define APG_SEED_FN(x) Pcg64{x, x, x, x | 1, 0, 0}
-#else
-#define APG_SEED_FN(x) seed_pcg64(x)
-#endif
     if (__syncthreads_or(pend)) {
       if constexpr (GEN == GEN_ROOMS) {
         // R1: the env's streams, its next map index and the map's primitives, generated with the
@@ -505,17 +640,12 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           rng = *reinterpret_cast<const Pcg64 *>(&S.rng[my_e]);
           it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[my_e]);
           midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
-          Pcg64 map_rng = APG_SEED_FN(midx);  // FloorMapDatasetRooms.get_data_point: default_rng(idx)
+          Pcg64 map_rng = seed_pcg64(midx);  // FloorMapDatasetRooms.get_data_point: default_rng(idx)
           const RoomsWork wk{reinterpret_cast<uint64_t *>(s_raw + L::stk) + my_el,
                              reinterpret_cast<int16_t *>(s_raw + L::cap) + my_el,
                              reinterpret_cast<int16_t *>(s_raw + L::size) + my_el,
                              reinterpret_cast<int16_t *>(s_raw + L::cut) + my_el, s_prims + my_el, EPB, ROOMS_STACK};
-#ifdef APG_X_NO_R1  // tuning experiment only (wrong results): an empty rooms map
-          wk.P(0) = 0u;
-          const int rc = 0;
-#else
           const int rc = rooms_primitives(map_rng, g.h, g.max_rooms, g.door_width, bt, wk);
-#endif
           if (rc != 0) atomicOr(O.err, APG_ERR_MAPGEN);
         }
         // R2 reads only the primitives its own wave wrote in R1 (wave w owns the envs j * W + w): a wave
@@ -529,12 +659,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         // start cell (place_start: the pick-th free cell in row-major order, drawn by the env's lane)
         uint64_t *mrow = s_mrow + (size_t)wave * MAX_MAP_ROWS * 2;
         const int m = P.h, wpr = P.wpr;
-#ifdef APG_X_NO_R2  // tuning experiment only (wrong results): no painting, start cell 0
-        if (pend) s_start[my_el] = 0;
-        for (int j = 0; j < 0; j++) {
-#else
         for (int j = 0; j < LPW; j++) {
-#endif
           if (!__shfl((int)pend, j)) continue;  // wave-uniform
           const int el = j * W + wave, e = base + el;
           const uint32_t *pr = s_prims + el;
@@ -622,19 +747,11 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           *reinterpret_cast<Pcg64 *>(&S.rng[my_e]) = rng;
           *reinterpret_cast<Pcg64 *>(&S.it_rng[my_e]) = it;
           S.map_idx[my_e] = midx;
-          if (O.map_idx) O.map_idx[my_e] = midx;
+          if (O.map_idx) oat(O.map_idx, P.row, my_e, 1) = midx;
         }
-      } else if constexpr (GEN == GEN_MAZE) {
-        // maze maps: one serial, divergent DFS per env, run lane-dense (env base + tid on the first EPB / 64
-        // waves) rather than env-major: a quarter of the wave instructions, which is what bounds the carving
-        // (reset step of 262 144 127 x 127 mazes: 155 -> 109 ms).  The DFS state lives in the dynamic LDS
-        // (maze_lds_at's layout over the EPB env slots), the map in the env's occupancy rows.
-        if (own && (pf_f & F_AUTORESET))
-          reset_one<GEN>(g, S, oe, pf_f, false, 0, S.occ + (size_t)oe * words, O.map_idx, O.err, bt,
-                         maze_lds_at(s_dyn, P.h, EPB, tid));
       } else {
         // static maps only draw a start cell
-        if (pend) reset_one<GEN>(g, S, my_e, f0, false, 0, nullptr, O.map_idx, O.err, bt, MazeLds{});
+        if (pend) reset_one<GEN>(g, S, my_e, f0, false, 0, nullptr, O.map_idx, O.err, bt);
       }
       __syncthreads();
       if (own && (pf_f & F_AUTORESET)) {  // this env was reset above
@@ -742,19 +859,11 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         if (total > 0.0f) {
           dirx = f32_div(dirx, total);
           diry = f32_div(diry, total);
-#ifdef APG_X_NO_MOVE_SCAN  // tuning experiment only (wrong results)
-          const float d = total;
-#else
           const float d = lidar_scan(rw, pos0, pos1, tx, ty).dist;
-#endif
           pos0 = __fadd_rn(pos0, __fmul_rn(dirx, d));
           pos1 = __fadd_rn(pos1, __fmul_rn(diry, d));
           const float rem = __fsub_rn(total, d);
-#ifdef APG_X_NO_SLIDE  // tuning experiment only (wrong results)
-          if (false) {
-#else
           if (rem > 1e-5f) {  // slide along the wall (:345-364)
-#endif
             const float rvx = __fmul_rn(dirx, rem), rvy = __fmul_rn(diry, rem);
             const bool kx = rvx > 1e-5f, ky = rvy > 1e-5f;
             if (kx || ky) {
@@ -801,16 +910,16 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
     if (own) {
       const float mapw = (float)P.w, maph = (float)P.h;
       if (was_reset || errbits) {  // NEXT_STEP autoreset (this env returned reset obs, reward 0) or NaN inputs
-        O.reward[e] = 0.0;
-        O.terminated[e] = 0;
-        O.truncated[e] = 0;
-        O.base_reward[e] = 0.0f;
-        O.target[2 * e] = 0.0f;
-        O.target[2 * e + 1] = 0.0f;
-        O.loss[e] = 0.0f;
-        O.info_mask[e] = 0;
-        if (P.log_stats) O.stats_len[e] = 0;
-        if (P.sparse) O.weight[e] = 0.0;
+        oat(O.reward, P.row, e, 1) = 0.0;
+        oat(O.terminated, P.row, e, 1) = 0;
+        oat(O.truncated, P.row, e, 1) = 0;
+        oat(O.base_reward, P.row, e, 1) = 0.0f;
+        oat(O.target, P.row, e, 2, 0) = 0.0f;
+        oat(O.target, P.row, e, 2, 1) = 0.0f;
+        oat(O.loss, P.row, e, 1) = 0.0f;
+        oat(O.info_mask, P.row, e, 1) = 0;
+        if (P.log_stats) oat(O.stats_len, P.row, e, 1) = 0;
+        if (P.sparse) oat(O.weight, P.row, e, 1) = 0.0;
         if (was_reset) f &= (uint8_t)~(F_JUST_RESET | F_AUTORESET);
       }
       if (moved) {
@@ -848,43 +957,39 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         const float ex = __fsub_rn(prx, tgx), ey = __fsub_rn(pry, tgy);
         const float mse = __fmul_rn(__fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey)), 0.5f);  // exact / 2
         const float loss = __fadd_rn(__fmul_rn(mse, P.loss_scale), P.loss_offset);
-#ifdef APG_X_NO_STATS  // tuning experiment only (wrong results)
-        if (false) {
-#else
         if (P.log_stats) {
-#endif
           float *hist = S.stats_hist;
           hist[(size_t)(el2 - 1) * P.n + e] = norm_f32(ex, ey);  // |target - prediction|: the signs do not matter
           hist[(size_t)(P.step_limit + el2 - 1) * P.n + e] = mse;
           if (term) log_episode_stats(P, O, e, hist, el2);
-          else O.stats_len[e] = 0;
+          else oat(O.stats_len, P.row, e, 1) = 0;
         }
-        O.base_reward[e] = br;
-        O.target[2 * e] = tgx;
-        O.target[2 * e + 1] = tgy;
-        O.loss[e] = loss;
+        oat(O.base_reward, P.row, e, 1) = br;
+        oat(O.target, P.row, e, 2, 0) = tgx;
+        oat(O.target, P.row, e, 2, 1) = tgy;
+        oat(O.loss, P.row, e, 1) = loss;
         if (P.sparse) {  // SparsifyWrapper: base_reward - loss * (1.0 if terminated else 0.0), in f32
-          O.weight[e] = term ? 1.0 : 0.0;
-          O.reward[e] = (double)__fsub_rn(br, __fmul_rn(loss, term ? 1.0f : 0.0f));
+          oat(O.weight, P.row, e, 1) = term ? 1.0 : 0.0;
+          oat(O.reward, P.row, e, 1) = (double)__fsub_rn(br, __fmul_rn(loss, term ? 1.0f : 0.0f));
         } else {
-          O.reward[e] = (double)__fsub_rn(br, loss);
+          oat(O.reward, P.row, e, 1) = (double)__fsub_rn(br, loss);
         }
-        O.terminated[e] = term;
-        O.truncated[e] = 0;
-        O.info_mask[e] = 1;
+        oat(O.terminated, P.row, e, 1) = term;
+        oat(O.truncated, P.row, e, 1) = 0;
+        oat(O.info_mask, P.row, e, 1) = 1;
         if (term) f |= F_AUTORESET;
         S.pos[2 * e] = pos0;
         S.pos[2 * e + 1] = pos1;
       }
       S.flags[e] = f;
-      if (O.reset_mask) O.reset_mask[e] = was_reset;
+      if (O.reset_mask) oat(O.reset_mask, P.row, e, 1) = was_reset;
       // odometry (:263-270) and TimeLimit time_step (time_limit.py:113-116)
       const float ox = __fsub_rn(pos0, ipx), oy = __fsub_rn(pos1, ipy);
-      O.odometry[2 * e] =
+      oat(O.odometry, P.row, e, 2, 0) =
           __fsub_rn(__fmul_rn(f32_div_inv(__fadd_rn(ox, mapw), 1.0 / (double)__fadd_rn(mapw, mapw)), 2.0f), 1.0f);
-      O.odometry[2 * e + 1] =
+      oat(O.odometry, P.row, e, 2, 1) =
           __fsub_rn(__fmul_rn(f32_div_inv(__fadd_rn(oy, maph), 1.0 / (double)__fadd_rn(maph, maph)), 2.0f), 1.0f);
-      O.time_step[e] = (float)(2.0 * (double)pf_el / (double)P.step_limit - 1.0);
+      oat(O.time_step, P.row, e, 1) = (float)(2.0 * (double)pf_el / (double)P.step_limit - 1.0);
       s_pos[el][0] = pos0;
       s_pos[el][1] = pos1;
     }
@@ -909,7 +1014,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
     for (int beam = tid / EPB; beam < P.beams; beam += T / EPB) {
       if (e < P.n) {
         const float qx = __fadd_rn(px, S.beam_dirs[2 * beam]), qy = __fadd_rn(py, S.beam_dirs[2 * beam + 1]);
-        O.lidar[(size_t)e * P.beams + beam] = beam_value(lidar_scan(rw, px, py, qx, qy).dist);
+        oat(O.lidar, P.row, e, P.beams, beam) = beam_value(lidar_scan(rw, px, py, qx, qy).dist);
       }
     }
     return;
@@ -963,7 +1068,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   const int B = P.beams, dl = T / B, db = T - dl * B;  // (env, beam) of element i advanced without divisions
   int l = tid / B, beam = tid - l * B;
   for (int i = tid; i < nenv * B; i += T) {
-    O.lidar[(size_t)base * B + i] = s_lid[l * LS + beam];
+    oat(O.lidar, P.row, base + l, B, beam) = s_lid[l * LS + beam];
     l += dl;
     beam += db;
     if (beam >= B) {
@@ -1008,7 +1113,7 @@ __global__ __launch_bounds__(RT_THREADS) void k_lidar_render_track(StepParams P,
   const int wpr32 = (P.w + 31) / 32;
   uint32_t *om = R.obs_map + (size_t)t * P.h * wpr32;
   float *pose = R.pose + 6 * (size_t)t;
-  const bool was_reset = O.reset_mask[e] != 0;
+  const bool was_reset = oat(O.reset_mask, P.row, e, 1) != 0;
   const float px = S.pos[2 * e], py = S.pos[2 * e + 1];
   if (was_reset)
     for (int k = threadIdx.x; k < P.h * wpr32; k += RT_THREADS) om[k] = 0u;  // np.zeros_like(map) (:301)
@@ -1026,7 +1131,7 @@ __global__ __launch_bounds__(RT_THREADS) void k_lidar_render_track(StepParams P,
       pose[3] = __fmul_rn(__fmul_rn(__fadd_rn(ay, 1.0f), 0.5f), (float)P.h);
       // prediction_quality = 1 - |prediction - normalized_last_pos| / 0.25 (:377-380); the step's target is
       // normalized_last_pos, and / 0.25 == * 4 exactly
-      const float d = norm_f32(__fsub_rn(ax, O.target[2 * e]), __fsub_rn(ay, O.target[2 * e + 1]));
+      const float d = norm_f32(__fsub_rn(ax, oat(O.target, P.row, e, 2, 0)), __fsub_rn(ay, oat(O.target, P.row, e, 2, 1)));
       const float q = __fsub_rn(1.0f, __fmul_rn(d, 4.0f));
       const int k = R.traj_len[t];
       if (k < P.step_limit) {
@@ -1125,16 +1230,29 @@ int gen_lanes(int n) {
   return lanes;
 }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) is per device: the bytes opted in are remembered per
+// (kernel, device), so an env on a second GPU of the process opts its kernels in too (the call costs host
+// time, so it is not repeated on every launch).
+int opt_in_lds(const void *kern, size_t bytes) {
+  if (bytes <= 64 * 1024) return APG_OK;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(APG_E_LAUNCH, "hipGetDevice failed");
+  static std::mutex mu;
+  static std::map<std::pair<const void *, int>, size_t> opted;
+  std::lock_guard<std::mutex> lock(mu);
+  size_t &have = opted[std::make_pair(kern, dev)];
+  if (have >= bytes) return APG_OK;
+  if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
+    return fail(APG_E_LAUNCH, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+  have = bytes;
+  return APG_OK;
+}
+
 // Dynamic LDS of a map-generation launch: rooms bitmaps [lanes][h * wpr] (opted in above 64 KiB).
 template <class K>
 int gen_lds(K kernel, int gen, const Geo &g, int lanes, size_t &dyn) {
-  dyn = gen == GEN_ROOMS  ? (size_t)lanes * g.h * g.wpr * sizeof(uint64_t)
-        : gen == GEN_MAZE ? maze_lds_bytes(g.h, lanes)
-                          : 0;
-  if (dyn > 64 * 1024 &&
-      hipFuncSetAttribute((const void *)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn) != hipSuccess)
-    return fail(APG_E_LAUNCH, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-  return APG_OK;
+  dyn = gen == GEN_ROOMS ? (size_t)lanes * g.h * g.wpr * sizeof(uint64_t) : 0;
+  return opt_in_lds((const void *)kernel, dyn);
 }
 
 template <int GEN>
@@ -1148,28 +1266,53 @@ int launch_reset_gen(const Geo &g, const apg_lidar_state *st, uint64_t seed, int
   return check_launch("k_lidar_reset");
 }
 
+// k_maze over n mazes (MZ_MAPS: occ / idx; MZ_RESET: the state's envs, all or the pending autoresets).
+// Dynamic LDS: the lanes' DFS state, at least one paint bitmap.
+int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, int n, uint64_t *occ, uint8_t *scratch,
+                int mode, uint64_t seed, int use_seed, int all, uint64_t *out_map_idx, float *map_obs, uint32_t *err,
+                hipStream_t s) {
+  if (!scratch) return fail(APG_E_INVALID, "maze maps need the maze scratch buffer (stack)");
+  const MazeGeom m = maze_geom(g.h, g.w);
+  if (m.ncx > 127 || m.ncy > 127) return fail(APG_E_INVALID, "maze maps must be at most 255 x 255");
+  const int lanes = gen_lanes(n);
+  size_t dyn = (size_t)lanes * maze_lane_lds_bytes(g.h, g.w);
+  const size_t bitmap = (size_t)g.h * g.wpr * sizeof(uint64_t);
+  if (dyn < bitmap) dyn = bitmap;
+  const bool onew = m.cw == 1;
+  const void *kern = onew ? (const void *)k_maze<true> : (const void *)k_maze<false>;
+  if (int rc = opt_in_lds(kern, dyn)) return rc;
+  if (onew)
+    hipLaunchKernelGGL(k_maze<true>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, st, idx, n, occ, scratch, mode, seed,
+                       use_seed, all, out_map_idx, map_obs, err, lanes);
+  else
+    hipLaunchKernelGGL(k_maze<false>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, st, idx, n, occ, scratch, mode,
+                       seed, use_seed, all, out_map_idx, map_obs, err, lanes);
+  return check_launch("k_maze");
+}
+
 int launch_reset(const Geo &g, const apg_lidar_state *st, uint64_t seed, int use_seed, int all,
                  const apg_lidar_outputs *out, hipStream_t s) {
   if (g.is_static) return launch_reset_gen<GEN_NONE>(g, st, seed, use_seed, all, out, s);
-  if (g.kind == APG_MAP_MAZE) return launch_reset_gen<GEN_MAZE>(g, st, seed, use_seed, all, out, s);
+  if (g.kind == APG_MAP_MAZE)
+    return launch_maze(g, *st, nullptr, g.n, nullptr, reinterpret_cast<uint8_t *>(st->stack), MZ_RESET, seed, use_seed,
+                       all, out->map_idx, out->map_obs, out->err, s);
   return launch_reset_gen<GEN_ROOMS>(g, st, seed, use_seed, all, out, s);
-}
-
-template <int GEN>
-int launch_map_generate(const Geo &g, const uint64_t *idx, int n, uint64_t *occ, uint16_t *stack, uint32_t *err,
-                        hipStream_t s) {
-  const int lanes = gen_lanes(n);
-  size_t dyn;
-  if (int rc = gen_lds(k_map_generate<GEN>, GEN, g, lanes, dyn)) return rc;
-  hipLaunchKernelGGL(k_map_generate<GEN>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, idx, n, occ, stack, err,
-                     make_binom_table(), lanes);
-  return check_launch("k_map_generate");
 }
 
 int launch_map_generate_any(const Geo &g, const uint64_t *idx, int n, uint64_t *occ, uint16_t *stack,
                             uint32_t *err, hipStream_t s) {
-  if (g.kind == APG_MAP_MAZE) return launch_map_generate<GEN_MAZE>(g, idx, n, occ, stack, err, s);
-  return launch_map_generate<GEN_ROOMS>(g, idx, n, occ, stack, err, s);
+  if (g.kind == APG_MAP_MAZE) {
+    apg_lidar_state none;
+    memset(&none, 0, sizeof(none));
+    return launch_maze(g, none, idx, n, occ, reinterpret_cast<uint8_t *>(stack), MZ_MAPS, 0, 0, 1, nullptr, nullptr, err,
+                       s);
+  }
+  const int lanes = gen_lanes(n);
+  size_t dyn;
+  if (int rc = gen_lds(k_map_generate_rooms, GEN_ROOMS, g, lanes, dyn)) return rc;
+  hipLaunchKernelGGL(k_map_generate_rooms, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, idx, n, occ, err,
+                     make_binom_table(), lanes);
+  return check_launch("k_map_generate");
 }
 
 // Dynamic LDS of a k_lidar_step instance: windows + staged lidar rows + walk queue; fused rooms resets
@@ -1183,7 +1326,7 @@ size_t step_lds_bytes(int epb, int beams) {
 
 int step_gen(const Geo &g) {
   if (g.is_static) return GEN_NONE;
-  return g.kind == APG_MAP_MAZE ? GEN_MAZE : GEN_ROOMS;
+  return GEN_ROOMS;  // mazes: k_maze (autoresets) + the unfused step kernel
 }
 
 int cu_count() {
@@ -1215,14 +1358,8 @@ int launch_step_t(const StepParams &P, const Geo &g, const apg_lidar_state *st, 
                   const apg_lidar_outputs *out, hipStream_t s, const BinomTable &bt) {
   size_t lds = step_lds_bytes(EPB, P.beams);
   if (FUSED && GEN == GEN_ROOMS && RoomsLds<EPB>::bytes > lds) lds = RoomsLds<EPB>::bytes;
-  if (FUSED && GEN == GEN_MAZE && maze_lds_bytes(P.h, EPB) > lds) lds = maze_lds_bytes(P.h, EPB);
   auto kern = k_lidar_step<GEN, FUSED, EPB>;
-  static size_t lds_opted_in = 64 * 1024;  // per instance: the attribute call costs host time on every step
-  if (lds > lds_opted_in) {
-    if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-      return fail(APG_E_LAUNCH, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-    lds_opted_in = lds;
-  }
+  if (int rc = opt_in_lds((const void *)kern, lds)) return rc;
   hipLaunchKernelGGL(kern, dim3(grid_for(P.n, EPB)), dim3(4 * EPB), lds, s, P, g, *st, act, pred, *out, bt);
   return check_launch("k_lidar_step");
 }
@@ -1234,7 +1371,6 @@ int launch_step_epb(const StepParams &P, const Geo &g, const apg_lidar_state *st
   if (!fused) return launch_step_t<GEN_NONE, false, EPB>(P, g, st, act, pred, out, s, bt);
   switch (step_gen(g)) {
     case GEN_ROOMS: return launch_step_t<GEN_ROOMS, true, EPB>(P, g, st, act, pred, out, s, bt);
-    case GEN_MAZE: return launch_step_t<GEN_MAZE, true, EPB>(P, g, st, act, pred, out, s, bt);
     default: return launch_step_t<GEN_NONE, true, EPB>(P, g, st, act, pred, out, s, bt);
   }
 }
@@ -1250,6 +1386,7 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   P.step_limit = cfg->step_limit;
   P.log_stats = cfg->log_stats ? 1 : 0;
   P.sparse = cfg->sparse ? 1 : 0;
+  P.row = cfg->out_row_bytes;
   P.is_static = cfg->is_static;
   P.R = (int)ceilf(cfg->lidar_range);
   P.wrows = MAX_WIN_ROWS;
@@ -1282,6 +1419,7 @@ int apg_lidar_query_sizes(const apg_lidar_config *cfg, apg_lidar_state_sizes *o)
   o->occ_bytes = (g.is_static ? 1 : (size_t)g.n) * words * sizeof(uint64_t);
   o->scratch_bytes = 0;  // reserved (rooms maps are painted from primitives, no scratch plane)
   o->stack_bytes = g.kind == APG_MAP_MAZE ? (size_t)g.frames * (g.is_static ? 1 : (size_t)g.n) * sizeof(uint16_t) : 0;
+  // (maze scratch: apg_maze.hpp's carve log + spilled DFS frames, maze_frames u16 per map)
   return APG_OK;
 }
 
@@ -1303,7 +1441,9 @@ int apg_lidar_reset(const apg_lidar_config *cfg, const apg_lidar_state *st, uint
   hipStream_t s = (hipStream_t)stream;
   Geo g = make_geo(cfg);
   if ((rc = launch_reset(g, st, seed, use_seed, 1, out, s))) return rc;
-  return launch_step_kernel(cfg, st, nullptr, nullptr, out, s, false);
+  apg_lidar_outputs o2 = *out;
+  if (g.kind == APG_MAP_MAZE && !g.is_static) o2.map_obs = nullptr;  // written by k_maze
+  return launch_step_kernel(cfg, st, nullptr, nullptr, &o2, s, false);
 }
 
 int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
@@ -1316,9 +1456,20 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
     return fail(APG_E_INVALID, "log_stats needs stats_hist, stats and stats_len buffers");
   if (cfg->sparse && !out->weight) return fail(APG_E_INVALID, "sparse needs the weight buffer");
   hipStream_t s = (hipStream_t)stream;
-  // one launch per step: the fused step kernel performs the NEXT_STEP autoresets itself
+  // rooms / static maps: one launch per step, the fused step kernel performs the NEXT_STEP autoresets itself;
+  // mazes: k_maze resets the envs with an autoreset pending (its waves exit at once when there are none),
+  // then the unfused step kernel
   if (ev_begin && hipEventRecord((hipEvent_t)ev_begin, s) != hipSuccess) return fail(APG_E_LAUNCH, "hipEventRecord");
-  rc = launch_step_kernel(cfg, st, action, prediction, out, s, true);
+  if (cfg->map_kind == APG_MAP_MAZE && !cfg->is_static) {
+    const Geo g = make_geo(cfg);
+    rc = launch_maze(g, *st, nullptr, g.n, nullptr, reinterpret_cast<uint8_t *>(st->stack), MZ_RESET, 0, 0, 0,
+                     out->map_idx, out->map_obs, out->err, s);
+    apg_lidar_outputs o2 = *out;
+    o2.map_obs = nullptr;  // written by k_maze
+    if (rc == APG_OK) rc = launch_step_kernel(cfg, st, action, prediction, &o2, s, false);
+  } else {
+    rc = launch_step_kernel(cfg, st, action, prediction, out, s, true);
+  }
   if (rc == APG_OK && ev_end && hipEventRecord((hipEvent_t)ev_end, s) != hipSuccess)
     return fail(APG_E_LAUNCH, "hipEventRecord");
   return rc;
@@ -1328,6 +1479,8 @@ int apg_lidar_step(const apg_lidar_config *cfg, const apg_lidar_state *st, const
                    const float *prediction, const apg_lidar_outputs *out, apg_stream_t stream) {
   return apg_lidar_step_profiled(cfg, st, action, prediction, out, stream, nullptr, nullptr);
 }
+
+int apg_maze_frames(int h, int w) { return (int)(maze_scratch_bytes(h, w) / 2); }
 
 int apg_map_generate(int map_kind, const uint64_t *idx, int n, int h, int w, int max_rooms, int door_width,
                      double branching_prob, uint64_t *occ, uint64_t *scratch, uint16_t *stack, uint32_t *err,
@@ -1381,6 +1534,7 @@ int apg_lidar_render_track(const apg_lidar_config *cfg, const apg_lidar_state *s
   P.beams = cfg->beams;
   P.step_limit = cfg->step_limit;
   P.is_static = cfg->is_static;
+  P.row = cfg->out_row_bytes;
   hipLaunchKernelGGL(k_lidar_render_track, dim3(rs->num_tracked), dim3(RT_THREADS), 0, (hipStream_t)stream, P, *st,
                      prediction, *out, *rs);
   return check_launch("k_lidar_render_track");

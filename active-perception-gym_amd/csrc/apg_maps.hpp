@@ -1,6 +1,6 @@
-// apg_maps.hpp — procedural floor maps on device, one GPU thread per map, bit-exact with
+// apg_maps.hpp — rooms floor maps on device, one GPU thread per map, bit-exact with
 //   FloorMapDatasetRooms.get_data_point  ap_gym/envs/floor_map/floor_map_dataset_rooms.py:25-89
-//   FloorMapDatasetMaze.get_data_point   ap_gym/envs/floor_map/floor_map_dataset_maze.py:24-55
+// (mazes: apg_maze.hpp)
 // Occupancy is bit-packed: row y of a map is `wpr` uint64 words, bit x%64 of word x/64 set = wall.
 // Bits at x >= width are always zero.
 #pragma once
@@ -229,126 +229,6 @@ APG_DEV int rooms_generate(Pcg64 &r, uint64_t *occ, int wpr, int m, int max_room
   const int rc = rooms_primitives(r, m, max_rooms, door_width, bt, W);
   rooms_paint(W, m, wpr, occ);
   return rc;
-}
-
-// Maze: recursive carve() as an explicit DFS. Frame (u16): perm 4x2 bits | k << 8 | first << 11 |
-// from << 12; frame f of this map lives at stack[f].
-// The DFS's dependent state lives in LDS, so the serial chain never waits on HBM:
-//  * vis: visited bits of the odd cells, row cy at vis[cy * st], bit cx = cell (2cx + 1, 2cy + 1).  An
-//    odd cell is cleared only when it is carved into, so `maze[next_pos] == 1` (maze.py:38) is exactly
-//    "not visited" (maps up to 127 x 127: at most 63 cells per row);
-//  * ring: the MAZE_RING most recently saved frames, frame p at ring[(p % MAZE_RING) * st]; a pop
-//    reads the HBM stack (written through at every push) only past them.
-// The occupancy rows are written once (all walls but (1, 1)) and then cleared with non-returning
-// atomics, which nothing in the loop waits on: call maze_publish() before reading them back.
-constexpr int MAZE_RING = 16;
-struct MazeLds {
-  uint64_t *vis;   // this lane's row 0
-  uint16_t *ring;  // this lane's slot 0
-  int st;          // element stride of both (lanes interleaved)
-};
-
-__host__ __device__ inline size_t maze_lds_bytes(int h, int lanes) {
-  return (size_t)lanes * (((size_t)(h - 1) / 2) * sizeof(uint64_t) + MAZE_RING * sizeof(uint16_t));
-}
-
-// Lane j's view of [rows][lanes] visited bits followed by [MAZE_RING][lanes] frames.
-APG_DEV MazeLds maze_lds_at(void *base, int h, int lanes, int j) {
-  uint64_t *vis = reinterpret_cast<uint64_t *>(base);
-  uint16_t *ring = reinterpret_cast<uint16_t *>(vis + (size_t)((h - 1) / 2) * lanes);
-  return MazeLds{vis + j, ring + j, lanes};
-}
-
-APG_DEV void maze_clear_bit(uint64_t *word, uint64_t mask) {
-  __hip_atomic_fetch_and(word, ~mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Wait for this lane's atomic clears and drop the CU's stale L1 lines of the map (the step kernel read
-// the previous map's rows through L1 before carving).
-APG_DEV void maze_publish() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-
-// rng.permutation of the 4 directions (maze.py:33): numpy's shuffle, j = random_interval(i), i = 3, 2, 1
-APG_DEV uint32_t draw_perm4(Pcg64 &r) {
-  uint32_t p = 0 | (1u << 2) | (2u << 4) | (3u << 6);
-#pragma unroll
-  for (int i = 3; i >= 1; i--) {
-    uint32_t j = random_interval_small(r, (uint32_t)i);
-    uint32_t vi = (p >> (2 * i)) & 3u, vj = (p >> (2 * j)) & 3u;
-    p &= ~((3u << (2 * i)) | (3u << (2 * j)));
-    p |= (vj << (2 * i)) | (vi << (2 * j));
-  }
-  return p;
-}
-
-APG_DEV int maze_generate(Pcg64 &r, Bits occ, int h, int w, double branching_prob, uint16_t *stack, int cap,
-                          const MazeLds &L) {
-  for (int y = 0; y < h; y++)
-    for (int k = 0; k < occ.wpr; k++) {
-      const int lo = k * 64;
-      uint64_t v = 0;
-      if (w > lo) v = (w - lo >= 64) ? ~0ULL : ((1ULL << (w - lo)) - 1ULL);
-      if (y == 1 && k == 0) v &= ~2ULL;  // maze[1, 1] = 0 (maze.py:51)
-      occ.w[y * occ.wpr + k] = v;
-    }
-  const int ch = (h - 1) / 2;
-  for (int cy = 0; cy < ch; cy++) L.vis[(size_t)cy * L.st] = cy == 0 ? 1ULL : 0ULL;
-  // directions [[2, 0], [-2, 0], [0, 2], [0, -2]] (maze.py:76) computed, not indexed: a runtime-indexed
-  // local array would live in scratch memory
-  auto dxs = [](uint32_t d) { return d == 0u ? 2 : (d == 1u ? -2 : 0); };
-  auto dys = [](uint32_t d) { return d == 2u ? 2 : (d == 3u ? -2 : 0); };
-  int x = 1, y = 1, sp = 1, cached = 0;
-  uint32_t top = draw_perm4(r) | (1u << 11);  // k = 0, first = 1
-  while (true) {
-    const uint32_t k = (top >> 8) & 7u;
-    if (k >= 4) {  // pop
-      if (--sp == 0) break;
-      const uint32_t from = (top >> 12) & 3u;
-      x -= dxs(from);
-      y -= dys(from);
-      if (cached > 0) {
-        cached--;
-        top = L.ring[(size_t)((sp - 1) & (MAZE_RING - 1)) * L.st];
-      } else {
-        top = stack[sp - 1];
-      }
-      continue;
-    }
-    const uint32_t d = (top >> (2 * k)) & 3u;
-    top = (top & ~(7u << 8)) | ((k + 1) << 8);
-    const int nx = x + dxs(d), ny = y + dys(d);
-    if (0 < nx && 0 < ny && nx < w - 1 && ny < h - 1) {
-      uint64_t *vr = L.vis + (size_t)(ny >> 1) * L.st;
-      const uint64_t vrow = *vr, vbit = 1ULL << (nx >> 1);
-      if ((vrow & vbit) == 0ULL) {
-        const bool first = (top >> 11) & 1u;
-        if (first || next_double(r) < branching_prob) {
-          *vr = vrow | vbit;
-          const int my = y + dys(d) / 2, mx = x + dxs(d) / 2;  // passage cell
-          uint64_t *wa = occ.w + my * occ.wpr + (mx >> 6), *wb = occ.w + ny * occ.wpr + (nx >> 6);
-          const uint64_t ma = 1ULL << (mx & 63), mb = 1ULL << (nx & 63);
-          if (wa == wb) {
-            maze_clear_bit(wa, ma | mb);
-          } else {
-            maze_clear_bit(wa, ma);
-            maze_clear_bit(wb, mb);
-          }
-          top &= ~(1u << 11);
-          if (sp >= cap) return -5;
-          stack[sp - 1] = (uint16_t)top;
-          L.ring[(size_t)((sp - 1) & (MAZE_RING - 1)) * L.st] = (uint16_t)top;
-          cached = cached < MAZE_RING ? cached + 1 : MAZE_RING;
-          sp++;
-          x = nx;
-          y = ny;
-          top = draw_perm4(r) | (1u << 11) | (d << 12);
-        }
-      }
-    }
-  }
-  return 0;
 }
 
 }  // namespace apg

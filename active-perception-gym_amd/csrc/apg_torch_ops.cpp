@@ -65,10 +65,10 @@ struct LidarEnv : torch::CustomClassHolder {
   at::Device dev = at::Device(at::kCUDA, 0);
 
   // ints: num_envs, height, width, map_kind, is_static, static_map_index, beams, step_limit, max_rooms,
-  // door_width, log_stats, sparse; reals: lidar_range, loss_scale, loss_offset, branching_prob
+  // door_width, log_stats, sparse, out_row_bytes; reals: lidar_range, loss_scale, loss_offset, branching_prob
   LidarEnv(std::vector<int64_t> ints, std::vector<double> reals, std::vector<at::Tensor> state,
            std::vector<at::Tensor> outputs) {
-    TORCH_CHECK(ints.size() == 12 && reals.size() == 4, "LidarEnv: 12 ints and 4 reals expected");
+    TORCH_CHECK(ints.size() == 13 && reals.size() == 4, "LidarEnv: 13 ints and 4 reals expected");
     cfg.num_envs = (int32_t)ints[0];
     cfg.height = (int32_t)ints[1];
     cfg.width = (int32_t)ints[2];
@@ -81,6 +81,7 @@ struct LidarEnv : torch::CustomClassHolder {
     cfg.door_width = (int32_t)ints[9];
     cfg.log_stats = (int32_t)ints[10];
     cfg.sparse = (int32_t)ints[11];
+    cfg.out_row_bytes = (int32_t)ints[12];
     cfg.lidar_range = (float)reals[0];
     cfg.loss_scale = (float)reals[1];
     cfg.loss_offset = (float)reals[2];

@@ -1,8 +1,9 @@
 """Throughput benchmark of the north-star hot path: LIDARLocRooms-v0 vectorized step on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]              # 1 GPU
+    python bench.py --gpus N [--steps K] [--warmup W]          # N GPUs: bench.py starts the N ranks itself
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
-        --master-port P bench.py --gpus N --steps K --warmup W        # N GPUs, one rank per GPU
+        --master-port P bench.py --gpus N --steps K --warmup W        # the same under torchrun
 
 Workload (BASELINE.json configs[1]): LIDARLocRooms-v0, num_envs = 65536 per GPU, 32 beams,
 64x64 procedurally generated rooms maps, TimeLimit(100) with NEXT_STEP autoreset (so the timed
@@ -204,19 +205,30 @@ def run_image(args, world, rank, dev):
     gather_ms = senv.gather_ms() or 0.0
     ev.close()
     if world > 1:
-        tt = torch.tensor([elapsed, step_ms, reset_ms, gather_ms], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed, step_ms, reset_ms, gather_ms], dtype=torch.float64,
+                          device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, step_ms, reset_ms, gather_ms = (float(x) for x in tt)
     if rank == 0:
         bpe = image_bytes_per_env_step(w["kind"], w["classes"], w["sensor"], c)
+        shape = {"num_envs": n_local, "sensor": list(w["sensor"]), "classes": w["classes"]}
+        # the step kernel's time: the rocprof duration table of these sources at this shape when there is one
+        # (the events around a launch the GPU is not backed up behind include the host's launch latency, and
+        # then exceed the wall time per step), else the events
+        dj, dpath = newest_table("durations", args.workload, "image", shape, lambda t: "step" in t.get("per_class", {}))
+        events_ms = step_ms
+        if dj is not None:
+            step_ms = dj["per_class"]["step"]["median_us"] / 1e3
         achieved = bpe * n_local / (step_ms * 1e-3) / 1e9
-        tj, tpath = pmc_table(args.workload, "image",
-                              {"num_envs": n_local, "sensor": list(w["sensor"]), "classes": w["classes"]})
-        traffic = issue = None
+        tj, tpath = pmc_table(args.workload, "image", shape)
+        traffic = issue = traffic_cal = None
         if tj is not None:
             traffic = tj["hbm_bytes_per_launch"]["step"]
             issue = issue_fractions(tj["per_launch"]["step"], step_ms)
             issue["source"] = tpath
+            # u8 tap rows: dword gathers in 64-B runs; f32 glimpse / output stores
+            traffic_cal = calibrated_traffic(tj["per_launch"]["step"], "k_seg64_4", "k_store4")
+        bound, basis = derive_bound(achieved / HBM_PEAK_GBS, issue)
         out = {
             "metric": "env-steps/sec (vectorized step) at 1/2/4/8 MI355X + achieved HBM GB/s",
             "value": n_total * args.steps / elapsed, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
@@ -229,9 +241,13 @@ def run_image(args, world, rank, dev):
                        "reset_ms": reset_ms, "parallelism": f"env-shard x{world}" + (" + all-gather" if senv.gather
                                                                                         else ""),
                        "gather_ms": gather_ms if senv.gather else None},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tpath,
-                         "kernel": "image step (all kernels, HIP events around the step's launches)", "kernel_ms": step_ms,
+            "roofline": {"bound": bound, "bound_basis": basis, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_calibrated": traffic_cal, "traffic_source": tpath,
+                         "kernel": "k_image_step_fused" if dj else "image step (all kernels, HIP events around the "
+                                                                   "step's launches)",
+                         "kernel_ms": step_ms, "kernel_ms_source": dpath or "hip events",
+                         "kernel_ms_events": events_ms,
                          "launches_timed": len(timed), "event_every": args.event_every,
                          "bytes_per_launch": bpe * n_local, "issue": issue},
         }
@@ -254,7 +270,8 @@ LIDAR_WORKLOADS = {
                          "maze needs odd sizes, SURVEY §0.6)"),
 }
 KERNEL_SOURCES = {
-    "lidar": ["apg_lidar.hip", "apg_scan.hpp", "apg_device.hpp", "apg_maps.hpp", "apg_rng.hpp", "apg_pairwise.hpp"],
+    "lidar": ["apg_lidar.hip", "apg_scan.hpp", "apg_device.hpp", "apg_maps.hpp", "apg_maze.hpp", "apg_rng.hpp",
+              "apg_pairwise.hpp"],
     "image": ["apg_image.hip", "apg_device.hpp", "apg_rng.hpp", "apg_pairwise.hpp"],
 }
 HIP_CLOCK_HZ = 2.4e9  # MI355X max engine clock (MI355X_MICROARCH.md); capacity of the issue fractions
@@ -285,6 +302,60 @@ def pmc_table(workload: str, family: str, shape: dict):
                 and tj.get("hbm_bytes_per_launch", {}).get("step") is not None):
             return tj, os.path.relpath(path, ROOT)
     return None, None
+
+
+def newest_table(kind: str, workload: str, family: str, shape: dict, need=lambda tj: True):
+    """The newest profiles/r*/<kind>_<workload>.json collected from these kernel sources at this run shape,
+    or (None, None)."""
+    import glob
+
+    sha = kernel_source_sha(family)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"{kind}_{workload}.json")), reverse=True):
+        with open(path) as f:
+            tj = json.load(f)
+        if tj.get("source_sha") == sha and tj.get("shape") == shape and need(tj):
+            return tj, os.path.relpath(path, ROOT)
+    return None, None
+
+
+def fetch_calibration():
+    """Newest profiles/r*/fetch_calibration.json (tools/fetch_calib.hip + tools/fetch_calib.py): bytes per
+    counted FETCH_SIZE / WRITE_SIZE byte for each measured access pattern, or (None, None)."""
+    import glob
+
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "fetch_calibration.json")), reverse=True)
+    if not paths:
+        return None, None
+    with open(paths[0]) as f:
+        return json.load(f)["patterns"], os.path.relpath(paths[0], ROOT)
+
+
+def calibrated_traffic(per_launch: dict, read_pattern: str, write_pattern: str):
+    """HBM bytes per launch from the raw FETCH_SIZE / WRITE_SIZE (KiB) scaled by the calibration factors of
+    the access patterns the kernel's reads / writes follow; None without counters or calibration."""
+    cal, path = fetch_calibration()
+    if cal is None or "FETCH_SIZE" not in per_launch or "WRITE_SIZE" not in per_launch:
+        return None
+    rf, wf = cal[read_pattern]["read_factor"], cal[write_pattern]["write_factor"]
+    if rf is None or wf is None:
+        return None
+    return {"bytes": 1024.0 * (per_launch["FETCH_SIZE"] * rf + per_launch["WRITE_SIZE"] * wf),
+            "read_pattern": read_pattern, "read_factor": rf, "write_pattern": write_pattern, "write_factor": wf,
+            "calibration": path}
+
+
+def derive_bound(frac: float, issue: dict | None):
+    """roofline.bound from the measurement instead of a label: "hbm" only when the algorithmic bytes move at
+    >= 50 % of the HBM peak; otherwise the kernel is issue/latency bound, with the PMC issue block's figures."""
+    if frac >= 0.5:
+        return "hbm", f"algorithmic bytes at {frac:.0%} of the HBM peak"
+    if not issue:
+        return "issue/latency", f"algorithmic bytes at {frac:.1%} of the HBM peak (no PMC table for these sources)"
+    parts = [f"HBM at {frac:.1%} of peak"]
+    for k, lab in (("valu_frac", "VALU issue"), ("lds_frac", "LDS issue"), ("wait_any_frac", "waves waiting")):
+        if issue.get(k) is not None:
+            parts.append(f"{lab} {issue[k]:.0%}")
+    return "issue/latency", ", ".join(parts)
 
 
 def issue_fractions(per_launch: dict, kernel_ms: float) -> dict:
@@ -326,9 +397,9 @@ def run_lidar(args, world, rank, dev):
     n_total = n_local * world
     ds = (apg.FloorMapDatasetRooms(msize, msize) if w["kind"] == "rooms" else apg.FloorMapDatasetMaze(msize, msize))
 
-    def make_local(num_envs, env_offset):
+    def make_local(num_envs, env_offset, **kw):  # kw: packed_outputs=True when gathering
         return apg.make_vec(w["env_id"], num_envs=num_envs, lidar_beam_count=beams, dataset=ds, device=dev,
-                            array_backend="torch", env_offset=env_offset)
+                            array_backend=args.array_backend, env_offset=env_offset, **kw)
 
     senv = ShardedVectorEnv(make_local, n_total, rank, world, beams, gather=args.gather and world > 1,
                             time_gather=True)
@@ -337,6 +408,8 @@ def run_lidar(args, world, rank, dev):
     g = torch.Generator(device=dev).manual_seed(1 + rank)
     acts = torch.rand((ring, n_local, 2), generator=g, device=dev) * 2 - 1
     preds = torch.rand((ring, n_local, 2), generator=g, device=dev) * 2 - 1
+    if args.array_backend == "numpy":  # the default drop-in mode: host arrays in and out of every step
+        acts, preds = acts.cpu().numpy(), preds.cpu().numpy()
     steps_done = 0
 
     def step(ev=None):
@@ -401,7 +474,7 @@ def run_lidar(args, world, rank, dev):
 
     if world > 1:
         tt = torch.tensor([elapsed, kernel_ms, median_ms, reset_ms, gather_ms] + (episode or [0.0] * 4),
-                          dtype=torch.float64, device=dev)
+                          dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         vals = [float(x) for x in tt]
         elapsed, kernel_ms, median_ms, reset_ms, gather_ms = vals[:5]
@@ -418,13 +491,17 @@ def run_lidar(args, world, rank, dev):
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
         shape = {"num_envs": n_local, "beams": beams, "map": msize}
         tj, tpath = pmc_table(args.workload, "lidar", shape)
-        traffic = issue = None
+        traffic = issue = traffic_cal = None
         if tj is not None:
             hb = tj["hbm_bytes_per_launch"]
             reset_b_pmc = hb.get("reset_step") or hb["step"]  # a table without a reset step: no reset in the window
             traffic = (hb["step"] * (len(timed) - reset_ev) + reset_b_pmc * reset_ev) / len(timed)
             issue = issue_fractions(tj["per_launch"]["step"], median_ms)
             issue["source"] = tpath
+            # state / action loads and the 32-row occupancy windows: 8-B lanes in 256-B runs; 4-B output stores
+            traffic_cal = calibrated_traffic(tj["per_launch"]["step"], "k_seg256_8", "k_store4")
+        dj, dpath = newest_table("durations", args.workload, "lidar", shape, lambda t: "step" in t.get("per_class", {}))
+        bound, basis = derive_bound(achieved / HBM_PEAK_GBS, issue)
         out = {
             "metric": "env-steps/sec (vectorized step) at 1/2/4/8 MI355X + achieved HBM GB/s",
             "value": value,
@@ -437,14 +514,22 @@ def run_lidar(args, world, rank, dev):
             "scaling": w["scaling"],
             "vs_baseline": None,
             "dtype": "f32 (f64 exact geometry predicates)",
-            "data": "synthetic (uniform(-1,1) actions/predictions generated on device; maps generated on device)",
-            "config": {"workload": w["env_id"], "num_envs_per_gpu": n_local, "num_envs_total": n_total,
+            "data": "synthetic (uniform(-1,1) actions/predictions generated on device; maps generated on device)"
+                    + ("; array_backend=numpy: host arrays in/out of every step (PCIe included)"
+                       if args.array_backend == "numpy" else ""),
+            "config": {"workload": w["env_id"], "array_backend": args.array_backend, "num_envs_per_gpu": n_local,
+                       "num_envs_total": n_total,
                        "beams": beams, "map": f"{msize}x{msize} {w['kind']}", "max_episode_steps": 100,
                        "reset_ms": reset_ms, "note": w["note"], "gather_ms": gather_ms if senv.gather else None,
                        "parallelism": f"env-shard x{world}" + (" + all-gather" if args.gather and world > 1 else "")},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_lidar_step", "kernel_ms": kernel_ms, "median_kernel_ms": median_ms,
+            "roofline": {"bound": bound, "bound_basis": basis, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_calibrated": traffic_cal,
+                         "kernel": "k_lidar_step" + (" (+ k_maze, a no-op wave exit on ordinary steps)"
+                                                     if w["kind"] == "maze" else ""),
+                         "kernel_ms": kernel_ms, "median_kernel_ms": median_ms,
+                         "kernel_ms_rocprof": ({c: v["median_us"] / 1e3 for c, v in dj["per_class"].items()}
+                                               if dj else None), "durations_source": dpath,
                          "bytes_per_launch": bytes_per_launch, "reset_steps_timed": reset_steps,
                          "launches_timed": len(timed), "event_every": args.event_every,
                          "traffic_source": tpath, "issue": issue},
@@ -462,6 +547,66 @@ def run_lidar(args, world, rank, dev):
                                                args.cpu_threads)
         print(json.dumps(out), flush=True)
     senv.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def self_launch(n: int) -> None:
+    """Start `n` rank processes of this same command line (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
+    rendezvous on 127.0.0.1) as children, wait for all of them and exit with the first non-zero status.
+    Rank 0 prints the JSON line; the other ranks print nothing on stdout."""
+    import subprocess
+
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        # rank 0's stdout is filtered below; the others' goes to stderr (libraries print there, e.g. gloo)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True))
+    for line in procs[0].stdout:  # only the JSON line reaches our stdout
+        (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+        sys.stdout.flush()
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    if bad:
+        raise SystemExit(bad[0])
+
+
+def run_dry(args, world, rank):
+    """--dry-run: the multi-rank plumbing of the bench (rendezvous, barrier-bracketed timing, max over
+    ranks, one JSON line from rank 0) over gloo on CPU, without envs."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.perf_counter()
+    x = torch.ones(1024)
+    for _ in range(args.steps):
+        x = x * 1.0
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tt = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "value": args.steps / float(tt[0]), "unit": "steps/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": float(tt[0]) * 1e3 / args.steps, "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "none", "data": "none",
+                          "config": {"workload": "dry-run", "ranks": world}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -487,8 +632,22 @@ def main():
                          "first launch after the synchronize): each event pair adds two stream packets between "
                          "kernels, measured +6..9 us of wall per step on MI355X (tools/host_overhead.py), so "
                          "sampling keeps `value` unperturbed")
+    ap.add_argument("--array-backend", default="torch", choices=["torch", "numpy"],
+                    help="LIDAR workloads: torch = device tensors in/out (the hot path, default); numpy = the "
+                         "drop-in default of make_vec (host arrays, one packed D2H copy per step)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend of multi-rank runs (nccl = RCCL; gloo for rehearsals with "
+                         "several ranks on one GPU)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: ranks rendezvous over gloo, time a barrier, rank 0 prints "
+                         "the JSON line")
     args = ap.parse_args()
     args.event_every = max(1, min(args.event_every, args.steps))  # at least one timed launch carries events
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # started as `python bench.py --gpus N`: launch the N ranks ourselves (fresh processes, before anything
+        # here touches a GPU), like torch.distributed.run would, and exit with the worst rank's status
+        return self_launch(args.gpus)
 
     import torch
     import torch.distributed as dist
@@ -496,13 +655,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("for --gpus > 1 launch with torch.distributed.run (one process per GPU)")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    if args.dry_run:
+        return run_dry(args, world, rank)
+    # one rank per GPU; with fewer visible GPUs than ranks (rehearsals with --dist-backend gloo) ranks share them
+    ndev = max(1, torch.cuda.device_count())  # counting devices does not initialise HIP
+    torch.cuda.set_device(local_rank % ndev)
+    dev = torch.device("cuda", local_rank % ndev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     if args.workload in IMAGE_WORKLOADS:
         return run_image(args, world, rank, dev)
     return run_lidar(args, world, rank, dev)

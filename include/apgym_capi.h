@@ -104,6 +104,12 @@ typedef struct apg_lidar_config {
   int32_t log_stats;            /* 1: ActiveRegressionLogWrapper episode statistics (registered ids) */
   int32_t sparse;               /* 1: the -sparse ids (SparsifyWrapper, sparsify_wrapper.py:93-161):
                                    reward = base_reward - loss * (terminated ? 1 : 0) */
+  int32_t out_row_bytes;        /* 0: dense outputs.  > 0 (a multiple of 8): packed rows — the per-env outputs
+                                   lidar, odometry, time_step, reward, terminated, truncated, base_reward,
+                                   target, loss, info_mask, map_idx, reset_mask, stats, stats_len, weight of
+                                   env e are at their pointer + e * out_row_bytes (element j of a field at
+                                   + j * element size; stats as [N][4]), i.e. the pointers are field offsets
+                                   into one [N][out_row_bytes] buffer that a sharded run all-gathers as is */
 } apg_lidar_config;
 
 /* Persistent per-env state.  Sizes come from apg_lidar_query_sizes(). */
@@ -116,7 +122,8 @@ typedef struct apg_lidar_state {
   apg_pcg64 *it_rng;   /* [N]   DatasetIterator rng (dynamic maps) */
   uint64_t *occ;       /* [N or 1][H][wpr] bit-packed occupancy, wpr = ceil(W/64) */
   uint64_t *scratch;   /* reserved, unused (may be NULL; query_sizes reports scratch_bytes = 0) */
-  uint16_t *stack;     /* [N][maze_frames] DFS frames, contiguous per env (dynamic maze only) */
+  uint16_t *stack;     /* [N or 1][maze_frames] maze scratch (carve log + spilled DFS frames), contiguous
+                          per map, 64-byte aligned (mazes only) */
   uint64_t *map_idx;   /* [N]   dataset index of the current map */
   const float *beam_dirs; /* [beams][2] lidar_directions (f32, computed by the host like the reference) */
   float *stats_hist;   /* [2][step_limit][N] per-step euclidean_distance, mse of the episode (log_stats) */
@@ -173,7 +180,11 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
                             const float *prediction, const apg_lidar_outputs *out, apg_stream_t stream,
                             void *ev_begin, void *ev_end);
 
-/* n maps from dataset indices idx[n] into occ[n][h][wpr]; stack [n][maze_frames] (mazes only);
+/* u16 units of maze scratch per map (apg_lidar_state.stack / apg_map_generate's stack) for an h x w maze;
+ * replaces the reference's recursion stack of carve() (floor_map_dataset_maze.py:31-45). */
+int apg_maze_frames(int h, int w);
+
+/* n maps from dataset indices idx[n] into occ[n][h][wpr]; stack [n][apg_maze_frames(h, w)] (mazes only);
  * scratch is reserved and unused (may be NULL). */
 int apg_map_generate(int map_kind, const uint64_t *idx, int n, int h, int w, int max_rooms,
                      int door_width, double branching_prob, uint64_t *occ, uint64_t *scratch,

@@ -19,13 +19,13 @@ pytestmark = pytest.mark.gpu
 N_TOTAL = 256
 
 
-def _make(kind, num_envs, env_offset=0, num_envs_total=None):
+def _make(kind, num_envs, env_offset=0, num_envs_total=None, **kw):
     import ap_gym_amd as ap
 
     if kind == "lidar":
         return ap.make_vec("LIDARLocRooms-v0", num_envs=num_envs, lidar_beam_count=16,
                            dataset=ap.FloorMapDatasetRooms(32, 32), device="cuda:0", array_backend="torch",
-                           env_offset=env_offset)
+                           env_offset=env_offset, **kw)
     ds = ap.SyntheticImageClassificationDataset(64, (32, 32, 3), 10, 3, seed=3)
     cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=(8, 8), step_limit=8)
     return ap.ImageLocalizationVectorEnv(num_envs, cfg, device="cuda:0", array_backend="torch",
@@ -60,10 +60,13 @@ def _flat(kind, obs, rew, term, info):
     return {k: v.detach().cpu().numpy().copy() for k, v in d.items()}
 
 
-def _reference(kind):
+def _reference(kind, with_reset=False):
     env = _make(kind, N_TOTAL)
-    env.reset(seed=5)
+    obs0, info0 = env.reset(seed=5)
     out = []
+    if with_reset:
+        out.append({k: obs0[k].detach().cpu().numpy().copy() for k in ("lidar", "odometry", "time_step")})
+        out[-1]["map_idx"] = info0["map_idx"].cpu().numpy().copy()
     for t in range(_steps(kind)):
         a, p = _actions(kind, t, N_TOTAL)
         obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
@@ -104,11 +107,16 @@ def _worker(rank, world, port, kind, outdir):
     import ap_gym_amd  # noqa: F401
     from ap_gym_amd.sharding import ShardedVectorEnv
 
-    senv = ShardedVectorEnv(lambda num_envs, env_offset: _make(kind, num_envs, env_offset, N_TOTAL), N_TOTAL, rank,
-                            world, gather=True, gather_glimpse=True)
+    senv = ShardedVectorEnv(lambda num_envs, env_offset, **kw: _make(kind, num_envs, env_offset, N_TOTAL, **kw),
+                            N_TOTAL, rank, world, beams=16 if kind == "lidar" else None, gather=True,
+                            gather_glimpse=True)
+    assert senv._packed == (kind == "lidar")  # LIDAR: the kernel writes the all-gather's send rows
     lo, n = senv.offset, senv.local_num_envs
-    senv.reset(seed=5)
+    obs0, info0 = senv.reset(seed=5)
     rows = []
+    if kind == "lidar":  # reset returns the gathered batch too
+        rows.append({k: obs0[k].detach().cpu().numpy().copy() for k in ("lidar", "odometry", "time_step")})
+        rows[-1]["map_idx"] = info0["map_idx"].cpu().numpy().copy()
     for t in range(_steps(kind)):
         a, p = _actions(kind, t, N_TOTAL)
         obs, rew, term, trunc, info = senv.step({"action": a[lo:lo + n], "prediction": p[lo:lo + n]})
@@ -132,9 +140,44 @@ def test_two_rank_gather_on_gpu_equals_unsharded(gpu, kind, tmp_path):
 
     mp.start_processes(_worker, args=(2, _free_port(), kind, str(tmp_path)), nprocs=2, join=True,
                        start_method="spawn")
-    ref = _reference(kind)
+    ref = _reference(kind, with_reset=kind == "lidar")
     got = [np.load(tmp_path / f"rank{r}.npz") for r in range(2)]
     for t, want in enumerate(ref):
         for k, v in want.items():
             for r in range(2):
                 assert np.array_equal(got[r][f"{t}_{k}"], v), f"rank {r} step {t}: {k}"
+
+
+@pytest.mark.parametrize("log_stats,sparse", [(False, False), (True, False), (False, True)])
+def test_packed_output_rows_equal_dense(gpu, log_stats, sparse):
+    """packed_outputs=True (the kernel writes [N, row] rows for the all-gather) vs the dense outputs."""
+    import torch
+
+    import ap_gym_amd as ap
+
+    def make(packed):
+        e = ap.LIDARLocalization2DVectorEnv(N_TOTAL, ap.FloorMapDatasetRooms(32, 32), lidar_beam_count=16,
+                                            device="cuda:0", array_backend="torch", log_stats=log_stats,
+                                            sparse=sparse, sparse_reset_info=True, packed_outputs=packed)
+        return e
+
+    envs = [make(False), make(True)]
+    assert envs[1].output_rows is not None and envs[0].output_rows is None
+    for e in envs:
+        e.reset(seed=11)
+    names = ["lidar", "odometry", "time_step", "reward", "terminated", "truncated", "base_reward", "target", "loss",
+             "info_mask", "map_idx_out", "reset_mask"] + (["stats", "stats_len"] if log_stats else []) + (
+        ["weight"] if sparse else [])
+    for t in range(_steps("lidar")):
+        a, p = _actions("lidar", t, N_TOTAL)
+        for e in envs:
+            e.step({"action": a, "prediction": p})
+        for k in names:
+            x, y = envs[0]._t[k], envs[1]._t[k]
+            if k == "map_idx_out":  # written only for envs that reset: compare where they did
+                m = envs[0]._t["reset_mask"]
+                x, y = x[m], y[m]
+            assert torch.equal(x.cpu(), y.cpu()), f"step {t}: {k}"
+    for e in envs:
+        e.check_errors()
+        e.close()

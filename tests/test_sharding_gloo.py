@@ -45,19 +45,51 @@ class _OracleShard:
         self.e.close()
 
 
+class _PackedOracleShard(_OracleShard):
+    """The oracle shard with the device env's packed output rows (packed_outputs=True): every step's
+    outputs land in one [n, row] buffer, laid out like the kernel writes it (lidar_output_row_layout)."""
+
+    def __init__(self, num_envs, env_offset, packed_outputs=False):
+        from ap_gym_amd.lidar_env import lidar_output_row_layout, row_views
+
+        super().__init__(num_envs, env_offset)
+        assert packed_outputs
+        self.output_layout, row = lidar_output_row_layout(BEAMS)
+        self.output_rows = torch.zeros((num_envs, row), dtype=torch.uint8)
+        self.v = row_views(self.output_rows, self.output_layout)
+
+    def _fill(self):
+        e, v = self.e, self.v
+        for k in ("lidar", "odometry", "time_step", "reward", "base_reward", "target", "loss"):
+            v[k].copy_(torch.from_numpy(getattr(e, k).copy()))
+        for k in ("terminated", "truncated", "info_mask"):
+            v[k].copy_(torch.from_numpy(getattr(e, k).astype(bool)))
+
+    def reset(self, *, seed=None, options=None):
+        out = super().reset(seed=seed, options=options)
+        self._fill()
+        return out
+
+    def step(self, action):
+        out = super().step(action)
+        self._fill()
+        return out
+
+
 def _actions():
     rng = np.random.default_rng(1)
     return (rng.uniform(-1, 1, (STEPS, N_TOTAL, 2)).astype(np.float32),
             rng.uniform(-1, 1, (STEPS, N_TOTAL, 2)).astype(np.float32))
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, packed=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from ap_gym_amd.sharding import ShardedVectorEnv
 
-    senv = ShardedVectorEnv(lambda num_envs, env_offset: _OracleShard(num_envs, env_offset), N_TOTAL, rank, world,
-                            BEAMS, gather=True)
+    make = _PackedOracleShard if packed else (lambda num_envs, env_offset: _OracleShard(num_envs, env_offset))
+    senv = ShardedVectorEnv(make, N_TOTAL, rank, world, BEAMS, gather=True)
+    assert senv._packed == packed
     acts, preds = _actions()
     lo, n = senv.offset, senv.local_num_envs
     senv.reset(seed=7)
@@ -65,15 +97,15 @@ def _worker(rank, world, port, outdir):
     for t in range(STEPS):
         obs, rew, term, trunc, info = senv.step({"action": torch.from_numpy(acts[t, lo:lo + n]),
                                                  "prediction": torch.from_numpy(preds[t, lo:lo + n])})
-        rows.append(np.concatenate([obs["lidar"].numpy().view(np.uint8).ravel(),
-                                    obs["odometry"].numpy().view(np.uint8).ravel(),
-                                    obs["time_step"].numpy().view(np.uint8).ravel(),
-                                    rew.numpy().view(np.uint8).ravel(),
-                                    info["base_reward"].numpy().view(np.uint8).ravel(),
-                                    info["prediction"]["target"].numpy().view(np.uint8).ravel(),
-                                    info["prediction"]["loss"].numpy().view(np.uint8).ravel(),
-                                    term.numpy().view(np.uint8).ravel(), trunc.numpy().view(np.uint8).ravel(),
-                                    info["_base_reward"].numpy().view(np.uint8).ravel()]))
+        rows.append(np.concatenate([np.ascontiguousarray(obs["lidar"].numpy()).view(np.uint8).ravel(),
+                                    np.ascontiguousarray(obs["odometry"].numpy()).view(np.uint8).ravel(),
+                                    np.ascontiguousarray(obs["time_step"].numpy()).view(np.uint8).ravel(),
+                                    np.ascontiguousarray(rew.numpy()).view(np.uint8).ravel(),
+                                    np.ascontiguousarray(info["base_reward"].numpy()).view(np.uint8).ravel(),
+                                    np.ascontiguousarray(info["prediction"]["target"].numpy()).view(np.uint8).ravel(),
+                                    np.ascontiguousarray(info["prediction"]["loss"].numpy()).view(np.uint8).ravel(),
+                                    np.ascontiguousarray(term.numpy()).view(np.uint8).ravel(), np.ascontiguousarray(trunc.numpy()).view(np.uint8).ravel(),
+                                    np.ascontiguousarray(info["_base_reward"].numpy()).view(np.uint8).ravel()]))
     np.save(os.path.join(outdir, f"rank{rank}.npy"), np.stack(rows))
     senv.close()
     dist.destroy_process_group()
@@ -93,8 +125,10 @@ def test_shard_bounds():
         shard_bounds(10, 0, 4)
 
 
-def test_two_rank_gather_equals_unsharded(tmp_path, oracle_mod):
-    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+@pytest.mark.parametrize("packed", [False, True], ids=["copying", "packed_rows"])
+def test_two_rank_gather_equals_unsharded(tmp_path, oracle_mod, packed):
+    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), packed), nprocs=2, join=True,
+                       start_method="spawn")
     r0, r1 = np.load(tmp_path / "rank0.npy"), np.load(tmp_path / "rank1.npy")
     assert np.array_equal(r0, r1)  # every rank holds the full batch
 

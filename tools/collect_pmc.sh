@@ -12,7 +12,7 @@ O=$R/gpurun_out/pmc_$WL
 rm -rf "$O"
 mkdir -p "$O"
 case $WL in
-  lidar | maze127) REGEX=k_lidar_step ;;
+  lidar | maze127) REGEX="k_lidar_step|k_maze" ;;
   *) REGEX='k_glimpse|k_image_env|k_image_step|k_fill|k_unique|k_loc_target' ;;
 esac
 # 110 steps from reset(seed=0): step 101 is the synchronized autoreset step

@@ -2,10 +2,11 @@
 
     python tools/pmc_tables.py gpurun_out/pmc_<workload> <workload>
 
-LIDAR workloads: every k_lidar_step dispatch is classified by the bench's step order (the first,
-unfused instance is reset(seed)'s observation pass; fused dispatch k is env step t = k + 1, and
-t % 101 == 0 is the synchronized autoreset step), and each counter is averaged per class:
-"step" (ordinary steps), "reset_step" and "reset_pass".  Image workloads: per kernel name, and
+LIDAR workloads: every k_lidar_step dispatch is classified by the bench's step order (the first is
+reset(seed)'s observation pass; dispatch k is env step t = k, and t % 101 == 0 is the synchronized
+autoreset step), and each counter is averaged per class: "step" (ordinary steps), "reset_step" and
+"reset_pass"; mazes also launch k_maze before every step (classes "maze_reset" for reset(seed), then
+"maze_step" / "maze_reset_step": a no-op wave exit, or every env's maze).  Image workloads: per kernel name, and
 "step" = the ordinary step's k_image_step_fused launch (else the sum over the kernels launched on
 every step).
 
@@ -52,10 +53,10 @@ def bench_line(d: str) -> dict:
     raise SystemExit(f"no bench JSON line under {d}")
 
 
-def lidar_class(kname: str, ordinal: int | None) -> str:
-    if ordinal is None:
-        return "reset_pass"
-    return "reset_step" if (ordinal + 1) % bench.EPISODE_PERIOD == 0 else "step"
+def lidar_class(ordinal: int, prefix: str = "") -> str:
+    if ordinal == 0:
+        return prefix + "reset_pass" if not prefix else prefix + "reset"
+    return prefix + ("reset_step" if ordinal % bench.EPISODE_PERIOD == 0 else "step")
 
 
 def main():
@@ -65,13 +66,13 @@ def main():
     acc: dict[str, dict[str, list[float]]] = collections.defaultdict(lambda: collections.defaultdict(list))
     for name in PASSES:
         rows = read_pass(d, name)
-        ordinal = 0
+        ordinal = {"k_lidar_step": 0, "k_maze": 0}
         for did in sorted(rows):
             kname, vals = rows[did]
             if wl in bench.LIDAR_WORKLOADS:
-                fused = re.search(r"k_lidar_step<\s*\d+\s*,\s*true", kname) is not None
-                cls = lidar_class(kname, ordinal if fused else None)
-                ordinal += 1 if fused else 0
+                fam = "k_maze" if re.search(r"k_maze<", kname) else "k_lidar_step"
+                cls = lidar_class(ordinal[fam], "maze_" if fam == "k_maze" else "")
+                ordinal[fam] += 1
             else:
                 cls = kname.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
             for c, v in vals.items():
