@@ -97,10 +97,36 @@ class ForeignDatasetView(ImageClassificationDataset):
     """Any object with the reference dataset interface (`load`, `__len__`, `num_classes`,
     `num_channels`, `_get_data_point_batch`) -- e.g. a subclass of the reference's own
     ImageClassificationDataset (image_classification_dataset.py:12-98) -- seen as a pool dataset:
-    `device_pool()` fetches every data point once through its `_get_data_point_batch`."""
+    `device_pool()` fetches every data point once through its `_get_data_point_batch`, in chunks of
+    FETCH_CHUNK indices, and freezes the result on the device.
+
+    Static-pool assumption: the reference env fetches a data point every time it draws it, so a dataset
+    whose `_get_data_point(_batch)` randomizes per fetch (augmentation) or that does not fit in memory
+    behaves differently here (every draw of index i sees the same frozen image).  Such datasets are not
+    supported: the view warns once, and parity for them is unpinned."""
+
+    FETCH_CHUNK = 4096
 
     def __init__(self, inner):
         self.inner = inner
+        import warnings
+
+        warnings.warn(f"{type(inner).__name__} is used through ForeignDatasetView: its data points are fetched "
+                      "once and frozen on the device (per-fetch randomization is not reproduced)", stacklevel=3)
+
+    def device_pool(self) -> tuple[np.ndarray, np.ndarray]:
+        n = len(self)
+        imgs, labels = [], []
+        for lo in range(0, n, self.FETCH_CHUNK):
+            i, l = self._get_data_point_batch(np.arange(lo, min(n, lo + self.FETCH_CHUNK)))
+            imgs.append(np.stack([np.asarray(x) for x in i]) if not isinstance(i, np.ndarray) else np.asarray(i))
+            labels.append(np.asarray(l))
+        im = np.concatenate(imgs)
+        if im.ndim == 3:
+            im = im[..., None]
+        if im.dtype != np.uint8:
+            im = im.astype(np.float32)
+        return np.ascontiguousarray(im), np.concatenate(labels).astype(np.int32)
 
     def load(self):
         if hasattr(self.inner, "load"):

@@ -296,7 +296,7 @@ template <bool ONEW>
 __global__ __launch_bounds__(64) void k_maze(Geo g, apg_lidar_state S, const uint64_t *idx, int n, uint64_t *occ,
                                              uint8_t *scratch, int mode, uint64_t seed, int use_seed, int all,
                                              uint64_t *out_map_idx, float *map_obs, uint32_t *err, int lanes) {
-  extern __shared__ uint64_t s_mz[];  // maze_lane_at's layout, then (after the DFS) the paint bitmap
+  extern __shared__ uint64_t s_mz[];  // apg_maze.hpp's workgroup layout, then (after the DFS) the paint bitmap
   const int lane = threadIdx.x;
   const int i = blockIdx.x * lanes + lane;
   const bool mine = lane < lanes && i < n;
@@ -313,6 +313,9 @@ __global__ __launch_bounds__(64) void k_maze(Geo g, apg_lidar_state S, const uin
     midx = idx[i];
   }
   if (__ballot(active) == 0ULL) return;
+  char *lds = reinterpret_cast<char *>(s_mz);
+  maze_table_init(lds, lane);
+  __syncthreads();
   Pcg64 rng, it, mr;
   if (active) {
     if (mode == MZ_RESET) {
@@ -328,8 +331,7 @@ __global__ __launch_bounds__(64) void k_maze(Geo g, apg_lidar_state S, const uin
     mr = seed_pcg64(midx);  // get_data_point: default_rng(idx)
   }
   uint8_t *mine_scr = scratch + (size_t)(active ? i : 0) * sb;
-  const int nlog = maze_dfs<ONEW>(mr, active, m, g.bp, maze_lane_at(s_mz, m, lanes, lane), mine_scr + lb,
-                                  reinterpret_cast<uint32_t *>(mine_scr));
+  const int nlog = maze_dfs<ONEW>(mr, active, m, g.bp, lds, lane, mine_scr + lb, reinterpret_cast<uint32_t *>(mine_scr));
   __syncthreads();  // the DFS state is dead: the LDS now holds one maze's bitmap at a time
   uint64_t *bm = s_mz;
   uint64_t *dst_base = mode == MZ_RESET ? S.occ : occ;
@@ -361,13 +363,7 @@ __global__ __launch_bounds__(64) void k_maze(Geo g, apg_lidar_state S, const uin
       nfree += wave_sum(fr);
     }
     if (mode != MZ_RESET) continue;
-    if (map_obs) {  // the f32 map obs from the bitmap, lane = column (coalesced row stores)
-      float *mo = map_obs + (size_t)e * g.h * g.w;
-      for (int y = 0; y < g.h; y++)
-        for (int x = lane; x < g.w; x += 64)
-          __builtin_nontemporal_store(((bm[y * g.wpr + (x >> 6)] >> (x & 63)) & 1ULL) ? 1.0f / 255.0f : 0.0f,
-                                      mo + (size_t)y * g.w + x);
-    }
+    if (map_obs) bitmap_map_obs(bm, g.h, g.w, g.wpr, map_obs + (size_t)e * g.h * g.w, lane);
     // place_start (reset :304): the pick-th free cell in row-major order, pick = integers(0, nfree)
     long long pick = -1;
     if (lane == j && nfree > 0) pick = (long long)integers(rng, 0, nfree);
@@ -473,6 +469,9 @@ __device__ unsigned long long g_step_prof[16384][8];
 #ifndef APG_SLIDE_SPLIT
 #define APG_SLIDE_SPLIT 1  // phase 1: second slide scan on the idle waves (0: both on the env's lane; A/B 36.4 -> 35.8 us)
 #endif
+#ifndef APG_QUEUE_ENV_MAJOR
+#define APG_QUEUE_ENV_MAJOR 1  // phase-2b walk queue in env-major order (0: grouped by beam; tuning A/B)
+#endif
 #ifndef APG_STEP_MIN_WAVES
 #define APG_STEP_MIN_WAVES 4  // keep k_lidar_step at <= 128 VGPRs: 4 waves per SIMD
 #endif
@@ -542,6 +541,10 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   __shared__ uint32_t s_start[EPB];  // rooms autoreset: start cell y << 8 | x, or ~0u (no free cell)
   __shared__ int s_cnt[4];           // 0: reset-list length, 1: queued walks, 2: walk cursor
   __shared__ float s_dirs[MAX_STAGED_BEAMS][2];  // beam_dirs, read inside the beam loops (LDS, not HBM latency)
+#if APG_QUEUE_ENV_MAJOR
+  __shared__ uint64_t s_bmask[EPB];  // phase 2a: the beams of each env that need a walk
+  __shared__ int s_wtot[4];          // per-wave totals of the walk-count scan
+#endif
 #if APG_SLIDE_SPLIT
   __shared__ float s_slide[EPB];  // phase 1: the second slide candidate's length, then its scan distance
 #endif
@@ -993,6 +996,9 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       s_pos[el][0] = pos0;
       s_pos[el][1] = pos1;
     }
+#if APG_QUEUE_ENV_MAJOR
+    s_bmask[el] = 0ULL;
+#endif
     if (errbits) atomicOr(O.err, errbits);  // rare: NaN inputs only
   }
   }
@@ -1035,13 +1041,45 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         s_lid[el * LS + beam] = k < (uint32_t)EMPTY_TAB ? s_tab[k] : beam_value(f32_sqrt(s2));
       }
     }
+#if APG_QUEUE_ENV_MAJOR
+    if (walk) __hip_atomic_fetch_or(&s_bmask[el], 1ULL << beam, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
     const unsigned long long m = __ballot(walk);
     int qbase = 0;
     if (lane == 0 && m) qbase = atomicAdd(&s_cnt[1], __popcll(m));
     qbase = __shfl(qbase, 0);
     if (walk) s_queue[qbase + __popcll(m & ((1ULL << lane) - 1ULL))] = (uint16_t)((beam << 8) | el);
+#endif
   }
   __syncthreads();
+#if APG_QUEUE_ENV_MAJOR
+  // The walk queue in env-major order (an exclusive scan of the envs' walk counts, then each env's thread
+  // writes its entries): a wave of 2b then walks the windows of one or two envs, whose rows sit in distinct
+  // LDS banks (stride 33), instead of 64 envs' windows at scattered rows (1.6 bank-conflict cycles per LDS
+  // instruction with the beam-grouped queue).
+  {
+    uint64_t bm = 0;
+    int c = 0;
+    if (tid < EPB) {
+      bm = s_bmask[tid];
+      c = __popcll(bm);
+    }
+    const int inc = wave_inclusive_scan(c, lane);
+    if (tid < EPB && lane == 63) s_wtot[wave] = inc;
+    __syncthreads();
+    if (tid < EPB) {
+      int off = inc - c;
+      for (int w = 0; w < wave; w++) off += s_wtot[w];
+      while (bm) {
+        const int b = __ffsll((long long)bm) - 1;
+        bm &= bm - 1ULL;
+        s_queue[off++] = (uint16_t)((b << 8) | tid);
+      }
+      if (tid == EPB - 1) s_cnt[1] = off;
+    }
+    __syncthreads();
+  }
+#endif
   STEP_MARK(3)
   STEP_STOP(3)
   // ---------------- phase 2b: the queued scans, densely over the workgroup's waves; each wave takes
@@ -1274,11 +1312,17 @@ int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, in
   if (!scratch) return fail(APG_E_INVALID, "maze maps need the maze scratch buffer (stack)");
   const MazeGeom m = maze_geom(g.h, g.w);
   if (m.ncx > 127 || m.ncy > 127) return fail(APG_E_INVALID, "maze maps must be at most 255 x 255");
-  const int lanes = gen_lanes(n);
-  size_t dyn = (size_t)lanes * maze_lane_lds_bytes(g.h, g.w);
+  int lanes = gen_lanes(n);
+  static int forced = -1;  // APG_MAZE_LANES (tuning A/B only: the mazes do not depend on it)
+  if (forced < 0) {
+    const char *e = getenv("APG_MAZE_LANES");
+    forced = e ? atoi(e) : 0;
+  }
+  if (forced > 0 && forced <= 64) lanes = forced;
+  size_t dyn = maze_wg_lds_bytes(g.h, g.w);  // laid out for 64 lanes whatever `lanes` is
   const size_t bitmap = (size_t)g.h * g.wpr * sizeof(uint64_t);
   if (dyn < bitmap) dyn = bitmap;
-  const bool onew = m.cw == 1;
+  const bool onew = m.ncx <= 63;
   const void *kern = onew ? (const void *)k_maze<true> : (const void *)k_maze<false>;
   if (int rc = opt_in_lds(kern, dyn)) return rc;
   if (onew)

@@ -430,11 +430,13 @@ def test_full_size_properties(gpu, oracle_mod, kind, size, beams, n):
         ref.close()
 
 
+@pytest.mark.parametrize("use_torch_op", [False, True], ids=["c_abi", "torch_op"])
 @pytest.mark.parametrize("kind,size,beams", [("rooms", 64, 32), ("maze", 21, 8)])
-def test_step_through_ops_and_graph_replay(gpu, kind, size, beams):
-    """The hot path is torch.ops.apgym.lidar_step; one step captured in a torch.cuda.CUDAGraph (hipGraph)
-    and replayed over 230 steps (two autoreset bursts, fused into the step kernel) is bit-identical to
-    eager env.step."""
+def test_step_through_ops_and_graph_replay(gpu, kind, size, beams, use_torch_op):
+    """Eager steps call the C ABI directly (use_torch_op=False, the default) or go through
+    torch.ops.apgym.lidar_step (use_torch_op=True); one step captured in a torch.cuda.CUDAGraph (hipGraph,
+    always through the op) and replayed over 230 steps (two autoreset bursts) is bit-identical to eager
+    env.step either way."""
     import torch
 
     import ap_gym_amd as ap
@@ -444,6 +446,7 @@ def test_step_through_ops_and_graph_replay(gpu, kind, size, beams):
     eager = ap.make_vec(f"LIDARLoc{'Rooms' if kind == 'rooms' else 'Maze'}-v0", **kw)
     graphed = ap.make_vec(f"LIDARLoc{'Rooms' if kind == 'rooms' else 'Maze'}-v0", **kw)
     assert eager._ops is torch.ops.apgym
+    eager.use_torch_op = use_torch_op
     eager.reset(seed=11)
     graphed.reset(seed=11)
     a_buf = torch.zeros((n, 2), dtype=torch.float32, device=gpu)

@@ -221,3 +221,37 @@ def test_torch_ops_library_registers_the_ops():
     assert torch.classes.apgym.LidarEnv is not None and torch.classes.apgym.ImageEnv is not None
     with pytest.raises(RuntimeError, match="13 ints"):
         torch.classes.apgym.LidarEnv([1], [0.0], [], [])
+
+
+def test_foreign_dataset_view_fetches_in_chunks_and_warns():
+    """A reference-interface dataset becomes a device pool: fetched once, in chunks, with a warning about the
+    frozen (static-pool) semantics."""
+    import warnings
+
+    import numpy as np
+
+    from ap_gym_amd.image_dataset import ForeignDatasetView
+
+    class RefLike:
+        num_classes, num_channels = 3, 1
+
+        def __init__(self):
+            self.calls = 0
+
+        def __len__(self):
+            return 10
+
+        def _get_data_point_batch(self, idx):
+            self.calls += 1
+            idx = np.asarray(idx)
+            return (idx[:, None, None] * np.ones((len(idx), 4, 5), np.uint8)).astype(np.uint8), idx % 3
+
+    inner = RefLike()
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        view = ForeignDatasetView(inner)
+    assert any("frozen" in str(x.message) for x in w)
+    view.FETCH_CHUNK = 4
+    imgs, labels = view.device_pool()
+    assert inner.calls == 3 and imgs.shape == (10, 4, 5, 1) and imgs.dtype == np.uint8
+    assert np.array_equal(imgs[:, 0, 0, 0], np.arange(10)) and np.array_equal(labels, np.arange(10) % 3)

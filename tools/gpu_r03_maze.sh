@@ -20,3 +20,6 @@ cd "$GRAFT_REPO_ROOT" && python3 tools/rocpd_stats.py gpurun_out/prof_maze --csv
 timeout -k 10 300 python -u bench.py --workload lidar --steps 20 --warmup 3 --no-cpu-baseline --array-backend numpy --no-episode \
   > gpurun_out/b_numpy.json 2> gpurun_out/b_numpy.err || { echo "numpy bench failed"; tail -20 gpurun_out/b_numpy.err; exit 1; }
 cat gpurun_out/b_numpy.json
+for L in 64 32 16; do
+  APG_MAZE_LANES=$L timeout -k 10 200 python tools/maze_reset_time.py || exit 1
+done

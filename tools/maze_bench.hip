@@ -1,0 +1,107 @@
+// maze_bench.hip — tuning tool (not shipped): times the two halves of apg_maze.hpp's generator on BASELINE config 3
+// (262144 mazes of 127 x 127) in isolation, with HIP events:
+//   k_dfs    the DFS of every maze (seeding from the index, vis / ring / log / spills), logs left in scratch
+//   k_paint  each maze's occupancy rows painted from its log (one wave paints its 64 mazes in turn)
+// and runs each twice (the second time is reported).  For PMC passes: rocprofv3 --pmc ... -- tools/maze_bench
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I active-perception-gym_amd/csrc \
+//       -o tools/maze_bench tools/maze_bench.hip
+//   tools/maze_bench [num_mazes] [size] [lanes]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#include "apg_maze.hpp"
+
+using namespace apg;
+
+#define CHECK(x)                                                      \
+  do {                                                                \
+    hipError_t e_ = (x);                                              \
+    if (e_ != hipSuccess) {                                           \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));         \
+      exit(1);                                                        \
+    }                                                                 \
+  } while (0)
+
+__global__ __launch_bounds__(64) void k_dfs(int n, int h, int w, uint8_t *scratch, int *nlog, int lanes) {
+  extern __shared__ uint64_t s_mz[];
+  const int lane = threadIdx.x, i = blockIdx.x * lanes + lane;
+  const bool active = lane < lanes && i < n;
+  const MazeGeom m = maze_geom(h, w);
+  const size_t sb = maze_scratch_bytes(h, w), lb = maze_log_bytes(h, w);
+  Pcg64 r{};
+  if (active) r = seed_pcg64((uint64_t)i * 2654435761ULL + 12345ULL);
+  uint8_t *my = scratch + (size_t)(active ? i : 0) * sb;
+  char *lds = reinterpret_cast<char *>(s_mz);
+  maze_table_init(lds, lane);
+  __syncthreads();
+  const int nl = maze_dfs<true>(r, active, m, 1.0, lds, lane, my + lb, reinterpret_cast<uint32_t *>(my));
+  if (active) nlog[i] = nl;
+}
+
+__global__ __launch_bounds__(64) void k_paint(int n, int h, int w, const uint8_t *scratch, const int *nlog,
+                                              uint64_t *occ, float *mo, int lanes) {
+  extern __shared__ uint64_t s_mz[];
+  const int lane = threadIdx.x;
+  const MazeGeom m = maze_geom(h, w);
+  const int wpr = (w + 63) / 64;
+  const size_t sb = maze_scratch_bytes(h, w);
+  for (int j = 0; j < lanes; j++) {
+    const int e = blockIdx.x * lanes + j;
+    if (e >= n) break;
+    maze_paint(m, wpr, reinterpret_cast<const uint32_t *>(scratch + (size_t)e * sb), nlog[e], s_mz, lane);
+    for (int y = lane; y < h; y += 64)
+      for (int k = 0; k < wpr; k++) occ[((size_t)e * h + y) * wpr + k] = s_mz[y * wpr + k];
+    if (mo) bitmap_map_obs(s_mz, h, w, wpr, mo + (size_t)e * h * w, lane);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+int main(int argc, char **argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 262144;
+  const int size = argc > 2 ? atoi(argv[2]) : 127;
+  const int lanes = argc > 3 ? atoi(argv[3]) : 64;
+  const size_t sb = maze_scratch_bytes(size, size);
+  const int wpr = (size + 63) / 64;
+  uint8_t *scratch;
+  int *nlog;
+  uint64_t *occ;
+  float *mo;
+  CHECK(hipMalloc(&scratch, (size_t)n * sb));
+  CHECK(hipMalloc(&mo, (size_t)n * size * size * sizeof(float)));
+  CHECK(hipMalloc(&nlog, (size_t)n * sizeof(int)));
+  CHECK(hipMalloc(&occ, (size_t)n * size * wpr * 8));
+  const size_t lds = maze_wg_lds_bytes(size, size);
+  const size_t lds_p = (size_t)size * wpr * 8;
+  if (lds > 65536) CHECK(hipFuncSetAttribute((const void *)k_dfs, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipEvent_t a, b, c;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  CHECK(hipEventCreate(&c));
+  const int grid = (n + lanes - 1) / lanes;
+  float t_dfs = 0, t_paint = 0, t_obs = 0;
+  for (int rep = 0; rep < 2; rep++) {
+    CHECK(hipEventRecord(a, 0));
+    hipLaunchKernelGGL(k_dfs, dim3(grid), dim3(64), lds, 0, n, size, size, scratch, nlog, lanes);
+    CHECK(hipEventRecord(b, 0));
+    hipLaunchKernelGGL(k_paint, dim3(grid), dim3(64), lds_p, 0, n, size, size, scratch, nlog, occ, (float *)nullptr,
+                       lanes);
+    CHECK(hipEventRecord(c, 0));
+    CHECK(hipEventSynchronize(c));
+    CHECK(hipEventElapsedTime(&t_dfs, a, b));
+    CHECK(hipEventElapsedTime(&t_paint, b, c));
+    CHECK(hipEventRecord(a, 0));
+    hipLaunchKernelGGL(k_paint, dim3(grid), dim3(64), lds_p, 0, n, size, size, scratch, nlog, occ, mo, lanes);
+    CHECK(hipEventRecord(b, 0));
+    CHECK(hipEventSynchronize(b));
+    CHECK(hipEventElapsedTime(&t_obs, a, b));
+  }
+  int nl0 = 0;
+  CHECK(hipMemcpy(&nl0, nlog, sizeof(int), hipMemcpyDeviceToHost));
+  printf("{\"mazes\": %d, \"size\": %d, \"lanes\": %d, \"lds_per_wg\": %zu, \"dfs_ms\": %.3f, \"paint_ms\": %.3f, "
+         "\"paint_map_obs_ms\": %.3f, \"log0\": %d}\n", n, size, lanes, lds, t_dfs, t_paint, t_obs, nl0);
+  return 0;
+}

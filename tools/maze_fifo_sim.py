@@ -1,6 +1,6 @@
 # FIFO-refill simulation of apg_maze.hpp (CPU, numpy): PCG64 outputs consumed per DFS iteration of a
-# 127 x 127 maze and the fraction of lane-iterations a refill rate / FIFO depth leaves short.  Needs /tmp/emu.py
-# (tools/maze_emu.py copied there).
+# 127 x 127 maze and the fraction of lane-iterations a refill rate / FIFO depth leaves short (uses maze_emu.py
+# next to it).
 import numpy as np
 exec(open(__import__('os').path.join(__import__('os').path.dirname(__file__), 'maze_emu.py')).read().split("sys.path.insert")[0].replace("class R:","class R0:"))
 # instrumented rng: count outputs consumed per DFS iteration
