@@ -469,9 +469,6 @@ __device__ unsigned long long g_step_prof[16384][8];
 #ifndef APG_SLIDE_SPLIT
 #define APG_SLIDE_SPLIT 1  // phase 1: second slide scan on the idle waves (0: both on the env's lane; A/B 36.4 -> 35.8 us)
 #endif
-#ifndef APG_QUEUE_ENV_MAJOR
-#define APG_QUEUE_ENV_MAJOR 1  // phase-2b walk queue in env-major order (0: grouped by beam; tuning A/B)
-#endif
 #ifndef APG_STEP_MIN_WAVES
 #define APG_STEP_MIN_WAVES 4  // keep k_lidar_step at <= 128 VGPRs: 4 waves per SIMD
 #endif
@@ -541,10 +538,6 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   __shared__ uint32_t s_start[EPB];  // rooms autoreset: start cell y << 8 | x, or ~0u (no free cell)
   __shared__ int s_cnt[4];           // 0: reset-list length, 1: queued walks, 2: walk cursor
   __shared__ float s_dirs[MAX_STAGED_BEAMS][2];  // beam_dirs, read inside the beam loops (LDS, not HBM latency)
-#if APG_QUEUE_ENV_MAJOR
-  __shared__ uint64_t s_bmask[EPB];  // phase 2a: the beams of each env that need a walk
-  __shared__ int s_wtot[4];          // per-wave totals of the walk-count scan
-#endif
 #if APG_SLIDE_SPLIT
   __shared__ float s_slide[EPB];  // phase 1: the second slide candidate's length, then its scan distance
 #endif
@@ -996,9 +989,6 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       s_pos[el][0] = pos0;
       s_pos[el][1] = pos1;
     }
-#if APG_QUEUE_ENV_MAJOR
-    s_bmask[el] = 0ULL;
-#endif
     if (errbits) atomicOr(O.err, errbits);  // rare: NaN inputs only
   }
   }
@@ -1041,45 +1031,13 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         s_lid[el * LS + beam] = k < (uint32_t)EMPTY_TAB ? s_tab[k] : beam_value(f32_sqrt(s2));
       }
     }
-#if APG_QUEUE_ENV_MAJOR
-    if (walk) __hip_atomic_fetch_or(&s_bmask[el], 1ULL << beam, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
     const unsigned long long m = __ballot(walk);
     int qbase = 0;
     if (lane == 0 && m) qbase = atomicAdd(&s_cnt[1], __popcll(m));
     qbase = __shfl(qbase, 0);
     if (walk) s_queue[qbase + __popcll(m & ((1ULL << lane) - 1ULL))] = (uint16_t)((beam << 8) | el);
-#endif
   }
   __syncthreads();
-#if APG_QUEUE_ENV_MAJOR
-  // The walk queue in env-major order (an exclusive scan of the envs' walk counts, then each env's thread
-  // writes its entries): a wave of 2b then walks the windows of one or two envs, whose rows sit in distinct
-  // LDS banks (stride 33), instead of 64 envs' windows at scattered rows (1.6 bank-conflict cycles per LDS
-  // instruction with the beam-grouped queue).
-  {
-    uint64_t bm = 0;
-    int c = 0;
-    if (tid < EPB) {
-      bm = s_bmask[tid];
-      c = __popcll(bm);
-    }
-    const int inc = wave_inclusive_scan(c, lane);
-    if (tid < EPB && lane == 63) s_wtot[wave] = inc;
-    __syncthreads();
-    if (tid < EPB) {
-      int off = inc - c;
-      for (int w = 0; w < wave; w++) off += s_wtot[w];
-      while (bm) {
-        const int b = __ffsll((long long)bm) - 1;
-        bm &= bm - 1ULL;
-        s_queue[off++] = (uint16_t)((b << 8) | tid);
-      }
-      if (tid == EPB - 1) s_cnt[1] = off;
-    }
-    __syncthreads();
-  }
-#endif
   STEP_MARK(3)
   STEP_STOP(3)
   // ---------------- phase 2b: the queued scans, densely over the workgroup's waves; each wave takes
