@@ -20,7 +20,7 @@ OUT = os.path.join(OUT_DIR, "libapgym_hip.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 SOURCES = ["apg_lidar.hip", "apg_image.hip", "apg_circle_square.hip", "apg_light_dark.hip"]
 HEADERS = ["apg_device.hpp", "apg_maps.hpp", "apg_scan.hpp", "apg_rng.hpp", "apg_host.hpp", "apg_pairwise.hpp",
-           "apg_ziggurat.hpp"]
+           "apg_ziggurat.hpp", "apg_maze.hpp"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = [

@@ -863,62 +863,86 @@ APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const EnvIn &in, doub
   if (err) atomicOr(out.err, err);
 }
 
-// One launch per ordinary (non-reset) step: a glimpse workgroup computes the glimpses of its `nu` envs at
-// their new positions (gs_axes / gs_pixels; every axis thread recomputes its env's move with move_pos,
-// so no barrier separates the env step from the glimpse) and runs their env steps (loc_env / cls1_env:
-// loss, stats, move).  KIND: APG_IMAGE_LOCALIZE, or APG_IMAGE_CLASSIFY with K <= CLS1_MAX_K (logits
-// staged in LDS with coalesced loads, one thread per env as k_image_env_cls1).
+// One launch per ordinary (non-reset) step: a workgroup computes the glimpses of its `nu` envs at their new
+// positions (gs_axes / gs_pixels) and runs their env steps (loc_env / cls1_env: loss, stats, move).  KIND:
+// APG_IMAGE_LOCALIZE, or APG_IMAGE_CLASSIFY with K <= CLS1_MAX_K (logits staged in LDS with coalesced loads,
+// one thread per env as k_image_env_cls1).
+// ENVW: the workgroup is GS_THREADS glimpse threads plus one env wave.  The env wave loads the env inputs,
+// moves the units (positions into LDS for the axes), and after the second barrier runs the env steps while
+// the glimpse waves compute the pixels: the serial per-env tail (exp / log / stats / move) overlaps the
+// glimpse instead of following it.  Without ENVW the first GS_THREADS threads do both in turn.
 #ifndef APG_FUSED_MIN_WAVES
 #define APG_FUSED_MIN_WAVES 8  // <= 64 VGPRs: every workgroup of the grid resident at once
 #endif
-template <int KIND, bool F32, int PC, int C>
-__global__ __launch_bounds__(GS_THREADS, APG_FUSED_MIN_WAVES) void k_image_step_fused(
-    EnvArgs a, GlimpseGeo g, const void *pool, const int64_t *index, const float *__restrict__ act,
-    const float *__restrict__ pred, const int32_t *label, double *pos, apg_image_outputs out, float *hist, int upb,
-    FastDiv per_div, FastDiv s1_div, FastDiv side_div, FastDiv k_div) {
+constexpr int ENV_WAVE = 64;
+template <int KIND, bool F32, int PC, int C, bool ENVW>
+__global__ __launch_bounds__(ENVW ? GS_THREADS + ENV_WAVE : GS_THREADS)
+__attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fused(EnvArgs a, GlimpseGeo g, const void *pool, const int64_t *index, const float *__restrict__ act,
+                   const float *__restrict__ pred, const int32_t *label, double *pos, apg_image_outputs out,
+                   float *hist, int upb, FastDiv per_div, FastDiv s1_div, FastDiv side_div, FastDiv k_div) {
   __shared__ float s_lut[256];
   __shared__ int64_t s_base[GS_MAX_UNITS];
   __shared__ double s_npos[GS_MAX_UNITS][2];  // the units' positions after this step's move
   extern __shared__ Axis s_ax[];  // [unit][rows s0 | columns s1], then (classify) the logits [unit][stride]
   const int tid = threadIdx.x;
-  for (int v = tid; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
   const int u0 = blockIdx.x * upb, nu = a.n - u0 < upb ? a.n - u0 : upb;
   float *s_logit = reinterpret_cast<float *>(s_ax + (size_t)upb * (g.s0 + g.s1));
-  if constexpr (KIND == APG_IMAGE_CLASSIFY) {
-    const int k = a.k, stride = cls1_stride(k);
-    for (int q = tid; q < nu * k; q += GS_THREADS) {
-      const int r = (int)k_div.div((uint32_t)q);
-      s_logit[r * stride + (q - r * k)] = pred[(size_t)u0 * k + q];
+  // env inputs of unit u by thread r of `nr` (the env wave, or the first GS_THREADS threads): logits staged,
+  // inputs loaded, image offset and the move (the env step repeats it for its outputs) into LDS for the axes
+  auto env_inputs = [&](int r, int nr, EnvIn &in) {
+    if constexpr (KIND == APG_IMAGE_CLASSIFY) {
+      const int k = a.k, stride = cls1_stride(k);
+      for (int q = r; q < nu * k; q += nr) {
+        const int row = (int)k_div.div((uint32_t)q);
+        s_logit[row * stride + (q - row * k)] = pred[(size_t)u0 * k + q];
+      }
     }
-  }
-  // each unit's env inputs and image offset, loaded first; its move once (the env step below repeats it
-  // for its outputs), shared with its axis threads
-  EnvIn in{};
-  if (tid < nu) {
-    const int e = u0 + tid;
-    in = load_env_in<KIND>(a, e, act, pred, label, pos, out);
-    s_base[tid] = index[e] * g.img_elems;
-    double px = in.px, py = in.py;
-    move_pos(a, in.a0, in.a1, px, py);
-    s_npos[tid][0] = px;
-    s_npos[tid][1] = py;
-  }
-  __syncthreads();
-  const uint32_t bad = gs_axes(g, nullptr, [&](int u, int c) { return s_npos[u][c]; }, u0, nu, 1, side_div, s_ax, s_base);
-  __syncthreads();
-  gs_pixels_t<F32, PC, C>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
-#ifdef APG_X_IMG_NOENV  // tuning experiment only (wrong results): no env step
-  if (false) {
-#else
-  if (tid < nu) {
-#endif
-    const int e = u0 + tid;
+    in = EnvIn{};
+    if (r < nu) {
+      const int e = u0 + r;
+      in = load_env_in<KIND>(a, e, act, pred, label, pos, out);
+      s_base[r] = index[e] * g.img_elems;
+      double px = in.px, py = in.py;
+      move_pos(a, in.a0, in.a1, px, py);
+      s_npos[r][0] = px;
+      s_npos[r][1] = py;
+    }
+  };
+  auto env_step = [&](int r, const EnvIn &in) {
+    if (r >= nu) return;
     if constexpr (KIND == APG_IMAGE_CLASSIFY)
-      cls1_env(a, e, s_logit + tid * cls1_stride(a.k), in, pos, out, hist);
+      cls1_env(a, u0 + r, s_logit + r * cls1_stride(a.k), in, pos, out, hist);
     else
-      loc_env(a, e, in, pos, out, hist);
+      loc_env(a, u0 + r, in, pos, out, hist);
+  };
+  if constexpr (ENVW) {
+    if (tid >= GS_THREADS) {  // the env wave (wave-uniform branch; it takes part in both barriers)
+      EnvIn in;
+      env_inputs(tid - GS_THREADS, ENV_WAVE, in);
+      __syncthreads();
+      __syncthreads();
+      env_step(tid - GS_THREADS, in);
+      return;
+    }
+    for (int v = tid; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
+    __syncthreads();
+    const uint32_t bad =
+        gs_axes(g, nullptr, [&](int u, int c) { return s_npos[u][c]; }, u0, nu, 1, side_div, s_ax, s_base);
+    __syncthreads();
+    gs_pixels_t<F32, PC, C>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
+    if (bad) atomicOr(out.err, bad);
+  } else {
+    for (int v = tid; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
+    EnvIn in;
+    env_inputs(tid, GS_THREADS, in);
+    __syncthreads();
+    const uint32_t bad =
+        gs_axes(g, nullptr, [&](int u, int c) { return s_npos[u][c]; }, u0, nu, 1, side_div, s_ax, s_base);
+    __syncthreads();
+    gs_pixels_t<F32, PC, C>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
+    env_step(tid, in);
+    if (bad) atomicOr(out.err, bad);
   }
-  if (bad) atomicOr(out.err, bad);
 }
 
 // ------------------------------------------------------------------ k_unique
@@ -1371,8 +1395,9 @@ int launch_uniform(apg_pcg64 *state, int64_t n, int cols, const double *low, con
 // Glimpse units (env x position) per k_glimpse_sep / k_image_step_fused workgroup: about APG_GLIMPSE_PPT
 // (default 4, clamped to [1, 16]: the Axis LDS stays far below 64 KiB) pixels per thread.  The output
 // does not depend on it.
-int glimpse_units_per_block(int per) {
-  static const int ppt = getenv("APG_GLIMPSE_PPT") ? std::max(1, std::min(16, atoi(getenv("APG_GLIMPSE_PPT")))) : 4;
+int glimpse_units_per_block(int per, int ppt_default = 4) {
+  static const int forced = getenv("APG_GLIMPSE_PPT") ? std::max(1, std::min(16, atoi(getenv("APG_GLIMPSE_PPT")))) : 0;
+  const int ppt = forced ? forced : ppt_default;
   return std::max(1, std::min(GS_MAX_UNITS, (ppt * GS_THREADS + per - 1) / per));
 }
 
@@ -1639,16 +1664,30 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
                        (c->kind == APG_IMAGE_LOCALIZE || c->num_classes <= CLS1_MAX_K);
   if (fusable) {
     const int per = g.s0 * g.s1;
-    const int upb = glimpse_units_per_block(per);
+    // The env wave pays off for classification (its env step is the long serial tail: exp, log, pairwise
+    // sum), with the workgroup's units at its 64 lanes; localization's short tail does not repay a fifth wave
+    // (MI355X, fused step: MNIST 11.6 vs 13.8 us, TinyImageNetLoc 29.7 vs 28.0 us).  APG_IMAGE_ENV_WAVE=0|1
+    // overrides (A/B knob; results do not depend on it).
+    static const int envw_knob = getenv("APG_IMAGE_ENV_WAVE") ? atoi(getenv("APG_IMAGE_ENV_WAVE")) : -1;
+    const bool envw = envw_knob >= 0 ? envw_knob != 0 : c->kind == APG_IMAGE_CLASSIFY;
+    const int upb = envw ? std::min(ENV_WAVE, glimpse_units_per_block(per, 8)) : glimpse_units_per_block(per, 4);
     size_t dyn = (size_t)upb * (g.s0 + g.s1) * sizeof(Axis);
     if (c->kind == APG_IMAGE_CLASSIFY) dyn += (size_t)upb * (c->num_classes + 2) * sizeof(float);
     const dim3 grid(grid_for(n, upb)), block(GS_THREADS);
     const FastDiv pd = make_fastdiv((uint32_t)per), sd = make_fastdiv((uint32_t)g.s1),
                   sid = make_fastdiv((uint32_t)(g.s0 + g.s1)), kd = make_fastdiv((uint32_t)std::max(1, c->num_classes));
     // one instance per env kind and pool format (u8 / f32, pool channels, glimpse channels)
-#define APG_FUSED(K, F, P, C)                                                                                  \
-  hipLaunchKernelGGL((k_image_step_fused<K, F, P, C>), grid, block, dyn, s, a, g, st->pool, st->index, action, \
-                     prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, sd, sid, kd)
+    const dim3 block_e(GS_THREADS + ENV_WAVE);
+    // one instance per env kind and pool format (u8 / f32, pool channels, glimpse channels)
+#define APG_FUSED(K, F, P, C)                                                                                    \
+  do {                                                                                                           \
+    if (envw)                                                                                                    \
+      hipLaunchKernelGGL((k_image_step_fused<K, F, P, C, true>), grid, block_e, dyn, s, a, g, st->pool, st->index, \
+                         action, prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, sd, sid, kd);    \
+    else                                                                                                         \
+      hipLaunchKernelGGL((k_image_step_fused<K, F, P, C, false>), grid, block, dyn, s, a, g, st->pool, st->index,\
+                         action, prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, sd, sid, kd);    \
+  } while (0)
 #define APG_FUSED_KIND(K)                                   \
   do {                                                      \
     if (g.pool_f32) {                                       \

@@ -292,10 +292,71 @@ __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, ui
 // them out coalesced (lane = row), counts free cells per row and draws the start cell like place_start.
 enum : int { MZ_MAPS = 0, MZ_RESET = 1 };
 
+// The dataset index of maze i (MZ_MAPS: idx[i]; MZ_RESET: the env's DatasetIterator draw, from its streams
+// or, on reset(seed), from default_rng(seed + i)), with the env's streams after it.
+APG_DEV uint64_t maze_index(const apg_lidar_state &S, const uint64_t *idx, int i, int mode, uint64_t seed,
+                            int use_seed, Pcg64 &rng, Pcg64 &it) {
+  if (mode != MZ_RESET) return idx[i];
+  if (use_seed) {
+    rng = seed_pcg64(seed + (uint64_t)i);
+    it = seed_pcg64(bounded_u64(rng, 0x100000000ULL));  // integers(0, 2**32, endpoint=True)
+  } else {
+    rng = *reinterpret_cast<const Pcg64 *>(&S.rng[i]);
+    it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[i]);
+  }
+  return next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
+}
+
+// The random streams of the mazes k_maze is about to generate (apg_maze.hpp): a workgroup per MZS_MAZES
+// mazes seeds them (default_rng(idx)) and tabulates the jumps to every item's first output, then its threads
+// generate the items (MZ_ITEM_GROUPS groups of 32 outputs each) and the state after the last one.  Full
+// occupancy, so the LCG work that held the DFS at one wave per SIMD runs at chip rate here.
+constexpr int MZS_THREADS = 256, MZS_MAZES = 64;
+__global__ __launch_bounds__(MZS_THREADS) void k_maze_stream(Geo g, apg_lidar_state S, const uint64_t *idx, int n,
+                                                             uint8_t *scratch, int mode, uint64_t seed, int use_seed,
+                                                             int all, int ng) {
+  __shared__ uint64_t s_seed[MZS_MAZES][4];  // s_hi, s_lo, i_hi, i_lo
+  __shared__ MzJump s_jump[MZ_MAX_ITEMS + 1];
+  const int tid = threadIdx.x, nitems = ng / MZ_ITEM_GROUPS;
+  bool act = false;
+  if (tid < MZS_MAZES) {
+    const int i = blockIdx.x * MZS_MAZES + tid;
+    if (i < n) act = mode != MZ_RESET || all || (S.flags[i] & F_AUTORESET);
+    if (act) {
+      Pcg64 rng, it;
+      const Pcg64 mr = seed_pcg64(maze_index(S, idx, i, mode, seed, use_seed, rng, it));
+      s_seed[tid][0] = mr.s_hi;
+      s_seed[tid][1] = mr.s_lo;
+      s_seed[tid][2] = mr.i_hi;
+      s_seed[tid][3] = mr.i_lo;
+    } else {
+      s_seed[tid][2] = s_seed[tid][3] = 0ULL;  // inactive: increments are odd, 0 never is one
+    }
+  } else if (tid - MZS_MAZES <= nitems) {
+    s_jump[tid - MZS_MAZES] = mz_jump((uint64_t)(tid - MZS_MAZES) * MZ_ITEM_GROUPS * MZ_GROUP);
+  }
+  if (__syncthreads_or(act) == 0) return;
+  const size_t sb = maze_scratch_bytes(g.h, g.w), so = maze_stream_off(g.h, g.w);
+  for (int q = tid; q < MZS_MAZES * (nitems + 1); q += MZS_THREADS) {
+    const int j = q / (nitems + 1), c = q - j * (nitems + 1), i = blockIdx.x * MZS_MAZES + j;
+    if (s_seed[j][3] == 0ULL) continue;
+    uint8_t *stream = scratch + (size_t)i * sb + so;
+    if (c < nitems) {
+      maze_stream_item(s_seed[j][0], s_seed[j][1], s_seed[j][2], s_seed[j][3], s_jump[c], g.bp, c, stream, ng);
+    } else {  // the state after the stream, for a maze that draws past it
+      uint64_t hi = s_seed[j][0], lo = s_seed[j][1];
+      mz_jump_state(s_jump[c], hi, lo, s_seed[j][2], s_seed[j][3]);
+      uint64_t *st = reinterpret_cast<uint64_t *>(stream + maze_stream_state_off(ng));
+      st[0] = hi;
+      st[1] = lo;
+    }
+  }
+}
+
 template <bool ONEW>
 __global__ __launch_bounds__(64) void k_maze(Geo g, apg_lidar_state S, const uint64_t *idx, int n, uint64_t *occ,
                                              uint8_t *scratch, int mode, uint64_t seed, int use_seed, int all,
-                                             uint64_t *out_map_idx, float *map_obs, uint32_t *err, int lanes) {
+                                             uint64_t *out_map_idx, float *map_obs, uint32_t *err, int lanes, int ng) {
   extern __shared__ uint64_t s_mz[];  // apg_maze.hpp's workgroup layout, then (after the DFS) the paint bitmap
   const int lane = threadIdx.x;
   const int i = blockIdx.x * lanes + lane;
@@ -316,22 +377,16 @@ __global__ __launch_bounds__(64) void k_maze(Geo g, apg_lidar_state S, const uin
   char *lds = reinterpret_cast<char *>(s_mz);
   maze_table_init(lds, lane);
   __syncthreads();
-  Pcg64 rng, it, mr;
+  Pcg64 rng{}, it{}, mr{};
   if (active) {
-    if (mode == MZ_RESET) {
-      if (use_seed) {
-        rng = seed_pcg64(seed + (uint64_t)i);
-        it = seed_pcg64(bounded_u64(rng, 0x100000000ULL));  // integers(0, 2**32, endpoint=True)
-      } else {
-        rng = *reinterpret_cast<const Pcg64 *>(&S.rng[i]);
-        it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[i]);
-      }
-      midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
-    }
-    mr = seed_pcg64(midx);  // get_data_point: default_rng(idx)
+    midx = maze_index(S, idx, i, mode, seed, use_seed, rng, it);
+    mr = seed_pcg64(midx);  // get_data_point: default_rng(idx) (its increment; the stream: k_maze_stream)
   }
   uint8_t *mine_scr = scratch + (size_t)(active ? i : 0) * sb;
-  const int nlog = maze_dfs<ONEW>(mr, active, m, g.bp, lds, lane, mine_scr + lb, reinterpret_cast<uint32_t *>(mine_scr));
+  bool bad = false;
+  const int nlog = maze_dfs<ONEW>(mr, mine_scr + maze_stream_off(g.h, g.w), ng, active, m, g.bp, lds, lane,
+                                  mine_scr + lb, reinterpret_cast<uint32_t *>(mine_scr), bad);
+  if (bad) atomicOr(err, APG_ERR_MAPGEN);
   __syncthreads();  // the DFS state is dead: the LDS now holds one maze's bitmap at a time
   uint64_t *bm = s_mz;
   uint64_t *dst_base = mode == MZ_RESET ? S.occ : occ;
@@ -1283,12 +1338,25 @@ int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, in
   const bool onew = m.ncx <= 63;
   const void *kern = onew ? (const void *)k_maze<true> : (const void *)k_maze<false>;
   if (int rc = opt_in_lds(kern, dyn)) return rc;
+  // stream groups per maze: APG_MAZE_STREAM_GROUPS (tests: fewer, so the DFS steps the LCG past them; the
+  // mazes do not depend on it) is clamped to [MZ_ITEM_GROUPS, maze_stream_groups], a multiple of MZ_ITEM_GROUPS
+  static int forced_ng = -1;
+  if (forced_ng < 0) {
+    const char *e = getenv("APG_MAZE_STREAM_GROUPS");
+    forced_ng = e ? atoi(e) : 0;
+  }
+  int ng = maze_stream_groups(g.h, g.w);
+  if (forced_ng > 0) ng = std::max(MZ_ITEM_GROUPS, std::min(ng, forced_ng / MZ_ITEM_GROUPS * MZ_ITEM_GROUPS));
+  if (ng / MZ_ITEM_GROUPS > MZ_MAX_ITEMS) return fail(APG_E_INVALID, "maze stream too long");
+  hipLaunchKernelGGL(k_maze_stream, dim3(grid_for(n, MZS_MAZES)), dim3(MZS_THREADS), 0, s, g, st, idx, n, scratch, mode,
+                     seed, use_seed, all, ng);
+  if (int rc = check_launch("k_maze_stream")) return rc;
   if (onew)
     hipLaunchKernelGGL(k_maze<true>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, st, idx, n, occ, scratch, mode, seed,
-                       use_seed, all, out_map_idx, map_obs, err, lanes);
+                       use_seed, all, out_map_idx, map_obs, err, lanes, ng);
   else
     hipLaunchKernelGGL(k_maze<false>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, st, idx, n, occ, scratch, mode,
-                       seed, use_seed, all, out_map_idx, map_obs, err, lanes);
+                       seed, use_seed, all, out_map_idx, map_obs, err, lanes, ng);
   return check_launch("k_maze");
 }
 

@@ -20,11 +20,16 @@
 // as one "move" (a return is a move against the entry direction): 2 * cells - 1 iterations for a perfect
 // maze, each with one LDS round trip for the current cell's three neighbour rows.
 //
-// The kernel is VALU-issue bound at one wave per SIMD (the LDS state of 256 mazes fills a CU): every
-// iteration executes the union of the carve and the return paths for its 64 lanes, so the paths are kept
-// branch-light (the permutation draw is a window over the queued random words, not a rejection loop).
+// The DFS is VALU-issue bound at one wave per SIMD (the LDS state of 256 mazes fills a CU): every iteration
+// executes the union of the carve and the return paths for its 64 lanes.  So the random numbers are not made
+// there: k_maze_stream (full occupancy, one LCG jump per 256 outputs) writes each maze's PCG64 outputs ahead
+// as the only bits the DFS reads of them — the two low bits of each 32-bit half (random_interval's masks
+// are 3, 3, 1) and next_double() < branching_prob — 5 bits per output, and the DFS keeps the next 32 outputs
+// in registers (topped up in the memory phase), reading every draw of an iteration off that window with a
+// few bit operations: the permutation's rejection loop is a count of leading rejected halves.
 #pragma once
 #include "apg_device.hpp"
+#include "apg_rng.hpp"
 
 namespace apg {
 
@@ -47,134 +52,186 @@ APG_DEV uint32_t mz_perm_of(uint32_t pidx) {
   return (uint32_t)(t >> ((pidx & 7u) * 8u)) & 255u;
 }
 
-// The maze's numpy stream (PCG64 + next_uint32's buffered half word), with the PCG64 outputs generated
-// ahead into a small register FIFO: the DFS loop produces MZ_FILL outputs per iteration in uniform control
-// flow, and the draw sites (rng.random(), the permutation's next_uint32 calls) only take from the FIFO.
-// Without it a wave executed the 128-bit LCG step once per draw site any of its lanes reached (up to five
-// per iteration).  The outputs are consumed in the same order, so the draws are unchanged.  A DFS iteration
-// consumes 0.88 outputs on average but up to ~3 on a forward run: one fill per iteration leaves lanes short
-// on 26 % of the iterations of a 127 x 127 maze, two fills into 4 slots on 0.03 % (tools/maze_fifo_sim.py);
-// a short lane steps the LCG inline.
-constexpr int MZ_FIFO = 4, MZ_FILL = 2;
-struct MzRng {
-  uint64_t s_hi, s_lo, i_hi, i_lo;
-  uint32_t f[2 * MZ_FIFO];  // queued outputs, front first: f[2i] low, f[2i + 1] high word
-  int cnt;
-  uint32_t has32, u32;
+// ---- the precomputed stream.  Group g of a maze's stream = its outputs 32g .. 32g+31:
+//   H[g]  128 bits: output k's low half's two low bits at bits 4k, 4k+1, its high half's at 4k+2, 4k+3
+//   D[g]  32 bits:  bit k = (output k >> 11) * 2^-53 < branching_prob (numpy next_double)
+// laid out per maze as H[ng] (16 B each), D[ng], then the generator state after the ng * 32 outputs (s_hi, s_lo:
+// a maze that needs more — about 1.77 outputs per cell are drawn, ng * 32 >= 1.8 per cell + 64 — steps the LCG
+// from there in the memory phase).
+constexpr int MZ_GROUP = 32;       // outputs per stream group
+constexpr int MZ_ITEM_GROUPS = 8;  // groups per k_maze_stream item (one jump)
+constexpr int MZ_MAX_ITEMS = 63;   // items per maze (+ 1 for the end state) within one 64-entry jump table
+
+__host__ __device__ inline int maze_stream_groups(int h, int w) {
+  const int cells = ((w - 1) / 2) * ((h - 1) / 2);
+  const int outputs = (9 * cells) / 5 + 64;
+  const int per_item = MZ_GROUP * MZ_ITEM_GROUPS;
+  return (outputs + per_item - 1) / per_item * MZ_ITEM_GROUPS;
+}
+__host__ __device__ inline size_t maze_stream_state_off(int ng) { return ((size_t)ng * 20 + 15) & ~(size_t)15; }
+__host__ __device__ inline size_t maze_stream_bytes(int ng) { return maze_stream_state_off(ng) + 16; }
+
+// (A, G): the state d LCG steps on is A * s + G * inc (mod 2^128), A = MUL^d, G = 1 + MUL + ... + MUL^(d-1)
+struct MzJump {
+  U128 A, G;
+};
+APG_DEV MzJump mz_jump(uint64_t d) {
+  U128 am{0, 1}, ap{0, 0}, cm{PCG_MUL_HI, PCG_MUL_LO}, cp{0, 1};
+  while (d) {
+    if (d & 1ULL) {
+      am = mul128(am, cm);
+      ap = add128(mul128(ap, cm), cp);
+    }
+    cp = mul128(add128(cm, U128{0, 1}), cp);
+    cm = mul128(cm, cm);
+    d >>= 1;
+  }
+  return MzJump{am, ap};
+}
+APG_DEV void mz_jump_state(const MzJump &j, uint64_t &s_hi, uint64_t &s_lo, uint64_t i_hi, uint64_t i_lo) {
+  const U128 s = add128(mul128(j.A, U128{s_hi, s_lo}), mul128(j.G, U128{i_hi, i_lo}));
+  s_hi = s.hi;
+  s_lo = s.lo;
+}
+
+// numpy next64 (XSL-RR of the stepped state) and its 5 stream bits
+APG_DEV uint64_t mz_next64(uint64_t &s_hi, uint64_t &s_lo, uint64_t i_hi, uint64_t i_lo) {
+  pcg_step(s_hi, s_lo, i_hi, i_lo);
+  const uint64_t x = s_hi ^ s_lo;
+  const unsigned rot = (unsigned)(s_hi >> 58);
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+APG_DEV uint32_t mz_nibble(uint64_t o) { return (uint32_t)(o & 3u) | ((uint32_t)(o >> 30) & 0xCu); }
+APG_DEV uint32_t mz_dbit(uint64_t o, double bp) {
+  return (double)(o >> 11) * (1.0 / 9007199254740992.0) < bp ? 1u : 0u;
+}
+
+// Item c of a maze: its groups c * MZ_ITEM_GROUPS .. + MZ_ITEM_GROUPS - 1, from the seeded state (s, inc) and
+// the jump to output c * MZ_ITEM_GROUPS * MZ_GROUP.
+APG_DEV void maze_stream_item(uint64_t s_hi, uint64_t s_lo, uint64_t i_hi, uint64_t i_lo, const MzJump &j, double bp,
+                              int c, uint8_t *stream, int ng) {
+  mz_jump_state(j, s_hi, s_lo, i_hi, i_lo);
+  uint4 *H = reinterpret_cast<uint4 *>(stream) + (size_t)c * MZ_ITEM_GROUPS;
+  uint32_t *D = reinterpret_cast<uint32_t *>(stream + (size_t)ng * 16) + (size_t)c * MZ_ITEM_GROUPS;
+  for (int gi = 0; gi < MZ_ITEM_GROUPS; gi++) {
+    uint32_t hw[4] = {0u, 0u, 0u, 0u}, dw = 0u;
+#pragma unroll
+    for (int k = 0; k < MZ_GROUP; k++) {
+      const uint64_t o = mz_next64(s_hi, s_lo, i_hi, i_lo);
+      hw[k >> 3] |= mz_nibble(o) << (4 * (k & 7));
+      dw |= mz_dbit(o, bp) << k;
+    }
+    H[gi] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+    D[gi] = dw;
+  }
+}
+
+// The DFS's window: the next `avail` (<= 32) outputs of the stream, output k at bits 4k.. of h1:h0 and bit k of
+// d; numpy's buffered high half (has_uint32) and its two low bits; e = stream index after the window; the two
+// staged groups (e >> 5, +1) loaded one memory phase ahead; past the precomputed outputs, the generator.
+struct MzWin {
+  uint64_t h0, h1;
+  uint32_t d;
+  int avail, e;
+  uint32_t has32, b2;
+  uint64_t s[4];
+  uint32_t sd[2];
+  uint64_t ov_hi, ov_lo;
+  int ov;
 };
 
-APG_DEV void mz_step(MzRng &R, uint32_t &lo, uint32_t &hi) {
-  pcg_step(R.s_hi, R.s_lo, R.i_hi, R.i_lo);
-  const uint64_t x = R.s_hi ^ R.s_lo;
-  const unsigned rot = (unsigned)(R.s_hi >> 58);
-  const uint64_t o = (x >> rot) | (x << ((64u - rot) & 63u));
-  lo = (uint32_t)o;
-  hi = (uint32_t)(o >> 32);
+// h1:h0 >> 4p, d >> p (p in [0, 32])
+APG_DEV void mz_win_shift(MzWin &W, int p) {
+  const uint32_t s = 4u * (uint32_t)p, sm = s & 63u;
+  const uint64_t a = W.h0 >> sm, b = W.h1 >> sm, c = (W.h1 << 1) << (63u - sm);
+  W.h0 = s < 64u ? (a | c) : (s < 128u ? b : 0ULL);
+  W.h1 = s < 64u ? b : 0ULL;
+  W.d = p >= 32 ? 0u : W.d >> p;
+  W.avail -= p;
 }
 
-// one output into the FIFO when there is room (state advanced only then)
-APG_DEV void mz_fill(MzRng &R) {
-  const uint64_t sh = R.s_hi, sl = R.s_lo;
-  uint32_t lo, hi;
-  mz_step(R, lo, hi);
-  const bool room = R.cnt < MZ_FIFO;
-  if (!room) {
-    R.s_hi = sh;
-    R.s_lo = sl;
-  }
+// groups gq, gq + 1 of the stream into the staging registers (zeros past its end)
+APG_DEV void mz_win_stage(MzWin &W, const uint8_t *stream, int ng, int gq) {
+  const uint4 *H = reinterpret_cast<const uint4 *>(stream);
+  const uint32_t *D = reinterpret_cast<const uint32_t *>(stream + (size_t)ng * 16);
 #pragma unroll
-  for (int i = 0; i < MZ_FIFO; i++) {
-    const bool here = room && R.cnt == i;
-    R.f[2 * i] = here ? lo : R.f[2 * i];
-    R.f[2 * i + 1] = here ? hi : R.f[2 * i + 1];
+  for (int i = 0; i < 2; i++) {
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t dv = 0u;
+    if (gq + i < ng) {
+      v = H[gq + i];
+      dv = D[gq + i];
+    }
+    W.s[2 * i] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    W.s[2 * i + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    W.sd[i] = dv;
   }
-  R.cnt += room ? 1 : 0;
 }
 
-// drop the front p (0..MZ_FIFO) outputs: two conditional shifts
-APG_DEV void mz_drop(MzRng &R, int p) {
-  if (p & 2) {
-#pragma unroll
-    for (int i = 0; i < 2 * MZ_FIFO - 4; i++) R.f[i] = R.f[i + 4];
+// The window topped up to 32 outputs: the staged outputs e .. (those below the precomputed end N = 32 ng),
+// then outputs >= N from the generator (its state at N loaded on first use).
+APG_DEV void mz_win_refill(MzWin &W, const uint8_t *stream, int ng, uint64_t i_hi, uint64_t i_lo, double bp) {
+  const int need = 32 - W.avail;
+  if (need <= 0) return;
+  const int N = ng * MZ_GROUP;
+  const uint32_t off = (uint32_t)(W.e & 31), bo = 4u * off, q = bo >> 6, r = bo & 63u;
+  const uint64_t w0 = q ? W.s[1] : W.s[0], w1 = q ? W.s[2] : W.s[1], w2 = q ? W.s[3] : W.s[2];
+  uint64_t t0 = (w0 >> r) | ((w1 << 1) << (63u - r)), t1 = (w1 >> r) | ((w2 << 1) << (63u - r));
+  uint32_t td = (uint32_t)((((uint64_t)W.sd[1] << 32) | W.sd[0]) >> off);
+  int ok = N - W.e;
+  ok = ok < 0 ? 0 : (ok > need ? need : ok);
+  if (ok < 32) {  // keep the staged outputs below N only
+    const uint32_t kb = 4u * (uint32_t)ok;
+    t0 = kb >= 64u ? t0 : t0 & ((1ULL << kb) - 1ULL);
+    t1 = kb >= 64u ? t1 & ((1ULL << (kb - 64u)) - 1ULL) : 0ULL;
+    td &= (1u << ok) - 1u;
   }
-  if (p & 1) {
-#pragma unroll
-    for (int i = 0; i < 2 * MZ_FIFO - 2; i++) R.f[i] = R.f[i + 2];
+  // append at output `avail`: (t1:t0) << 4 avail, td << avail
+  const uint32_t a = 4u * (uint32_t)W.avail, am = a & 63u;
+  W.h0 |= a < 64u ? t0 << am : 0ULL;
+  W.h1 |= a < 64u ? ((t1 << am) | ((t0 >> 1) >> (63u - am))) : (a < 128u ? t0 << am : 0ULL);
+  W.d |= W.avail < 32 ? td << W.avail : 0u;
+  for (int k = ok; k < need; k++) {  // past the precomputed stream (rare)
+    if (!W.ov) {
+      const uint64_t *st = reinterpret_cast<const uint64_t *>(stream + maze_stream_state_off(ng));
+      W.ov_hi = st[0];
+      W.ov_lo = st[1];
+      W.ov = 1;
+    }
+    const uint64_t o = mz_next64(W.ov_hi, W.ov_lo, i_hi, i_lo);
+    const int pos = W.avail + k;
+    const uint64_t nib = (uint64_t)mz_nibble(o);
+    if (pos < 16) W.h0 |= nib << (4 * pos);
+    else W.h1 |= nib << (4 * (pos - 16));
+    W.d |= mz_dbit(o, bp) << pos;
   }
-  R.cnt -= p;
+  W.e += need;
+  W.avail = 32;
 }
 
-APG_DEV void mz_pop64(MzRng &R, uint32_t &lo, uint32_t &hi) {
-  if (R.cnt == 0) {  // rare: a burst of draws outran the refill
-    mz_step(R, lo, hi);
-    return;
-  }
-  lo = R.f[0];
-  hi = R.f[1];
-  mz_drop(R, 1);
-}
-
-APG_DEV uint32_t mz_next32(MzRng &R) {  // numpy next_uint32
-  if (R.has32) {
-    R.has32 = 0;
-    return R.u32;
-  }
-  uint32_t lo, hi;
-  mz_pop64(R, lo, hi);
-  R.has32 = 1;
-  R.u32 = hi;
-  return lo;
-}
-
-APG_DEV double mz_next_double(MzRng &R) {  // numpy next_double: a whole output, the half-word buffer untouched
-  uint32_t lo, hi;
-  mz_pop64(R, lo, hi);
-  return (double)((((uint64_t)hi << 32) | lo) >> 11) * (1.0 / 9007199254740992.0);
-}
-
-// rng.permutation(directions) (maze.py:33): random_interval's masked rejection on next_uint32, reference form
-APG_DEV uint32_t mz_draw_perm_loop(MzRng &R) {
-  const uint32_t j3 = mz_next32(R) & 3u;
-  uint32_t j2;
-  do {
-    j2 = mz_next32(R) & 3u;
-  } while (j2 > 2u);
-  const uint32_t j1 = mz_next32(R) & 1u;
-  return j3 * 6u + j2 * 2u + j1;
-}
-
-// The same draw read off the window of queued next_uint32 values S = [buffered half?] f0lo f0hi f1lo ...
-// without a loop: j3 = S0, j2 = the first of S1.. whose two low bits are not 3, j1 = the value after it.
-// Falls back to the loop when the window does not hold the draw (> 5 rejections, or a short FIFO).
-APG_DEV uint32_t mz_draw_perm(MzRng &R) {
-  uint32_t S[2 * MZ_FIFO + 1];
-  S[0] = R.has32 ? R.u32 : R.f[0];
-#pragma unroll
-  for (int i = 1; i < 2 * MZ_FIFO + 1; i++) S[i] = R.has32 ? R.f[i - 1] : (i < 2 * MZ_FIFO ? R.f[i] : 0u);
-  const int avail = (int)R.has32 + 2 * R.cnt;
-  uint32_t rej = 0;  // bit i - 1: S_i rejected (low bits 3), i = 1..6
-#pragma unroll
-  for (int i = 1; i <= 6; i++) rej |= ((S[i] & 3u) == 3u ? 1u : 0u) << (i - 1);
-  const int i2 = 1 + __builtin_ctz(~rej);  // position of j2
-  const int t = i2 + 2;                    // next_uint32 values consumed
-  if (i2 > 6 || t > avail) return mz_draw_perm_loop(R);
-  uint32_t s2 = S[1], s1 = S[2];
-#pragma unroll
-  for (int i = 2; i <= 6; i++) {
-    s2 = i2 == i ? S[i] : s2;
-    s1 = i2 == i ? S[i + 1] : s1;
-  }
-  const uint32_t j3 = S[0] & 3u, j2 = s2 & 3u, j1 = s1 & 1u;
-  // consume t values: the buffered half first, then outputs (an output whose high half is left over is
-  // buffered)
-  const int q = t - (int)R.has32, p = (q + 1) >> 1;
-  uint32_t hi_last = R.f[1];
-#pragma unroll
-  for (int i = 2; i <= MZ_FIFO; i++) hi_last = p == i ? R.f[2 * i - 1] : hi_last;
-  R.has32 = (uint32_t)(q & 1);
-  R.u32 = hi_last;
-  mz_drop(R, p);
-  return j3 * 6u + j2 * 2u + j1;
+// rng.permutation(directions) (maze.py:33) read off the window after `u0` outputs (the double drawn before
+// it): numpy's shuffle draws j3 = random_interval(3), j2 = random_interval(2) (rejecting 3), j1 =
+// random_interval(1), each from next_uint32 (the buffered half first) masked to 2 / 2 / 1 bits.
+struct MzPerm {
+  uint32_t pidx;
+  int p;     // outputs consumed
+  int q;     // halves taken from outputs (odd: the last output's high half is buffered)
+  bool ok;   // the window holds the draw
+};
+APG_DEV MzPerm mz_perm_draw(const MzWin &W, uint64_t hs, int u0) {
+  const uint64_t X = W.has32 ? ((hs << 2) | W.b2) : hs;  // half i (S_i) at bits 2i, 2i+1
+  const uint64_t rejected = X & (X >> 1) & 0x5555555555555554ULL;  // bit 2i: S_i == 3 (i >= 1)
+  const uint64_t kept = ~rejected & 0x5555555555555554ULL;
+  const int i2 = (int)(__builtin_ctzll(kept | (1ULL << 62)) >> 1);  // first S_i != 3 (31: none up to 30)
+  const int t = i2 + 2;                                             // halves drawn
+  const int ic = i2 > 30 ? 30 : i2;
+  MzPerm r;
+  r.pidx = ((uint32_t)X & 3u) * 6u + ((uint32_t)(X >> (2 * ic)) & 3u) * 2u + ((uint32_t)(X >> (2 * ic + 2)) & 1u);
+  r.q = t - (int)W.has32;
+  r.p = (r.q + 1) >> 1;
+  const int valid = 2 * (W.avail - u0) + (int)W.has32;  // halves of X from the window
+  r.ok = t <= (valid < 32 ? valid : 32);
+  return r;
 }
 
 struct MazeGeom {
@@ -192,14 +249,17 @@ __host__ __device__ inline MazeGeom maze_geom(int h, int w) {
 }
 
 // Global scratch per maze: the carve log (one entry per carve, padded to whole 16-byte groups at the end),
-// then the spilled frames (<= cells, whole chunks).
+// the spilled frames (<= cells, whole chunks), the precomputed stream (maze_stream_groups groups at most).
 __host__ __device__ inline size_t maze_log_bytes(int h, int w) {
   const size_t cells = (size_t)((w - 1) / 2) * ((h - 1) / 2);
   return (2 * cells + 16 + 15) & ~(size_t)15;
 }
-__host__ __device__ inline size_t maze_scratch_bytes(int h, int w) {
+__host__ __device__ inline size_t maze_stream_off(int h, int w) {
   const size_t cells = (size_t)((w - 1) / 2) * ((h - 1) / 2);
-  return (maze_log_bytes(h, w) + cells + MZ_CHUNK + 63) & ~(size_t)63;
+  return (maze_log_bytes(h, w) + cells + MZ_CHUNK + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t maze_scratch_bytes(int h, int w) {
+  return (maze_stream_off(h, w) + maze_stream_bytes(maze_stream_groups(h, w)) + 63) & ~(size_t)63;
 }
 
 // LDS of one k_maze workgroup (always laid out for 64 lanes, so every stride is a compile-time immediate):
@@ -241,22 +301,15 @@ APG_DEV uint64_t mz_load_coherent(const uint64_t *p) {
 
 // The DFS of one maze per lane.  Every lane of the wave must call it (wave-uniform memory phases); lanes
 // with active == false only take part in them.  `lds` is the workgroup's dynamic LDS (table initialized),
-// `spill` / `logg` this maze's global scratch (16-byte aligned).  ONEW: ncx <= 63 (one vis word per row,
-// the left neighbour of column 0 reads the pad bit 63).  Returns the log length in entries (a multiple of
-// 8, the tail padded).
+// `spill` / `logg` / `stream` this maze's global scratch (16-byte aligned; the stream of ng groups written by
+// k_maze_stream), r0 the maze's seeded generator (its increment steps the LCG past the stream).  ONEW: ncx
+// <= 63 (one vis word per row, the left neighbour of column 0 reads the pad bit 63).  Returns the log length
+// in entries (a multiple of 8, the tail padded); `bad` is set when a draw does not fit in a full window
+// (30 rejected halves in one permutation: never in practice) and that maze is abandoned.
 template <bool ONEW>
-APG_DEV int maze_dfs(const Pcg64 &r0, bool active, const MazeGeom &m, double bp, char *lds, int lane, uint8_t *spill,
-                     uint32_t *logg) {
-  MzRng R;
-  R.s_hi = r0.s_hi;
-  R.s_lo = r0.s_lo;
-  R.i_hi = r0.i_hi;
-  R.i_lo = r0.i_lo;
-  R.has32 = r0.has32;
-  R.u32 = r0.u32;
-  R.cnt = 0;
-#pragma unroll
-  for (int i = 0; i < 2 * MZ_FIFO; i++) R.f[i] = 0u;
+APG_DEV int maze_dfs(const Pcg64 &r0, const uint8_t *stream, int ng, bool active, const MazeGeom &m, double bp,
+                     char *lds, int lane, uint8_t *spill, uint32_t *logg, bool &bad) {
+  MzWin W{};
   const int CW = ONEW ? 1 : m.cw;
   const int RB = CW * 8 * MZ_LANES;  // bytes per vis row (all lanes)
   char *vis = lds + MZ_V + lane * 8;
@@ -287,15 +340,25 @@ APG_DEV int maze_dfs(const Pcg64 &r0, bool active, const MazeGeom &m, double bp,
     pmt = (uint64_t)t.x | ((uint64_t)t.y << 32);
     pinfo = t.z;
   };
-  if (active) {
-    pidx = mz_draw_perm_loop(R);
-    load_perm(pidx);
+  if (active) {  // the first window (a synchronous load), the groups after it staged, the first permutation
+    mz_win_stage(W, stream, ng, 0);
+    mz_win_refill(W, stream, ng, r0.i_hi, r0.i_lo, bp);
+    mz_win_stage(W, stream, ng, W.e >> 5);
+    const MzPerm pr = mz_perm_draw(W, W.h0, 0);
+    if (pr.ok) {
+      pidx = pr.pidx;
+      W.has32 = (uint32_t)(pr.q & 1);
+      W.b2 = (uint32_t)(W.h0 >> (4 * (pr.p - 1) + 2)) & 3u;
+      mz_win_shift(W, pr.p);
+      load_perm(pidx);
+    } else {
+      bad = true;
+      done = true;
+    }
   }
   for (;;) {
     for (int it = 0; it < MZ_PERIOD; it++) {
       if (done) continue;
-#pragma unroll
-      for (int q = 0; q < MZ_FILL; q++) mz_fill(R);
       // eligible directions of the current cell: in bounds (pad bits, row compares) and not visited
       const uint64_t *vr = reinterpret_cast<const uint64_t *>(vis + arow);
       uint32_t E;
@@ -317,9 +380,26 @@ APG_DEV int maze_dfs(const Pcg64 &r0, bool active, const MazeGeom &m, double bp,
       const uint32_t pm = (uint32_t)(pmt >> (4 * E)) & (0xFu << k) & 0xFu;
       const int j = __builtin_ctz(pm | 0x10u);
       const uint32_t d = (pinfo >> (2 * j)) & 3u;
-      // first eligible branch always; later ones only if rng.random() < branching_prob (maze.py:42)
-      bool carve = pm != 0u;
-      if (carve && !first) carve = mz_next_double(R) < bp;
+      // first eligible branch always; later ones only if rng.random() < branching_prob (maze.py:42): the
+      // window's next output; a carve then draws the child's permutation from the outputs after it
+      const bool dneed = pm != 0u && !first;
+      const bool carve = pm != 0u && (first || (W.d & 1u) != 0u);
+      const int u0 = dneed ? 1 : 0;
+      const uint64_t hs = dneed ? ((W.h0 >> 4) | (W.h1 << 60)) : W.h0;
+      const MzPerm pr = mz_perm_draw(W, hs, u0);
+      const int used = u0 + (carve ? pr.p : 0);
+      if (used > W.avail || (carve && !pr.ok)) {  // not in the window: wait for the next memory phase
+        if (W.avail == 32) {
+          bad = true;
+          done = true;
+        }
+        continue;
+      }
+      if (carve) {
+        W.has32 = (uint32_t)(pr.q & 1);
+        W.b2 = (uint32_t)(hs >> (4 * (pr.p - 1) + 2)) & 3u;
+      }
+      mz_win_shift(W, used);
       if (pm != 0u) k = j + 1;
       const bool back = pm == 0u && sp > lo;  // sp == lo > 0: the parent's chunk arrives at the next phase
       if (pm == 0u && sp == 0) done = true;   // carve(starting_pos) returned
@@ -340,7 +420,7 @@ APG_DEV int maze_dfs(const Pcg64 &r0, bool active, const MazeGeom &m, double bp,
           *reinterpret_cast<uint16_t *>(logb + (lg >> 1) * (4 * MZ_LANES) + (lg & 1) * 2) =
               (uint16_t)((uint32_t)cx | ((uint32_t)cy << 7) | (d << 14));
           lg++;
-          np = mz_draw_perm(R);
+          np = pr.pidx;
           nfrom = d;
         } else {
           const uint32_t fb = (uint8_t)*rb;
@@ -360,6 +440,7 @@ APG_DEV int maze_dfs(const Pcg64 &r0, bool active, const MazeGeom &m, double bp,
     // before any reload is issued below (vmcnt(0): issued MZ_PERIOD iterations ago).
     const bool more = __ballot(!done) != 0ULL;
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    if (!done) mz_win_refill(W, stream, ng, r0.i_hi, r0.i_lo, bp);  // the staged groups into the window
     const int cnt = sp - lo;
     uint32_t *ringw = reinterpret_cast<uint32_t *>(ring);
     // (a) the chunk below the ring back into it, once there is room for it and a period of pushes
@@ -414,6 +495,7 @@ APG_DEV int maze_dfs(const Pcg64 &r0, bool active, const MazeGeom &m, double bp,
       }
       pend = true;
     }
+    if (!done) mz_win_stage(W, stream, ng, W.e >> 5);  // the groups after the window, for the next phase
     if (!more) break;
   }
   return logpos;

@@ -503,12 +503,10 @@ APG_DEV ScanOut lidar_scan_general(const Rows &rows, float fpx, float fpy, float
 template <class Rows, bool kContact = false>
 APG_DEV ScanOut lidar_scan_walk(const Rows &rows, float fpx, float fpy, float fqx, float fqy,
                                 ScanContact *contact = nullptr) {
-#ifndef APG_X_NO_FAST_WALK  // tuning / test builds: general walk only
   if constexpr (!kContact) {
     ScanOut fo;
     if (lidar_scan_fast(rows, fpx, fpy, fqx, fqy, fo)) return fo;
   }
-#endif
   return lidar_scan_general<Rows, kContact>(rows, fpx, fpy, fqx, fqy, contact);
 }
 

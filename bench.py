@@ -175,13 +175,14 @@ def run_image(args, world, rank, dev):
         preds = torch.randn((ring, n_local, w["classes"]), generator=g, device=dev)
     else:
         preds = torch.rand((ring, n_local, 2), generator=g, device=dev) * 2 - 1
+    inputs = [{"action": acts[k], "prediction": preds[k]} for k in range(ring)]  # prepared up front
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     env.reset(seed=0)
     torch.cuda.synchronize(dev)
     reset_ms = (time.perf_counter() - t0) * 1e3
     for t in range(args.warmup):
-        senv.step({"action": acts[t % ring], "prediction": preds[t % ring]})
+        senv.step(inputs[t % ring])
     senv.gather_ms()
     ev = HipEvents(args.steps)
     torch.cuda.synchronize(dev)
@@ -189,12 +190,15 @@ def run_image(args, world, rank, dev):
         dist.barrier()
     t0 = time.perf_counter()
     timed = [t for t in range(args.steps) if t % args.event_every == args.event_every - 1]  # steps with hipEvents
+    stepper = senv.step if senv.gather else env.step
     for t in range(args.steps):
-        k = (args.warmup + t) % ring
         # hipEvents right around the step's kernel launches (inside env.step), on sampled steps
-        env.set_kernel_timing_events(*(ev.pair(t) if t % args.event_every == args.event_every - 1 else (None, None)))
-        env.step({"action": acts[k], "prediction": preds[k]}) if not senv.gather else \
-            senv.step({"action": acts[k], "prediction": preds[k]})
+        if t % args.event_every == args.event_every - 1:
+            env.set_kernel_timing_events(*ev.pair(t))
+            stepper(inputs[(args.warmup + t) % ring])
+            env.set_kernel_timing_events(None)
+        else:
+            stepper(inputs[(args.warmup + t) % ring])
     env.set_kernel_timing_events(None)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -410,14 +414,15 @@ def run_lidar(args, world, rank, dev):
     preds = torch.rand((ring, n_local, 2), generator=g, device=dev) * 2 - 1
     if args.array_backend == "numpy":  # the default drop-in mode: host arrays in and out of every step
         acts, preds = acts.cpu().numpy(), preds.cpu().numpy()
+    # the per-step input batches prepared up front, as a policy hands them over (no indexing in the loop)
+    inputs = [{"action": acts[k], "prediction": preds[k]} for k in range(ring)]
     steps_done = 0
 
     def step(ev=None):
         nonlocal steps_done
         if ev is not None:
             env.set_kernel_timing_events(*ev)  # (None, None): no events on this step
-        k = steps_done % ring
-        senv.step({"action": acts[k], "prediction": preds[k]})
+        senv.step(inputs[steps_done % ring])
         steps_done += 1
 
     torch.cuda.synchronize(dev)

@@ -509,11 +509,13 @@ def test_image_loc_full_size_cfg5(gpu):
 
 
 @pytest.mark.parametrize("knobs", [{"APG_GLIMPSE_PPT": "9"}, {"APG_CLS_LANES8": "1"}, {"APG_IMAGE_UNFUSED": "1"},
-                                   {"APG_GLIMPSE_PPT": "16", "APG_IMAGE_UNFUSED": "1"}])
+                                   {"APG_GLIMPSE_PPT": "16", "APG_IMAGE_UNFUSED": "1"}, {"APG_IMAGE_ENV_WAVE": "0"},
+                                   {"APG_IMAGE_ENV_WAVE": "1", "APG_GLIMPSE_PPT": "3"}])
 def test_tuning_knobs_do_not_change_results(gpu, tmp_path, knobs):
     """The library reads its tuning knobs once per process, so each setting runs in a child process
     (tests/knob_child.py) and must reproduce the default-knob child bit for bit: another glimpse
-    workgroup size, the 8-lane classification kernel for K <= 16, and the two-launch step."""
+    workgroup size, the 8-lane classification kernel for K <= 16, the two-launch step, the fused step with
+    and without its env wave."""
     import os
     import subprocess
     import sys

@@ -75,6 +75,46 @@ def test_device_maps_match_oracle_random_idx(gpu, oracle_mod, kind, size, count)
         assert np.array_equal(got[i], m.astype(bool)), (kind, size, int(idx[i]))
 
 
+@pytest.mark.parametrize("h,w,bp,count", [(21, 21, 0.5, 512), (21, 35, 0.0, 512), (63, 63, 0.3, 256),
+                                           (127, 127, 0.7, 64), (3, 3, 1.0, 16), (127, 9, 1.0, 64)])
+def test_device_maze_branching_matches_oracle(gpu, oracle_mod, h, w, bp, count):
+    """branching_prob < 1 (rng.random() draws decide later branches; mazes need not be perfect, so the
+    stream consumption differs from the bp = 1 mazes the stream length is sized for) and odd rectangles."""
+    import ap_gym_amd as ap
+
+    idx = np.random.default_rng(h * w).integers(0, 2**32, count).astype(np.uint64)
+    got = ap.FloorMapDatasetMaze(w, h, branching_prob=bp).get_data_point_batch(idx, device=gpu)
+    for i in range(count):
+        assert np.array_equal(got[i], oracle_mod.maze_map(int(idx[i]), h, w, bp).astype(bool)), (h, w, bp, int(idx[i]))
+
+
+def test_device_maze_stream_overflow_matches_oracle(gpu, oracle_mod, tmp_path):
+    """APG_MAZE_STREAM_GROUPS=8 (256 precomputed outputs per maze instead of ~7400 at 127 x 127): every maze
+    draws past its precomputed stream and the DFS steps the LCG from the stored state, in a child process
+    (the library reads the knob once)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "maps.npy"
+    code = (f"import sys, numpy as np; sys.path.insert(0, {os.path.join(root, 'active-perception-gym_amd')!r}); "
+            "import ap_gym_amd as ap; "
+            "idx = np.random.default_rng(5).integers(0, 2**32, 96).astype(np.uint64); "
+            "m = np.concatenate([ap.FloorMapDatasetMaze(s, s, branching_prob=bp).get_data_point_batch(idx[:32], "
+            "device='cuda:0').reshape(32, -1) for s, bp in ((127, 1.0), (63, 0.5), (21, 1.0))], axis=1); "
+            f"np.save({str(out)!r}, m)")
+    env = {k: v for k, v in os.environ.items() if not k.startswith("APG_")}
+    env["APG_MAZE_STREAM_GROUPS"] = "8"
+    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=300)
+    got = np.load(out)
+    idx = np.random.default_rng(5).integers(0, 2**32, 96).astype(np.uint64)
+    for i in range(32):
+        ref = np.concatenate([oracle_mod.maze_map(int(idx[i]), s, s, bp).astype(bool).reshape(-1)
+                              for s, bp in ((127, 1.0), (63, 0.5), (21, 1.0))])
+        assert np.array_equal(got[i], ref), int(idx[i])
+
+
 @pytest.mark.parametrize("size,max_rooms,door_width", [(128, 17, 3), (128, 10, 3), (96, 17, 2), (48, 6, 4)])
 def test_device_rooms_parameters_match_oracle(gpu, oracle_mod, size, max_rooms, door_width):
     import ap_gym_amd as ap

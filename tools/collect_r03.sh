@@ -24,4 +24,6 @@ python3 tools/durations_table.py $O/trace_$WL $WL $O/trace_$WL.json > profiles/r
 python3 tools/rocpd_stats.py $O/trace_$WL --csv profiles/r03/kernel_stats_$WL.csv > /dev/null
 timeout -k 10 400 python3 bench.py --workload $WL --steps 20 --warmup 5 "$@" > $O/bench_$WL.json 2> $O/bench_$WL.err
 cp $O/bench_$WL.json profiles/r03/bench_${WL}_driver_shape.json
+# profiles/ of the box's tree does not travel back: copies under gpurun_out/r03/profiles
+mkdir -p $O/profiles && cp profiles/r03/*_$WL* $O/profiles/
 tail -1 $O/bench_$WL.json | cut -c1-400

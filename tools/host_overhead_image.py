@@ -55,3 +55,17 @@ for _ in range(2):
     loop("_torch_step", lambda t: env._torch_step(False, False))
     loop("check_errors(block=False)", lambda t: env.check_errors(block=False))
 print("ok")
+
+if "--profile" in sys.argv:  # where env.step's host time goes, by function (prebuilt inputs, as bench.py)
+    import cProfile
+    import pstats
+
+    inputs = [{"action": acts[t], "prediction": preds[t]} for t in range(8)]
+    loop("env.step (prebuilt inputs)", lambda t: env.step(inputs[t % 8]))
+    pr = cProfile.Profile()
+    pr.enable()
+    for t in range(2000):
+        env.step(inputs[t % 8])
+    pr.disable()
+    torch.cuda.synchronize()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(25)

@@ -1,6 +1,7 @@
-// maze_bench.hip — tuning tool (not shipped): times the two halves of apg_maze.hpp's generator on BASELINE config 3
+// maze_bench.hip — tuning tool (not shipped): times the parts of apg_maze.hpp's generator on BASELINE config 3
 // (262144 mazes of 127 x 127) in isolation, with HIP events:
-//   k_dfs    the DFS of every maze (seeding from the index, vis / ring / log / spills), logs left in scratch
+//   k_stream the precomputed random stream of every maze (one thread per item, as k_maze_stream)
+//   k_dfs    the DFS of every maze (vis / ring / log / spills), logs left in scratch
 //   k_paint  each maze's occupancy rows painted from its log (one wave paints its 64 mazes in turn)
 // and runs each twice (the second time is reported).  For PMC passes: rocprofv3 --pmc ... -- tools/maze_bench
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I active-perception-gym_amd/csrc \
@@ -24,7 +25,18 @@ using namespace apg;
     }                                                                 \
   } while (0)
 
-__global__ __launch_bounds__(64) void k_dfs(int n, int h, int w, uint8_t *scratch, int *nlog, int lanes) {
+__global__ __launch_bounds__(256) void k_stream(int n, int h, int w, uint8_t *scratch, int ng) {
+  const int nitems = ng / MZ_ITEM_GROUPS;
+  const long q = blockIdx.x * 256L + threadIdx.x;
+  if (q >= (long)n * nitems) return;
+  const int i = (int)(q / nitems), c = (int)(q % nitems);
+  const Pcg64 r = seed_pcg64((uint64_t)i * 2654435761ULL + 12345ULL);
+  const MzJump j = mz_jump((uint64_t)c * MZ_ITEM_GROUPS * MZ_GROUP);
+  maze_stream_item(r.s_hi, r.s_lo, r.i_hi, r.i_lo, j, 1.0, c, scratch + (size_t)i * maze_scratch_bytes(h, w) +
+                   maze_stream_off(h, w), ng);
+}
+
+__global__ __launch_bounds__(64) void k_dfs(int n, int h, int w, uint8_t *scratch, int *nlog, int lanes, int ng) {
   extern __shared__ uint64_t s_mz[];
   const int lane = threadIdx.x, i = blockIdx.x * lanes + lane;
   const bool active = lane < lanes && i < n;
@@ -36,7 +48,9 @@ __global__ __launch_bounds__(64) void k_dfs(int n, int h, int w, uint8_t *scratc
   char *lds = reinterpret_cast<char *>(s_mz);
   maze_table_init(lds, lane);
   __syncthreads();
-  const int nl = maze_dfs<true>(r, active, m, 1.0, lds, lane, my + lb, reinterpret_cast<uint32_t *>(my));
+  bool bad = false;
+  const int nl = maze_dfs<true>(r, my + maze_stream_off(h, w), ng, active, m, 1.0, lds, lane, my + lb,
+                                reinterpret_cast<uint32_t *>(my), bad);
   if (active) nlog[i] = nl;
 }
 
@@ -82,10 +96,17 @@ int main(int argc, char **argv) {
   CHECK(hipEventCreate(&b));
   CHECK(hipEventCreate(&c));
   const int grid = (n + lanes - 1) / lanes;
-  float t_dfs = 0, t_paint = 0, t_obs = 0;
+  float t_dfs = 0, t_paint = 0, t_obs = 0, t_stream = 0;
+  const int ng = maze_stream_groups(size, size);
+  const long items = (long)n * (ng / MZ_ITEM_GROUPS);
   for (int rep = 0; rep < 2; rep++) {
     CHECK(hipEventRecord(a, 0));
-    hipLaunchKernelGGL(k_dfs, dim3(grid), dim3(64), lds, 0, n, size, size, scratch, nlog, lanes);
+    hipLaunchKernelGGL(k_stream, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, 0, n, size, size, scratch, ng);
+    CHECK(hipEventRecord(b, 0));
+    CHECK(hipEventSynchronize(b));
+    CHECK(hipEventElapsedTime(&t_stream, a, b));
+    CHECK(hipEventRecord(a, 0));
+    hipLaunchKernelGGL(k_dfs, dim3(grid), dim3(64), lds, 0, n, size, size, scratch, nlog, lanes, ng);
     CHECK(hipEventRecord(b, 0));
     hipLaunchKernelGGL(k_paint, dim3(grid), dim3(64), lds_p, 0, n, size, size, scratch, nlog, occ, (float *)nullptr,
                        lanes);
@@ -101,7 +122,8 @@ int main(int argc, char **argv) {
   }
   int nl0 = 0;
   CHECK(hipMemcpy(&nl0, nlog, sizeof(int), hipMemcpyDeviceToHost));
-  printf("{\"mazes\": %d, \"size\": %d, \"lanes\": %d, \"lds_per_wg\": %zu, \"dfs_ms\": %.3f, \"paint_ms\": %.3f, "
-         "\"paint_map_obs_ms\": %.3f, \"log0\": %d}\n", n, size, lanes, lds, t_dfs, t_paint, t_obs, nl0);
+  printf("{\"mazes\": %d, \"size\": %d, \"lanes\": %d, \"lds_per_wg\": %zu, \"stream_ms\": %.3f, \"dfs_ms\": %.3f, "
+         "\"paint_ms\": %.3f, \"paint_map_obs_ms\": %.3f, \"log0\": %d}\n", n, size, lanes, lds, t_stream, t_dfs,
+         t_paint, t_obs, nl0);
   return 0;
 }
