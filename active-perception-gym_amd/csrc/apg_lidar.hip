@@ -281,15 +281,13 @@ __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, ui
   if constexpr (GEN == GEN_ROOMS) copy_out_maps(s_rows, todo, words, S.occ + (size_t)blockIdx.x * lanes * words, lane);
 }
 
-// Mazes (FloorMapDatasetMaze.get_data_point, floor_map_dataset_maze.py:24-55, see apg_maze.hpp), one lane
-// per maze, `lanes` (<= 64) mazes per one-wave workgroup:
+// Mazes (FloorMapDatasetMaze.get_data_point, floor_map_dataset_maze.py:24-55, see apg_maze.hpp) in three
+// launches: k_maze_stream (the random streams), k_maze (the DFS, one lane per maze, `lanes` <= 64 mazes per
+// one-wave workgroup, carve logs into the scratch), k_maze_paint (rows, map obs, start cell, state), for
 //   MZ_MAPS   maps of dataset indices idx[0, n) into occ (static map, dataset access);
-//   MZ_RESET  reset_one for mazes: the envs of the workgroup that reset (all, or those with an autoreset
-//             pending), their streams, map index, maze into S.occ, its f32 map obs (bool map / 255,
-//             lidar_localization2d.py:299: the step kernel launched after it is given no map obs), start
-//             cell (place_start), state.
-// After the DFS of its mazes the wave paints each one's occupancy rows from its carve log in LDS, writes
-// them out coalesced (lane = row), counts free cells per row and draws the start cell like place_start.
+//   MZ_RESET  reset_one for mazes: the envs that reset (all, or those with an autoreset pending), their
+//             streams, map index, maze into S.occ, its f32 map obs (bool map / 255, lidar_localization2d.py:299:
+//             the step kernel launched after it is given no map obs), start cell (place_start), state.
 enum : int { MZ_MAPS = 0, MZ_RESET = 1 };
 
 // The dataset index of maze i (MZ_MAPS: idx[i]; MZ_RESET: the env's DatasetIterator draw, from its streams
@@ -318,10 +316,11 @@ __global__ __launch_bounds__(MZS_THREADS) void k_maze_stream(Geo g, apg_lidar_st
   __shared__ uint64_t s_seed[MZS_MAZES][4];  // s_hi, s_lo, i_hi, i_lo
   __shared__ MzJump s_jump[MZ_MAX_ITEMS + 1];
   const int tid = threadIdx.x, nitems = ng / MZ_ITEM_GROUPS;
+  const int i = blockIdx.x * MZS_MAZES + tid;
   bool act = false;
+  if (tid < MZS_MAZES && i < n) act = mode != MZ_RESET || all || (S.flags[i] & F_AUTORESET);
+  if (__syncthreads_or(act) == 0) return;  // (most steps: no autoreset pending)
   if (tid < MZS_MAZES) {
-    const int i = blockIdx.x * MZS_MAZES + tid;
-    if (i < n) act = mode != MZ_RESET || all || (S.flags[i] & F_AUTORESET);
     if (act) {
       Pcg64 rng, it;
       const Pcg64 mr = seed_pcg64(maze_index(S, idx, i, mode, seed, use_seed, rng, it));
@@ -335,12 +334,12 @@ __global__ __launch_bounds__(MZS_THREADS) void k_maze_stream(Geo g, apg_lidar_st
   } else if (tid - MZS_MAZES <= nitems) {
     s_jump[tid - MZS_MAZES] = mz_jump((uint64_t)(tid - MZS_MAZES) * MZ_ITEM_GROUPS * MZ_GROUP);
   }
-  if (__syncthreads_or(act) == 0) return;
+  __syncthreads();
   const size_t sb = maze_scratch_bytes(g.h, g.w), so = maze_stream_off(g.h, g.w);
   for (int q = tid; q < MZS_MAZES * (nitems + 1); q += MZS_THREADS) {
-    const int j = q / (nitems + 1), c = q - j * (nitems + 1), i = blockIdx.x * MZS_MAZES + j;
+    const int j = q / (nitems + 1), c = q - j * (nitems + 1);
     if (s_seed[j][3] == 0ULL) continue;
-    uint8_t *stream = scratch + (size_t)i * sb + so;
+    uint8_t *stream = scratch + (size_t)(blockIdx.x * MZS_MAZES + j) * sb + so;
     if (c < nitems) {
       maze_stream_item(s_seed[j][0], s_seed[j][1], s_seed[j][2], s_seed[j][3], s_jump[c], g.bp, c, stream, ng);
     } else {  // the state after the stream, for a maze that draws past it
@@ -354,125 +353,119 @@ __global__ __launch_bounds__(MZS_THREADS) void k_maze_stream(Geo g, apg_lidar_st
 }
 
 template <bool ONEW>
-__global__ __launch_bounds__(64) void k_maze(Geo g, apg_lidar_state S, const uint64_t *idx, int n, uint64_t *occ,
-                                             uint8_t *scratch, int mode, uint64_t seed, int use_seed, int all,
-                                             uint64_t *out_map_idx, float *map_obs, uint32_t *err, int lanes, int ng) {
-  extern __shared__ uint64_t s_mz[];  // apg_maze.hpp's workgroup layout, then (after the DFS) the paint bitmap
+__global__ __launch_bounds__(64) void k_maze(Geo g, apg_lidar_state S, const uint64_t *idx, int n, uint8_t *scratch,
+                                             int mode, uint64_t seed, int use_seed, int all, uint32_t *err, int lanes,
+                                             int ng) {
+  extern __shared__ uint64_t s_mz[];  // apg_maze.hpp's workgroup layout
   const int lane = threadIdx.x;
   const int i = blockIdx.x * lanes + lane;
   const bool mine = lane < lanes && i < n;
   const MazeGeom m = maze_geom(g.h, g.w);
-  const size_t words = (size_t)g.h * g.wpr;
   const size_t sb = maze_scratch_bytes(g.h, g.w), lb = maze_log_bytes(g.h, g.w);
-  uint8_t f = 0;
-  bool active = mine;
-  uint64_t midx = 0;
-  if (mode == MZ_RESET) {
-    f = mine ? S.flags[i] : 0;
-    active = mine && (all || (f & F_AUTORESET));
-  } else if (mine) {
-    midx = idx[i];
-  }
+  const bool active = mine && (mode != MZ_RESET || all || (S.flags[i] & F_AUTORESET));
   if (__ballot(active) == 0ULL) return;
   char *lds = reinterpret_cast<char *>(s_mz);
   maze_table_init(lds, lane);
   __syncthreads();
-  Pcg64 rng{}, it{}, mr{};
-  if (active) {
-    midx = maze_index(S, idx, i, mode, seed, use_seed, rng, it);
-    mr = seed_pcg64(midx);  // get_data_point: default_rng(idx) (its increment; the stream: k_maze_stream)
+  Pcg64 mr{};
+  if (active) {  // get_data_point: default_rng(idx) (its increment; the stream: k_maze_stream)
+    Pcg64 rng, it;
+    mr = seed_pcg64(maze_index(S, idx, i, mode, seed, use_seed, rng, it));
   }
   uint8_t *mine_scr = scratch + (size_t)(active ? i : 0) * sb;
   bool bad = false;
   const int nlog = maze_dfs<ONEW>(mr, mine_scr + maze_stream_off(g.h, g.w), ng, active, m, g.bp, lds, lane,
                                   mine_scr + lb, reinterpret_cast<uint32_t *>(mine_scr), bad);
   if (bad) atomicOr(err, APG_ERR_MAPGEN);
-  __syncthreads();  // the DFS state is dead: the LDS now holds one maze's bitmap at a time
-  uint64_t *bm = s_mz;
-  uint64_t *dst_base = mode == MZ_RESET ? S.occ : occ;
-  int sx = -1, sy = -1;
-  unsigned long long todo = __ballot(active);
-  while (todo) {
-    const int j = __ffsll((long long)todo) - 1;
-    todo &= todo - 1ULL;
-    const int e = blockIdx.x * lanes + j;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous maze's reads of the bitmap are done
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    maze_paint(m, g.wpr, reinterpret_cast<const uint32_t *>(scratch + (size_t)e * sb), __shfl(nlog, j), bm, lane);
-    uint64_t *dst = dst_base + (size_t)e * words;
-    // rows out, lane = row (passes of 64 rows); free cells per row for the start draw
-    int off = 0, nfree = 0;
-    for (int y0 = 0; y0 < g.h; y0 += 64) {
-      const int y = y0 + lane;
-      int fr = 0;
-      if (y < g.h) {
-        int oc = 0;
-        for (int k = 0; k < g.wpr; k++) {
-          const uint64_t v = bm[y * g.wpr + k];
-          dst[y * g.wpr + k] = v;
-          oc += __popcll(v);
-        }
-        fr = g.w - oc;
-      }
-      nfree += wave_sum(fr);
+  if (active) *reinterpret_cast<int *>(mine_scr + maze_stream_off(g.h, g.w) + maze_stream_state_off(ng) + 16) = nlog;
+}
+
+// After k_maze's DFS, at full occupancy: a workgroup per MP_ENVS consecutive envs lists the mazes k_maze
+// generated and, one maze at a time with all its threads, paints the occupancy rows from the carve log
+// (maze_paint), writes them out (occ, or S.occ), and for MZ_RESET writes the map obs (bool map / 255,
+// lidar_localization2d.py:299), draws the start cell like place_start (reset :304: the pick-th free cell in
+// row-major order, pick = integers(0, nfree) on the env's stream) and resets the env's state.
+constexpr int MP_THREADS = 256, MP_ENVS = 64;
+__global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_state S, const uint64_t *idx, int n,
+                                                           uint64_t *occ, const uint8_t *scratch, int mode,
+                                                           uint64_t seed, int use_seed, int all, int ng,
+                                                           uint64_t *out_map_idx, float *map_obs, uint32_t *err) {
+  __shared__ uint16_t s_list[MP_ENVS];
+  __shared__ int s_cnt, s_wsum[MP_THREADS / 64], s_hit[2];
+  extern __shared__ uint64_t s_bm[];  // one maze's rows
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e0 = blockIdx.x * MP_ENVS;
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  if (tid < MP_ENVS && e0 + tid < n && (mode != MZ_RESET || all || (S.flags[e0 + tid] & F_AUTORESET)))
+    s_list[atomicAdd(&s_cnt, 1)] = (uint16_t)tid;
+  __syncthreads();
+  const int cnt = s_cnt;
+  const MazeGeom m = maze_geom(g.h, g.w);
+  const size_t words = (size_t)g.h * g.wpr, sb = maze_scratch_bytes(g.h, g.w);
+  for (int k = 0; k < cnt; k++) {
+    const int e = e0 + s_list[k];
+    const uint8_t *scr = scratch + (size_t)e * sb;
+    const int nlog = *reinterpret_cast<const int *>(scr + maze_stream_off(g.h, g.w) + maze_stream_state_off(ng) + 16);
+    maze_paint<MP_THREADS>(m, g.wpr, reinterpret_cast<const uint32_t *>(scr), nlog, s_bm, tid);
+    uint64_t *dst = (mode == MZ_RESET ? S.occ : occ) + (size_t)e * words;
+    for (int q = tid; q < (int)words; q += MP_THREADS) dst[q] = s_bm[q];
+    if (mode != MZ_RESET) {
+      __syncthreads();  // the bitmap is read before the next maze paints it
+      continue;
     }
-    if (mode != MZ_RESET) continue;
-    if (map_obs) bitmap_map_obs(bm, g.h, g.w, g.wpr, map_obs + (size_t)e * g.h * g.w, lane);
-    // place_start (reset :304): the pick-th free cell in row-major order, pick = integers(0, nfree)
-    long long pick = -1;
-    if (lane == j && nfree > 0) pick = (long long)integers(rng, 0, nfree);
-    pick = __shfl(pick, j);
-    int hx = -1, hy = -1;
-    for (int y0 = 0; y0 < g.h; y0 += 64) {
-      const int y = y0 + lane;
-      int fr = 0;
-      if (y < g.h) {
-        int oc = 0;
-        for (int k = 0; k < g.wpr; k++) oc += __popcll(bm[y * g.wpr + k]);
-        fr = g.w - oc;
-      }
-      const int incl = wave_inclusive_scan(fr, lane) + off, excl = incl - fr;
-      if (y < g.h && pick >= excl && pick < incl) {
-        int k2 = (int)(pick - excl);
-        for (int k = 0; k < g.wpr && hx < 0; k++) {
-          const int lo = 64 * k;
-          const uint64_t valid = g.w - lo >= 64 ? ~0ULL : ((1ULL << (g.w - lo)) - 1ULL);
-          const uint64_t fm = ~bm[y * g.wpr + k] & valid;
-          const int c = __popcll(fm);
-          if (k2 < c) hx = lo + select_bit(fm, k2);
-          else k2 -= c;
-        }
-        hy = y;
-      }
-      off = __shfl(incl, 63);
+    if (map_obs) bitmap_map_obs<MP_THREADS>(s_bm, g.h, g.w, g.wpr, map_obs + (size_t)e * g.h * g.w, tid);
+    // free cells per row, their inclusive scan (rows <= 128: two waves), the row holding the pick
+    int fr = 0;
+    if (tid < g.h) {
+      int oc = 0;
+      for (int kk = 0; kk < g.wpr; kk++) oc += __popcll(s_bm[tid * g.wpr + kk]);
+      fr = g.w - oc;
     }
-    const unsigned long long hit = __ballot(hx >= 0);
-    const int src = hit ? __ffsll((long long)hit) - 1 : 0;
-    const int bx = __shfl(hx, src), by = __shfl(hy, src);
-    if (lane == j && hit) {
-      sx = bx;
-      sy = by;
+    const int incl_w = wave_inclusive_scan(fr, lane);
+    if (lane == 63) s_wsum[wave] = incl_w;
+    if (tid == 0) s_hit[0] = -1;
+    __syncthreads();
+    const int incl = incl_w + (wave == 1 ? s_wsum[0] : 0), excl = incl - fr;
+    const int nfree = s_wsum[0] + s_wsum[1];
+    Pcg64 rng, it;
+    const uint64_t midx = maze_index(S, idx, e, mode, seed, use_seed, rng, it);
+    const long long pick = nfree > 0 ? (long long)integers(rng, 0, nfree) : -1;  // every thread: same draw
+    if (tid < g.h && pick >= excl && pick < incl) {
+      int k2 = (int)(pick - excl), hx = -1;
+      for (int kk = 0; kk < g.wpr && hx < 0; kk++) {
+        const int lo = 64 * kk;
+        const uint64_t valid = g.w - lo >= 64 ? ~0ULL : ((1ULL << (g.w - lo)) - 1ULL);
+        const uint64_t fm = ~s_bm[tid * g.wpr + kk] & valid;
+        const int c = __popcll(fm);
+        if (k2 < c) hx = lo + select_bit(fm, k2);
+        else k2 -= c;
+      }
+      s_hit[0] = hx;
+      s_hit[1] = tid;
     }
+    __syncthreads();
+    if (tid == 0) {
+      const uint8_t f = S.flags[e];
+      float px = 0.5f, py = 0.5f;
+      if (s_hit[0] < 0) {
+        atomicOr(err, APG_ERR_MAPGEN);
+      } else {
+        px = __fadd_rn((float)s_hit[0], 0.5f);
+        py = __fadd_rn((float)s_hit[1], 0.5f);
+      }
+      S.pos[2 * e] = px;
+      S.pos[2 * e + 1] = py;
+      S.init_pos[2 * e] = px;
+      S.init_pos[2 * e + 1] = py;
+      S.elapsed[e] = 0;
+      S.flags[e] = (uint8_t)((f & F_AUTORESET) | F_JUST_RESET | F_FIRST);
+      *reinterpret_cast<Pcg64 *>(&S.rng[e]) = rng;
+      *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
+      S.map_idx[e] = midx;
+      if (out_map_idx) oat(out_map_idx, g.row, e, 1) = midx;
+    }
+    __syncthreads();  // s_hit / the bitmap are reused by the next maze
   }
-  if (mode != MZ_RESET || !active) return;
-  float px = 0.5f, py = 0.5f;
-  if (sx < 0) {
-    atomicOr(err, APG_ERR_MAPGEN);
-  } else {
-    px = __fadd_rn((float)sx, 0.5f);
-    py = __fadd_rn((float)sy, 0.5f);
-  }
-  S.pos[2 * i] = px;
-  S.pos[2 * i + 1] = py;
-  S.init_pos[2 * i] = px;
-  S.init_pos[2 * i + 1] = py;
-  S.elapsed[i] = 0;
-  S.flags[i] = (uint8_t)((f & F_AUTORESET) | F_JUST_RESET | F_FIRST);
-  *reinterpret_cast<Pcg64 *>(&S.rng[i]) = rng;
-  *reinterpret_cast<Pcg64 *>(&S.it_rng[i]) = it;
-  S.map_idx[i] = midx;
-  if (out_map_idx) oat(out_map_idx, g.row, i, 1) = midx;
 }
 
 struct StepParams {
@@ -1332,9 +1325,7 @@ int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, in
     forced = e ? atoi(e) : 0;
   }
   if (forced > 0 && forced <= 64) lanes = forced;
-  size_t dyn = maze_wg_lds_bytes(g.h, g.w);  // laid out for 64 lanes whatever `lanes` is
-  const size_t bitmap = (size_t)g.h * g.wpr * sizeof(uint64_t);
-  if (dyn < bitmap) dyn = bitmap;
+  const size_t dyn = maze_wg_lds_bytes(g.h, g.w);  // laid out for 64 lanes whatever `lanes` is
   const bool onew = m.ncx <= 63;
   const void *kern = onew ? (const void *)k_maze<true> : (const void *)k_maze<false>;
   if (int rc = opt_in_lds(kern, dyn)) return rc;
@@ -1352,12 +1343,15 @@ int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, in
                      seed, use_seed, all, ng);
   if (int rc = check_launch("k_maze_stream")) return rc;
   if (onew)
-    hipLaunchKernelGGL(k_maze<true>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, st, idx, n, occ, scratch, mode, seed,
-                       use_seed, all, out_map_idx, map_obs, err, lanes, ng);
+    hipLaunchKernelGGL(k_maze<true>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, st, idx, n, scratch, mode, seed,
+                       use_seed, all, err, lanes, ng);
   else
-    hipLaunchKernelGGL(k_maze<false>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, st, idx, n, occ, scratch, mode,
-                       seed, use_seed, all, out_map_idx, map_obs, err, lanes, ng);
-  return check_launch("k_maze");
+    hipLaunchKernelGGL(k_maze<false>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, st, idx, n, scratch, mode, seed,
+                       use_seed, all, err, lanes, ng);
+  if (int rc = check_launch("k_maze")) return rc;
+  hipLaunchKernelGGL(k_maze_paint, dim3(grid_for(n, MP_ENVS)), dim3(MP_THREADS), (size_t)g.h * g.wpr * sizeof(uint64_t),
+                     s, g, st, idx, n, occ, scratch, mode, seed, use_seed, all, ng, out_map_idx, map_obs, err);
+  return check_launch("k_maze_paint");
 }
 
 int launch_reset(const Geo &g, const apg_lidar_state *st, uint64_t seed, int use_seed, int all,

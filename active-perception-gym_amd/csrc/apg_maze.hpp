@@ -69,7 +69,7 @@ __host__ __device__ inline int maze_stream_groups(int h, int w) {
   return (outputs + per_item - 1) / per_item * MZ_ITEM_GROUPS;
 }
 __host__ __device__ inline size_t maze_stream_state_off(int ng) { return ((size_t)ng * 20 + 15) & ~(size_t)15; }
-__host__ __device__ inline size_t maze_stream_bytes(int ng) { return maze_stream_state_off(ng) + 16; }
+__host__ __device__ inline size_t maze_stream_bytes(int ng) { return maze_stream_state_off(ng) + 32; }  // + nlog
 
 // (A, G): the state d LCG steps on is A * s + G * inc (mod 2^128), A = MUL^d, G = 1 + MUL + ... + MUL^(d-1)
 struct MzJump {
@@ -356,85 +356,82 @@ APG_DEV int maze_dfs(const Pcg64 &r0, const uint8_t *stream, int ng, bool active
       done = true;
     }
   }
+  // nothing in flight at the loop entry: otherwise the compiler's wait for the first window sits inside the
+  // loop, where it also catches every memory phase's prefetches in the iteration after it
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   for (;;) {
     for (int it = 0; it < MZ_PERIOD; it++) {
       if (done) continue;
-      // eligible directions of the current cell: in bounds (pad bits, row compares) and not visited
+      // eligible directions of the current cell: in bounds (pad bits, row compares) and not visited.  The
+      // body is kept branch-light (selects, not nested ifs): the wave executes every path any lane takes.
       const uint64_t *vr = reinterpret_cast<const uint64_t *>(vis + arow);
       uint32_t E;
       if constexpr (ONEW) {
         // rows -1 and ncy read other LDS (the table / the ring): masked by the compares
         const uint64_t rc = ~vr[0], ru = ~vr[MZ_LANES], rd = ~vr[-MZ_LANES];
         E = (uint32_t)((rc >> ((cx + 1) & 63)) & 1ULL) | ((uint32_t)((rc >> ((cx - 1) & 63)) & 1ULL) << 1) |
-            ((uint32_t)(cy + 1 < m.ncy && ((ru >> cx) & 1ULL)) << 2) | ((uint32_t)(cy > 0 && ((rd >> cx) & 1ULL)) << 3);
+            (((uint32_t)(ru >> cx) & (uint32_t)(cy + 1 < m.ncy) & 1u) << 2) |
+            (((uint32_t)(rd >> cx) & (uint32_t)(cy > 0) & 1u) << 3);
       } else {
         const int wc = CW * MZ_LANES, kx = cx >> 6, kr = (cx + 1) >> 6, kl = (cx - 1) >> 6;
         const uint64_t ru = ~vr[(cy + 1 < m.ncy ? wc : 0) + kx * MZ_LANES], rd = ~vr[(cy > 0 ? -wc : 0) + kx * MZ_LANES];
         const uint64_t rr = ~vr[(kr < CW ? kr : kx) * MZ_LANES], rl = ~vr[(cx > 0 ? kl : kx) * MZ_LANES];
-        E = (uint32_t)(kr < CW && ((rr >> ((cx + 1) & 63)) & 1ULL)) |
-            ((uint32_t)(cx > 0 && ((rl >> ((cx - 1) & 63)) & 1ULL)) << 1) |
-            ((uint32_t)(cy + 1 < m.ncy && ((ru >> (cx & 63)) & 1ULL)) << 2) |
-            ((uint32_t)(cy > 0 && ((rd >> (cx & 63)) & 1ULL)) << 3);
+        E = ((uint32_t)(rr >> ((cx + 1) & 63)) & (uint32_t)(kr < CW) & 1u) |
+            (((uint32_t)(rl >> ((cx - 1) & 63)) & (uint32_t)(cx > 0) & 1u) << 1) |
+            (((uint32_t)(ru >> (cx & 63)) & (uint32_t)(cy + 1 < m.ncy) & 1u) << 2) |
+            (((uint32_t)(rd >> (cx & 63)) & (uint32_t)(cy > 0) & 1u) << 3);
       }
       // the eligible permutation positions >= k
       const uint32_t pm = (uint32_t)(pmt >> (4 * E)) & (0xFu << k) & 0xFu;
       const int j = __builtin_ctz(pm | 0x10u);
       const uint32_t d = (pinfo >> (2 * j)) & 3u;
       // first eligible branch always; later ones only if rng.random() < branching_prob (maze.py:42): the
-      // window's next output; a carve then draws the child's permutation from the outputs after it
+      // window's next output; a carve then draws the child's permutation from the outputs after it.  An
+      // iteration whose draws are not all in the window waits for the next memory phase (go == false).
       const bool dneed = pm != 0u && !first;
-      const bool carve = pm != 0u && (first || (W.d & 1u) != 0u);
+      const bool want = pm != 0u && (first || (W.d & 1u) != 0u);
       const int u0 = dneed ? 1 : 0;
       const uint64_t hs = dneed ? ((W.h0 >> 4) | (W.h1 << 60)) : W.h0;
       const MzPerm pr = mz_perm_draw(W, hs, u0);
-      const int used = u0 + (carve ? pr.p : 0);
-      if (used > W.avail || (carve && !pr.ok)) {  // not in the window: wait for the next memory phase
-        if (W.avail == 32) {
-          bad = true;
-          done = true;
-        }
-        continue;
+      const int need = u0 + (want ? pr.p : 0);
+      const bool go = need <= W.avail && (!want || pr.ok);
+      if (!go && W.avail == 32) {  // a permutation of > 30 rejected halves: abandoned, reported
+        bad = true;
+        done = true;
       }
+      const bool carve = want && go;
+      const bool back = go && pm == 0u && sp > lo;  // sp == lo > 0: the parent's chunk arrives at the next phase
+      done = done || (go && pm == 0u && sp == 0);   // carve(starting_pos) returned
+      W.has32 = carve ? (uint32_t)(pr.q & 1) : W.has32;
+      W.b2 = carve ? (uint32_t)(hs >> (4 * (pr.p - 1) + 2)) & 3u : W.b2;
+      mz_win_shift(W, go ? need : 0);
+      k = go && pm != 0u ? j + 1 : k;
+      // one move: into d, or back against the entry direction
+      const bool move = carve || back;
+      const uint32_t mv = carve ? d : (from ^ 1u);
+      const int dx = move ? (mv == 0u) - (mv == 1u) : 0, dy = move ? (mv == 2u) - (mv == 3u) : 0;
+      cx += dx;
+      cy += dy;
+      arow += dy * RB;
+      const int slot = carve ? sp : sp - 1;
+      char *rb = ring + ((slot >> 2) & (MZ_RING / 4 - 1)) * (4 * MZ_LANES) + (slot & 3);
       if (carve) {
-        W.has32 = (uint32_t)(pr.q & 1);
-        W.b2 = (uint32_t)(hs >> (4 * (pr.p - 1) + 2)) & 3u;
+        *rb = (char)(pidx | (from << 5));
+        __hip_atomic_fetch_or(reinterpret_cast<uint64_t *>(vis + arow + (cx >> 6) * 8 * MZ_LANES), 1ULL << (cx & 63),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        *reinterpret_cast<uint16_t *>(logb + (lg >> 1) * (4 * MZ_LANES) + (lg & 1) * 2) =
+            (uint16_t)((uint32_t)cx | ((uint32_t)cy << 7) | (d << 14));
       }
-      mz_win_shift(W, used);
-      if (pm != 0u) k = j + 1;
-      const bool back = pm == 0u && sp > lo;  // sp == lo > 0: the parent's chunk arrives at the next phase
-      if (pm == 0u && sp == 0) done = true;   // carve(starting_pos) returned
-      if (carve || back) {
-        // one move: into d, or back against the entry direction
-        const uint32_t mv = carve ? d : (from ^ 1u);
-        const int dx = (mv == 0u) - (mv == 1u), dy = (mv == 2u) - (mv == 3u);
-        cx += dx;
-        cy += dy;
-        arow += dy * RB;
-        const int slot = carve ? sp : sp - 1;
-        char *rb = ring + ((slot >> 2) & (MZ_RING / 4 - 1)) * (4 * MZ_LANES) + (slot & 3);
-        uint32_t np, nfrom;
-        if (carve) {
-          *rb = (char)(pidx | (from << 5));
-          __hip_atomic_fetch_or(reinterpret_cast<uint64_t *>(vis + arow + (cx >> 6) * 8 * MZ_LANES), 1ULL << (cx & 63),
-                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-          *reinterpret_cast<uint16_t *>(logb + (lg >> 1) * (4 * MZ_LANES) + (lg & 1) * 2) =
-              (uint16_t)((uint32_t)cx | ((uint32_t)cy << 7) | (d << 14));
-          lg++;
-          np = pr.pidx;
-          nfrom = d;
-        } else {
-          const uint32_t fb = (uint8_t)*rb;
-          np = fb & 31u;
-          nfrom = fb >> 5;
-        }
-        sp += carve ? 1 : -1;
-        const uint32_t child = from;
-        pidx = np;
-        from = nfrom;
-        first = carve;
-        load_perm(np);
-        k = carve ? 0 : (int)((pinfo >> (8 + 2 * child)) & 3u) + 1;  // the child's position + 1
-      }
+      uint32_t fb = 0u;
+      if (back) fb = (uint8_t)*rb;
+      lg += carve ? 1 : 0;
+      sp += carve ? 1 : (back ? -1 : 0);
+      const uint32_t child = from;
+      pidx = carve ? pr.pidx : (back ? fb & 31u : pidx);
+      from = carve ? d : (back ? fb >> 5 : from);
+      first = move ? carve : first;
+      load_perm(pidx);  // (the same entry again when nothing moved)
+      k = carve ? 0 : (back ? (int)((pinfo >> (8 + 2 * child)) & 3u) + 1 : k);
     }
     // ---- memory phase (wave-uniform).  Everything this lane stored in the previous phase is complete
     // before any reload is issued below (vmcnt(0): issued MZ_PERIOD iterations ago).
@@ -501,23 +498,33 @@ APG_DEV int maze_dfs(const Pcg64 &r0, const uint8_t *stream, int ng, bool active
   return logpos;
 }
 
-// Paint maze j's occupancy rows from its log into the wave's LDS bitmap bm[h][wpr] (all walls, then the
-// start cell (1, 1), every carved cell and the passage it was entered through), wave-cooperatively.
+// Paint a maze's occupancy rows from its log into the LDS bitmap bm[h][wpr] (all walls, then the start cell
+// (1, 1), every carved cell and the passage it was entered through) by NT cooperating threads t: one wave
+// (NT = 64, wave fences) or a workgroup (__syncthreads).
+template <int NT = 64>
 APG_DEV void maze_paint(const MazeGeom &m, int wpr, const uint32_t *logg, int nlog, uint64_t *bm, int lane) {
-  for (int i = lane; i < m.h * wpr; i += 64) {
+  auto sync = [] {
+    if constexpr (NT == 64) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+      __syncthreads();
+    }
+  };
+  for (int i = lane; i < m.h * wpr; i += NT) {
     const int y = i / wpr, kk = i - y * wpr, lo = 64 * kk;
     uint64_t v = 0;
     if (m.w > lo) v = (m.w - lo >= 64) ? ~0ULL : ((1ULL << (m.w - lo)) - 1ULL);
     if (y == 1 && kk == 0) v &= ~2ULL;  // maze[1, 1] = 0 (maze.py:51)
     bm[i] = v;
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  sync();
   const int nq = (nlog + 7) >> 3;  // 16-byte rows of 8 entries
   const uint4 *src = reinterpret_cast<const uint4 *>(logg);
+  constexpr auto scope = NT == 64 ? __HIP_MEMORY_SCOPE_WAVEFRONT : __HIP_MEMORY_SCOPE_WORKGROUP;
 #pragma unroll 4
-  for (int q = lane; q < nq; q += 64) {  // unrolled: four rows' loads in flight before their atomics
+  for (int q = lane; q < nq; q += NT) {  // unrolled: four rows' loads in flight before their atomics
     const uint4 v = src[q];
     const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -530,28 +537,25 @@ APG_DEV void maze_paint(const MazeGeom &m, int wpr, const uint32_t *logg, int nl
       if (py == y) {  // same row: one or two words
         const int k0 = x >> 6, k1 = px >> 6;
         if (k0 == k1) {
-          __hip_atomic_fetch_and(&bm[y * wpr + k0], ~((1ULL << (x & 63)) | (1ULL << (px & 63))), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WAVEFRONT);
+          __hip_atomic_fetch_and(&bm[y * wpr + k0], ~((1ULL << (x & 63)) | (1ULL << (px & 63))), __ATOMIC_RELAXED, scope);
         } else {
-          __hip_atomic_fetch_and(&bm[y * wpr + k0], ~(1ULL << (x & 63)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-          __hip_atomic_fetch_and(&bm[y * wpr + k1], ~(1ULL << (px & 63)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+          __hip_atomic_fetch_and(&bm[y * wpr + k0], ~(1ULL << (x & 63)), __ATOMIC_RELAXED, scope);
+          __hip_atomic_fetch_and(&bm[y * wpr + k1], ~(1ULL << (px & 63)), __ATOMIC_RELAXED, scope);
         }
       } else {
-        __hip_atomic_fetch_and(&bm[y * wpr + (x >> 6)], ~(1ULL << (x & 63)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        __hip_atomic_fetch_and(&bm[py * wpr + (px >> 6)], ~(1ULL << (px & 63)), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_and(&bm[y * wpr + (x >> 6)], ~(1ULL << (x & 63)), __ATOMIC_RELAXED, scope);
+        __hip_atomic_fetch_and(&bm[py * wpr + (px >> 6)], ~(1ULL << (px & 63)), __ATOMIC_RELAXED, scope);
       }
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  sync();
 }
 
 // The f32 map observation of a painted bitmap (bool map / 255, lidar_localization2d.py:299) into dst[h * w],
-// wave-cooperatively: 16-byte non-temporal stores over the 16-byte-aligned body of the map's floats (a
-// wave-store of dwords per row left the kernel store-issue bound), scalar stores for the unaligned head and
-// tail.  Cell c = y * w + x of float4 q is found once per store and then stepped (row wrap).
+// by NT cooperating threads (t = 0 .. NT - 1, NT >= 8): 16-byte non-temporal stores over the 16-byte-aligned
+// body of the map's floats (a wave-store of dwords per row left the kernel store-issue bound), scalar stores
+// for the unaligned head and tail.  Cell c = y * w + x of float4 q is found once per store and then stepped.
+template <int NT = 64>
 APG_DEV void bitmap_map_obs(const uint64_t *bm, int h, int w, int wpr, float *dst, int lane) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   const float wall = 1.0f / 255.0f;
@@ -566,7 +570,7 @@ APG_DEV void bitmap_map_obs(const uint64_t *bm, int h, int w, int wpr, float *ds
     x = c - y * w;
   };
   auto bit = [&](int y, int x) { return (uint32_t)(bm[y * wpr + (x >> 6)] >> (x & 63)) & 1u; };
-  for (int q = lane; q < nbody; q += 64) {
+  for (int q = lane; q < nbody; q += NT) {
     int y, x;
     cell_of(head + 4 * q, y, x);
     f4 v;
