@@ -54,6 +54,7 @@ namespace {
 
 constexpr uint8_t F_AUTORESET = 1, F_JUST_RESET = 2, F_FIRST = 4;
 constexpr int MAX_WIN_ROWS = 32;
+constexpr int MAX_WIN_RANGE = 10;  // scan lengths the staged window covers (k_lidar_step); longer: RowsGlobal
 constexpr int WIN_STRIDE = MAX_WIN_ROWS + 1;  // LDS words per env window (+1: lanes = envs hit distinct banks)
 constexpr int MAX_STAGED_BEAMS = 64;          // lidar rows staged in LDS for coalesced stores
 // SCAN_EMPTY beam values by the bit pattern of |q - p|^2 (f32) around range^2: a beam of length range
@@ -119,10 +120,10 @@ int validate(const apg_lidar_config *c) {
     return fail(APG_E_INVALID, "unknown map kind");
   }
   if (c->beams <= 0 || c->beams > 4096) return fail(APG_E_INVALID, "beams must be in [1, 4096]");
-  if (!(c->lidar_range > 0.0f) || c->lidar_range > 10.0f)
-    return fail(APG_E_INVALID, "lidar_range must be in (0, 10] (occupancy window of the fused step kernel)");
+  if (!(c->lidar_range > 0.0f) || c->lidar_range > 28.0f)
+    return fail(APG_E_INVALID, "lidar_range must be in (0, 28] (32-column scan windows)");
   if (c->step_limit <= 0) return fail(APG_E_INVALID, "step_limit must be positive");
-  if (c->log_stats && c->step_limit > PW_PTR_MAX_N) return fail(APG_E_INVALID, "log_stats needs step_limit <= 968");
+  if (c->log_stats && c->step_limit > PW_DEEP_MAX_N) return fail(APG_E_INVALID, "log_stats needs step_limit <= 15368");
   if (c->out_row_bytes < 0 || (c->out_row_bytes & 7)) return fail(APG_E_INVALID, "out_row_bytes must be a multiple of 8");
   return APG_OK;
 }
@@ -478,10 +479,14 @@ struct StepParams {
 // pairwise float32 mean) and final = the last value.  The history is step-major,
 // stats_hist[metric][step][env] (metric 0 euclidean distance, 1 mse), so the per-step stores of a
 // wave are coalesced; the episode-end sums read an env's column with stride N.
+// DEEP: episodes longer than PW_PTR_MAX_N steps (k_episode_stats, after the step kernel, which left their
+// stats_len set and the sums to it).
+template <bool DEEP = false>
 APG_DEV void log_episode_stats(const StepParams &P, const apg_lidar_outputs &O, int e, const float *hist, int len) {
   for (int m = 0; m < 2; m++) {
     const float *h = hist + (size_t)m * P.step_limit * P.n + e;
-    const float avg = f32_div(__fadd_rn(0.0f, pw_sum_ptr(h, len, (size_t)P.n)), (float)len);
+    const float sum = DEEP ? pw_sum_ptr_deep(h, len, (size_t)P.n) : pw_sum_ptr(h, len, (size_t)P.n);
+    const float avg = f32_div(__fadd_rn(0.0f, sum), (float)len);
     const float fin = h[(size_t)(len - 1) * P.n];
     if (P.row) {
       oat(O.stats, P.row, e, 4, m) = avg;
@@ -573,7 +578,10 @@ struct RoomsLds {
 // GEN / FUSED: FUSED instances start with phase R, the NEXT_STEP autoresets of the envs whose episode
 // ended at the previous step (map generation of kind GEN, start cell), so a step is one launch; the
 // unfused instance (reset(seed)'s observation pass after k_lidar_reset) skips it.
-template <int GEN, bool FUSED, int EPB>
+// GR: every scan reads the occupancy rows from global memory through its own 32-column window (RowsGlobal at
+// floor(min(p.x, q.x)) - 1: scans up to 28 cells long) instead of the staged 32 x 32 window around the env,
+// for lidar_range > 10 (the staged window covers R <= 10).
+template <int GEN, bool FUSED, int EPB, bool GR = false>
 __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(StepParams P, Geo g, apg_lidar_state S,
                                                                  const float *__restrict__ act,
                                                                  const float *__restrict__ pred,
@@ -600,6 +608,14 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   float *s_tab = reinterpret_cast<float *>(s_queue + EPB * P.beams);  // EMPTY_TAB entries (staged instances)
   // first table entry's bit pattern (recomputed where used: nothing stays live across the phases)
   auto tab_base = [&]() { return __float_as_uint(__fmul_rn(P.range, P.range)) - (uint32_t)(EMPTY_TAB / 2); };
+  // the occupancy rows a scan of env slot el from x = ax to x = bx reads
+  auto rows_of = [&](int el, float ax, float bx) {
+    if constexpr (GR)
+      return RowsGlobal{S.occ + (P.is_static ? 0 : (size_t)(blockIdx.x * EPB + el) * (size_t)P.h * P.wpr), P.h, P.wpr,
+                        (int)floorf(fminf(ax, bx)) - 1};
+    else
+      return RowsWindow{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
+  };
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int base = blockIdx.x * EPB;
   const size_t words = (size_t)P.h * P.wpr;
@@ -660,7 +676,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       }
     }
   };
-  load_windows();
+  if constexpr (!GR) load_windows();
   const bool dir_thread = P.beams <= MAX_STAGED_BEAMS && tid < 2 * P.beams;
   const float dir_v = dir_thread ? S.beam_dirs[tid] : 0.0f;
   if constexpr (!FUSED) __syncthreads();
@@ -806,7 +822,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         pf_iy = S.init_pos[2 * oe + 1];
         pf_el = S.elapsed[oe];
       }
-      load_windows();  // the reset envs' new maps and positions
+      if constexpr (!GR) load_windows();  // the reset envs' new maps and positions
     }
   }
 
@@ -890,7 +906,6 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       if (isnan(prx) || isnan(pry)) errbits |= APG_ERR_NAN_PREDICTION;
       if (!errbits) {  // else the reference raises ValueError before touching this env's state
         moved = true;
-        const RowsWindow rw{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
         br = __fsub_rn(0.1f, __fmul_rn(0.001f, __fadd_rn(__fmul_rn(ax, ax), __fmul_rn(ay, ay))));
         const float mag = norm_f32(ax, ay);
         if (mag > 1.0f) {
@@ -903,7 +918,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         if (total > 0.0f) {
           dirx = f32_div(dirx, total);
           diry = f32_div(diry, total);
-          const float d = lidar_scan(rw, pos0, pos1, tx, ty).dist;
+          const float d = lidar_scan(rows_of(el, pos0, tx), pos0, pos1, tx, ty).dist;
           pos0 = __fadd_rn(pos0, __fmul_rn(dirx, d));
           pos1 = __fadd_rn(pos1, __fmul_rn(diry, d));
           const float rem = __fsub_rn(total, d);
@@ -932,22 +947,21 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
     const int j = tid - EPB;
     const float cy = s_slide[j];
     if (cy > 0.0f) {
-      const RowsWindow rwj{&s_win[j * WIN_STRIDE], s_x0[j], s_y0[j], P.wrows};
       const float q0 = s_pos[j][0], q1 = s_pos[j][1];
-      s_slide[j] = lidar_scan(rwj, q0, q1, __fadd_rn(q0, 0.0f), __fadd_rn(q1, cy)).dist;
+      s_slide[j] = lidar_scan(rows_of(j, q0, q0), q0, q1, __fadd_rn(q0, 0.0f), __fadd_rn(q1, cy)).dist;
     }
   }
   if (slide) {
-    const RowsWindow rw{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
-    d0 = lidar_scan(rw, pos0, pos1, __fadd_rn(pos0, c0x), __fadd_rn(pos1, 0.0f)).dist;
+    const float bx = __fadd_rn(pos0, c0x);
+    d0 = lidar_scan(rows_of(el, pos0, bx), pos0, pos1, bx, __fadd_rn(pos1, 0.0f)).dist;
   }
   __syncthreads();
   if (slide) d1 = s_slide[tid];
 #else
   if (slide) {
-    const RowsWindow rw{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
-    d0 = lidar_scan(rw, pos0, pos1, __fadd_rn(pos0, c0x), __fadd_rn(pos1, 0.0f)).dist;
-    d1 = lidar_scan(rw, pos0, pos1, __fadd_rn(pos0, 0.0f), __fadd_rn(pos1, c1y)).dist;
+    const float bx = __fadd_rn(pos0, c0x);
+    d0 = lidar_scan(rows_of(el, pos0, bx), pos0, pos1, bx, __fadd_rn(pos1, 0.0f)).dist;
+    d1 = lidar_scan(rows_of(el, pos0, pos0), pos0, pos1, __fadd_rn(pos0, 0.0f), __fadd_rn(pos1, c1y)).dist;
   }
 #endif
   if (tid < EPB) {
@@ -1005,8 +1019,8 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           float *hist = S.stats_hist;
           hist[(size_t)(el2 - 1) * P.n + e] = norm_f32(ex, ey);  // |target - prediction|: the signs do not matter
           hist[(size_t)(P.step_limit + el2 - 1) * P.n + e] = mse;
-          if (term) log_episode_stats(P, O, e, hist, el2);
-          else oat(O.stats_len, P.row, e, 1) = 0;
+          if (term && el2 <= PW_PTR_MAX_N) log_episode_stats(P, O, e, hist, el2);
+          else oat(O.stats_len, P.row, e, 1) = term ? el2 : 0;  // > PW_PTR_MAX_N steps: k_episode_stats
         }
         oat(O.base_reward, P.row, e, 1) = br;
         oat(O.target, P.row, e, 2, 0) = tgx;
@@ -1051,14 +1065,13 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   // beams walks in place and stores straight to HBM.
   const int el = tid & (EPB - 1), e = base + el;
   const float px = s_pos[el][0], py = s_pos[el][1];
-  const RowsWindow rw{&s_win[el * WIN_STRIDE], s_x0[el], s_y0[el], P.wrows};
   const double inv_range = 1.0 / (double)P.range;
   auto beam_value = [&](float d) { return fminf(fmaxf(f32_div_inv(d, inv_range), -1.0f), 1.0f); };
   if (P.beams > MAX_STAGED_BEAMS) {
     for (int beam = tid / EPB; beam < P.beams; beam += T / EPB) {
       if (e < P.n) {
         const float qx = __fadd_rn(px, S.beam_dirs[2 * beam]), qy = __fadd_rn(py, S.beam_dirs[2 * beam + 1]);
-        oat(O.lidar, P.row, e, P.beams, beam) = beam_value(lidar_scan(rw, px, py, qx, qy).dist);
+        oat(O.lidar, P.row, e, P.beams, beam) = beam_value(lidar_scan(rows_of(el, px, qx), px, py, qx, qy).dist);
       }
     }
     return;
@@ -1071,7 +1084,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       // the box spans <= floor(|qy - py|) + 2 <= floor(|dy| + 1e-4) + 2 rows (positions < 1024): a bound
       // uniform per wave
       const int hmax = __builtin_amdgcn_readfirstlane((int)floorf(fabsf(dy) + 1e-4f) + 2);
-      walk = scan_may_hit(rw, px, py, qx, qy, hmax);
+      walk = scan_may_hit(rows_of(el, px, qx), px, py, qx, qy, hmax);
       if (!walk) {  // SCAN_EMPTY: |q - p| (f32 norm), its value from the table
         const float ex = __fsub_rn(qx, px), ey = __fsub_rn(qy, py);
         const float s2 = __fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey));
@@ -1100,9 +1113,8 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
     if (i < nq) {
       const int ent = s_queue[i], qe = ent & 255, beam = ent >> 8;
       const float qpx = s_pos[qe][0], qpy = s_pos[qe][1];
-      const RowsWindow qrw{&s_win[qe * WIN_STRIDE], s_x0[qe], s_y0[qe], P.wrows};
       const float qx = __fadd_rn(qpx, s_dirs[beam][0]), qy = __fadd_rn(qpy, s_dirs[beam][1]);
-      s_lid[qe * LS + beam] = beam_value(lidar_scan_walk(qrw, qpx, qpy, qx, qy).dist);
+      s_lid[qe * LS + beam] = beam_value(lidar_scan_walk(rows_of(qe, qpx, qx), qpx, qpy, qx, qy).dist);
     }
   }
   __syncthreads();
@@ -1417,12 +1429,12 @@ int step_epb(int n) {
   return (int64_t)n >= (int64_t)256 * cu_count() ? 256 : 64;
 }
 
-template <int GEN, bool FUSED, int EPB>
+template <int GEN, bool FUSED, int EPB, bool GR = false>
 int launch_step_t(const StepParams &P, const Geo &g, const apg_lidar_state *st, const float *act, const float *pred,
                   const apg_lidar_outputs *out, hipStream_t s, const BinomTable &bt) {
   size_t lds = step_lds_bytes(EPB, P.beams);
   if (FUSED && GEN == GEN_ROOMS && RoomsLds<EPB>::bytes > lds) lds = RoomsLds<EPB>::bytes;
-  auto kern = k_lidar_step<GEN, FUSED, EPB>;
+  auto kern = k_lidar_step<GEN, FUSED, EPB, GR>;
   if (int rc = opt_in_lds((const void *)kern, lds)) return rc;
   hipLaunchKernelGGL(kern, dim3(grid_for(P.n, EPB)), dim3(4 * EPB), lds, s, P, g, *st, act, pred, *out, bt);
   return check_launch("k_lidar_step");
@@ -1432,11 +1444,27 @@ template <int EPB>
 int launch_step_epb(const StepParams &P, const Geo &g, const apg_lidar_state *st, const float *act, const float *pred,
                     const apg_lidar_outputs *out, hipStream_t s, bool fused) {
   const BinomTable bt = make_binom_table();
+  if (P.R > MAX_WIN_RANGE) {  // scans longer than the staged window covers: rows from global memory (EPB 64)
+    if (!fused) return launch_step_t<GEN_NONE, false, 64, true>(P, g, st, act, pred, out, s, bt);
+    switch (step_gen(g)) {
+      case GEN_ROOMS: return launch_step_t<GEN_ROOMS, true, 64, true>(P, g, st, act, pred, out, s, bt);
+      default: return launch_step_t<GEN_NONE, true, 64, true>(P, g, st, act, pred, out, s, bt);
+    }
+  }
   if (!fused) return launch_step_t<GEN_NONE, false, EPB>(P, g, st, act, pred, out, s, bt);
   switch (step_gen(g)) {
     case GEN_ROOMS: return launch_step_t<GEN_ROOMS, true, EPB>(P, g, st, act, pred, out, s, bt);
     default: return launch_step_t<GEN_NONE, true, EPB>(P, g, st, act, pred, out, s, bt);
   }
+}
+
+// ActiveRegressionLogWrapper's episode-end stats of the episodes longer than PW_PTR_MAX_N steps that ended
+// this step (the step kernel wrote their stats_len): one thread per env, after the step kernel.
+__global__ __launch_bounds__(256) void k_episode_stats(StepParams P, const float *hist, apg_lidar_outputs O) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= P.n) return;
+  const int len = oat(O.stats_len, P.row, e, 1);
+  if (len > PW_PTR_MAX_N) log_episode_stats<true>(P, O, e, hist, len);
 }
 
 int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *act,
@@ -1458,11 +1486,15 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   P.loss_scale = cfg->loss_scale;
   P.loss_offset = cfg->loss_offset;
   const Geo g = make_geo(cfg);
+  int rc;
   switch (step_epb(P.n)) {
-    case 256: return launch_step_epb<256>(P, g, st, act, pred, out, s, fused);
-    case 128: return launch_step_epb<128>(P, g, st, act, pred, out, s, fused);
-    default: return launch_step_epb<64>(P, g, st, act, pred, out, s, fused);
+    case 256: rc = launch_step_epb<256>(P, g, st, act, pred, out, s, fused); break;
+    case 128: rc = launch_step_epb<128>(P, g, st, act, pred, out, s, fused); break;
+    default: rc = launch_step_epb<64>(P, g, st, act, pred, out, s, fused); break;
   }
+  if (rc || !P.log_stats || P.step_limit <= PW_PTR_MAX_N) return rc;
+  hipLaunchKernelGGL(k_episode_stats, dim3(grid_for(P.n, 256)), dim3(256), 0, s, P, st->stats_hist, *out);
+  return check_launch("k_episode_stats");
 }
 
 }  // namespace

@@ -93,5 +93,8 @@ APG_DEV float pw_sum_ptr_d(const float *x, int n, size_t st) {
 // Call-free pairwise sum of n <= PW_PTR_MAX_N values (three split levels, eight inline leaves).
 constexpr int PW_PTR_MAX_N = 968;  // three split levels leave every leaf <= 128 up to here
 APG_DEV float pw_sum_ptr(const float *x, int n, size_t st = 1) { return pw_sum_ptr_d<3>(x, n, st); }
+// The same for n <= PW_DEEP_MAX_N (seven levels, 128 inline leaves: for the kernels of long episodes only)
+constexpr int PW_DEEP_MAX_N = 15368;
+APG_DEV float pw_sum_ptr_deep(const float *x, int n, size_t st = 1) { return pw_sum_ptr_d<7>(x, n, st); }
 
 }  // namespace apg

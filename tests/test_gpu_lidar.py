@@ -353,6 +353,75 @@ def test_vector_env_matches_oracle(gpu, oracle_mod, kind, size, beams, n, steps,
     env.close()
 
 
+@pytest.mark.parametrize("kind,size,static,beams,lidar_range,n", [("rooms", 64, False, 16, 12.0, 512),
+                                                                   ("maze", 63, False, 32, 20.0, 256),
+                                                                   ("rooms", 32, True, 8, 10.5, 256),
+                                                                   ("rooms", 64, False, 8, 28.0, 128)])
+def test_long_range_matches_oracle(gpu, oracle_mod, kind, size, static, beams, lidar_range, n):
+    """lidar_range > 10 (the step kernel's rows-from-global-memory instance): observations, rewards and
+    terminations of 110 steps (one autoreset) against the oracle env."""
+    import ap_gym_amd as ap
+
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_ds(ap, kind, size), lidar_beam_count=beams,
+                                          lidar_range=lidar_range, static_map=static, device=gpu)
+    ref = oracle_mod.OracleLidarVectorEnv(n, kind, size, static, 0, beams, lidar_range=lidar_range)
+    obs, _ = env.reset(seed=11)
+    ref.reset(11)
+    assert np.array_equal(obs["lidar"], ref.lidar)
+    rng = np.random.default_rng(4)
+    for t in range(110):
+        a = rng.uniform(-1.5, 1.5, (n, 2)).astype(np.float32)
+        p = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        ref.step(a, p)
+        assert np.array_equal(obs["lidar"], ref.lidar), t
+        assert np.array_equal(obs["odometry"], ref.odometry), t
+        assert np.array_equal(rew, ref.reward, equal_nan=True), t
+        assert np.array_equal(term, ref.terminated.astype(bool)), t
+        if not static:
+            assert np.array_equal(obs["map"][..., 0], ref.map), t
+    env.close()
+
+
+@pytest.mark.parametrize("step_limit,n,steps", [(1200, 64, 1210), (969, 32, 975)])
+def test_long_episode_stats_match_oracle(gpu, oracle_mod, step_limit, n, steps):
+    """log_stats past 968 steps (the episode-end pairwise sums of k_episode_stats, seven split levels):
+    the ActiveRegressionLogWrapper scalars of every episode end against numpy's means of the restated
+    per-step metrics, the observations against the oracle env."""
+    import ap_gym_amd as ap
+
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_ds(ap, "rooms", 32), lidar_beam_count=8, device=gpu,
+                                          log_stats=True, max_episode_steps=step_limit)
+    ref = oracle_mod.OracleLidarVectorEnv(n, "rooms", 32, False, 0, 8, step_limit=step_limit)
+    env.reset(seed=7)
+    ref.reset(7)
+    rng = np.random.default_rng(3)
+    hist = [[] for _ in range(n)]
+    ends = 0
+    for t in range(steps):
+        a = rng.uniform(-1.5, 1.5, (n, 2)).astype(np.float32)
+        p = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        ref.step(a, p)
+        for i in np.nonzero(ref.info_mask)[0]:
+            d = ref.target[i] - p[i]
+            hist[i].append((np.linalg.norm(d), np.mean(d ** 2)))
+        done = (ref.terminated | ref.truncated).astype(bool)
+        assert np.array_equal(info.get("_stats", np.zeros(n, bool)), done), t
+        for i in np.nonzero(done)[0]:
+            ed = np.array([h[0] for h in hist[i]], np.float32)
+            ms = np.array([h[1] for h in hist[i]], np.float32)
+            sc = info["stats"]["scalar"]
+            assert sc["avg_euclidean_distance"][i] == float(np.mean(ed)) and sc["final_mse"][i] == float(ms[-1])
+            assert sc["avg_mse"][i] == float(np.mean(ms)) and sc["final_euclidean_distance"][i] == float(ed[-1])
+            hist[i] = []
+            ends += 1
+        assert np.array_equal(obs["lidar"], ref.lidar), t
+        assert np.array_equal(rew, ref.reward, equal_nan=True), t
+    assert ends >= n  # every env ended at least one long episode
+    env.close()
+
+
 @pytest.mark.parametrize("env_id", ["LIDARLocRooms-v0", "LIDARLocRooms-sparse-v0"])
 def test_torch_backend_matches_numpy_backend(gpu, env_id):
     import torch
