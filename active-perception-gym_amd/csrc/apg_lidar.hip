@@ -65,7 +65,7 @@ BinomTable make_binom_table() {
   BinomTable t;
   t.p = 0.3;
   t.q = 1.0 - t.p;
-  for (int n = 0; n < 16; n++) {
+  for (int n = 0; n < ROOMS_MAX; n++) {
     // random_binomial_inversion's cached constants, evaluated with the host libm like numpy
     double np_ = n * t.p;
     t.qn[n] = std::exp(n * std::log(t.q));
@@ -107,15 +107,16 @@ Geo make_geo(const apg_lidar_config *c) {
 int validate(const apg_lidar_config *c) {
   if (!c) return fail(APG_E_INVALID, "null config");
   if (c->num_envs <= 0) return fail(APG_E_INVALID, "num_envs must be positive");
-  if (c->height < 3 || c->width < 3 || c->height > 128 || c->width > 128)
-    return fail(APG_E_INVALID, "map size must be within [3, 128]");
+  if (c->height < 3 || c->width < 3 || c->height > 255 || c->width > 255)
+    return fail(APG_E_INVALID, "map size must be within [3, 255]");
   if (c->map_kind == APG_MAP_ROOMS) {
     if (c->height != c->width) return fail(APG_E_INVALID, "rooms maps must be square");
-    if (c->max_rooms < 1 || c->max_rooms > 17) return fail(APG_E_INVALID, "max_rooms must be in [1, 17]");
+    if (c->max_rooms < 1 || c->max_rooms > ROOMS_MAX) return fail(APG_E_INVALID, "max_rooms must be in [1, 32]");
     if (c->door_width < 1) return fail(APG_E_INVALID, "door_width must be positive");
   } else if (c->map_kind == APG_MAP_MAZE) {
     if ((c->height % 2) == 0 || (c->width % 2) == 0)
       return fail(APG_E_INVALID, "Width and height must be odd.");
+    if (c->height > 127 || c->width > 127) return fail(APG_E_INVALID, "maze maps must be at most 127 x 127");
   } else {
     return fail(APG_E_INVALID, "unknown map kind");
   }
@@ -172,6 +173,7 @@ APG_DEV void copy_out_maps(const uint64_t *s_maps, unsigned long long done, size
   }
 }
 
+template <int MR>
 __global__ __launch_bounds__(64) void k_map_generate_rooms(Geo g, const uint64_t *idx, int n, uint64_t *occ,
                                                            uint32_t *err, BinomTable bt, int lanes) {
   extern __shared__ uint64_t s_rows[];  // [lanes][h * wpr]
@@ -182,7 +184,7 @@ __global__ __launch_bounds__(64) void k_map_generate_rooms(Geo g, const uint64_t
   int rc = 0;
   if (active) {
     Pcg64 r = seed_pcg64(idx[i]);
-    rc = rooms_generate(r, s_rows + lane * words, g.wpr, g.h, g.max_rooms, g.door_width, bt);
+    rc = rooms_generate<MR>(r, s_rows + lane * words, g.wpr, g.h, g.max_rooms, g.door_width, bt);
   }
   copy_out_maps(s_rows, __ballot(active), words, occ + (size_t)blockIdx.x * lanes * words, lane);
   if (rc != 0 && err) atomicOr(err, APG_ERR_MAPGEN);
@@ -222,7 +224,7 @@ APG_DEV int select_bit(uint64_t m, int k) {
 // reseed (use_seed) or continue the env's streams, next map index from the DatasetIterator stream,
 // rooms map generation into `own` (the caller's LDS bitmap), start cell draw.  Mazes: k_maze.
 // Returns the env's new flags.
-template <int GEN>
+template <int GEN, int MR = 17>
 APG_DEV uint8_t reset_one(const Geo &g, const apg_lidar_state &S, int e, uint8_t f, bool use_seed, uint64_t seed,
                           uint64_t *own, uint64_t *out_map_idx, uint32_t *err, const BinomTable &bt) {
   static_assert(GEN == GEN_NONE || GEN == GEN_ROOMS, "mazes reset in k_maze");
@@ -240,7 +242,7 @@ APG_DEV uint8_t reset_one(const Geo &g, const apg_lidar_state &S, int e, uint8_t
   if constexpr (GEN != GEN_NONE) {
     midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
     Pcg64 map_rng = seed_pcg64(midx);  // FloorMapDataset*.get_data_point: default_rng(idx)
-    int rc = rooms_generate(map_rng, own, g.wpr, g.h, g.max_rooms, g.door_width, bt);
+    int rc = rooms_generate<MR>(map_rng, own, g.wpr, g.h, g.max_rooms, g.door_width, bt);
     if (place_start(rng, own, g.h, g.w, g.wpr, px, py) != 0) rc = -6;
     if (rc != 0) atomicOr(err, APG_ERR_MAPGEN);
     *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
@@ -265,7 +267,7 @@ APG_DEV uint8_t reset_one(const Geo &g, const apg_lidar_state &S, int e, uint8_t
 // Map generation is a long serial, divergent chain per env whose speed is set by instruction latency,
 // not by lanes, so the host spreads the envs over as many waves as fit on the chip at once (gen_lanes).
 // Waves with nothing to reset exit after one flag load.
-template <int GEN>
+template <int GEN, int MR = 17>
 __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, uint64_t seed, int use_seed,
                                                     int all, uint64_t *out_map_idx, uint32_t *err, BinomTable bt,
                                                     int lanes) {
@@ -278,7 +280,7 @@ __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, ui
   const unsigned long long todo = __ballot(active);
   if (todo == 0ULL) return;
   const size_t words = (size_t)g.h * g.wpr;
-  if (active) reset_one<GEN>(g, S, e, f, use_seed != 0, seed, s_rows + lane * words, out_map_idx, err, bt);
+  if (active) reset_one<GEN, MR>(g, S, e, f, use_seed != 0, seed, s_rows + lane * words, out_map_idx, err, bt);
   if constexpr (GEN == GEN_ROOMS) copy_out_maps(s_rows, todo, words, S.occ + (size_t)blockIdx.x * lanes * words, lane);
 }
 
@@ -704,7 +706,8 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           const RoomsWork wk{reinterpret_cast<uint64_t *>(s_raw + L::stk) + my_el,
                              reinterpret_cast<int16_t *>(s_raw + L::cap) + my_el,
                              reinterpret_cast<int16_t *>(s_raw + L::size) + my_el,
-                             reinterpret_cast<int16_t *>(s_raw + L::cut) + my_el, s_prims + my_el, EPB, ROOMS_STACK};
+                             reinterpret_cast<int16_t *>(s_raw + L::cut) + my_el, s_prims + my_el, EPB, ROOMS_STACK,
+                             16};  // ROOMS_PRIM_WORDS: 17 rooms (larger max_rooms: k_lidar_reset + unfused step)
           const int rc = rooms_primitives(map_rng, g.h, g.max_rooms, g.door_width, bt, wk);
           if (rc != 0) atomicOr(O.err, APG_ERR_MAPGEN);
         }
@@ -1311,15 +1314,31 @@ int gen_lds(K kernel, int gen, const Geo &g, int lanes, size_t &dyn) {
   return opt_in_lds((const void *)kernel, dyn);
 }
 
+// lanes of a rooms-generation wave: gen_lanes(n), fewer when their LDS bitmaps would pass 160 KiB (large maps)
+int rooms_lanes(const Geo &g, int n) {
+  int lanes = gen_lanes(n);
+  const size_t per = (size_t)g.h * g.wpr * sizeof(uint64_t);
+  while (lanes > 1 && lanes * per > 160 * 1024) lanes /= 2;
+  return lanes;
+}
+
+template <int GEN, int MR>
+int launch_reset_mr(const Geo &g, const apg_lidar_state *st, uint64_t seed, int use_seed, int all,
+                    const apg_lidar_outputs *out, hipStream_t s) {
+  const int lanes = GEN == GEN_NONE ? 64 : rooms_lanes(g, g.n);
+  size_t dyn;
+  if (int rc = gen_lds(k_lidar_reset<GEN, MR>, GEN, g, lanes, dyn)) return rc;
+  hipLaunchKernelGGL((k_lidar_reset<GEN, MR>), dim3(grid_for(g.n, lanes)), dim3(64), dyn, s, g, *st, seed, use_seed,
+                     all, out->map_idx, out->err, make_binom_table(), lanes);
+  return check_launch("k_lidar_reset");
+}
+
+// the generator's private arrays hold 17 rooms (every registered env), ROOMS_MAX for larger max_rooms
 template <int GEN>
 int launch_reset_gen(const Geo &g, const apg_lidar_state *st, uint64_t seed, int use_seed, int all,
                      const apg_lidar_outputs *out, hipStream_t s) {
-  const int lanes = GEN == GEN_NONE ? 64 : gen_lanes(g.n);
-  size_t dyn;
-  if (int rc = gen_lds(k_lidar_reset<GEN>, GEN, g, lanes, dyn)) return rc;
-  hipLaunchKernelGGL(k_lidar_reset<GEN>, dim3(grid_for(g.n, lanes)), dim3(64), dyn, s, g, *st, seed, use_seed, all,
-                     out->map_idx, out->err, make_binom_table(), lanes);
-  return check_launch("k_lidar_reset");
+  if (GEN == GEN_ROOMS && g.max_rooms > 17) return launch_reset_mr<GEN, ROOMS_MAX>(g, st, seed, use_seed, all, out, s);
+  return launch_reset_mr<GEN, 17>(g, st, seed, use_seed, all, out, s);
 }
 
 // k_maze over n mazes (MZ_MAPS: occ / idx; MZ_RESET: the state's envs, all or the pending autoresets).
@@ -1383,11 +1402,17 @@ int launch_map_generate_any(const Geo &g, const uint64_t *idx, int n, uint64_t *
     return launch_maze(g, none, idx, n, occ, reinterpret_cast<uint8_t *>(stack), MZ_MAPS, 0, 0, 1, nullptr, nullptr, err,
                        s);
   }
-  const int lanes = gen_lanes(n);
+  const int lanes = rooms_lanes(g, n);
   size_t dyn;
-  if (int rc = gen_lds(k_map_generate_rooms, GEN_ROOMS, g, lanes, dyn)) return rc;
-  hipLaunchKernelGGL(k_map_generate_rooms, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, idx, n, occ, err,
-                     make_binom_table(), lanes);
+  const bool big = g.max_rooms > 17;
+  const void *kern = big ? (const void *)k_map_generate_rooms<ROOMS_MAX> : (const void *)k_map_generate_rooms<17>;
+  if (int rc = gen_lds(kern, GEN_ROOMS, g, lanes, dyn)) return rc;
+  if (big)
+    hipLaunchKernelGGL(k_map_generate_rooms<ROOMS_MAX>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, idx, n, occ, err,
+                       make_binom_table(), lanes);
+  else
+    hipLaunchKernelGGL(k_map_generate_rooms<17>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, idx, n, occ, err,
+                       make_binom_table(), lanes);
   return check_launch("k_map_generate");
 }
 
@@ -1398,6 +1423,10 @@ size_t step_lds_bytes(int epb, int beams) {
   if (beams <= MAX_STAGED_BEAMS)
     b += (size_t)epb * (beams + 1) * sizeof(float) + (size_t)epb * beams * sizeof(uint16_t) + EMPTY_TAB * sizeof(float);
   return b;
+}
+
+bool big_rooms(const apg_lidar_config *c) {
+  return c->map_kind == APG_MAP_ROOMS && !c->is_static && (c->max_rooms > 17 || c->height > MAX_MAP_ROWS);
 }
 
 int step_gen(const Geo &g) {
@@ -1556,7 +1585,12 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
   // mazes: k_maze resets the envs with an autoreset pending (its waves exit at once when there are none),
   // then the unfused step kernel
   if (ev_begin && hipEventRecord((hipEvent_t)ev_begin, s) != hipSuccess) return fail(APG_E_LAUNCH, "hipEventRecord");
-  if (cfg->map_kind == APG_MAP_MAZE && !cfg->is_static) {
+  if (big_rooms(cfg)) {
+    // rooms the fused step kernel's LDS generator does not hold (max_rooms > 17, maps > 128): the pending
+    // autoresets in k_lidar_reset, then the unfused step kernel (it writes their map obs)
+    rc = launch_reset_gen<GEN_ROOMS>(make_geo(cfg), st, 0, 0, 0, out, s);
+    if (rc == APG_OK) rc = launch_step_kernel(cfg, st, action, prediction, out, s, false);
+  } else if (cfg->map_kind == APG_MAP_MAZE && !cfg->is_static) {
     const Geo g = make_geo(cfg);
     rc = launch_maze(g, *st, nullptr, g.n, nullptr, reinterpret_cast<uint8_t *>(st->stack), MZ_RESET, 0, 0, 0,
                      out->map_idx, out->map_obs, out->err, s);
@@ -1603,7 +1637,7 @@ int apg_map_generate(int map_kind, const uint64_t *idx, int n, int h, int w, int
 
 int apg_lidar_scan_batch(const uint64_t *occ, const int32_t *map_index, int h, int w, const float *seg, int n,
                          float *dist, int32_t *kind, apg_stream_t stream) {
-  if (n <= 0 || h <= 0 || w <= 0 || w > 128) return fail(APG_E_INVALID, "bad scan batch arguments");
+  if (n <= 0 || h <= 0 || w <= 0 || w > 255) return fail(APG_E_INVALID, "bad scan batch arguments");
   // segments must span <= 28 columns (32-column row window); callers check this on the host
   hipLaunchKernelGGL(k_scan_batch, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, occ, map_index, h,
                      w, (w + 63) / 64, seg, n, dist, kind);

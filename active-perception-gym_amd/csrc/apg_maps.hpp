@@ -8,9 +8,10 @@
 
 namespace apg {
 
-struct BinomTable {  // random_binomial_inversion constants for n = 0..15 at p = 0.3 (host libm)
-  double qn[16];
-  int32_t bound[16];
+constexpr int ROOMS_MAX = 32;  // max_rooms of the generator (binomial draws of n = mrl - 2 < ROOMS_MAX)
+struct BinomTable {  // random_binomial_inversion constants for n = 0..ROOMS_MAX-1 at p = 0.3 (host libm)
+  double qn[ROOMS_MAX];
+  int32_t bound[ROOMS_MAX];
   double p, q;
 };
 
@@ -44,22 +45,25 @@ APG_DEV int64_t pyfloordiv(int64_t a, int64_t b) {
 // Working storage of the rooms generator, strided so that a workgroup can interleave its threads'
 // copies in LDS ([index][thread], conflict-free) or a thread can point it at private arrays (stride 1):
 // the task stack, the capacities and sizes of the current split, distribute_integers' cut points, and
-// the output primitives prim[0] = nw | nd << 8, prim[1 + i] walls, prim[17 + i] doors.
+// the output primitives prim[0] = nw | nd << 8, prim[1 + i] walls, prim[1 + maxw + i] doors (i < maxw =
+// max_rooms - 1: every split adds k - 1 walls and doors to the k rooms it makes of one).
 struct RoomsWork {
   uint64_t *stk;
   int16_t *cap, *size, *cut;
   uint32_t *prim;
   int st;       // element stride
   int stk_cap;  // stack capacity
+  int maxw;     // walls (= doors) the primitives hold
   APG_DEV uint64_t &S(int i) const { return stk[i * st]; }
   APG_DEV int16_t &C(int i) const { return cap[i * st]; }
   APG_DEV int16_t &Z(int i) const { return size[i * st]; }
   APG_DEV int16_t &K(int i) const { return cut[i * st]; }
   APG_DEV uint32_t &P(int i) const { return prim[i * st]; }
 };
-constexpr int ROOMS_PRIM_WORDS = 33;
+constexpr int ROOMS_PRIM_WORDS = 33;  // 17 rooms (the fused step kernel's LDS layout)
+__host__ __device__ constexpr int rooms_prim_words(int max_rooms) { return 1 + 2 * (max_rooms - 1); }
 
-// distribute_integers(n, k) (rooms.py:36-40) with k <= 17, n < 2^15: out(i) for i < k
+// distribute_integers(n, k) (rooms.py:36-40) with k <= ROOMS_MAX, n < 2^15: out(i) for i < k
 template <class Out>
 APG_DEV void distribute_integers(Pcg64 &r, int64_t n, int k, const RoomsWork &W, Out out) {
   const int64_t nz = k > n ? k - n : 0;
@@ -137,14 +141,14 @@ APG_DEV int rooms_primitives(Pcg64 &r, int m, int max_rooms, int door_width, con
     int64_t mrl = pyfloordiv(n0 - min_size, min_size + 1) + 1;
     if (mr < mrl) mrl = mr;
     if (mrl <= 1) continue;
-    if (mrl > 17) return -2;  // max_rooms <= 17 (binomial table: mrl - 2 <= 15)
+    if (mrl > ROOMS_MAX) return -2;  // the binomial table: mrl - 2 < ROOMS_MAX
     const int k = (int)binomial_inv(r, mrl - 2, bt) + 2;
     distribute_integers(r, mrl, k, W, [&](int i) -> int16_t & { return W.C(i); });
     distribute_integers(r, n0 - (int64_t)k * (1 + min_size) + 1, k, W, [&](int i) -> int16_t & { return W.Z(i); });
     // sizes += min_size; room i spans view rows [starts[i], ends[i]] with ends[i] = acc_i - 1,
     // starts[i] = acc_{i-1} + 1 (starts[0] = 0), acc_i = sum_{j <= i} (sizes[j] + 1)
     for (int i = 0; i < k; i++) W.Z(i) = (int16_t)(W.Z(i) + min_size);
-    if (nw + k - 1 > 16) return -4;
+    if (nw + k - 1 > W.maxw) return -4;
     int acc = (int)W.Z(0) + 1;
     for (int i = 1; i < k; i++) {
       const int wp = acc;  // starts[i] - 1
@@ -155,11 +159,11 @@ APG_DEV int rooms_primitives(Pcg64 &r, int m, int max_rooms, int door_width, con
       const int lo = wp - (door_width - 1), span = 2 * door_width - 1;
       if (t == 0) {
         W.P(1 + nw++) = ((uint32_t)(y0 + wp) << 16) | ((uint32_t)x0 << 8) | (uint32_t)n1;
-        W.P(17 + nd++) = ((uint32_t)(y0 + lo) << 24) | ((uint32_t)(x0 + dp) << 16) | ((uint32_t)span << 8) |
+        W.P(1 + W.maxw + nd++) = ((uint32_t)(y0 + lo) << 24) | ((uint32_t)(x0 + dp) << 16) | ((uint32_t)span << 8) |
                          (uint32_t)door_width;
       } else {
         W.P(1 + nw++) = (1u << 31) | ((uint32_t)(x0 + wp) << 16) | ((uint32_t)y0 << 8) | (uint32_t)n1;
-        W.P(17 + nd++) = ((uint32_t)(y0 + dp) << 24) | ((uint32_t)(x0 + lo) << 16) | ((uint32_t)door_width << 8) |
+        W.P(1 + W.maxw + nd++) = ((uint32_t)(y0 + dp) << 24) | ((uint32_t)(x0 + lo) << 16) | ((uint32_t)door_width << 8) |
                          (uint32_t)span;
       }
     }
@@ -178,8 +182,9 @@ APG_DEV int rooms_primitives(Pcg64 &r, int m, int max_rooms, int door_width, con
   if (integers(r, 0, 2) == 0) {  // map_int = map_int.T: transpose the primitives
     for (int i = 0; i < nw; i++) W.P(1 + i) ^= 1u << 31;
     for (int i = 0; i < nd; i++) {
-      const uint32_t d = W.P(17 + i);
-      W.P(17 + i) = (((d >> 16) & 255u) << 24) | (((d >> 24) & 255u) << 16) | ((d & 255u) << 8) | ((d >> 8) & 255u);
+      const uint32_t d = W.P(1 + W.maxw + i);
+      W.P(1 + W.maxw + i) =
+          (((d >> 16) & 255u) << 24) | (((d >> 24) & 255u) << 16) | ((d & 255u) << 8) | ((d >> 8) & 255u);
     }
   }
   W.P(0) = (uint32_t)nw | ((uint32_t)nd << 8);
@@ -212,20 +217,21 @@ APG_DEV void rooms_paint(const RoomsWork &W, int m, int wpr, uint64_t *rows) {
     }
   }
   for (int i = 0; i < nd; i++) {
-    const uint32_t d = W.P(17 + i);
+    const uint32_t d = W.P(1 + W.maxw + i);
     const int r0 = (int)(d >> 24), c0 = (int)((d >> 16) & 255u), hh = (int)((d >> 8) & 255u), ww = (int)(d & 255u);
     for (int y = r0; y < r0 + hh; y++)
       for (int k = 0; k < wpr; k++) rows[y * wpr + k] &= ~span_mask(c0, ww, k);
   }
 }
 
-// generate + paint: occ rows [m][wpr]; working storage in this thread's private arrays
+// generate + paint: occ rows [m][wpr]; working storage in this thread's private arrays, sized for MR rooms
+template <int MR = 17>
 APG_DEV int rooms_generate(Pcg64 &r, uint64_t *occ, int wpr, int m, int max_rooms, int door_width,
                            const BinomTable &bt) {
-  uint64_t stk[24];
-  int16_t cap[17], size[17], cut[16];
-  uint32_t prim[ROOMS_PRIM_WORDS];
-  const RoomsWork W{stk, cap, size, cut, prim, 1, 24};
+  uint64_t stk[MR + 7];
+  int16_t cap[MR], size[MR], cut[MR - 1];
+  uint32_t prim[rooms_prim_words(MR)];
+  const RoomsWork W{stk, cap, size, cut, prim, 1, MR + 7, MR - 1};
   const int rc = rooms_primitives(r, m, max_rooms, door_width, bt, W);
   rooms_paint(W, m, wpr, occ);
   return rc;

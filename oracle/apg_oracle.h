@@ -61,6 +61,8 @@ orc_lidar_env *orc_lidar_create(int num_envs, int map_kind /*0 rooms, 1 maze*/, 
                                 int static_map, int static_map_index, int beams, float lidar_range,
                                 int step_limit, const float *beam_dirs /*[beams][2], scaled*/);
 void orc_lidar_destroy(orc_lidar_env *e);
+/* rooms parameters of the dynamic maps of later resets (defaults 10, 3) */
+void orc_lidar_set_rooms(orc_lidar_env *e, int max_rooms, int door_width);
 /* reset(seed=seed): sub-env i seeded with seed+i. Writes obs. */
 void orc_lidar_reset(orc_lidar_env *e, uint64_t seed, float *lidar, float *odometry,
                      float *time_step, float *map_obs /*may be NULL*/, uint64_t *map_idx);

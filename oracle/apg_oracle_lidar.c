@@ -335,6 +335,7 @@ float orc_lidar_scan(const uint8_t *map, int h, int w, float fpx, float fpy, flo
 /* ------------------------------------------------------------ vectorised env */
 struct orc_lidar_env {
   int n, kind, h, w, is_static, beams, step_limit;
+  int max_rooms, door_width; /* FloorMapDatasetRooms parameters of the dynamic maps (default 10, 3) */
   float range;
   float *dirs;        /* [beams][2] scaled beam vectors (lidar_directions) */
   orc_pcg64 *rng;     /* env np_random */
@@ -359,6 +360,8 @@ orc_lidar_env *orc_lidar_create(int num_envs, int map_kind, int h, int w, int st
   e->beams = beams;
   e->range = lidar_range;
   e->step_limit = step_limit;
+  e->max_rooms = 10;
+  e->door_width = 3;
   e->dirs = (float *)malloc(sizeof(float) * 2 * beams);
   memcpy(e->dirs, beam_dirs, sizeof(float) * 2 * beams);
   e->rng = (orc_pcg64 *)calloc(num_envs, sizeof(orc_pcg64));
@@ -428,7 +431,7 @@ static void env_reset_one(orc_lidar_env *e, int i) {
     uint64_t idx = (uint64_t)orc_next32(&e->it_rng[i]); /* integers(0, 2**32) */
     uint8_t *m = e->maps + (size_t)i * e->h * e->w;
     if (e->kind == 0)
-      orc_rooms_map(idx, e->h, e->w, 10, 3, m);
+      orc_rooms_map(idx, e->h, e->w, e->max_rooms, e->door_width, m);
     else
       orc_maze_map(idx, e->h, e->w, 1.0, m);
     e->map_idx[i] = idx;
@@ -597,4 +600,10 @@ void orc_lidar_get_state(const orc_lidar_env *e, float *pos, float *init_pos, in
   if (init_pos) memcpy(init_pos, e->init_pos, sizeof(float) * 2 * e->n);
   if (elapsed) memcpy(elapsed, e->elapsed, sizeof(int32_t) * e->n);
   if (autoreset) memcpy(autoreset, e->autoreset, e->n);
+}
+
+/* FloorMapDatasetRooms(max_rooms=..., door_width=...) for the dynamic maps of later resets */
+void orc_lidar_set_rooms(orc_lidar_env *e, int max_rooms, int door_width) {
+  e->max_rooms = max_rooms;
+  e->door_width = door_width;
 }

@@ -40,6 +40,7 @@ def lib():
         L.orc_lidar_create.restype = vp
         L.orc_lidar_create.argtypes = [i32, i32, i32, i32, i32, i32, i32, f32, i32, vp]
         L.orc_lidar_destroy.argtypes = [vp]
+        L.orc_lidar_set_rooms.argtypes = [vp, i32, i32]
         L.orc_lidar_reset.argtypes = [vp, u64, vp, vp, vp, vp, vp]
         L.orc_lidar_step.restype = i32
         L.orc_lidar_step.argtypes = [vp] + [vp] * 14
@@ -87,7 +88,7 @@ class OracleLidarVectorEnv:
     """SyncVectorEnv(TimeLimit(LIDARLocalization2DEnv)) restated in C; numpy in/out."""
 
     def __init__(self, num_envs, map_kind="rooms", size=32, static_map=False, static_map_index=0, beams=8,
-                 lidar_range=5, step_limit=100, sparse=False):
+                 lidar_range=5, step_limit=100, sparse=False, max_rooms=10, door_width=3):
         self.n, self.h, self.w, self.beams = num_envs, size, size, beams
         self.static = static_map
         self.dirs = beam_directions(beams, lidar_range)
@@ -95,6 +96,8 @@ class OracleLidarVectorEnv:
                                          static_map_index, beams, float(lidar_range), step_limit, _p(self.dirs))
         if not self._e:
             raise ValueError("invalid map configuration")
+        if (max_rooms, door_width) != (10, 3):
+            lib().orc_lidar_set_rooms(self._e, max_rooms, door_width)
         n = num_envs
         self.lidar = np.zeros((n, beams), np.float32)
         self.odometry = np.zeros((n, 2), np.float32)

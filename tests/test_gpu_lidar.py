@@ -115,7 +115,8 @@ def test_device_maze_stream_overflow_matches_oracle(gpu, oracle_mod, tmp_path):
         assert np.array_equal(got[i], ref), int(idx[i])
 
 
-@pytest.mark.parametrize("size,max_rooms,door_width", [(128, 17, 3), (128, 10, 3), (96, 17, 2), (48, 6, 4)])
+@pytest.mark.parametrize("size,max_rooms,door_width", [(128, 17, 3), (128, 10, 3), (96, 17, 2), (48, 6, 4),
+                                                       (160, 24, 3), (200, 32, 2), (255, 17, 3), (64, 24, 2)])
 def test_device_rooms_parameters_match_oracle(gpu, oracle_mod, size, max_rooms, door_width):
     import ap_gym_amd as ap
 
@@ -380,6 +381,33 @@ def test_long_range_matches_oracle(gpu, oracle_mod, kind, size, static, beams, l
         assert np.array_equal(term, ref.terminated.astype(bool)), t
         if not static:
             assert np.array_equal(obs["map"][..., 0], ref.map), t
+    env.close()
+
+
+@pytest.mark.parametrize("size,max_rooms,n", [(160, 24, 256), (130, 10, 256), (64, 24, 512)])
+def test_large_rooms_env_matches_oracle(gpu, oracle_mod, size, max_rooms, n):
+    """Rooms maps past the fused step kernel's generator (maps > 128, max_rooms > 17: the autoresets run
+    in k_lidar_reset before the unfused step kernel): 110 steps (one autoreset) against the oracle env."""
+    import ap_gym_amd as ap
+
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=ap.FloorMapDatasetRooms(size, size, max_rooms=max_rooms),
+                                          lidar_beam_count=16, device=gpu)
+    ref = oracle_mod.OracleLidarVectorEnv(n, "rooms", size, False, 0, 16, max_rooms=max_rooms)
+    obs, _ = env.reset(seed=21)
+    ref.reset(21)
+    assert np.array_equal(obs["lidar"], ref.lidar)
+    assert np.array_equal(obs["map"][..., 0], ref.map)
+    rng = np.random.default_rng(6)
+    for t in range(110):
+        a = rng.uniform(-1.5, 1.5, (n, 2)).astype(np.float32)
+        p = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        ref.step(a, p)
+        assert np.array_equal(obs["lidar"], ref.lidar), t
+        assert np.array_equal(obs["odometry"], ref.odometry), t
+        assert np.array_equal(rew, ref.reward, equal_nan=True), t
+        assert np.array_equal(term, ref.terminated.astype(bool)), t
+        assert np.array_equal(obs["map"][..., 0], ref.map), t
     env.close()
 
 
