@@ -583,13 +583,16 @@ struct RoomsLds {
 // GR: every scan reads the occupancy rows from global memory through its own 32-column window (RowsGlobal at
 // floor(min(p.x, q.x)) - 1: scans up to 28 cells long) instead of the staged 32 x 32 window around the env,
 // for lidar_range > 10 (the staged window covers R <= 10).
-template <int GEN, bool FUSED, int EPB, bool GR = false>
-__global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(StepParams P, Geo g, apg_lidar_state S,
+// ROWP: packed output rows (apg_lidar_config.out_row_bytes > 0); the dense instance has P.row = 0 folded in.
+template <int GEN, bool FUSED, int EPB, bool GR = false, bool ROWP = false>
+__global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(StepParams P_in, Geo g, apg_lidar_state S,
                                                                  const float *__restrict__ act,
                                                                  const float *__restrict__ pred,
                                                                  apg_lidar_outputs O, BinomTable bt) {
   using SS = StepShape<EPB>;
   constexpr int T = SS::T, W = SS::W, LPW = SS::LPW;
+  StepParams P = P_in;
+  if constexpr (!ROWP) P.row = 0;
   __shared__ float s_pos[EPB][2];
   __shared__ int s_x0[EPB], s_y0[EPB];
   __shared__ uint16_t s_rlist[EPB];  // envs that reset this step (map obs pass)
@@ -1463,7 +1466,7 @@ int launch_step_t(const StepParams &P, const Geo &g, const apg_lidar_state *st, 
                   const apg_lidar_outputs *out, hipStream_t s, const BinomTable &bt) {
   size_t lds = step_lds_bytes(EPB, P.beams);
   if (FUSED && GEN == GEN_ROOMS && RoomsLds<EPB>::bytes > lds) lds = RoomsLds<EPB>::bytes;
-  auto kern = k_lidar_step<GEN, FUSED, EPB, GR>;
+  auto kern = P.row ? k_lidar_step<GEN, FUSED, EPB, GR, true> : k_lidar_step<GEN, FUSED, EPB, GR, false>;
   if (int rc = opt_in_lds((const void *)kern, lds)) return rc;
   hipLaunchKernelGGL(kern, dim3(grid_for(P.n, EPB)), dim3(4 * EPB), lds, s, P, g, *st, act, pred, *out, bt);
   return check_launch("k_lidar_step");

@@ -530,8 +530,8 @@ def run_lidar(args, world, rank, dev):
             "roofline": {"bound": bound, "bound_basis": basis, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_calibrated": traffic_cal,
-                         "kernel": "k_lidar_step" + (" (+ k_maze, a no-op wave exit on ordinary steps)"
-                                                     if w["kind"] == "maze" else ""),
+                         "kernel": "k_lidar_step" + (" (+ k_maze_stream, k_maze, k_maze_paint: workgroups that exit at "
+                                                     "once on ordinary steps)" if w["kind"] == "maze" else ""),
                          "kernel_ms": kernel_ms, "median_kernel_ms": median_ms,
                          "kernel_ms_rocprof": ({c: v["median_us"] / 1e3 for c, v in dj["per_class"].items()}
                                                if dj else None), "durations_source": dpath,

@@ -6,6 +6,7 @@ like the PMC tables by the kernel-source hash and the run shape, for bench.py's 
 Classes as in tools/pmc_tables.py (LIDAR: reset_pass / step / reset_step of k_lidar_step, maze_* of k_maze;
 image: the kernel name, and "step" = the ordinary step's k_image_step_fused).
 """
+import collections
 import glob
 import json
 import os
@@ -18,7 +19,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import bench  # noqa: E402
 import rocpd_stats  # noqa: E402
-from pmc_tables import lidar_class  # noqa: E402
+from pmc_tables import lidar_class, lidar_family  # noqa: E402
 
 
 def main():
@@ -27,13 +28,13 @@ def main():
     b = [json.loads(x) for x in open(line_file).read().splitlines() if x.startswith("{")][-1]
     cfg = b["config"]
     acc = {}
-    ordinal = {"k_lidar_step": 0, "k_maze": 0}
+    ordinal = collections.Counter()
     for name, s, e, g, w in rocpd_stats.load(db):
         us = (e - s) / 1e3
         if wl in bench.LIDAR_WORKLOADS:
-            if "k_lidar_step" in name or "k_maze<" in name:
-                fam = "k_maze" if "k_maze<" in name else "k_lidar_step"
-                cls = lidar_class(ordinal[fam], "maze_" if fam == "k_maze" else "")
+            if "k_lidar_step" in name or "k_maze" in name:
+                fam, prefix = lidar_family(name)
+                cls = lidar_class(ordinal[fam], prefix)
                 ordinal[fam] += 1
             else:
                 continue

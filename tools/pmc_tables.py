@@ -53,6 +53,17 @@ def bench_line(d: str) -> dict:
     raise SystemExit(f"no bench JSON line under {d}")
 
 
+def lidar_family(kname: str):
+    """(kernel family, class prefix) of a LIDAR-workload dispatch: the step kernel, or one of the three maze
+    reset kernels (each launched once per step, exiting at once on steps without autoresets)."""
+    for fam, prefix in (("k_maze_stream", "maze_stream_"), ("k_maze_paint", "maze_paint_")):
+        if fam in kname:
+            return fam, prefix
+    if re.search(r"k_maze<", kname):
+        return "k_maze", "maze_"
+    return "k_lidar_step", ""
+
+
 def lidar_class(ordinal: int, prefix: str = "") -> str:
     if ordinal == 0:
         return prefix + "reset_pass" if not prefix else prefix + "reset"
@@ -66,12 +77,12 @@ def main():
     acc: dict[str, dict[str, list[float]]] = collections.defaultdict(lambda: collections.defaultdict(list))
     for name in PASSES:
         rows = read_pass(d, name)
-        ordinal = {"k_lidar_step": 0, "k_maze": 0}
+        ordinal = collections.Counter()
         for did in sorted(rows):
             kname, vals = rows[did]
             if wl in bench.LIDAR_WORKLOADS:
-                fam = "k_maze" if re.search(r"k_maze<", kname) else "k_lidar_step"
-                cls = lidar_class(ordinal[fam], "maze_" if fam == "k_maze" else "")
+                fam, prefix = lidar_family(kname)
+                cls = lidar_class(ordinal[fam], prefix)
                 ordinal[fam] += 1
             else:
                 cls = kname.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
