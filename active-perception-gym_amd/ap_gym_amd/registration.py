@@ -176,8 +176,11 @@ def make_vec(id: str | EnvSpec, num_envs: int = 1, vectorization_mode: str | Non
     spec = id if isinstance(id, EnvSpec) else registry.get(id)
     if spec is None:
         raise KeyError(f"Environment id {id!r} is not provided by the MI355X backend. Known ids: {sorted(registry)}")
-    if vectorization_mode not in (None, "vector_entry_point", "sync"):
-        raise ValueError("the MI355X backend always runs the batched vector env (vectorization_mode=None)")
+    mode = getattr(vectorization_mode, "value", vectorization_mode)  # gymnasium.VectorizeMode members too
+    if mode not in (None, "vector_entry_point", "sync", "async"):
+        raise ValueError(f"unknown vectorization_mode {vectorization_mode!r}")
+    # "sync" / "async": gymnasium's SyncVectorEnv and AsyncVectorEnv return the same batches for the same
+    # seeds (both autoreset NEXT_STEP); the batched env reproduces them, the worker processes are not needed
     if wrappers:
         raise NotImplementedError("per-sub-env wrappers are not supported by the batched backend")
     kw = dict(spec.kwargs)

@@ -107,6 +107,26 @@ def test_registry_and_spaces():
         ap.FloorMapDatasetMaze(128, 128)
 
 
+def test_make_vec_vectorization_modes():
+    """registration.py:753-767 passes vectorization_mode through to gymnasium: "sync" and "async" give the
+    same batches, so both build the batched env; unknown modes and per-sub-env wrappers are refused."""
+    from ap_gym_amd.registration import EnvSpec, make_vec
+
+    built = []
+    spec = EnvSpec("Probe-v0", lambda num_envs, **kw: built.append((num_envs, kw)) or "env", {"a": 1}, 7)
+
+    class Mode:  # a gymnasium.VectorizeMode-like enum member
+        value = "async"
+
+    for mode in (None, "vector_entry_point", "sync", "async", Mode()):
+        assert make_vec(spec, 3, vectorization_mode=mode, b=2) == "env"
+    assert built == [(3, {"a": 1, "max_episode_steps": 7, "b": 2})] * 5
+    with pytest.raises(ValueError):
+        make_vec(spec, 3, vectorization_mode="threads")
+    with pytest.raises(NotImplementedError):
+        make_vec(spec, 3, wrappers=[lambda e: e])
+
+
 def test_beam_directions_match_reference_formula():
     from ap_gym_amd import lidar_beam_directions
 
