@@ -166,7 +166,7 @@ def run_image(args, world, rank, dev):
 
     senv = ShardedVectorEnv(lambda num_envs, env_offset: cls(num_envs, cfg, device=dev, array_backend="torch",
                                                              num_envs_total=n_total, env_offset=env_offset),
-                            n_total, rank, world, gather=args.gather and world > 1, time_gather=True)
+                            n_total, rank, world, gather=args.gather, time_gather=True)
     env = senv.env
     ring = 17
     g = torch.Generator(device=dev).manual_seed(1 + rank)
@@ -261,7 +261,7 @@ def run_image(args, world, rank, dev):
             out["cpu_baseline"] = image_cpu_baseline(w, pool, labels, c, n_cpu, s_cpu)
         print(json.dumps(out), flush=True)
     env.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -405,8 +405,7 @@ def run_lidar(args, world, rank, dev):
         return apg.make_vec(w["env_id"], num_envs=num_envs, lidar_beam_count=beams, dataset=ds, device=dev,
                             array_backend=args.array_backend, env_offset=env_offset, **kw)
 
-    senv = ShardedVectorEnv(make_local, n_total, rank, world, beams, gather=args.gather and world > 1,
-                            time_gather=True)
+    senv = ShardedVectorEnv(make_local, n_total, rank, world, beams, gather=args.gather, time_gather=True)
     env = senv.env
     ring = 128  # distinct synthetic action/prediction batches, cycled
     g = torch.Generator(device=dev).manual_seed(1 + rank)
@@ -526,7 +525,7 @@ def run_lidar(args, world, rank, dev):
                        "num_envs_total": n_total,
                        "beams": beams, "map": f"{msize}x{msize} {w['kind']}", "max_episode_steps": 100,
                        "reset_ms": reset_ms, "note": w["note"], "gather_ms": gather_ms if senv.gather else None,
-                       "parallelism": f"env-shard x{world}" + (" + all-gather" if args.gather and world > 1 else "")},
+                       "parallelism": f"env-shard x{world}" + (" + all-gather" if senv.gather else "")},
             "roofline": {"bound": bound, "bound_basis": basis, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_calibrated": traffic_cal,
@@ -552,7 +551,7 @@ def run_lidar(args, world, rank, dev):
                                                args.cpu_threads)
         print(json.dumps(out), flush=True)
     senv.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -666,7 +665,9 @@ def main():
     ndev = max(1, torch.cuda.device_count())  # counting devices does not initialise HIP
     torch.cuda.set_device(local_rank % ndev)
     dev = torch.device("cuda", local_rank % ndev)
-    if world > 1:
+    if world == 1 and args.gather:  # one GPU: a one-rank group still runs the all-gather's collective code path
+        os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    if world > 1 or args.gather:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:

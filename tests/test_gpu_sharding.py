@@ -3,7 +3,8 @@ env bit for bit, and ShardedVectorEnv's packed all-gather reassembles that batch
 
 * single process: two shard envs on cuda:0 stepped side by side, concatenated, vs one unsharded env;
 * two processes (torch.multiprocessing, gloo — RCCL refuses two ranks on one device) sharing cuda:0,
-  ShardedVectorEnv(gather=True) on each: the gathered batch of every rank vs the unsharded env.
+  ShardedVectorEnv(gather=True) on each: the gathered batch of every rank vs the unsharded env;
+* one process in a one-rank RCCL ("nccl") group: the device-side all_gather_into_tensor branch.
 Both for the LIDAR path (LIDARLocRooms) and the image path (ImageLocalizationVectorEnv with the
 unique-sampler reset), across autoresets.
 """
@@ -98,12 +99,15 @@ def test_shards_union_equals_unsharded(gpu, kind):
     torch.cuda.synchronize()
 
 
-def _worker(rank, world, port, kind, outdir):
+def _worker(rank, world, port, kind, outdir, backend="gloo"):
     import torch
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    assert dist.get_backend() == backend
     import ap_gym_amd  # noqa: F401
     from ap_gym_amd.sharding import ShardedVectorEnv
 
@@ -146,6 +150,22 @@ def test_two_rank_gather_on_gpu_equals_unsharded(gpu, kind, tmp_path):
         for k, v in want.items():
             for r in range(2):
                 assert np.array_equal(got[r][f"{t}_{k}"], v), f"rank {r} step {t}: {k}"
+
+
+@pytest.mark.parametrize("kind", ["lidar", "image"])
+def test_rccl_gather_branch_single_rank(gpu, kind, tmp_path):
+    """The RCCL branch of ShardedVectorEnv._all_gather_rows (dist.all_gather_into_tensor on the device rows;
+    sharding.py) on a one-rank "nccl" group: RCCL refuses two ranks on one device, so this is the only way
+    one GPU runs that branch.  The gathered batch must equal the unsharded env."""
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_worker, args=(1, _free_port(), kind, str(tmp_path), "nccl"), nprocs=1, join=True,
+                       start_method="spawn")
+    ref = _reference(kind, with_reset=kind == "lidar")
+    got = np.load(tmp_path / "rank0.npz")
+    for t, want in enumerate(ref):
+        for k, v in want.items():
+            assert np.array_equal(got[f"{t}_{k}"], v), f"step {t}: {k}"
 
 
 @pytest.mark.parametrize("log_stats,sparse", [(False, False), (True, False), (False, True)])
