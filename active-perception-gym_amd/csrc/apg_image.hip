@@ -63,6 +63,16 @@ GlimpseGeo make_geo(const apg_image_config *c) {
 // the f64 quotient rounded once more to f32 equals numpy's correctly rounded f32 division for all
 // 256 values (checked bit for bit by the glimpse parity tests, which cover every u8 value)
 APG_DEV float u8_value(unsigned v) { return (float)__dmul_rn((double)v, 1.0 / 255.0); }
+// The same f32 value in registers: v * (1/255) as an unevaluated f32 pair c_hi + c_lo, fma(v, c_hi, v * c_lo).
+// The pair carries 1/255 to ~2^-48 relative, and no v / 255 (v in 0..255; a repeating 8-bit pattern) lies that
+// close to a rounding midpoint of f32, so the fma rounds to the correctly rounded v / 255 = u8_value(v) for every
+// v (checked exhaustively with exact rationals, tests/test_host.py).  The glimpse's tap reads use it instead of
+// the LDS table: random bytes of 64 lanes hit the table's 32 banks with ~2.5 extra cycles per read.
+#ifndef APG_U8_ARITH
+#define APG_U8_ARITH 1
+#endif
+constexpr float U8_C_HI = 0x1.010102p-8f, U8_C_LO = -0x1.fdfdfep-33f;
+APG_DEV float u8_value_f32(uint32_t v) { return __fmaf_rn((float)v, U8_C_HI, __fmul_rn((float)v, U8_C_LO)); }
 APG_DEV void load_u8_table(float *lut) {
   // v * (1/255) in f64 rounds to the same f32 as the correctly rounded v / 255 for every v in 0..255
   // (checked exhaustively against numpy on the host); cheaper than an f64 division per entry
@@ -472,7 +482,10 @@ APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, 
                               __builtin_amdgcn_alignbit(cur.a02, cur.a01, 8u * cur.o0)};
       const uint32_t b1[2] = {__builtin_amdgcn_alignbit(cur.a11, cur.a10, 8u * cur.o1),
                               __builtin_amdgcn_alignbit(cur.a12, cur.a11, 8u * cur.o1)};
-      auto tap = [&](const uint32_t *b, int t) { return s_lut[(b[t >> 2] >> (8 * (t & 3))) & 0xffu]; };
+      auto tap = [&](const uint32_t *b, int t) {
+        const uint32_t v = (b[t >> 2] >> (8 * (t & 3))) & 0xffu;  // a compile-time byte: v_cvt_f32_ubyteN
+        return APG_U8_ARITH ? u8_value_f32(v) : s_lut[v];
+      };
       float res[C];
 #pragma unroll
       for (int ch = 0; ch < C; ch++) {
@@ -512,7 +525,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_glimpse_sep(GlimpseGeo g, const 
   __shared__ float s_lut[256];
   extern __shared__ Axis s_ax[];  // [unit][rows s0 | columns s1]
   __shared__ int64_t s_base[GS_MAX_UNITS];
-  for (int v = threadIdx.x; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
+  if (!APG_U8_ARITH) for (int v = threadIdx.x; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
   const int u0 = blockIdx.x * upb, nu = units - u0 < upb ? units - u0 : upb;
   const uint32_t bad = gs_axes(g, index, [&](int u, int c) { return (double)pos[2 * (u0 + u) + c]; }, u0, nu, npos,
                                side_div, s_ax, s_base);
@@ -924,7 +937,7 @@ __attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fuse
       env_step(tid - GS_THREADS, in);
       return;
     }
-    for (int v = tid; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
+    if (!APG_U8_ARITH) for (int v = tid; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
     __syncthreads();
     const uint32_t bad =
         gs_axes(g, nullptr, [&](int u, int c) { return s_npos[u][c]; }, u0, nu, 1, side_div, s_ax, s_base);
@@ -932,7 +945,7 @@ __attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fuse
     gs_pixels_t<F32, PC, C>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
     if (bad) atomicOr(out.err, bad);
   } else {
-    for (int v = tid; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
+    if (!APG_U8_ARITH) for (int v = tid; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
     EnvIn in;
     env_inputs(tid, GS_THREADS, in);
     __syncthreads();

@@ -275,3 +275,30 @@ def test_foreign_dataset_view_fetches_in_chunks_and_warns():
     imgs, labels = view.device_pool()
     assert inner.calls == 3 and imgs.shape == (10, 4, 5, 1) and imgs.dtype == np.uint8
     assert np.array_equal(imgs[:, 0, 0, 0], np.arange(10)) and np.array_equal(labels, np.arange(10) % 3)
+
+
+def test_u8_tap_value_pair_is_exact():
+    """apg_image.hip u8_value_f32: fma(v, c_hi, v * c_lo) in f32 (c_hi + c_lo = 1/255 to ~2^-48) equals the
+    correctly rounded v / 255 (the reference's u8 -> float32 / 255 value path) for every byte, checked with
+    exact rationals (the kernel's glimpse taps use it instead of an LDS table)."""
+    from fractions import Fraction
+
+    def round_f32(fr):
+        c = np.float32(float(fr))
+        best = None
+        for k in range(-2, 3):
+            v = c
+            for _ in range(abs(k)):
+                v = np.nextafter(v, np.float32(np.inf if k > 0 else -np.inf))
+            err = abs(Fraction(float(v)) - fr)
+            even = (np.array(v, dtype=np.float32).view(np.uint32) & 1) == 0
+            if best is None or err < best[0] or (err == best[0] and even):
+                best = (err, float(v))
+        return best[1]
+
+    c_hi, c_lo = float.fromhex("0x1.010102p-8"), float.fromhex("-0x1.fdfdfep-33")
+    assert float(np.float32(c_hi)) == c_hi and float(np.float32(c_lo)) == c_lo
+    for v in range(256):
+        p = round_f32(Fraction(v) * Fraction(c_lo))
+        got = round_f32(Fraction(v) * Fraction(c_hi) + Fraction(p))
+        assert got == round_f32(Fraction(v, 255)) == float(np.float32(v / 255.0)), v
