@@ -472,7 +472,7 @@ __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_stat
 }
 
 struct StepParams {
-  int n, h, w, wpr, beams, step_limit, is_static, R, wrows, log_stats, sparse, row;
+  int n, h, w, wpr, beams, step_limit, is_static, R, wrows, log_stats, sparse, row, wlo, whi;
   float range, loss_scale, loss_offset;
 };
 
@@ -672,7 +672,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       const int r = tid + k * T;
       const int el = r / MAX_WIN_ROWS, row = r - el * MAX_WIN_ROWS;
       wv[k] = 0;
-      if (base + el < P.n) {
+      if (base + el < P.n && row >= P.wlo && row < P.whi) {  // rows outside [wlo, whi) are never read
         const float wpx = S.pos[2 * (base + el)], wpy = S.pos[2 * (base + el) + 1];
         const int y = (int)floorf(wpy) - 15 + row;
         if ((unsigned)y < (unsigned)P.h)
@@ -1514,6 +1514,10 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   P.is_static = cfg->is_static;
   P.R = (int)ceilf(cfg->lidar_range);
   P.wrows = MAX_WIN_ROWS;
+  // window rows a step can read (see load_windows): map rows [floor(p0) - R - 5, floor(p0) + R + 5] are the cells
+  // of its scans, plus two rows for the walk's one-crossing-ahead row reads past the segment's end
+  P.wlo = std::max(0, 15 - (P.R + 5) - 2);
+  P.whi = std::min(MAX_WIN_ROWS, 15 + (P.R + 5) + 2 + 1);
   P.range = cfg->lidar_range;
   P.loss_scale = cfg->loss_scale;
   P.loss_offset = cfg->loss_offset;
