@@ -130,9 +130,10 @@ APG_DEV uint32_t glimpse_pixel(const GlimpseGeo &g, const void *pool, const floa
 // A batch of n draws from ONE numpy stream, spread over the chip: every thread jumps to its own
 // stretch of FILL_PER_THREAD words of the stream (pcg_advance) and walks it.  integers() rejects
 // candidates (Lemire), so output i is the i-th accepted candidate: k_fill_count counts per thread,
-// k_fill_write places each thread's accepted draws at its prefix, k_fill_finish advances the
-// generator state past the consumed words (and, if the candidates ran out, which is astronomically
-// rare for the sizes used, finishes sequentially).
+// k_fill_write places each thread's accepted draws at its prefix, and its last workgroup to finish (a
+// ticket counter in work[0], left at zero) advances the generator state past the consumed words (and, if
+// the candidates ran out, which is astronomically rare for the sizes used, finishes sequentially) once
+// every workgroup has read the state.  Uniform draws finish the same way when given a counter.
 constexpr int FILL_THREADS = 256;
 constexpr int FILL_PER_THREAD = 32;
 constexpr int FILL_PER_BLOCK = FILL_THREADS * FILL_PER_THREAD;
@@ -148,12 +149,31 @@ struct FillArgs {
   int nblocks;
 };
 
-// work layout (int64): [nblocks] block totals, [nblocks * FILL_THREADS] thread counts, consumed
-APG_DEV int64_t *fill_consumed(int64_t *work, int nblocks) { return work + (size_t)nblocks * (FILL_THREADS + 1); }
+// work layout (int64): the finishing ticket counter, then (`wk` = work + 1) [nblocks] block totals,
+// [nblocks * FILL_THREADS] thread counts, consumed
+APG_DEV int64_t *fill_consumed(int64_t *wk, int nblocks) { return wk + (size_t)nblocks * (FILL_THREADS + 1); }
 
 int64_t fill_work_elems(int64_t cand) {
   const int64_t nb = (cand + FILL_PER_BLOCK - 1) / FILL_PER_BLOCK;
-  return nb * (FILL_THREADS + 1) + 1;
+  return 1 + nb * (FILL_THREADS + 1) + 1;
+}
+
+// true in exactly one thread of the grid: thread 0 of the last workgroup to get here (every workgroup calls
+// it, all of its threads; the counter returns to zero).  Whatever the grid wrote before is visible to it.
+APG_DEV bool last_block_done(int64_t *counter) {
+  __shared__ bool s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned long long t = atomicAdd(reinterpret_cast<unsigned long long *>(counter), 1ULL);
+    s_last = t == (unsigned long long)(gridDim.x - 1);
+    if (s_last) {
+      __threadfence();
+      *counter = 0;
+    }
+  }
+  __syncthreads();
+  return s_last && threadIdx.x == 0;
 }
 
 struct LemireSpec {
@@ -178,17 +198,25 @@ APG_DEV int64_t lemire_value(const LemireSpec &l, uint32_t u) {
   return (int64_t)(l.full ? (uint64_t)u : (((uint64_t)u * l.rex) >> 32));
 }
 
-__global__ __launch_bounds__(FILL_THREADS) void k_fill_uniform(const apg_pcg64 *st, FillArgs a, double *out) {
+// counter != nullptr: the last workgroup advances the state (else k_fill_uniform_finish does)
+__global__ __launch_bounds__(FILL_THREADS) void k_fill_uniform(apg_pcg64 *st, FillArgs a, double *out,
+                                                               int64_t *counter) {
   // random_uniform: off + scale * next_double, one next64 per value, C order over (n, cols)
   const int64_t m = a.n * a.cols;
   const int64_t k0 = ((int64_t)blockIdx.x * FILL_THREADS + threadIdx.x) * FILL_PER_THREAD;
-  if (k0 >= m) return;
-  const int64_t k1 = k0 + FILL_PER_THREAD < m ? k0 + FILL_PER_THREAD : m;
-  Pcg64 r = *reinterpret_cast<const Pcg64 *>(st);
-  pcg_advance(r, (uint64_t)k0);
-  for (int64_t k = k0; k < k1; k++) {
-    const int c = a.cols == 1 ? 0 : (int)(k & 1);
-    out[k] = __dadd_rn(a.low[c], __dmul_rn(a.range[c], next_double(r)));
+  if (k0 < m) {
+    const int64_t k1 = k0 + FILL_PER_THREAD < m ? k0 + FILL_PER_THREAD : m;
+    Pcg64 r = *reinterpret_cast<const Pcg64 *>(st);
+    pcg_advance(r, (uint64_t)k0);
+    for (int64_t k = k0; k < k1; k++) {
+      const int c = a.cols == 1 ? 0 : (int)(k & 1);
+      out[k] = __dadd_rn(a.low[c], __dmul_rn(a.range[c], next_double(r)));
+    }
+  }
+  if (counter && last_block_done(counter)) {
+    Pcg64 r = *reinterpret_cast<const Pcg64 *>(st);
+    pcg_advance(r, (uint64_t)m);
+    *reinterpret_cast<Pcg64 *>(st) = r;
   }
 }
 
@@ -198,7 +226,8 @@ __global__ void k_fill_uniform_finish(apg_pcg64 *st, int64_t m) {
   *reinterpret_cast<Pcg64 *>(st) = r;
 }
 
-__global__ __launch_bounds__(FILL_THREADS) void k_fill_count(const apg_pcg64 *st, FillArgs a, int64_t *work) {
+__global__ __launch_bounds__(FILL_THREADS) void k_fill_count(const apg_pcg64 *st, FillArgs a, int64_t *work_all) {
+  int64_t *work = work_all + 1;
   __shared__ int s_sum[FILL_THREADS / 64];
   const LemireSpec l = lemire_spec(a.bound);
   const int64_t k0 = ((int64_t)blockIdx.x * FILL_THREADS + threadIdx.x) * FILL_PER_THREAD;
@@ -220,8 +249,11 @@ __global__ __launch_bounds__(FILL_THREADS) void k_fill_count(const apg_pcg64 *st
   }
 }
 
-__global__ __launch_bounds__(FILL_THREADS) void k_fill_write(const apg_pcg64 *st, FillArgs a, int64_t *out,
-                                                             int64_t *work) {
+APG_DEV void fill_finish(apg_pcg64 *st, const FillArgs &a, int64_t *out, int64_t *work);
+
+__global__ __launch_bounds__(FILL_THREADS) void k_fill_write(apg_pcg64 *st, FillArgs a, int64_t *out,
+                                                             int64_t *work_all) {
+  int64_t *work = work_all + 1;
   __shared__ int64_t s_wave[FILL_THREADS / 64];
   __shared__ int64_t s_base;
   const LemireSpec l = lemire_spec(a.bound);
@@ -242,20 +274,22 @@ __global__ __launch_bounds__(FILL_THREADS) void k_fill_write(const apg_pcg64 *st
   int64_t q = s_base + inc - cnt;
   for (int w = 0; w < wave; w++) q += s_wave[w];
   const int64_t k0 = ((int64_t)blockIdx.x * FILL_THREADS + threadIdx.x) * FILL_PER_THREAD;
-  if (cnt == 0 || q >= a.n) return;
-  const int64_t k1 = k0 + FILL_PER_THREAD < a.cand ? k0 + FILL_PER_THREAD : a.cand;
-  Next32Walker wk(*reinterpret_cast<const Pcg64 *>(st), (uint64_t)k0);
-  for (int64_t k = k0; k < k1 && q < a.n; k++) {
-    const uint32_t u = wk.next();
-    if (lemire_accept(l, u)) {
-      out[q] = a.lo + lemire_value(l, u);
-      if (q == a.n - 1) *fill_consumed(work, a.nblocks) = k + 1;
-      q++;
+  if (cnt != 0 && q < a.n) {
+    const int64_t k1 = k0 + FILL_PER_THREAD < a.cand ? k0 + FILL_PER_THREAD : a.cand;
+    Next32Walker wk(*reinterpret_cast<const Pcg64 *>(st), (uint64_t)k0);
+    for (int64_t k = k0; k < k1 && q < a.n; k++) {
+      const uint32_t u = wk.next();
+      if (lemire_accept(l, u)) {
+        out[q] = a.lo + lemire_value(l, u);
+        if (q == a.n - 1) *fill_consumed(work, a.nblocks) = k + 1;
+        q++;
+      }
     }
   }
+  if (last_block_done(work_all)) fill_finish(st, a, out, work);
 }
 
-__global__ void k_fill_finish(apg_pcg64 *st, FillArgs a, int64_t *out, int64_t *work) {
+APG_DEV void fill_finish(apg_pcg64 *st, const FillArgs &a, int64_t *out, int64_t *work) {
   const LemireSpec l = lemire_spec(a.bound);
   const Pcg64 base = *reinterpret_cast<const Pcg64 *>(st);
   int64_t total = 0;
@@ -876,8 +910,10 @@ APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const EnvIn &in, doub
   if (err) atomicOr(out.err, err);
 }
 
-// One launch per ordinary (non-reset) step: a workgroup computes the glimpses of its `nu` envs at their new
-// positions (gs_axes / gs_pixels) and runs their env steps (loc_env / cls1_env: loss, stats, move).  KIND:
+// One launch per step: a workgroup computes the glimpses of its `nu` envs at their new positions (gs_axes /
+// gs_pixels) and runs their env steps (loc_env / cls1_env: loss, stats, move).  On the batch autoreset step
+// (a.resetting, after module_reset's draws and gather) nothing moves: the glimpses are taken at the new batch's
+// start positions, as observe() does.  KIND:
 // APG_IMAGE_LOCALIZE, or APG_IMAGE_CLASSIFY with K <= CLS1_MAX_K (logits staged in LDS with coalesced loads,
 // one thread per env as k_image_env_cls1).
 // ENVW: the workgroup is GS_THREADS glimpse threads plus one env wave.  The env wave loads the env inputs,
@@ -916,7 +952,7 @@ __attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fuse
       in = load_env_in<KIND>(a, e, act, pred, label, pos, out);
       s_base[r] = index[e] * g.img_elems;
       double px = in.px, py = in.py;
-      move_pos(a, in.a0, in.a1, px, py);
+      if (!a.resetting) move_pos(a, in.a0, in.a1, px, py);  // the autoreset step observes the new batch in place
       s_npos[r][0] = px;
       s_npos[r][1] = py;
     }
@@ -1384,12 +1420,12 @@ int launch_integers(apg_pcg64 *state, int64_t n, int64_t lo, uint64_t bound, int
   a.nblocks = grid_for(a.cand, FILL_PER_BLOCK);
   hipLaunchKernelGGL(k_fill_count, dim3(a.nblocks), dim3(FILL_THREADS), 0, s, state, a, work);
   hipLaunchKernelGGL(k_fill_write, dim3(a.nblocks), dim3(FILL_THREADS), 0, s, state, a, out, work);
-  hipLaunchKernelGGL(k_fill_finish, dim3(1), dim3(1), 0, s, state, a, out, work);
   return check_launch("k_fill_*");
 }
 
+// counter: a zeroed int64 the last workgroup uses to finish in the same launch (left at zero), or nullptr
 int launch_uniform(apg_pcg64 *state, int64_t n, int cols, const double *low, const double *range, double *out,
-                   hipStream_t s) {
+                   hipStream_t s, int64_t *counter = nullptr) {
   if (n <= 0) return APG_OK;
   FillArgs a{};
   a.kind = APG_DRAW_UNIFORM;
@@ -1400,8 +1436,9 @@ int launch_uniform(apg_pcg64 *state, int64_t n, int cols, const double *low, con
     a.range[c] = range[c];
   }
   const int64_t m = n * cols;
-  hipLaunchKernelGGL(k_fill_uniform, dim3(grid_for(m, FILL_PER_BLOCK)), dim3(FILL_THREADS), 0, s, state, a, out);
-  hipLaunchKernelGGL(k_fill_uniform_finish, dim3(1), dim3(1), 0, s, state, m);
+  hipLaunchKernelGGL(k_fill_uniform, dim3(grid_for(m, FILL_PER_BLOCK)), dim3(FILL_THREADS), 0, s, state, a, out,
+                     counter);
+  if (!counter) hipLaunchKernelGGL(k_fill_uniform_finish, dim3(1), dim3(1), 0, s, state, m);
   return check_launch("k_fill_uniform");
 }
 
@@ -1556,7 +1593,7 @@ int apg_rng_fill(apg_pcg64 *state, int kind, int64_t n, int cols, const double *
   hipStream_t s = (hipStream_t)stream;
   if (kind == APG_DRAW_UNIFORM) {
     if (cols < 1 || cols > 2 || !low || !range) return fail(APG_E_INVALID, "uniform draws need 1 or 2 columns");
-    return launch_uniform(state, n, cols, low, range, static_cast<double *>(out), s);
+    return launch_uniform(state, n, cols, low, range, static_cast<double *>(out), s, work);
   }
   if (kind == APG_DRAW_INTEGERS) {
     if (bound < 1 || bound > 0x100000000ULL) return fail(APG_E_INVALID, "integers range must be in [1, 2**32]");
@@ -1583,7 +1620,7 @@ static int module_reset(const apg_image_config *c, const apg_image_state *st, co
   if (c->invert_labels && (rc = launch_integers(st->rng + 1, nt, 0, 2, inv_draw, st->rng_work, s))) return rc;
   // current_rng.uniform(-1, 1, size=(N, 2))
   const double low[2] = {-1.0, -1.0}, range[2] = {2.0, 2.0};
-  if ((rc = launch_uniform(st->rng + 1, nt, 2, low, range, st->scratch_f64, s))) return rc;
+  if ((rc = launch_uniform(st->rng + 1, nt, 2, low, range, st->scratch_f64, s, st->rng_work))) return rc;
   hipLaunchKernelGGL(k_image_gather, dim3(grid_for(n, 256)), dim3(256), 0, s, n, c->env_offset, st->pool_labels,
                      idx_draw, c->invert_labels, inv_draw, st->scratch_f64, c->num_classes, st->index, st->label,
                      st->inverted, st->pos);
@@ -1616,7 +1653,7 @@ int apg_image_reset(const apg_image_config *c, const apg_image_state *st, const 
     if ((rc = launch_integers(st->rng + 1, nt, 0, (uint64_t)c->top_k, st->scratch_i64, st->rng_work, s))) return rc;
     const double low[2] = {-c->cell[0], -c->cell[1]};
     const double range[2] = {c->cell[0] - -c->cell[0], c->cell[1] - -c->cell[1]};
-    if ((rc = launch_uniform(st->rng + 1, nt, 2, low, range, st->scratch_f64, s))) return rc;
+    if ((rc = launch_uniform(st->rng + 1, nt, 2, low, range, st->scratch_f64, s, st->rng_work))) return rc;
     hipLaunchKernelGGL(k_unique_finish, dim3(grid_for(n, 256)), dim3(256), 0, s, n, c->env_offset, c->top_k,
                        st->top_k, st->scratch_i64, st->unique_grid, st->scratch_f64, st->target);
     if ((rc = check_launch("k_unique_finish"))) return rc;
@@ -1642,7 +1679,8 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
     // prediction_target = target.copy(); target[prev_done] = np_random.uniform(-1, 1, (k, 2)) as f32
     if (prev_done) {
       const double low[2] = {-1.0, -1.0}, range[2] = {2.0, 2.0};
-      if ((rc = launch_uniform(st->rng + 0, c->num_envs_total, 2, low, range, st->scratch_f64, s))) return rc;
+      if ((rc = launch_uniform(st->rng + 0, c->num_envs_total, 2, low, range, st->scratch_f64, s, st->rng_work)))
+        return rc;
     }
     if (prev_done) {  // otherwise the copy is folded into k_image_env_loc
       hipLaunchKernelGGL(k_loc_target, dim3(grid_for(n, 256)), dim3(256), 0, s, n, c->env_offset, prev_done,
@@ -1673,7 +1711,7 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
   static const bool unfused = getenv("APG_IMAGE_UNFUSED") != nullptr, generic = getenv("APG_GLIMPSE_GENERIC") != nullptr,
                     lanes8 = getenv("APG_CLS_LANES8") != nullptr;
   const GlimpseGeo g = make_geo(c);
-  const bool fusable = !prev_done && !unfused && !generic && !lanes8 && g.s0 <= GS_MAX_SIDE && g.s1 <= GS_MAX_SIDE &&
+  const bool fusable = !unfused && !generic && !lanes8 && g.s0 <= GS_MAX_SIDE && g.s1 <= GS_MAX_SIDE &&
                        (c->kind == APG_IMAGE_LOCALIZE || c->num_classes <= CLS1_MAX_K);
   if (fusable) {
     const int per = g.s0 * g.s1;
@@ -1717,7 +1755,10 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
     else APG_FUSED_KIND(APG_IMAGE_CLASSIFY);
 #undef APG_FUSED_KIND
 #undef APG_FUSED
-    return check_launch("k_image_step_fused");  // the target glimpse only changes on the autoreset step
+    if ((rc = check_launch("k_image_step_fused"))) return rc;
+    // the target glimpse only changes with the target and the images, i.e. on the autoreset step
+    if (!prev_done || c->kind != APG_IMAGE_LOCALIZE) return APG_OK;
+    return launch_glimpse<float>(g, st->pool, st->index, st->target, n, 1, out->target_glimpse, out->err, s);
   }
   if (c->kind == APG_IMAGE_CLASSIFY && c->num_classes <= CLS1_MAX_K && !lanes8) {
     const size_t lds = (size_t)CLS1_ENVS * (c->num_classes + 2) * sizeof(float);

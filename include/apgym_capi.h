@@ -228,7 +228,9 @@ int apg_rng_draws(const uint64_t *seeds, int m, int kind, int64_t a, int64_t b, 
 
 /* n draws (n x cols for uniform, cols <= 2) from the ONE stream *state (device), advancing it
  * exactly as numpy would.  integers: bound = hi - lo (exclusive range, 1 <= bound <= 2**32) and
- * `work` holds apg_rng_fill_work_elems(n, bound) int64 (device; unused for uniform draws). */
+ * `work` holds apg_rng_fill_work_elems(n, bound) int64 (device), zeroed before its first use and left zeroed
+ * (work[0] counts the finished workgroups, so the last one advances the generator state in the same launch);
+ * uniform draws use only work[0] and accept work == NULL (then a second launch advances the state). */
 int64_t apg_rng_fill_work_elems(int64_t n, uint64_t bound);
 int apg_rng_fill(apg_pcg64 *state, int kind, int64_t n, int cols, const double *low, const double *range,
                  int64_t lo, uint64_t bound, void *out, int64_t *work, apg_stream_t stream);
