@@ -105,6 +105,49 @@ def row_views_np(buf: np.ndarray, layout) -> dict:
     return v
 
 
+# The numpy backend's output block: the same fields in the dense layout (field-major, each contiguous and
+# 256-byte aligned) inside one buffer, so a step's outputs come to the host in ONE D2H copy and every host
+# field is a contiguous array (its copy a plain memcpy; packed rows would need strided gathers).
+def lidar_output_block_layout(num_envs: int, beams: int, log_stats: bool = False, sparse: bool = False):
+    """[(name, torch dtype, shape, byte offset)] of the field-major output block, and its size."""
+    import torch
+
+    n = num_envs
+    f64, i64, f32, i32, b8 = torch.float64, torch.int64, torch.float32, torch.int32, torch.bool
+    fields = [("reward", f64, (n,)), ("map_idx_out", i64, (n,))] + ([("weight", f64, (n,))] if sparse else []) + [
+        ("lidar", f32, (n, beams)), ("odometry", f32, (n, 2)), ("target", f32, (n, 2)), ("time_step", f32, (n,)),
+        ("base_reward", f32, (n,)), ("loss", f32, (n,))] + (
+        [("stats", f32, (4, n)), ("stats_len", i32, (n,))] if log_stats else []) + [
+        ("terminated", b8, (n,)), ("truncated", b8, (n,)), ("info_mask", b8, (n,)), ("reset_mask", b8, (n,))]
+    out, off = [], 0
+    for name, dt, sh in fields:
+        out.append((name, dt, sh, off))
+        off += torch.empty((), dtype=dt).element_size() * int(np.prod(sh, dtype=np.int64))
+        off += (-off) % 256
+    return out, off
+
+
+def block_views(buf, layout) -> dict:
+    """Field views of a flat uint8 output block (torch or numpy)."""
+    v = {}
+    for name, dt, sh, off in layout:
+        if isinstance(buf, np.ndarray):
+            import torch
+
+            npdt = torch.empty((), dtype=dt).numpy().dtype
+            v[name] = buf[off:off + npdt.itemsize * int(np.prod(sh, dtype=np.int64))].view(npdt).reshape(sh)
+        else:
+            nb = torch_elem(dt) * int(np.prod(sh, dtype=np.int64))
+            v[name] = buf[off:off + nb].view(dt).view(sh)
+    return v
+
+
+def torch_elem(dt) -> int:
+    import torch
+
+    return torch.empty((), dtype=dt).element_size()
+
+
 def torch_index(idx: np.ndarray, device):
     import torch
 
@@ -177,8 +220,7 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         p = dataset.native_params()
         scale, offset = affine_f32(inner_loss)
         self.output_layout, row_bytes = lidar_output_row_layout(self.lidar_beam_count, self.log_stats, self.sparse)
-        # the numpy backend always uses the packed rows: one D2H copy per step for every per-env output
-        if not (packed_outputs or array_backend == "numpy"):
+        if not packed_outputs:
             self.output_layout, row_bytes = None, 0
         self._cfg = N.LidarConfig(num_envs=self.num_envs, height=h, width=w, map_kind=dataset.map_kind,
                                   is_static=int(self.static_map), static_map_index=int(static_map_index),
@@ -227,9 +269,14 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         )
         # packed_outputs: the per-env outputs are field views of one [n, row] buffer (ShardedVectorEnv's send)
         self.output_rows = None
+        self._out_block = self._block_layout = None
         if row_bytes:
             self.output_rows = t.zeros((n, row_bytes), dtype=t.uint8, device=dev)
             self._t.update(row_views(self.output_rows, self.output_layout))
+        elif array_backend == "numpy":  # dense fields inside one block: one D2H copy per step (_host_rows)
+            self._block_layout, nbytes = lidar_output_block_layout(n, B, self.log_stats, self.sparse)
+            self._out_block = t.zeros(nbytes, dtype=t.uint8, device=dev)
+            self._t.update(block_views(self._out_block, self._block_layout))
         T = self._t
         self._state = N.LidarState(*[N.ptr(T[k]) for k in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng",
                                                             "occ", "scratch", "stack", "map_idx", "beam_dirs",
@@ -602,14 +649,17 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         return obs
 
     def _host_rows(self) -> dict:
-        """numpy backend: the packed output rows and the error word copied D2H into pinned host memory in one
-        go, then one synchronize; returns numpy field views of the host rows (valid until the next call)."""
+        """numpy backend: the output block (or the packed output rows) and the error word copied D2H into pinned
+        host memory in one go, then one synchronize; returns numpy field views of the host copy (valid until the
+        next call)."""
         import torch
 
+        src = self.output_rows if self._out_block is None else self._out_block
         if self._rows_host is None:
-            self._rows_host = torch.empty(tuple(self.output_rows.shape), dtype=torch.uint8).pin_memory()
-            self._rows_np = row_views_np(self._rows_host.numpy(), self.output_layout)
-        self._rows_host.copy_(self.output_rows, non_blocking=True)
+            self._rows_host = torch.empty(tuple(src.shape), dtype=torch.uint8).pin_memory()
+            self._rows_np = (row_views_np(self._rows_host.numpy(), self.output_layout) if self._out_block is None
+                             else block_views(self._rows_host.numpy(), self._block_layout))
+        self._rows_host.copy_(src, non_blocking=True)
         self._err_host.copy_(self._t["err"], non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
         self._err_pending = False
@@ -681,7 +731,7 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             self._t = {}
             self._h = None  # the op handle keeps every state/output buffer alive
             self._c_args = None
-            self.output_rows = None
+            self.output_rows = self._out_block = None
 
     def __repr__(self):
         kind = "maze" if isinstance(self.dataset, FloorMapDatasetMaze) else "rooms"
