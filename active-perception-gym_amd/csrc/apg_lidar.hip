@@ -1082,7 +1082,11 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
     }
     return;
   }
-  for (int beam = tid / EPB; beam < P.beams; beam += T / EPB) {
+  // the wave's walk flags first (bit it of wbits: iteration it's beam), then ONE queue reservation per wave
+  // (an LDS atomic per beam iteration serialized the waves' pre-tests), then the entries, grouped by beam
+  uint32_t wbits = 0;
+  int wtot = 0;  // wave-uniform
+  for (int beam = tid / EPB, it = 0; beam < P.beams; beam += T / EPB, it++) {
     bool walk = false;
     if (e < P.n) {
       const float dy = s_dirs[beam][1];
@@ -1098,11 +1102,19 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         s_lid[el * LS + beam] = k < (uint32_t)EMPTY_TAB ? s_tab[k] : beam_value(f32_sqrt(s2));
       }
     }
-    const unsigned long long m = __ballot(walk);
+    wbits |= walk ? 1u << it : 0u;
+    wtot += __popcll(__ballot(walk));
+  }
+  {
     int qbase = 0;
-    if (lane == 0 && m) qbase = atomicAdd(&s_cnt[1], __popcll(m));
+    if (lane == 0 && wtot) qbase = atomicAdd(&s_cnt[1], wtot);
     qbase = __shfl(qbase, 0);
-    if (walk) s_queue[qbase + __popcll(m & ((1ULL << lane) - 1ULL))] = (uint16_t)((beam << 8) | el);
+    for (int beam = tid / EPB, it = 0; beam < P.beams && wtot; beam += T / EPB, it++) {
+      const bool walk = (wbits >> it) & 1u;
+      const unsigned long long m = __ballot(walk);
+      if (walk) s_queue[qbase + __popcll(m & ((1ULL << lane) - 1ULL))] = (uint16_t)((beam << 8) | el);
+      qbase += __popcll(m);
+    }
   }
   __syncthreads();
   STEP_MARK(3)
