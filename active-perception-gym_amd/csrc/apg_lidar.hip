@@ -1139,15 +1139,31 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   STEP_MARK(4)
   STEP_STOP(4)
   const int nenv = P.n - base < EPB ? P.n - base : EPB;
-  const int B = P.beams, dl = T / B, db = T - dl * B;  // (env, beam) of element i advanced without divisions
-  int l = tid / B, beam = tid - l * B;
-  for (int i = tid; i < nenv * B; i += T) {
-    oat(O.lidar, P.row, base + l, B, beam) = s_lid[l * LS + beam];
-    l += dl;
-    beam += db;
-    if (beam >= B) {
-      beam -= B;
-      l++;
+  if (!ROWP && (P.beams & 3) == 0) {  // dense rows (16-B aligned): four beams per 16-byte store
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const int B4 = P.beams >> 2, dl = T / B4, db = T - dl * B4;
+    int l = tid / B4, b4 = tid - l * B4;
+    for (int i = tid; i < nenv * B4; i += T) {
+      const float *src = s_lid + l * LS + 4 * b4;
+      *reinterpret_cast<f4 *>(O.lidar + (size_t)(base + l) * P.beams + 4 * b4) = f4{src[0], src[1], src[2], src[3]};
+      l += dl;
+      b4 += db;
+      if (b4 >= B4) {
+        b4 -= B4;
+        l++;
+      }
+    }
+  } else {
+    const int B = P.beams, dl = T / B, db = T - dl * B;  // (env, beam) of element i advanced without divisions
+    int l = tid / B, beam = tid - l * B;
+    for (int i = tid; i < nenv * B; i += T) {
+      oat(O.lidar, P.row, base + l, B, beam) = s_lid[l * LS + beam];
+      l += dl;
+      beam += db;
+      if (beam >= B) {
+        beam -= B;
+        l++;
+      }
     }
   }
 #ifdef APG_STEP_PROFILE
