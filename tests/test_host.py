@@ -302,3 +302,28 @@ def test_u8_tap_value_pair_is_exact():
         p = round_f32(Fraction(v) * Fraction(c_lo))
         got = round_f32(Fraction(v) * Fraction(c_hi) + Fraction(p))
         assert got == round_f32(Fraction(v, 255)) == float(np.float32(v / 255.0)), v
+
+
+def test_lidar_output_block_layout():
+    """The numpy backend's field-major output block: every field 256-byte aligned, contiguous, disjoint, and
+    views of one buffer (torch and numpy) that alias the same bytes."""
+    import torch
+
+    from ap_gym_amd.lidar_env import block_views, lidar_output_block_layout
+
+    for n, beams, stats, sparse in ((1, 8, False, False), (1000, 32, True, True), (65536, 64, True, False)):
+        layout, nbytes = lidar_output_block_layout(n, beams, stats, sparse)
+        names = [f[0] for f in layout]
+        assert ("stats" in names) == stats and ("weight" in names) == sparse and "lidar" in names
+        end = 0
+        for name, dt, shape, off in layout:
+            assert off % 256 == 0 and off >= end
+            end = off + torch.empty((), dtype=dt).element_size() * int(np.prod(shape))
+        assert end <= nbytes and nbytes % 256 == 0
+        if n <= 1000:
+            buf = torch.zeros(nbytes, dtype=torch.uint8)
+            tv, nv = block_views(buf, layout), block_views(buf.numpy(), layout)
+            tv["lidar"][-1, -1] = 2.5
+            tv["reward"][0] = -1.25
+            assert nv["lidar"][-1, -1] == 2.5 and nv["reward"][0] == -1.25
+            assert all(v.is_contiguous() for v in tv.values()) and all(v.flags.c_contiguous for v in nv.values())
