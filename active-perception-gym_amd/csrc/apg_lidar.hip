@@ -116,7 +116,7 @@ int validate(const apg_lidar_config *c) {
   } else if (c->map_kind == APG_MAP_MAZE) {
     if ((c->height % 2) == 0 || (c->width % 2) == 0)
       return fail(APG_E_INVALID, "Width and height must be odd.");
-    if (c->height > 127 || c->width > 127) return fail(APG_E_INVALID, "maze maps must be at most 127 x 127");
+    if (c->height > 255 || c->width > 255) return fail(APG_E_INVALID, "maze maps must be at most 255 x 255");
   } else {
     return fail(APG_E_INVALID, "unknown map kind");
   }
@@ -313,6 +313,7 @@ APG_DEV uint64_t maze_index(const apg_lidar_state &S, const uint64_t *idx, int i
 // generate the items (MZ_ITEM_GROUPS groups of 32 outputs each) and the state after the last one.  Full
 // occupancy, so the LCG work that held the DFS at one wave per SIMD runs at chip rate here.
 constexpr int MZS_THREADS = 256, MZS_MAZES = 64;
+static_assert(MZ_MAX_ITEMS + 1 <= MZS_THREADS - MZS_MAZES, "a jump-table entry per thread after the seeding ones");
 __global__ __launch_bounds__(MZS_THREADS) void k_maze_stream(Geo g, apg_lidar_state S, const uint64_t *idx, int n,
                                                              uint8_t *scratch, int mode, uint64_t seed, int use_seed,
                                                              int all, int ng) {
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(MZS_THREADS) void k_maze_stream(Geo g, apg_lidar_st
     } else {
       s_seed[tid][2] = s_seed[tid][3] = 0ULL;  // inactive: increments are odd, 0 never is one
     }
-  } else if (tid - MZS_MAZES <= nitems) {
+  } else if (tid - MZS_MAZES <= nitems) {  // nitems <= MZ_MAX_ITEMS = MZS_THREADS - MZS_MAZES - 1
     s_jump[tid - MZS_MAZES] = mz_jump((uint64_t)(tid - MZS_MAZES) * MZ_ITEM_GROUPS * MZ_GROUP);
   }
   __syncthreads();
@@ -417,7 +418,7 @@ __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_stat
       continue;
     }
     if (map_obs) bitmap_map_obs<MP_THREADS>(s_bm, g.h, g.w, g.wpr, map_obs + (size_t)e * g.h * g.w, tid);
-    // free cells per row, their inclusive scan (rows <= 128: two waves), the row holding the pick
+    // free cells per row, their inclusive scan (rows <= MP_THREADS = 256: one per thread), the row holding the pick
     int fr = 0;
     if (tid < g.h) {
       int oc = 0;
@@ -428,8 +429,13 @@ __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_stat
     if (lane == 63) s_wsum[wave] = incl_w;
     if (tid == 0) s_hit[0] = -1;
     __syncthreads();
-    const int incl = incl_w + (wave == 1 ? s_wsum[0] : 0), excl = incl - fr;
-    const int nfree = s_wsum[0] + s_wsum[1];
+    int before = 0, nfree = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < MP_THREADS / 64; w2++) {
+      before += w2 < wave ? s_wsum[w2] : 0;
+      nfree += s_wsum[w2];
+    }
+    const int incl = incl_w + before, excl = incl - fr;
     Pcg64 rng, it;
     const uint64_t midx = maze_index(S, idx, e, mode, seed, use_seed, rng, it);
     const long long pick = nfree > 0 ? (long long)integers(rng, 0, nfree) : -1;  // every thread: same draw

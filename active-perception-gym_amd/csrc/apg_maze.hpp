@@ -60,7 +60,7 @@ APG_DEV uint32_t mz_perm_of(uint32_t pidx) {
 // from there in the memory phase).
 constexpr int MZ_GROUP = 32;       // outputs per stream group
 constexpr int MZ_ITEM_GROUPS = 8;  // groups per k_maze_stream item (one jump)
-constexpr int MZ_MAX_ITEMS = 63;   // items per maze (+ 1 for the end state) within one 64-entry jump table
+constexpr int MZ_MAX_ITEMS = 191;  // items per maze (+ 1 for the end state): k_maze_stream's 192 jump threads (255 x 255: 114)
 
 __host__ __device__ inline int maze_stream_groups(int h, int w) {
   const int cells = ((w - 1) / 2) * ((h - 1) / 2);

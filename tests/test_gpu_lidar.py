@@ -76,7 +76,8 @@ def test_device_maps_match_oracle_random_idx(gpu, oracle_mod, kind, size, count)
 
 
 @pytest.mark.parametrize("h,w,bp,count", [(21, 21, 0.5, 512), (21, 35, 0.0, 512), (63, 63, 0.3, 256),
-                                           (127, 127, 0.7, 64), (3, 3, 1.0, 16), (127, 9, 1.0, 64)])
+                                           (127, 127, 0.7, 64), (3, 3, 1.0, 16), (127, 9, 1.0, 64),
+                                           (255, 255, 1.0, 32), (255, 101, 0.6, 32)])
 def test_device_maze_branching_matches_oracle(gpu, oracle_mod, h, w, bp, count):
     """branching_prob < 1 (rng.random() draws decide later branches; mazes need not be perfect, so the
     stream consumption differs from the bp = 1 mazes the stream length is sized for) and odd rectangles."""
@@ -307,6 +308,7 @@ def test_vector_env_matches_reference_trace(gpu, name):
 @pytest.mark.parametrize("kind,size,beams,n,steps,sparse", [("rooms", 64, 32, 1024, 230, False),
                                                             ("maze", 21, 8, 1024, 120, False),
                                                             ("maze", 127, 64, 64, 40, False),
+                                                            ("maze", 255, 32, 32, 110, False),
                                                             ("rooms", 32, 16, 512, 120, False),
                                                             ("rooms", 64, 32, 1024, 120, True)])
 def test_vector_env_matches_oracle(gpu, oracle_mod, kind, size, beams, n, steps, sparse):
