@@ -310,6 +310,7 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         self._err_pending = False
         self._autoreset_host = np.zeros(n, dtype=bool)
         self._rows_host = self._rows_np = self._map_host = None  # numpy backend: pinned host mirrors
+        self._in_host = self._in_dev = None  # numpy backend: pinned input staging and its device copy
         self._seeded = False
         self._closed = False
         self._kernel_events = None
@@ -553,8 +554,16 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             if bad_a.any() or bad_p.any():  # first offending sub-env decides, action checked first
                 i = int(np.argmax(bad_a | bad_p))
                 raise ValueError(NAN_ACTION_MSG if bad_a[i] else NAN_PREDICTION_MSG)
-            a_t = torch.from_numpy(a_np).to(self.device, non_blocking=True)
-            p_t = torch.from_numpy(p_np).to(self.device, non_blocking=True)
+            # one H2D copy of both inputs from a pinned staging buffer (the previous step synchronized, so neither
+            # the staging buffer nor the device copy is still in use)
+            if self._in_host is None:
+                self._in_host = torch.empty((2, self.num_envs, 2), dtype=torch.float32).pin_memory()
+                self._in_dev = torch.empty((2, self.num_envs, 2), dtype=torch.float32, device=self.device)
+            staged = self._in_host.numpy()
+            staged[0] = a_np
+            staged[1] = p_np
+            self._in_dev.copy_(self._in_host, non_blocking=True)
+            a_t, p_t = self._in_dev[0], self._in_dev[1]
         else:
             self.check_errors(block=False)
             a_t = N.as_device_f32(a, self._dev, 2 * self.num_envs, name="action")
