@@ -1151,7 +1151,8 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
     int l = tid / B4, b4 = tid - l * B4;
     for (int i = tid; i < nenv * B4; i += T) {
       const float *src = s_lid + l * LS + 4 * b4;
-      *reinterpret_cast<f4 *>(O.lidar + (size_t)(base + l) * P.beams + 4 * b4) = f4{src[0], src[1], src[2], src[3]};
+      __builtin_nontemporal_store(f4{src[0], src[1], src[2], src[3]},
+                                  reinterpret_cast<f4 *>(O.lidar + (size_t)(base + l) * P.beams + 4 * b4));
       l += dl;
       b4 += db;
       if (b4 >= B4) {
