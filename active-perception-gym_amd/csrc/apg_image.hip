@@ -453,7 +453,7 @@ APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, 
       };
       *reinterpret_cast<F3 *>(dst) = F3{res[0], res[1], res[2]};  // one 12-byte store per pixel
     } else {
-      dst[0] = res[0];
+      __builtin_nontemporal_store(res[0], dst);  // the glimpses are read by the consumer, not by this kernel
     }
   };
   if constexpr (F32) {
