@@ -20,8 +20,11 @@ from ap_gym_amd import _native as N  # noqa: E402
 
 n = int(os.environ.get("NENV", 65536))
 M = int(os.environ.get("MAP", 64))  # bench.py's workload: BASELINE config 2 (64x64 rooms, 32 beams)
-env = ap.make_vec("LIDARLocRooms-v0", num_envs=n, lidar_beam_count=32, dataset=ap.FloorMapDatasetRooms(M, M),
-                  array_backend="torch")
+KIND = os.environ.get("KIND", "rooms")  # maze: BASELINE config 3 (MAP=127 BEAMS=64 NENV=262144)
+B = int(os.environ.get("BEAMS", 32))
+ds = ap.FloorMapDatasetRooms(M, M) if KIND == "rooms" else ap.FloorMapDatasetMaze(M, M)
+env = ap.make_vec("LIDARLocRooms-v0" if KIND == "rooms" else "LIDARLocMaze-v0", num_envs=n, lidar_beam_count=B,
+                  dataset=ds, array_backend="torch")
 env.reset(seed=0)
 g = torch.Generator(device="cuda")
 g.manual_seed(0)
