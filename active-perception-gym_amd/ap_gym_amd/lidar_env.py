@@ -26,11 +26,16 @@ HBM plus one fused kernel launch per step (include/apgym_capi.h):
                   semantics
 
 Two I/O modes (constructor `array_backend`), inputs of either type are accepted:
-  "numpy" (default) -> numpy out, host copies and host-side NaN checks, like the reference
+  "numpy" (default) -> numpy out, host copies and host-side NaN checks, like the reference.  By default
+                       (copy=None -> True, SyncVectorEnv's default) no returned array is ever written
+                       again: obs["map"] is a read-only array shared by the steps between two steps with
+                       resets (the map obs changes only at resets; a step with resets returns a new
+                       array), every other field is a fresh copy.  copy=False returns the pinned host
+                       mirror of the map obs itself (writable, refreshed in place at resets)
   "torch"           -> torch out on the env's device, no host synchronisation.  Returned tensors
                        are persistent buffers overwritten by the next step (gymnasium's copy=False
-                       contract); pass copy=True to get fresh tensors.  NaN errors are raised
-                       lazily (at a later step) unless strict_errors=True.
+                       contract, the default here: copy=None -> False); pass copy=True to get fresh
+                       tensors.  NaN errors are raised lazily (at a later step) unless strict_errors=True.
 """
 
 from __future__ import annotations
@@ -181,9 +186,10 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
     def __init__(self, num_envs: int = 1, dataset: FloorMapDataset | None = None, render_mode: str = "rgb_array",
                  static_map: bool = False, lidar_beam_count: int = 8, lidar_range: float = 5,
                  static_map_index: int = 0, prefetch: bool = True, prefetch_buffer_size: int = 128,
-                 max_episode_steps: int = 100, device=None, env_offset: int = 0, copy: bool = False,
+                 max_episode_steps: int = 100, device=None, env_offset: int = 0, copy: bool | None = None,
                  strict_errors: bool = False, array_backend: str = "numpy", log_stats: bool = False,
-                 sparse: bool = False, render_envs=None, sparse_reset_info: bool = False, packed_outputs: bool = False):
+                 sparse: bool = False, render_envs=None, sparse_reset_info: bool = False, packed_outputs: bool = False,
+                 vector_stats: str = "list"):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -198,13 +204,16 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         self.lidar_range = lidar_range
         self.max_episode_steps = int(max_episode_steps)
         self.env_offset = int(env_offset)
-        self.copy = copy
-        self.strict_errors = strict_errors
-        self.log_stats = bool(log_stats)
-        self.sparse = bool(sparse)
-        self.sparse_reset_info = bool(sparse_reset_info)
         if array_backend not in ("numpy", "torch"):
             raise ValueError("array_backend must be 'numpy' or 'torch'")
+        self.copy = (array_backend == "numpy") if copy is None else bool(copy)
+        self.strict_errors = strict_errors
+        self.log_stats = bool(log_stats)
+        if vector_stats not in ("list", "array"):
+            raise ValueError("vector_stats must be 'list' (the reference's lists of np.float32) or 'array'")
+        self.vector_stats = vector_stats  # numpy backend: form of info["stats"]["vector"] entries
+        self.sparse = bool(sparse)
+        self.sparse_reset_info = bool(sparse_reset_info)
         self.array_backend = array_backend
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
@@ -310,6 +319,7 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         self._err_pending = False
         self._autoreset_host = np.zeros(n, dtype=bool)
         self._rows_host = self._rows_np = self._map_host = None  # numpy backend: pinned host mirrors
+        self._map_snapshot = None  # numpy backend, copy=True: read-only map obs shared until the next reset
         self._in_host = self._in_dev = None  # numpy backend: pinned input staging and its device copy
         self._seeded = False
         self._closed = False
@@ -638,10 +648,17 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             scalar[name] = np.where(done, st[j].astype(np.float64), 0.0)
             scalar["_" + name] = done.copy()
         vector: dict[str, Any] = {}
+        ln = lens[idx].tolist()
         for m, name in enumerate(("euclidean_distance", "mse")):
             arr = np.full(self.num_envs, None, dtype=object)
-            for row, i in enumerate(idx):
-                arr[i] = list(hist[row, m, :lens[i]])
+            hm = hist[:, m, :]
+            if self.vector_stats == "array":  # float32 views of one host block (opt-in: ndarray, not list)
+                rows = [r[:n] for r, n in zip(hm, ln)]
+            else:  # the reference's list of np.float32 (ActiveRegressionLogWrapper's deque -> list(v)):
+                # one np.float32 object per logged value, ~50 ns each, is what an episode end costs
+                rows = [list(r[:n]) for r, n in zip(hm, ln)]
+            for i, r in zip(idx.tolist(), rows):
+                arr[i] = r
             vector[name] = arr
             vector["_" + name] = done.copy()
         info["stats"] = {"scalar": scalar, "_scalar": done.copy(), "vector": vector, "_vector": done.copy()}
@@ -676,7 +693,10 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
 
     def _map_refresh(self, reset_mask: np.ndarray | None):
         """The host mirror of the map observation, refreshed only for the sub-envs that reset (the map obs
-        changes only then); None refreshes every sub-env.  Returned as is (copy=False) or copied."""
+        changes only then); None refreshes every sub-env.  copy=False: the mirror itself.  copy=True: a
+        read-only snapshot of it, taken again only when the mirror changed, so an array returned at step t
+        keeps its values after later autoresets (SyncVectorEnv(copy=True)) without a 4*H*W-byte host copy per
+        env on every step."""
         import torch
 
         if self.static_map:
@@ -685,13 +705,19 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         if self._map_host is None:
             self._map_host = torch.empty(tuple(T["map_obs"].shape), dtype=torch.float32).pin_memory()
             reset_mask = None
+        changed = reset_mask is None or bool(reset_mask.any())
         if reset_mask is None or reset_mask.all():
             self._map_host.copy_(T["map_obs"])
-        elif reset_mask.any():
+        elif changed:
             idx = np.nonzero(reset_mask)[0]
             self._map_host.numpy()[idx] = T["map_obs"][torch_index(idx, self.device)].cpu().numpy()
         m = self._map_host.numpy()
-        return m.copy() if self.copy else m
+        if not self.copy:
+            return m
+        if changed or self._map_snapshot is None:
+            self._map_snapshot = m.copy()
+            self._map_snapshot.flags.writeable = False
+        return self._map_snapshot
 
     def _to_numpy_obs(self, R: dict | None = None, reset_mask: np.ndarray | None = None):
         if R is None:

@@ -104,6 +104,13 @@ Geo make_geo(const apg_lidar_config *c) {
   return g;
 }
 
+// Bytes of a packed output row (apg_lidar_config.out_row_bytes): reward, map_idx (8 B each), weight (sparse),
+// lidar, odometry, target, time_step, base_reward, loss, stats + stats_len (log_stats), four flag bytes
+int min_row_bytes(const apg_lidar_config *c) {
+  const int b = 16 + (c->sparse ? 8 : 0) + 4 * c->beams + 8 + 8 + 12 + (c->log_stats ? 20 : 0) + 4;
+  return (b + 7) & ~7;
+}
+
 int validate(const apg_lidar_config *c) {
   if (!c) return fail(APG_E_INVALID, "null config");
   if (c->num_envs <= 0) return fail(APG_E_INVALID, "num_envs must be positive");
@@ -126,6 +133,8 @@ int validate(const apg_lidar_config *c) {
   if (c->step_limit <= 0) return fail(APG_E_INVALID, "step_limit must be positive");
   if (c->log_stats && c->step_limit > PW_DEEP_MAX_N) return fail(APG_E_INVALID, "log_stats needs step_limit <= 15368");
   if (c->out_row_bytes < 0 || (c->out_row_bytes & 7)) return fail(APG_E_INVALID, "out_row_bytes must be a multiple of 8");
+  if (c->out_row_bytes > 0 && c->out_row_bytes < min_row_bytes(c))
+    return fail(APG_E_INVALID, "out_row_bytes is smaller than the packed output row of the enabled fields");
   return APG_OK;
 }
 
@@ -479,6 +488,7 @@ __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_stat
 
 struct StepParams {
   int n, h, w, wpr, beams, step_limit, is_static, R, wrows, log_stats, sparse, row, wlo, whi;
+  int lidar16;  // dense lidar rows 16-byte aligned (base pointer and row pitch): vector stores
   float range, loss_scale, loss_offset;
 };
 
@@ -1145,7 +1155,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   STEP_MARK(4)
   STEP_STOP(4)
   const int nenv = P.n - base < EPB ? P.n - base : EPB;
-  if (!ROWP && (P.beams & 3) == 0) {  // dense rows (16-B aligned): four beams per 16-byte store
+  if (!ROWP && P.lidar16) {  // dense rows 16-byte aligned: four beams per 16-byte store
     typedef float f4 __attribute__((ext_vector_type(4)));
     const int B4 = P.beams >> 2, dl = T / B4, db = T - dl * B4;
     int l = tid / B4, b4 = tid - l * B4;
@@ -1553,6 +1563,7 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   // of its scans, plus two rows for the walk's one-crossing-ahead row reads past the segment's end
   P.wlo = std::max(0, 15 - (P.R + 5) - 2);
   P.whi = std::min(MAX_WIN_ROWS, 15 + (P.R + 5) + 2 + 1);
+  P.lidar16 = (P.beams & 3) == 0 && (reinterpret_cast<uintptr_t>(out->lidar) & 15) == 0;
   P.range = cfg->lidar_range;
   P.loss_scale = cfg->loss_scale;
   P.loss_offset = cfg->loss_offset;
@@ -1572,7 +1583,7 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
 
 extern "C" {
 
-const char *apg_version(void) { return "apgym-mi355x 0.1.0 (gfx950)"; }
+const char *apg_version(void) { return "apgym-mi355x 0.2.0 (gfx950)"; }
 const char *apg_last_error(void) { return g_err; }
 
 int apg_lidar_query_sizes(const apg_lidar_config *cfg, apg_lidar_state_sizes *o) {

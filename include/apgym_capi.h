@@ -91,7 +91,7 @@ typedef struct apg_pcg64 {
 
 typedef struct apg_lidar_config {
   int32_t num_envs;
-  int32_t height, width;        /* map size in cells (<= 128 each); rooms maps must be square */
+  int32_t height, width;        /* map size in cells, 3 .. 255 each; rooms maps must be square, mazes odd */
   int32_t map_kind;             /* APG_MAP_ROOMS | APG_MAP_MAZE */
   int32_t is_static;            /* 1: one map for all envs (static_map=True) */
   int32_t static_map_index;     /* dataset index of the static map */
@@ -109,7 +109,11 @@ typedef struct apg_lidar_config {
                                    target, loss, info_mask, map_idx, reset_mask, stats, stats_len, weight of
                                    env e are at their pointer + e * out_row_bytes (element j of a field at
                                    + j * element size; stats as [N][4]), i.e. the pointers are field offsets
-                                   into one [N][out_row_bytes] buffer that a sharded run all-gathers as is */
+                                   into one [N][out_row_bytes] buffer that a sharded run all-gathers as is.
+                                   It must hold every enabled field (apg_lidar_step rejects a row smaller than
+                                   16 + 4 * beams + 36 bytes, + 8 with sparse, + 20 with log_stats, rounded up to
+                                   a multiple of 8).  Added in ABI 0.2 (apg_version): callers built against 0.1
+                                   must zero it. */
 } apg_lidar_config;
 
 /* Persistent per-env state.  Sizes come from apg_lidar_query_sizes(). */
@@ -130,7 +134,7 @@ typedef struct apg_lidar_state {
 } apg_lidar_state;
 
 typedef struct apg_lidar_outputs {
-  float *lidar;        /* [N][beams] */
+  float *lidar;        /* [N][beams] (any 4-byte alignment; 16-byte aligned rows take vector stores) */
   float *odometry;     /* [N][2] */
   float *time_step;    /* [N] */
   float *map_obs;      /* [N][H][W] (dynamic maps; rewritten only for envs that reset) or NULL */

@@ -63,8 +63,11 @@ def test_rng_fill_integers_matches_numpy(gpu, bound, n, pre):
     assert _state_equal(st.cpu().numpy(), gen)
 
 
+@pytest.mark.parametrize("with_work", [False, True])
 @pytest.mark.parametrize("n,cols", [(1, 2), (513, 2), (65536, 2), (1000, 1)])
-def test_rng_fill_uniform_matches_numpy(gpu, n, cols):
+def test_rng_fill_uniform_matches_numpy(gpu, n, cols, with_work):
+    """Uniform draws with work=NULL (a second launch advances the state) and with a zeroed work buffer (the last
+    workgroup advances it in the same launch, counting finished workgroups in work[0], which it leaves at 0)."""
     import torch
 
     from ap_gym_amd import _native as N
@@ -77,11 +80,15 @@ def test_rng_fill_uniform_matches_numpy(gpu, n, cols):
     out = torch.zeros((n, cols), dtype=torch.float64, device=gpu)
     lo_c = (ctypes.c_double * cols)(*low.tolist())
     rg_c = (ctypes.c_double * cols)(*(high - low).tolist())
-    N.check(N.lib().apg_rng_fill(N.ptr(st), N.APG_DRAW_UNIFORM, n, cols, lo_c, rg_c, 0, 0, N.ptr(out), None,
-                                 N.stream_handle(gpu)))
-    want = gen.uniform(low, high, (n, cols))
-    assert np.array_equal(out.cpu().numpy(), want)
-    assert _state_equal(st.cpu().numpy(), gen)
+    work = torch.zeros(1, dtype=torch.int64, device=gpu) if with_work else None
+    for rep in range(2):  # the work buffer is reused as the env does: it must come back zeroed
+        N.check(N.lib().apg_rng_fill(N.ptr(st), N.APG_DRAW_UNIFORM, n, cols, lo_c, rg_c, 0, 0, N.ptr(out),
+                                     N.ptr(work) if with_work else None, N.stream_handle(gpu)))
+        want = gen.uniform(low, high, (n, cols))
+        assert np.array_equal(out.cpu().numpy(), want)
+        assert _state_equal(st.cpu().numpy(), gen)
+        if with_work:
+            assert int(work[0]) == 0
 
 
 # ---------------------------------------------------------------------------------------- glimpse

@@ -57,6 +57,19 @@ def test_capi_validation_without_gpu():
     assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0
     cfg.lidar_range = 28.5
     assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == -1
+    cfg.lidar_range = 5.0
+    # packed output rows must hold every enabled field (the Python row layout's size is the minimum)
+    from ap_gym_amd.lidar_env import lidar_output_row_layout
+
+    for log_stats, sparse in ((0, 0), (1, 0), (0, 1), (1, 1)):
+        cfg.log_stats, cfg.sparse = log_stats, sparse
+        _, row = lidar_output_row_layout(cfg.beams, bool(log_stats), bool(sparse))
+        cfg.out_row_bytes = row
+        assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0
+        cfg.out_row_bytes = row - 8
+        assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == -1
+        assert b"out_row_bytes" in N.lib().apg_last_error()
+    cfg.out_row_bytes = cfg.log_stats = cfg.sparse = 0
 
 
 def test_mse_loss_matches_reference_golden():

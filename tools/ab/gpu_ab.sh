@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of library variants on one workload, interleaved: bash tools/gpu_ab.sh <workload> <steps> <variant.so>...
+# A/B of library variants on one workload, interleaved: bash tools/ab/gpu_ab.sh <workload> <steps> <variant.so>...
 # ("default" = the in-tree library).  Prints value and ms_per_step of each run.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"

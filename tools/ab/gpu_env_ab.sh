@@ -1,6 +1,6 @@
 #!/bin/bash
 # Tuning-knob A/B through environment variables (same library), two interleaved rounds:
-#   bash tools/gpu_env_ab.sh <workload> <steps> "<VAR=value ...>" ...   ("-" = no variables)
+#   bash tools/ab/gpu_env_ab.sh <workload> <steps> "<VAR=value ...>" ...   ("-" = no variables)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 WL=$1; STEPS=$2; shift 2

@@ -1,5 +1,5 @@
 #!/bin/bash
-# EPB A/B through APG_STEP_EPB (same library): bash tools/gpu_epb_env_ab.sh <workload> <steps> <epb>...
+# EPB A/B through APG_STEP_EPB (same library): bash tools/ab/gpu_epb_env_ab.sh <workload> <steps> <epb>...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 WL=$1; STEPS=$2; shift 2

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Image step A/B: staged tap windows (default) vs direct tap loads (APG_GLIMPSE_NO_WINDOW), interleaved, with a
-# rocprofv3 kernel trace of each for the fused step's duration.  bash tools/gpu_img_ab.sh [workloads...]
+# rocprofv3 kernel trace of each for the fused step's duration.  bash tools/ab/gpu_img_ab.sh [workloads...]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

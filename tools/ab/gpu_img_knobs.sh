@@ -1,7 +1,7 @@
 #!/bin/bash
 # Image fused-step knob sweep: for each workload and each "NAME=VAL[,NAME=VAL]" setting (or "default"), a
 # rocprofv3 kernel trace of a 200-step bench run and the fused step's duration.
-#   bash tools/gpu_img_knobs.sh "<workloads>" <setting>...
+#   bash tools/ab/gpu_img_knobs.sh "<workloads>" <setting>...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

@@ -1,6 +1,6 @@
 #!/bin/bash
 # LIDAR iteration loop on the GPU box: parity tests, benches (default EPB and APG_STEP_EPB=64), a kernel trace.
-#   bash tools/gpu_lidar_iter.sh [pytest selection]
+#   bash tools/ab/gpu_lidar_iter.sh [pytest selection]
 set -e
 mkdir -p gpurun_out
 SEL=${1:-tests/test_gpu_lidar.py tests/test_gpu_render.py}

@@ -1,5 +1,5 @@
 #!/bin/bash
-# maze_bench timing + PMC passes on its kernels (k_stream, k_dfs, k_paint): bash tools/gpu_maze_pmc.sh <outdir>
+# maze_bench timing + PMC passes on its kernels (k_stream, k_dfs, k_paint): bash tools/ab/gpu_maze_pmc.sh <outdir>
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
