@@ -25,6 +25,7 @@ APG_ERR_NAN_PREDICTION = 2
 APG_ERR_MAPGEN = 4
 APG_ERR_OOB_Y = 8
 APG_ERR_OOB_X = 16
+APG_ERR_PREFETCH = 32
 APG_MAP_ROOMS = 0
 APG_MAP_MAZE = 1
 APG_DRAW_UNIFORM = 0
@@ -64,7 +65,7 @@ class LidarConfig(ctypes.Structure):
 
 class LidarState(ctypes.Structure):
     _fields_ = [(n, _vp) for n in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng", "occ", "scratch", "stack",
-                                   "map_idx", "beam_dirs", "stats_hist")]
+                                   "map_idx", "beam_dirs", "stats_hist", "prefetch", "prefetcher")]
 
 
 class LidarOutputs(ctypes.Structure):
@@ -81,7 +82,8 @@ class LidarRenderState(ctypes.Structure):
 
 class LidarSizes(ctypes.Structure):
     _fields_ = [("occ_bytes", ctypes.c_size_t), ("scratch_bytes", ctypes.c_size_t),
-                ("stack_bytes", ctypes.c_size_t), ("wpr", ctypes.c_int32), ("maze_frames", ctypes.c_int32)]
+                ("stack_bytes", ctypes.c_size_t), ("wpr", ctypes.c_int32), ("maze_frames", ctypes.c_int32),
+                ("prefetch_bytes", ctypes.c_size_t)]
 
 
 class ImageConfig(ctypes.Structure):
@@ -92,7 +94,7 @@ class ImageConfig(ctypes.Structure):
         ("pool_len", ctypes.c_int64), ("sensor_scale", ctypes.c_double), ("max_step", ctypes.c_double * 2),
         ("cell", ctypes.c_double * 2), ("ce_scale", ctypes.c_double), ("ce_offset", ctypes.c_double),
         ("mse_scale", ctypes.c_float), ("mse_offset", ctypes.c_float), ("log_stats", ctypes.c_int32),
-        ("sparse", ctypes.c_int32)]
+        ("sparse", ctypes.c_int32), ("out_row_bytes", ctypes.c_int32)]
 
 
 class ImageState(ctypes.Structure):
@@ -147,6 +149,9 @@ SYMBOLS = [
                                       ctypes.POINTER(LidarOutputs), _vp]),
     ("apg_lidar_step_profiled", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(LidarState), _vp, _vp,
                                                ctypes.POINTER(LidarOutputs), _vp, _vp, _vp]),
+    ("apg_lidar_prefetcher_create", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(_vp)]),
+    ("apg_lidar_prefetcher_destroy", ctypes.c_int, [_vp]),
+    ("apg_lidar_prefetcher_stats", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64)]),
     ("apg_maze_frames", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("apg_map_generate", ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp]),

@@ -79,6 +79,42 @@ def softmax_nan_rows(logits: np.ndarray) -> np.ndarray:
     return np.isnan(logits).any(-1) | np.isposinf(logits).any(-1) | np.isneginf(logits).all(-1)
 
 
+# Packed output rows (apg_image_config.out_row_bytes): every per-env output of a step in one row per env, 8-byte
+# fields first, so ShardedVectorEnv all-gathers the [N, row] buffer as is (no packing copies) and the gathered fields
+# are strided views of the receive buffer.  Names are the env's output buffer names.
+def image_output_row_layout(kind: int, sensor: tuple, channels: int, log_stats: bool = False):
+    """[(name, torch dtype, per-env shape, byte offset)] of the packed output row, and the row size."""
+    import torch
+
+    f64, f32, i32 = torch.float64, torch.float32, torch.int32
+    g = (int(sensor[0]), int(sensor[1]), int(channels))
+    cls = kind == N.APG_IMAGE_CLASSIFY
+    fields = [("reward", f64, ())] + ([("loss_f64", f64, ())] if cls else []) + [("glimpse", f32, g)] + (
+        [] if cls else [("target_glimpse", f32, g)]) + [
+        ("glimpse_pos", f32, (2,)), ("time_step", f32, ()), ("base_reward", f32, ())] + (
+        [("label_target", i32, ())] if cls else [("target_out", f32, (2,)), ("loss_f32", f32, ())]) + (
+        [("stats", f32, (4,))] if log_stats else []) + ([("stats_idx", i32, (2,))] if log_stats and cls else [])
+    out, off = [], 0
+    for name, dt, sh in fields:
+        out.append((name, dt, sh, off))
+        off += torch.empty((), dtype=dt).element_size() * int(np.prod(sh, dtype=np.int64))
+    return out, off + (-off) % 8
+
+
+def image_row_views(buf, layout) -> dict:
+    """Field views of a packed [rows, row_bytes] uint8 buffer (stats / stats_idx as [M, rows] like the dense
+    layout)."""
+    import torch
+
+    v = {}
+    for name, dt, sh, off in layout:
+        nb = torch.empty((), dtype=dt).element_size() * int(np.prod(sh, dtype=np.int64))
+        t = buf[:, off:off + nb].view(dt)
+        t = t[:, 0] if not sh else t.view(buf.shape[0], *sh)
+        v[name] = t.T if name in ("stats", "stats_idx") else t
+    return v
+
+
 class _ImageVectorEnv(VectorEnv):
     metadata = {"render_modes": ["rgb_array"], "render_fps": 2, "autoreset_mode": "NextStep"}
     ERROR_POLL_INTERVAL = 32
@@ -87,7 +123,7 @@ class _ImageVectorEnv(VectorEnv):
     def __init__(self, num_envs: int, image_perception_config: ImagePerceptionConfig,
                  render_mode: str = "rgb_array", device=None, copy: bool = False, strict_errors: bool = False,
                  array_backend: str = "numpy", num_envs_total: int | None = None, env_offset: int = 0,
-                 log_stats: bool = False, sparse: bool = False, render_envs=None):
+                 log_stats: bool = False, sparse: bool = False, render_envs=None, packed_outputs: bool = False):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -105,6 +141,8 @@ class _ImageVectorEnv(VectorEnv):
             raise ValueError("the shard [env_offset, env_offset + num_envs) must lie inside num_envs_total")
         self.render_mode = render_mode
         self.copy, self.strict_errors, self.array_backend = copy, strict_errors, array_backend
+        if packed_outputs and array_backend != "torch":
+            raise ValueError("packed_outputs (the all-gather row layout) needs array_backend='torch'")
         # the registered ids wrap the env in ActiveClassificationVectorLogWrapper /
         # ActiveRegressionVectorLogWrapper (registration.py:185-192, 263-269): info["stats"]
         self.log_stats = bool(log_stats)
@@ -185,6 +223,10 @@ class _ImageVectorEnv(VectorEnv):
             sensor_scale=float(cfg.sensor_scale), max_step=(ctypes.c_double * 2)(*msl.tolist()),
             cell=(ctypes.c_double * 2)(*cell.tolist()), ce_scale=ce_scale, ce_offset=ce_offset,
             mse_scale=mse_scale, mse_offset=mse_offset, log_stats=int(self.log_stats), sparse=int(self.sparse))
+        self.output_layout, row_bytes = image_output_row_layout(self.kind, cfg.sensor_size, c, self.log_stats)
+        if not packed_outputs:
+            self.output_layout, row_bytes = None, 0
+        self._cfg.out_row_bytes = row_bytes
 
         t, dev = torch, self.device
         gshape = (n, s0, s1, c)
@@ -213,6 +255,11 @@ class _ImageVectorEnv(VectorEnv):
                         else None),
             stats=t.zeros((4, n), dtype=t.float32, device=dev) if self.log_stats else None,
             stats_idx=t.zeros((2, n), dtype=t.int32, device=dev) if self.log_stats else None)
+        # packed_outputs: the per-env outputs are field views of one [n, row] buffer (ShardedVectorEnv's send)
+        self.output_rows = None
+        if row_bytes:
+            self.output_rows = t.zeros((n, row_bytes), dtype=t.uint8, device=dev)
+            T.update(image_row_views(self.output_rows, self.output_layout))
         self._state = N.ImageState(*[N.ptr(T[k_]) for k_ in ("pool", "pool_labels", "unique_grid", "index", "label",
                                                               "inverted", "pos", "target", "rng", "scratch_i64",
                                                               "scratch_f64", "top_k", "rng_work", "stats_hist")])
@@ -232,7 +279,7 @@ class _ImageVectorEnv(VectorEnv):
         self._h = t.classes.apgym.ImageEnv(
             [c.num_envs, c.kind, c.height, c.width, c.pool_channels, c.channels, c.pool_dtype, c.sensor_h,
              c.sensor_w, c.step_limit, c.num_classes, c.invert_labels, c.top_k, c.unique_points, c.num_envs_total,
-             c.env_offset, c.pool_len, c.log_stats, c.sparse],
+             c.env_offset, c.pool_len, c.log_stats, c.sparse, c.out_row_bytes],
             [c.sensor_scale, c.max_step[0], c.max_step[1], c.cell[0], c.cell[1], c.ce_scale, c.ce_offset,
              c.mse_scale, c.mse_offset],
             N.op_buffers([T[k_] for k_ in ("pool", "pool_labels", "unique_grid", "index", "label", "inverted", "pos",
@@ -687,6 +734,7 @@ class _ImageVectorEnv(VectorEnv):
             self._t = {}
             self._h = None  # the op handle keeps every state/output buffer alive
             self._c_args = None
+            self.output_rows = None
 
 
 class ImageClassificationVectorEnv(_ImageVectorEnv):

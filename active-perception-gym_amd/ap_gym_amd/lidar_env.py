@@ -275,6 +275,10 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             stats=t.zeros((4, n), dtype=t.float32, device=dev) if self.log_stats else None,
             stats_len=t.zeros(n, dtype=t.int32, device=dev) if self.log_stats else None,
             weight=t.zeros(n, dtype=t.float64, device=dev) if self.sparse else None,
+            # the next map of every env, generated ahead of its autoreset on a side stream (dynamic mazes): the
+            # reference's DataLoader(prefetch=True) thread (lidar_localization2d.py:130-131, 296-298)
+            prefetch=(t.zeros(sizes.prefetch_bytes, dtype=t.uint8, device=dev)
+                      if prefetch and sizes.prefetch_bytes else None),
         )
         # packed_outputs: the per-env outputs are field views of one [n, row] buffer (ShardedVectorEnv's send)
         self.output_rows = None
@@ -287,9 +291,17 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             self._out_block = t.zeros(nbytes, dtype=t.uint8, device=dev)
             self._t.update(block_views(self._out_block, self._block_layout))
         T = self._t
+        # the prefetcher (C++ in the library): side stream, pinned per-step reset counts, batch events
+        self._prefetcher = None
+        if T["prefetch"] is not None:
+            h_pf = ctypes.c_void_p()
+            with torch.cuda.device(dev):
+                N.check(L.apg_lidar_prefetcher_create(ctypes.byref(self._cfg), ctypes.byref(h_pf)),
+                        "apg_lidar_prefetcher_create")
+            self._prefetcher = h_pf.value
         self._state = N.LidarState(*[N.ptr(T[k]) for k in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng",
                                                             "occ", "scratch", "stack", "map_idx", "beam_dirs",
-                                                            "stats_hist")])
+                                                            "stats_hist", "prefetch")], self._prefetcher)
         self._out = N.LidarOutputs(N.ptr(T["lidar"]), N.ptr(T["odometry"]), N.ptr(T["time_step"]),
                                    N.ptr(T["map_obs"]), N.ptr(T["reward"]), N.ptr(T["terminated"]),
                                    N.ptr(T["truncated"]), N.ptr(T["base_reward"]), N.ptr(T["target"]),
@@ -307,10 +319,10 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         self._c_args = None
         self._h = t.classes.apgym.LidarEnv(
             [c.num_envs, c.height, c.width, c.map_kind, c.is_static, c.static_map_index, c.beams, c.step_limit,
-             c.max_rooms, c.door_width, c.log_stats, c.sparse, c.out_row_bytes],
+             c.max_rooms, c.door_width, c.log_stats, c.sparse, c.out_row_bytes, self._prefetcher or 0],
             [c.lidar_range, c.loss_scale, c.loss_offset, c.branching_prob],
             N.op_buffers([T[k] for k in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng", "occ", "scratch",
-                                         "stack", "map_idx", "beam_dirs", "stats_hist")], dev),
+                                         "stack", "map_idx", "beam_dirs", "stats_hist", "prefetch")] + [None], dev),
             N.op_buffers([T[k] for k in ("lidar", "odometry", "time_step", "map_obs", "reward", "terminated",
                                          "truncated", "base_reward", "target", "loss", "info_mask", "map_idx_out",
                                          "reset_mask", "err", "stats", "stats_len", "weight")], dev))
@@ -484,6 +496,8 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             raise ValueError(NAN_PREDICTION_MSG)
         if bits & N.APG_ERR_MAPGEN:
             raise N.ApgError("map generation exceeded an internal bound")
+        if bits & N.APG_ERR_PREFETCH:
+            raise N.ApgError("an autoreset found no prefetched map (prefetch protocol violated)")
 
     def check_errors(self, block: bool = True):
         """Raise the reference's exception for any error flagged by the kernels so far."""
@@ -759,14 +773,32 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         self._autoreset_host = term | trunc
         return obs, reward, term, trunc, info
 
+    def prefetch_stats(self) -> dict | None:
+        """Counters of the map prefetcher (None without one): batches launched, steps whose stream waited for a
+        batch still running, resets observed, step calls since the last reset."""
+        if not self._prefetcher:
+            return None
+        v = (ctypes.c_int64 * 4)()
+        N.check(N.lib().apg_lidar_prefetcher_stats(self._prefetcher, v), "apg_lidar_prefetcher_stats")
+        return dict(zip(("batches", "waits", "resets", "steps"), list(v)))
+
     def close(self, **kwargs):
         if not getattr(self, "_closed", True):
             self._closed = True
             self.closed = True
+            if getattr(self, "_prefetcher", None):
+                N.lib().apg_lidar_prefetcher_destroy(self._prefetcher)  # synchronizes its side stream
+                self._prefetcher = None
             self._t = {}
             self._h = None  # the op handle keeps every state/output buffer alive
             self._c_args = None
             self.output_rows = self._out_block = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
 
     def __repr__(self):
         kind = "maze" if isinstance(self.dataset, FloorMapDatasetMaze) else "rooms"

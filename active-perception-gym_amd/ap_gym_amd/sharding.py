@@ -18,10 +18,15 @@ gloo on CPU — for consumers that need the full batch (the north star's obs/rew
          fields are strided views of the receive buffer: no packing or unpacking copies.  The per-reset map
          observation (4*H*W bytes per env) and the per-step stats history stay sharded: they are returned
          as info["local_obs"] / the local env's buffers.
-  image  glimpse_pos, time_step, reward, base_reward, target, loss, index, terminated, truncated
-         (+ glimpse and target_glimpse with gather_glimpse=True), packed per step by copies
+  image  likewise packed_outputs=True: the fused step kernel writes reward, loss, glimpse (+ target glimpse), glimpse
+         position, time step, base reward, target and the episode statistics into the row
+         (image_env.image_output_row_layout); info["index"] changes only with the batch, so it is gathered on
+         reset and autoreset steps only, and terminated / truncated are the same for the whole batch (episodes
+         end together), so they are not gathered at all
 (image_classification.py:117-151 and image_localization.py:131-181 are the outputs gathered).
-Envs without packed rows (e.g. test doubles) take the copying path for LIDAR too.
+Envs without packed rows (e.g. test doubles) take the copying path (fields packed by copies, glimpses only with
+gather_glimpse=True).  Gathered tensors are views of the receive buffer, rewritten by the next step, unless the
+local env was built with copy=True (then they are cloned).
 """
 
 from __future__ import annotations
@@ -93,7 +98,7 @@ class ShardedVectorEnv:
         self.rank, self.world, self.gather, self.group = rank, world, gather, group
         self.offset, self.local_num_envs = shard_bounds(num_envs_total, rank, world)
         self.num_envs = num_envs_total
-        kw = {"packed_outputs": True} if gather and beams is not None and _accepts(make_local, "packed_outputs") else {}
+        kw = {"packed_outputs": True} if gather and _accepts(make_local, "packed_outputs") else {}
         self.env = make_local(num_envs=self.local_num_envs, env_offset=self.offset, **kw)
         self._lidar = _is_lidar(self.env, beams)
         self._packed = gather and getattr(self.env, "output_rows", None) is not None
@@ -102,14 +107,28 @@ class ShardedVectorEnv:
         self._row += (-self._row) % 8
         self._send = self._recv = None
         self._views = None
+        self._index_full = None  # image envs: the gathered info["index"] (changes only with the batch)
         self.time_gather = time_gather
         self.gather_events: list = []  # (begin, end) torch.cuda.Event pairs around each all-gather
 
     # ------------------------------------------------------------------ collectives
+    def _all_gather_into(self, recv, send):
+        """All-gather of `send` ([n, ...]) into `recv` ([world * n, ...]): RCCL in place, gloo through host buffers
+        (CPU tests, or several ranks sharing one GPU)."""
+        import torch
+        import torch.distributed as dist
+
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(recv, send, group=self.group)
+        else:
+            parts = [torch.empty_like(send, device="cpu") for _ in range(self.world)]
+            dist.all_gather(parts, send.cpu(), group=self.group)
+            recv.copy_(torch.cat(parts))
+        return recv
+
     def _all_gather_rows(self, send):
         """All-gather of a [n, row] uint8 buffer into self._recv [world * n, row] (allocated once)."""
         import torch
-        import torch.distributed as dist
 
         if self._recv is None:
             self._recv = torch.zeros((self.world * send.shape[0], send.shape[1]), dtype=torch.uint8,
@@ -118,25 +137,37 @@ class ShardedVectorEnv:
         if self.time_gather and send.is_cuda:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        if dist.get_backend(self.group) == "nccl":
-            dist.all_gather_into_tensor(self._recv, send, group=self.group)
-        else:  # gloo (CPU tests, or several ranks sharing one GPU): through host buffers
-            recv = [torch.empty_like(send, device="cpu") for _ in range(self.world)]
-            dist.all_gather(recv, send.cpu(), group=self.group)
-            self._recv.copy_(torch.cat(recv))
+        self._all_gather_into(self._recv, send)
         if ev is not None:
             ev[1].record()
             self.gather_events.append(ev)
         return self._recv
 
     def _gathered_rows(self) -> dict:
-        """The packed path: gather the local env's output rows; field views of the receive buffer."""
-        from .lidar_env import row_views
-
+        """The packed path: gather the local env's output rows; field views of the receive buffer (cloned when
+        the local env copies its outputs)."""
         recv = self._all_gather_rows(self.env.output_rows)
         if self._views is None:
-            self._views = row_views(recv, self.env.output_layout)
+            if self._lidar:
+                from .lidar_env import row_views
+
+                self._views = row_views(recv, self.env.output_layout)
+            else:
+                from .image_env import image_row_views
+
+                self._views = image_row_views(recv, self.env.output_layout)
+        if getattr(self.env, "copy", False):
+            return {k: v.clone() for k, v in self._views.items()}
         return self._views
+
+    def _gathered_index(self, local_index):
+        """Image envs: info["index"] of the whole batch, gathered when the batch changes (reset, autoreset)."""
+        import torch
+
+        if self._index_full is None:
+            self._index_full = torch.zeros(self.world * self.local_num_envs, dtype=torch.int64,
+                                           device=local_index.device)
+        return self._all_gather_into(self._index_full, local_index.contiguous())
 
     def _pack(self, fields: dict):
         import torch
@@ -177,17 +208,30 @@ class ShardedVectorEnv:
         return ms
 
     # ------------------------------------------------------------------ API
+    def _c(self, x):
+        return x.clone() if getattr(self.env, "copy", False) else x
+
+    def _image_obs(self, v: dict) -> dict:
+        obs = {k: v[k] for k in ("glimpse", "glimpse_pos", "time_step", "target_glimpse") if k in v}
+        return obs
+
     def reset(self, *, seed=None, options=None):
         obs, info = self.env.reset(seed=seed, options=options)
         if not (self.gather and self._packed):
             # the copying path gathers step outputs only (a reset has no reward / prediction fields)
             return obs, info
         v = self._gathered_rows()
+        if not self._lidar:
+            gobs = self._image_obs(v)
+            if "inverted_label" in obs:
+                gobs["inverted_label"] = obs["inverted_label"]  # (local: drawn per shard like the index)
+            return gobs, {"index": self._c(self._gathered_index(info["index"])), "local_obs": obs,
+                          "local_info": info}
         gobs = {"lidar": v["lidar"], "odometry": v["odometry"], "time_step": v["time_step"]}
         return gobs, {"map_idx": v["map_idx_out"], "_map_idx": v["reset_mask"], "local_obs": obs,
                       "local_info": info}
 
-    def _packed_step_info(self, v: dict, obs: dict) -> dict:
+    def _packed_step_info(self, v: dict, obs: dict, local_info: dict | None = None) -> dict:
         mask = v["info_mask"]
         target = v["target"]
         if "weight" in v:  # -sparse ids
@@ -204,16 +248,57 @@ class ShardedVectorEnv:
                 scalar["_" + name] = done
             info["stats"] = {"scalar": scalar, "_scalar": done, "length": v["stats_len"]}
             info["_stats"] = done
+            local = local_info.get("stats") if local_info else None
+            if local is not None and "vector" in local:  # the per-step history stays local (this shard's envs)
+                info["stats"]["vector"] = local["vector"]
+                info["stats"]["_vector"] = local["_vector"]
         return info
 
+    def _packed_image_step(self, v: dict, obs, term, trunc, info, resetting: bool):
+        import torch
+
+        n = self.num_envs
+        if resetting or self._index_full is None:
+            self._gathered_index(info["index"])
+        cls = "label_target" in v
+        target = v["label_target"] if cls else v["target_out"]
+        loss = v["loss_f64"] if cls else v["loss_f32"]
+        tflag, fflag = bool(term[0]), bool(trunc[0])  # the whole batch terminates together
+        g_term = torch.full((n,), tflag, dtype=torch.bool, device=target.device)
+        g_trunc = torch.full((n,), fflag, dtype=torch.bool, device=target.device)
+        pt = info["prediction"]["target"]
+        if isinstance(pt, dict):  # -sparse ids: weight = terminated as float32
+            target = {"target": target, "weight": g_term.to(torch.float32)}
+        ginfo = {"index": self._c(self._index_full), "base_reward": v["base_reward"],
+                 "prediction": {"target": target, "loss": loss}, "local_obs": obs}
+        if "stats" in info:  # the vector log wrapper's scalars of the whole batch from the rows; the per-step
+            done = g_term  # history ("vector") stays local to this shard's envs
+            scalar = {}
+            for j, nm in enumerate(self.env._metric_names()):
+                scalar[f"final_{nm}"] = v["stats"][j]
+                scalar[f"_final_{nm}"] = done
+                scalar[f"avg_{nm}"] = v["stats"][2 + j]
+                scalar[f"_avg_{nm}"] = done
+            if cls:
+                scalar.update(first_correct=v["stats_idx"][0], last_incorrect=v["stats_idx"][1])
+            ginfo["stats"] = {"scalar": scalar, "_scalar": done, "vector": info["stats"]["vector"],
+                              "_vector": info["stats"]["_vector"]}
+        gobs = self._image_obs(v)
+        if "inverted_label" in obs:
+            gobs["inverted_label"] = obs["inverted_label"]
+        return gobs, v["reward"], g_term, g_trunc, ginfo
+
     def step(self, action):
+        resetting = bool(getattr(self.env, "_prev_done", False))
         obs, rew, term, trunc, info = self.env.step(action)
         if not self.gather:
             return obs, rew, term, trunc, info
         if self._packed:
             v = self._gathered_rows()
+            if not self._lidar:
+                return self._packed_image_step(v, obs, term, trunc, info, resetting)
             gobs = {"lidar": v["lidar"], "odometry": v["odometry"], "time_step": v["time_step"]}
-            return gobs, v["reward"], v["terminated"], v["truncated"], self._packed_step_info(v, obs)
+            return gobs, v["reward"], v["terminated"], v["truncated"], self._packed_step_info(v, obs, info)
         if self._lidar:
             full = self.all_gather({"lidar": obs["lidar"], "odometry": obs["odometry"], "time_step": obs["time_step"],
                                     "reward": rew, "base_reward": info["base_reward"],

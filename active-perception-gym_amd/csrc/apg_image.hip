@@ -38,6 +38,7 @@ struct GlimpseGeo {
   double scale, cy, cx;  // grid centres (h - 1) / 2, (w - 1) / 2
   int pool_f32;
   int64_t img_elems;     // h * w * pc
+  int64_t pitch;         // output floats per glimpse unit: s0 * s1 * c (dense), out_row_bytes / 4 (packed env rows)
 };
 
 GlimpseGeo make_geo(const apg_image_config *c) {
@@ -56,7 +57,29 @@ GlimpseGeo make_geo(const apg_image_config *c) {
   g.cx = ((double)c->width - 1.0) / 2.0;
   g.pool_f32 = c->pool_dtype == APG_POOL_F32;
   g.img_elems = (int64_t)c->height * c->width * c->pool_channels;
+  g.pitch = (int64_t)c->sensor_h * c->sensor_w * c->channels;
   return g;
+}
+
+// The geometry of the env's own glimpse outputs (one unit per env): packed rows step by out_row_bytes.
+GlimpseGeo env_geo(const apg_image_config *c) {
+  GlimpseGeo g = make_geo(c);
+  if (c->out_row_bytes > 0) g.pitch = c->out_row_bytes / 4;
+  return g;
+}
+
+// Output element j of env e: a dense [N][k] array, or (row > 0: apg_image_config.out_row_bytes) a field of env e's
+// packed output row.
+template <class T>
+APG_DEV T &ro(T *p, int row, int e, int k, int j = 0) {
+  return row ? *reinterpret_cast<T *>(reinterpret_cast<char *>(p) + (size_t)e * (size_t)row + (size_t)j * sizeof(T))
+             : p[(size_t)e * k + j];
+}
+// statistic m of env e: dense [M][N], packed [N][M]
+template <class T>
+APG_DEV T &ro_t(T *p, int row, int n, int e, int m) {
+  return row ? *reinterpret_cast<T *>(reinterpret_cast<char *>(p) + (size_t)e * (size_t)row + (size_t)m * sizeof(T))
+             : p[(size_t)m * n + e];
 }
 
 // float32(v) / 255 for v = 0..255 (_process_imgs_np), staged in LDS by every glimpse workgroup:
@@ -366,7 +389,8 @@ __global__ __launch_bounds__(256) void k_glimpse(GlimpseGeo g, const void *pool,
   const double px = (double)pos[2 * np_], py = (double)pos[2 * np_ + 1];
   float v[3];
   const uint32_t bad = glimpse_pixel(g, pool, s_lut, index[e] * g.img_elems, px, py, i, j, v);
-  for (int ch = 0; ch < g.c; ch++) out[(size_t)t * g.c + ch] = v[ch];
+  float *dst = out + (size_t)np_ * g.pitch + (size_t)pix * g.c;
+  for (int ch = 0; ch < g.c; ch++) dst[ch] = v[ch];
   if (bad) atomicOr(err, bad);
 }
 
@@ -445,8 +469,8 @@ APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, 
     w00 = __dmul_rn(ay.nw, axx.nw), w01 = __dmul_rn(ay.nw, axx.w), w10 = __dmul_rn(ay.w, axx.nw),
     w11 = __dmul_rn(ay.w, axx.w);
   };
-  auto store = [&](int q, const float *res) {
-    float *dst = out + ((size_t)u0 * per + q) * C;
+  auto store = [&](int q, int u, const float *res) {
+    float *dst = out + (size_t)(u0 + u) * g.pitch + (size_t)(q - u * per) * C;
     if constexpr (C == 3) {
       struct F3 {
         float x, y, z;
@@ -475,7 +499,7 @@ APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, 
         v = __dadd_rn(v, __dmul_rn((double)im[r1 + PC + cc], w11));
         res[ch] = (float)(v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v));  // np.clip(0, 1)
       }
-      store(q, res);
+      store(q, u, res);
     }
   } else {
     // the 2 * PC tap bytes of each row are contiguous: aligned dword loads, only the ones they occupy (issuing
@@ -531,7 +555,7 @@ APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, 
         v = __dadd_rn(v, __dmul_rn((double)tap(b1, PC + cc), w11));
         res[ch] = (float)fmin(v, 1.0);
       }
-      store(q, res);
+      store(q, u, res);
     }
   }
 }
@@ -571,6 +595,7 @@ __global__ __launch_bounds__(GS_THREADS) void k_glimpse_sep(GlimpseGeo g, const 
 // ------------------------------------------------------------------ k_image_env
 struct EnvArgs {
   int n, kind, k, resetting, log_stats, limit, t_new;
+  int row;  // apg_image_config.out_row_bytes (0: dense outputs)
   double msl[2];
   double ce_scale, ce_offset;
   float mse_scale, mse_offset;
@@ -609,10 +634,10 @@ APG_DEV void log_regression(const EnvArgs &a, int e, const apg_image_outputs &ou
   h0[a.t_new - 1] = ed;
   h1[a.t_new - 1] = mse;
   if (a.t_new < a.limit) return;
-  out.stats[e] = ed;
-  out.stats[(size_t)a.n + e] = mse;
-  out.stats[(size_t)2 * a.n + e] = episode_mean(h0, a.limit);
-  out.stats[(size_t)3 * a.n + e] = episode_mean(h1, a.limit);
+  ro_t(out.stats, a.row, a.n, e, 0) = ed;
+  ro_t(out.stats, a.row, a.n, e, 1) = mse;
+  ro_t(out.stats, a.row, a.n, e, 2) = episode_mean(h0, a.limit);
+  ro_t(out.stats, a.row, a.n, e, 3) = episode_mean(h1, a.limit);
 }
 
 APG_DEV void log_classification(const EnvArgs &a, int e, const apg_image_outputs &out, float *hist, float prob) {
@@ -630,12 +655,12 @@ APG_DEV void log_classification(const EnvArgs &a, int e, const apg_image_outputs
     if (c && first_correct < 0) first_correct = i;
     if (!c) last_incorrect = i;
   }
-  out.stats[e] = prob;
-  out.stats[(size_t)a.n + e] = acc[a.limit - 1];
-  out.stats[(size_t)2 * a.n + e] = episode_mean(h, a.limit);
-  out.stats[(size_t)3 * a.n + e] = episode_mean(acc, a.limit);
-  out.stats_idx[e] = first_correct;
-  out.stats_idx[(size_t)a.n + e] = last_incorrect;
+  ro_t(out.stats, a.row, a.n, e, 0) = prob;
+  ro_t(out.stats, a.row, a.n, e, 1) = acc[a.limit - 1];
+  ro_t(out.stats, a.row, a.n, e, 2) = episode_mean(h, a.limit);
+  ro_t(out.stats, a.row, a.n, e, 3) = episode_mean(acc, a.limit);
+  ro_t(out.stats_idx, a.row, a.n, e, 0) = first_correct;
+  ro_t(out.stats_idx, a.row, a.n, e, 1) = last_incorrect;
 }
 
 // ImagePerceptionModule.step's move (:197-213): project_sphere (util.py:94-97) in f32, then
@@ -675,9 +700,8 @@ APG_DEV EnvIn load_env_in(const EnvArgs &a, int e, const float *__restrict__ act
   if constexpr (KIND == APG_IMAGE_LOCALIZE) {
     in.p0 = pred[2 * e];
     in.p1 = pred[2 * e + 1];
-    const float *tg = a.copy_target ? a.copy_target : out.target;
-    in.t0 = tg[2 * e];
-    in.t1 = tg[2 * e + 1];
+    in.t0 = a.copy_target ? a.copy_target[2 * e] : ro(out.target, a.row, e, 2, 0);
+    in.t1 = a.copy_target ? a.copy_target[2 * e + 1] : ro(out.target, a.row, e, 2, 1);
   } else {
     in.label = label[e];
   }
@@ -697,8 +721,8 @@ APG_DEV uint32_t env_tail(const EnvArgs &a, int e, const EnvIn &in, double *pos,
   if (a.kind != APG_IMAGE_CLASSIFY) loss_d = (double)loss_f;
   if (a.resetting) {
     // module.reset() replaced the batch; base_reward = np.zeros(N) (float64)
-    out.base_reward[e] = 0.0f;
-    out.reward[e] = __dsub_rn(0.0, loss_d);
+    ro(out.base_reward, a.row, e, 1) = 0.0f;
+    ro(out.reward, a.row, e, 1) = __dsub_rn(0.0, loss_d);
   } else {
     const float a0 = in.a0, a1 = in.a1;
     if (a0 != a0 || a1 != a1) err |= APG_ERR_NAN_ACTION;
@@ -706,13 +730,13 @@ APG_DEV uint32_t env_tail(const EnvArgs &a, int e, const EnvIn &in, double *pos,
     pos[2 * e] = px;
     pos[2 * e + 1] = py;
     const float base = __fmul_rn(-mag, 1e-3f);  // -norm(action) * 1e-3 (f32, weak Python scalar)
-    out.base_reward[e] = base;
-    out.reward[e] = a.kind == APG_IMAGE_CLASSIFY ? __dsub_rn((double)base, loss_d)
-                                                 : (double)__fsub_rn(base, loss_f);
+    ro(out.base_reward, a.row, e, 1) = base;
+    ro(out.reward, a.row, e, 1) = a.kind == APG_IMAGE_CLASSIFY ? __dsub_rn((double)base, loss_d)
+                                                               : (double)__fsub_rn(base, loss_f);
   }
-  out.glimpse_pos[2 * e] = (float)px;
-  out.glimpse_pos[2 * e + 1] = (float)py;
-  out.time_step[e] = a.time_value;
+  ro(out.glimpse_pos, a.row, e, 2, 0) = (float)px;
+  ro(out.glimpse_pos, a.row, e, 2, 1) = (float)py;
+  ro(out.time_step, a.row, e, 1) = a.time_value;
   return err;
 }
 
@@ -724,14 +748,14 @@ APG_DEV void loc_env(const EnvArgs &a, int e, const EnvIn &in, double *pos, cons
   if (p0 != p0 || p1 != p1) err |= APG_ERR_NAN_PREDICTION;  // 1 - |pred - target| / 2 is NaN
   const float t0 = in.t0, t1 = in.t1;
   if (a.copy_target) {  // k_loc_target folded in (no refresh this step)
-    out.target[2 * e] = t0;
-    out.target[2 * e + 1] = t1;
+    ro(out.target, a.row, e, 2, 0) = t0;
+    ro(out.target, a.row, e, 2, 1) = t1;
   }
   const float d0 = __fsub_rn(p0, t0), d1 = __fsub_rn(p1, t1);
   // np.mean(f32 [2]): (0 + d0^2 + d1^2) / 2, then * scale + offset in f32
   const float mse = f32_div(__fadd_rn(__fadd_rn(0.0f, __fmul_rn(d0, d0)), __fmul_rn(d1, d1)), 2.0f);
   const float loss_f = __fadd_rn(__fmul_rn(mse, a.mse_scale), a.mse_offset);
-  out.loss_f32[e] = loss_f;
+  ro(out.loss_f32, a.row, e, 1) = loss_f;
   log_regression(a, e, out, hist, norm_f32(d0, d1), mse);  // |target - prediction|: signs do not matter
   err |= env_tail(a, e, in, pos, out, (double)loss_f, loss_f);
   if (err) atomicOr(out.err, err);
@@ -828,8 +852,8 @@ __global__ __launch_bounds__(256) void k_image_env_cls(EnvArgs a, int envs_per_b
   uint32_t err = (nan || pos_inf || all_neg_inf) ? APG_ERR_NAN_PREDICTION : 0u;
   const float ce = -__fsub_rn(__fsub_rn(xt, m), logf(sum));
   const double loss_d = __dadd_rn(__dmul_rn((double)ce, a.ce_scale), a.ce_offset);
-  out.loss_f64[e] = loss_d;
-  out.label_target[e] = l;
+  ro(out.loss_f64, a.row, e, 1) = loss_d;
+  ro(out.label_target, a.row, e, 1) = l;
   // scipy.special.softmax(prediction)[label] = exp(x_l - max) / sum(exp(x - max)) (finite logits)
   log_classification(a, e, out, hist, f32_div(row[lc], sum));
   err |= env_tail(a, e, load_env_in<APG_IMAGE_CLASSIFY>(a, e, act, pred, label, pos, out), pos, out, loss_d, 0.0f);
@@ -903,8 +927,8 @@ APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const EnvIn &in, doub
   uint32_t err = (nan || pos_inf || all_neg_inf) ? APG_ERR_NAN_PREDICTION : 0u;
   const float ce = -__fsub_rn(__fsub_rn(xt, m), logf(sum));
   const double loss_d = __dadd_rn(__dmul_rn((double)ce, a.ce_scale), a.ce_offset);
-  out.loss_f64[e] = loss_d;
-  out.label_target[e] = l;
+  ro(out.loss_f64, a.row, e, 1) = loss_d;
+  ro(out.label_target, a.row, e, 1) = l;
   log_classification(a, e, out, hist, f32_div(row[lc], sum));
   err |= env_tail(a, e, in, pos, out, loss_d, 0.0f);
   if (err) atomicOr(out.err, err);
@@ -1330,22 +1354,23 @@ __global__ void k_unique_finish(int n, int offset, int k, const int32_t *top_k, 
 }
 
 // target[prev_done] = np_random.uniform(-1, 1, (k, 2)).astype(float32); out_prev = pre-update copy
-__global__ void k_loc_target(int n, int offset, int refresh, const double *draw, float *target, float *out_prev) {
+__global__ void k_loc_target(int n, int offset, int refresh, const double *draw, float *target, float *out_prev,
+                             int row) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   for (int c = 0; c < 2; c++) {
-    out_prev[2 * e + c] = target[2 * e + c];
+    ro(out_prev, row, e, 2, c) = target[2 * e + c];
     if (refresh) target[2 * e + c] = (float)draw[2 * (offset + e) + c];
   }
 }
 
 // glimpse_pos = pos.astype(float32); time_step = full(N, value)
-__global__ void k_obs_pos(int n, const double *pos, float *glimpse_pos, float *time_step, float value) {
+__global__ void k_obs_pos(int n, const double *pos, float *glimpse_pos, float *time_step, float value, int row) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
-  glimpse_pos[2 * e] = (float)pos[2 * e];
-  glimpse_pos[2 * e + 1] = (float)pos[2 * e + 1];
-  time_step[e] = value;
+  ro(glimpse_pos, row, e, 2, 0) = (float)pos[2 * e];
+  ro(glimpse_pos, row, e, 2, 1) = (float)pos[2 * e + 1];
+  ro(time_step, row, e, 1) = value;
 }
 
 // ------------------------------------------------------------------ standalone losses
@@ -1372,6 +1397,19 @@ __global__ void k_loss_mse(const float *pred, const float *target, int n, int d,
 // ------------------------------------------------------------------ host side
 int grid_for(int64_t n, int threads) { return (int)((n + threads - 1) / threads); }
 
+// Bytes of a packed output row (apg_image_config.out_row_bytes): reward (f64), the glimpse, glimpse_pos, time_step,
+// base_reward; classification: loss_f64, label_target; localization: target_glimpse, target, loss_f32; stats (4 f32)
+// with log_stats, stats_idx (2 i32) for classification
+int image_min_row_bytes(const apg_image_config *c) {
+  const int64_t glimpse = 4LL * c->sensor_h * c->sensor_w * c->channels;
+  int64_t b = 8 + glimpse + 8 + 4 + 4;
+  if (c->kind == APG_IMAGE_CLASSIFY) b += 8 + 4 + (c->log_stats ? 8 : 0);
+  else b += glimpse + 8 + 4;
+  if (c->log_stats) b += 16;
+  b = (b + 7) & ~7LL;
+  return b > 0x7fffffff ? 0x7fffffff : (int)b;
+}
+
 int validate(const apg_image_config *c) {
   if (c->num_envs <= 0) return fail(APG_E_INVALID, "num_envs must be positive");
   if (c->height < 2 || c->width < 2) return fail(APG_E_INVALID, "images must be at least 2 x 2");
@@ -1390,6 +1428,9 @@ int validate(const apg_image_config *c) {
   if (c->log_stats && c->step_limit > PW_PTR_MAX_N) return fail(APG_E_INVALID, "log_stats needs step_limit <= 968");
   if (c->env_offset < 0 || (int64_t)c->env_offset + c->num_envs > c->num_envs_total)
     return fail(APG_E_INVALID, "shard [env_offset, env_offset + num_envs) must lie inside num_envs_total");
+  if (c->out_row_bytes < 0 || (c->out_row_bytes & 7)) return fail(APG_E_INVALID, "out_row_bytes must be a multiple of 8");
+  if (c->out_row_bytes > 0 && c->out_row_bytes < image_min_row_bytes(c))
+    return fail(APG_E_INVALID, "out_row_bytes is smaller than the packed output row of the enabled fields");
   return APG_OK;
 }
 
@@ -1629,7 +1670,7 @@ static int module_reset(const apg_image_config *c, const apg_image_state *st, co
 
 static int observe(const apg_image_config *c, const apg_image_state *st, const apg_image_outputs *out, hipStream_t s,
                    bool target_changed) {
-  const GlimpseGeo g = make_geo(c);
+  const GlimpseGeo g = env_geo(c);
   int rc = launch_glimpse<double>(g, st->pool, st->index, st->pos, c->num_envs, 1, out->glimpse, out->err, s);
   if (rc || c->kind != APG_IMAGE_LOCALIZE || !target_changed) return rc;
   return launch_glimpse<float>(g, st->pool, st->index, st->target, c->num_envs, 1, out->target_glimpse, out->err, s);
@@ -1660,7 +1701,7 @@ int apg_image_reset(const apg_image_config *c, const apg_image_state *st, const 
   }
   // obs: glimpse, glimpse_pos, time_step (= (0 / limit) * 2 - 1 = -1)
   hipLaunchKernelGGL(k_obs_pos, dim3(grid_for(n, 256)), dim3(256), 0, s, n, st->pos, out->glimpse_pos,
-                     out->time_step, -1.0f);
+                     out->time_step, -1.0f, c->out_row_bytes);
   if ((rc = check_launch("k_obs_pos"))) return rc;
   return observe(c, st, out, s, true);
 }
@@ -1684,7 +1725,7 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
     }
     if (prev_done) {  // otherwise the copy is folded into k_image_env_loc
       hipLaunchKernelGGL(k_loc_target, dim3(grid_for(n, 256)), dim3(256), 0, s, n, c->env_offset, prev_done,
-                         st->scratch_f64, st->target, out->target);
+                         st->scratch_f64, st->target, out->target, c->out_row_bytes);
       if ((rc = check_launch("k_loc_target"))) return rc;
     }
   }
@@ -1707,10 +1748,11 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
   a.time_value = (float)(((double)t_new / (double)c->step_limit) * 2.0 - 1.0);
   a.loss_weight = !c->sparse ? 1.0f : (!prev_done && t_new >= c->step_limit ? 1.0f : 0.0f);
   a.copy_target = c->kind == APG_IMAGE_LOCALIZE && !prev_done ? st->target : nullptr;
+  a.row = c->out_row_bytes;
   // tuning knobs, read once: APG_IMAGE_UNFUSED (two launches per step), APG_GLIMPSE_GENERIC, APG_CLS_LANES8
   static const bool unfused = getenv("APG_IMAGE_UNFUSED") != nullptr, generic = getenv("APG_GLIMPSE_GENERIC") != nullptr,
                     lanes8 = getenv("APG_CLS_LANES8") != nullptr;
-  const GlimpseGeo g = make_geo(c);
+  const GlimpseGeo g = env_geo(c);
   const bool fusable = !unfused && !generic && !lanes8 && g.s0 <= GS_MAX_SIDE && g.s1 <= GS_MAX_SIDE &&
                        (c->kind == APG_IMAGE_LOCALIZE || c->num_classes <= CLS1_MAX_K);
   if (fusable) {

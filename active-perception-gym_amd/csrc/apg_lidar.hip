@@ -18,8 +18,11 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
+#include <deque>
 #include <map>
 #include <mutex>
+#include <vector>
 
 #include "../../include/apgym_capi.h"
 #include "apg_host.hpp"
@@ -170,7 +173,7 @@ APG_DEV int place_start(Pcg64 &rng, const uint64_t *rows, int h, int w, int wpr,
 // ------------------------------------------------------------------ kernels
 // Map generator of a kernel instance (template parameter GEN): static maps are generated once by
 // apg_lidar_init, so the reset kernel for them only draws start cells.
-enum : int { GEN_NONE = 0, GEN_ROOMS = 1 };  // mazes: k_maze
+enum : int { GEN_NONE = 0, GEN_ROOMS = 1, GEN_PF = 2 };  // mazes: k_maze (synchronous) or prefetched (GEN_PF)
 
 // Rooms maps are painted into the lane's LDS bitmap (row words are read-modify-written once per
 // primitive), then the wave copies its bitmaps out with coalesced stores.
@@ -302,6 +305,90 @@ __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, ui
 //             the step kernel launched after it is given no map obs), start cell (place_start), state.
 enum : int { MZ_MAPS = 0, MZ_RESET = 1 };
 
+// ------------------------------------------------------------------ map prefetch (apgym_capi.h, "map prefetch")
+// apg_lidar_state.prefetch holds, per env, the result of its NEXT reset computed ahead (the reference's
+// DataLoader prefetch thread, lidar_localization2d.py:130-131, buffered_iterator.py:11-61): map index, occupancy
+// rows, start cell, and the env / iterator streams after those draws.  Ownership: gen[] (resets done) is written
+// only by the step / reset kernels on the env's stream; every other field only by the prefetch batch on the side
+// stream.  A record is valid for the env's current episode when pf_gen[e] == gen[e].  The batch selects the envs
+// whose record is stale (acquire of gen, release in the consuming step kernel: their streams are read after it),
+// the step kernel consumes a record only after its stream waited for the batch that wrote it.
+struct PfLayout {
+  size_t gen, pf_gen, sel_gen, start, list, ctl, idx, rng, it, occ, bytes;
+};
+__host__ __device__ inline PfLayout pf_layout(int n, int h, int wpr) {
+  PfLayout L;
+  size_t o = 0;
+  auto take = [&](size_t &f, size_t bytes) {
+    f = o;
+    o = (o + bytes + 255) & ~(size_t)255;
+  };
+  const size_t N = (size_t)n;
+  take(L.gen, 4 * N);
+  take(L.pf_gen, 4 * N);
+  take(L.sel_gen, 4 * N);
+  take(L.start, 4 * N);
+  take(L.list, 4 * N);
+  take(L.ctl, 64);  // [0] envs selected by the batch, [1] resets of the current step, [2] step workgroup ticket
+  take(L.idx, 8 * N);
+  take(L.rng, sizeof(Pcg64) * N);
+  take(L.it, sizeof(Pcg64) * N);
+  take(L.occ, 8 * N * (size_t)h * (size_t)wpr);
+  L.bytes = o;
+  return L;
+}
+struct PfView {
+  uint32_t *gen, *pf_gen, *sel_gen, *start, *list;
+  unsigned long long *ctl;
+  uint64_t *idx;
+  Pcg64 *rng, *it;
+  uint64_t *occ;
+  uint32_t *host_slot;  // step kernels: pinned host word that receives the step's reset count (NULL: none)
+};
+PfView pf_view(uint8_t *base, int n, int h, int wpr) {
+  const PfLayout L = pf_layout(n, h, wpr);
+  PfView v;
+  v.gen = reinterpret_cast<uint32_t *>(base + L.gen);
+  v.pf_gen = reinterpret_cast<uint32_t *>(base + L.pf_gen);
+  v.sel_gen = reinterpret_cast<uint32_t *>(base + L.sel_gen);
+  v.start = reinterpret_cast<uint32_t *>(base + L.start);
+  v.list = reinterpret_cast<uint32_t *>(base + L.list);
+  v.ctl = reinterpret_cast<unsigned long long *>(base + L.ctl);
+  v.idx = reinterpret_cast<uint64_t *>(base + L.idx);
+  v.rng = reinterpret_cast<Pcg64 *>(base + L.rng);
+  v.it = reinterpret_cast<Pcg64 *>(base + L.it);
+  v.occ = reinterpret_cast<uint64_t *>(base + L.occ);
+  v.host_slot = nullptr;
+  return v;
+}
+static_assert(sizeof(Pcg64) == sizeof(apg_pcg64), "prefetch records hold apg_pcg64 streams");
+APG_DEV uint32_t pf_load_gen(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
+APG_DEV void pf_store_gen(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT); }
+
+// Batch kernel 1: the envs whose record is stale (pf_gen != gen), their streams copied into the records (the
+// only read of the env state by the batch), appended to the list.  ctl[0] was zeroed before the launch.
+__global__ __launch_bounds__(256) void k_pf_select(int n, apg_lidar_state S, PfView V) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  bool sel = false;
+  uint32_t g = 0;
+  if (e < n) {
+    g = pf_load_gen(&V.gen[e]);
+    sel = g != V.pf_gen[e];
+  }
+  const unsigned long long m = __ballot(sel);
+  if (m == 0ULL) return;
+  const int lane = threadIdx.x & 63;
+  unsigned long long base = 0;
+  if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&V.ctl[0], (unsigned long long)__popcll(m));
+  base = __shfl(base, __ffsll((long long)m) - 1);
+  if (sel) {
+    V.rng[e] = *reinterpret_cast<const Pcg64 *>(&S.rng[e]);
+    V.it[e] = *reinterpret_cast<const Pcg64 *>(&S.it_rng[e]);
+    V.sel_gen[e] = g;
+    V.list[base + __popcll(m & ((1ULL << lane) - 1ULL))] = (uint32_t)e;
+  }
+}
+
 // The dataset index of maze i (MZ_MAPS: idx[i]; MZ_RESET: the env's DatasetIterator draw, from its streams
 // or, on reset(seed), from default_rng(seed + i)), with the env's streams after it.
 APG_DEV uint64_t maze_index(const apg_lidar_state &S, const uint64_t *idx, int i, int mode, uint64_t seed,
@@ -402,7 +489,8 @@ constexpr int MP_THREADS = 256, MP_ENVS = 64;
 __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_state S, const uint64_t *idx, int n,
                                                            uint64_t *occ, const uint8_t *scratch, int mode,
                                                            uint64_t seed, int use_seed, int all, int ng,
-                                                           uint64_t *out_map_idx, float *map_obs, uint32_t *err) {
+                                                           uint64_t *out_map_idx, float *map_obs, uint32_t *err,
+                                                           uint32_t *pf_gen_main) {
   __shared__ uint16_t s_list[MP_ENVS];
   __shared__ int s_cnt, s_wsum[MP_THREADS / 64], s_hit[2];
   extern __shared__ uint64_t s_bm[];  // one maze's rows
@@ -481,6 +569,145 @@ __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_stat
       *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
       S.map_idx[e] = midx;
       if (out_map_idx) oat(out_map_idx, g.row, e, 1) = midx;
+      if (pf_gen_main) pf_store_gen(&pf_gen_main[e], pf_gen_main[e] + 1u);  // a prefetched next map is stale now
+    }
+    __syncthreads();  // s_hit / the bitmap are reused by the next maze
+  }
+}
+
+// Batch kernel 2: the random streams of the listed envs' next mazes (k_maze_stream's work): the DatasetIterator
+// draw of each env's next map index (lidar_localization2d.py:296-298, dataset_iterator.py:26-32) from the record's
+// iterator stream, then default_rng(idx)'s outputs into the env's maze scratch.
+__global__ __launch_bounds__(MZS_THREADS) void k_pf_stream(Geo g, PfView V, uint8_t *scratch, int ng) {
+  __shared__ uint64_t s_seed[MZS_MAZES][4];
+  __shared__ uint32_t s_env[MZS_MAZES];
+  __shared__ MzJump s_jump[MZ_MAX_ITEMS + 1];
+  const int tid = threadIdx.x, nitems = ng / MZ_ITEM_GROUPS;
+  const int cnt = (int)V.ctl[0];
+  const int i0 = blockIdx.x * MZS_MAZES;
+  if (i0 >= cnt) return;  // workgroup-uniform: most of the grid when few envs reset
+  if (tid < MZS_MAZES) {
+    if (i0 + tid < cnt) {
+      const uint32_t e = V.list[i0 + tid];
+      Pcg64 it = V.it[e];
+      const uint64_t midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
+      V.it[e] = it;
+      V.idx[e] = midx;
+      const Pcg64 mr = seed_pcg64(midx);  // FloorMapDatasetMaze.get_data_point: default_rng(idx)
+      s_seed[tid][0] = mr.s_hi;
+      s_seed[tid][1] = mr.s_lo;
+      s_seed[tid][2] = mr.i_hi;
+      s_seed[tid][3] = mr.i_lo;
+      s_env[tid] = e;
+    } else {
+      s_seed[tid][2] = s_seed[tid][3] = 0ULL;
+    }
+  } else if (tid - MZS_MAZES <= nitems) {
+    s_jump[tid - MZS_MAZES] = mz_jump((uint64_t)(tid - MZS_MAZES) * MZ_ITEM_GROUPS * MZ_GROUP);
+  }
+  __syncthreads();
+  const size_t sb = maze_scratch_bytes(g.h, g.w), so = maze_stream_off(g.h, g.w);
+  for (int q = tid; q < MZS_MAZES * (nitems + 1); q += MZS_THREADS) {
+    const int j = q / (nitems + 1), c = q - j * (nitems + 1);
+    if (s_seed[j][3] == 0ULL) continue;
+    uint8_t *stream = scratch + (size_t)s_env[j] * sb + so;
+    if (c < nitems) {
+      maze_stream_item(s_seed[j][0], s_seed[j][1], s_seed[j][2], s_seed[j][3], s_jump[c], g.bp, c, stream, ng);
+    } else {
+      uint64_t hi = s_seed[j][0], lo = s_seed[j][1];
+      mz_jump_state(s_jump[c], hi, lo, s_seed[j][2], s_seed[j][3]);
+      uint64_t *st = reinterpret_cast<uint64_t *>(stream + maze_stream_state_off(ng));
+      st[0] = hi;
+      st[1] = lo;
+    }
+  }
+}
+
+// Batch kernel 3: the DFS of the listed envs' next mazes (k_maze's work), carve logs into their scratch.
+template <bool ONEW>
+__global__ __launch_bounds__(64) void k_pf_dfs(Geo g, PfView V, uint8_t *scratch, uint32_t *err, int lanes, int ng) {
+  extern __shared__ uint64_t s_mz[];
+  const int lane = threadIdx.x;
+  const int cnt = (int)V.ctl[0];
+  if (blockIdx.x * lanes >= cnt) return;
+  const int i = blockIdx.x * lanes + lane;
+  const bool active = lane < lanes && i < cnt;
+  const uint32_t e = active ? V.list[i] : 0u;
+  const MazeGeom m = maze_geom(g.h, g.w);
+  const size_t sb = maze_scratch_bytes(g.h, g.w), lb = maze_log_bytes(g.h, g.w);
+  char *lds = reinterpret_cast<char *>(s_mz);
+  maze_table_init(lds, lane);
+  __syncthreads();
+  Pcg64 mr{};
+  if (active) mr = seed_pcg64(V.idx[e]);
+  uint8_t *mine_scr = scratch + (size_t)e * sb;
+  bool bad = false;
+  const int nlog = maze_dfs<ONEW>(mr, mine_scr + maze_stream_off(g.h, g.w), ng, active, m, g.bp, lds, lane,
+                                  mine_scr + lb, reinterpret_cast<uint32_t *>(mine_scr), bad);
+  if (bad) atomicOr(err, APG_ERR_MAPGEN);
+  if (active) *reinterpret_cast<int *>(mine_scr + maze_stream_off(g.h, g.w) + maze_stream_state_off(ng) + 16) = nlog;
+}
+
+// Batch kernel 4: the listed envs' next occupancy rows painted from their carve logs (k_maze_paint's work) into the
+// records, the start cell drawn like place_start (lidar_localization2d.py:304: the pick-th free cell in row-major
+// order, pick = integers(0, nfree) on the env's stream), the record's env stream advanced past that draw, and the
+// record published for the generation k_pf_select saw.  Maps of <= MP_THREADS rows.
+__global__ __launch_bounds__(MP_THREADS) void k_pf_paint(Geo g, PfView V, const uint8_t *scratch, int ng,
+                                                         uint32_t *err) {
+  __shared__ int s_wsum[MP_THREADS / 64], s_hit[2];
+  extern __shared__ uint64_t s_bm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cnt = (int)V.ctl[0];
+  const int i0 = blockIdx.x * MP_ENVS;
+  if (i0 >= cnt) return;
+  const int kn = cnt - i0 < MP_ENVS ? cnt - i0 : MP_ENVS;
+  const MazeGeom m = maze_geom(g.h, g.w);
+  const size_t words = (size_t)g.h * g.wpr, sb = maze_scratch_bytes(g.h, g.w);
+  for (int k = 0; k < kn; k++) {
+    const uint32_t e = V.list[i0 + k];
+    const uint8_t *scr = scratch + (size_t)e * sb;
+    const int nlog = *reinterpret_cast<const int *>(scr + maze_stream_off(g.h, g.w) + maze_stream_state_off(ng) + 16);
+    maze_paint<MP_THREADS>(m, g.wpr, reinterpret_cast<const uint32_t *>(scr), nlog, s_bm, tid);
+    uint64_t *dst = V.occ + (size_t)e * words;
+    for (int q = tid; q < (int)words; q += MP_THREADS) dst[q] = s_bm[q];
+    int fr = 0;
+    if (tid < g.h) {
+      int oc = 0;
+      for (int kk = 0; kk < g.wpr; kk++) oc += __popcll(s_bm[tid * g.wpr + kk]);
+      fr = g.w - oc;
+    }
+    const int incl_w = wave_inclusive_scan(fr, lane);
+    if (lane == 63) s_wsum[wave] = incl_w;
+    if (tid == 0) s_hit[0] = -1;
+    __syncthreads();
+    int before = 0, nfree = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < MP_THREADS / 64; w2++) {
+      before += w2 < wave ? s_wsum[w2] : 0;
+      nfree += s_wsum[w2];
+    }
+    const int incl = incl_w + before, excl = incl - fr;
+    Pcg64 rng = V.rng[e];
+    const long long pick = nfree > 0 ? (long long)integers(rng, 0, nfree) : -1;  // every thread: the same draw
+    if (tid < g.h && pick >= excl && pick < incl) {
+      int k2 = (int)(pick - excl), hx = -1;
+      for (int kk = 0; kk < g.wpr && hx < 0; kk++) {
+        const int lo = 64 * kk;
+        const uint64_t valid = g.w - lo >= 64 ? ~0ULL : ((1ULL << (g.w - lo)) - 1ULL);
+        const uint64_t fm = ~s_bm[tid * g.wpr + kk] & valid;
+        const int c = __popcll(fm);
+        if (k2 < c) hx = lo + select_bit(fm, k2);
+        else k2 -= c;
+      }
+      s_hit[0] = hx;
+      s_hit[1] = tid;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      if (s_hit[0] < 0) atomicOr(err, APG_ERR_MAPGEN);
+      V.start[e] = s_hit[0] < 0 ? ~0u : ((uint32_t)s_hit[1] << 8) | (uint32_t)s_hit[0];
+      V.rng[e] = rng;
+      V.pf_gen[e] = V.sel_gen[e];
     }
     __syncthreads();  // s_hit / the bitmap are reused by the next maze
   }
@@ -489,6 +716,8 @@ __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_stat
 struct StepParams {
   int n, h, w, wpr, beams, step_limit, is_static, R, wrows, log_stats, sparse, row, wlo, whi;
   int lidar16;  // dense lidar rows 16-byte aligned (base pointer and row pitch): vector stores
+  int pretest;  // phase 2a's bounding-box pre-test (rooms: ~1/3 of the beams walk); 0: every beam walks (mazes:
+                // ~98 % of the beams touch a wall, the pre-test only delays them)
   float range, loss_scale, loss_offset;
 };
 
@@ -604,7 +833,7 @@ template <int GEN, bool FUSED, int EPB, bool GR = false, bool ROWP = false>
 __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(StepParams P_in, Geo g, apg_lidar_state S,
                                                                  const float *__restrict__ act,
                                                                  const float *__restrict__ pred,
-                                                                 apg_lidar_outputs O, BinomTable bt) {
+                                                                 apg_lidar_outputs O, BinomTable bt, PfView V) {
   using SS = StepShape<EPB>;
   constexpr int T = SS::T, W = SS::W, LPW = SS::LPW;
   StepParams P = P_in;
@@ -707,8 +936,85 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   if constexpr (FUSED) {
     const uint8_t f0 = my_valid ? S.flags[my_e] : 0;
     const bool pend = my_valid && (f0 & F_AUTORESET);
-    if (__syncthreads_or(pend)) {
-      if constexpr (GEN == GEN_ROOMS) {
+    int npend;
+    if constexpr (GEN == GEN_PF) {
+      // the step's reset count to the prefetcher (pinned host word): every workgroup adds its count, the last one
+      // to finish this point (ticket) publishes the total and rearms the counters for the next step
+      npend = __syncthreads_count(pend);
+      if (tid == 0) {
+        if (npend) __hip_atomic_fetch_add(&V.ctl[1], (unsigned long long)npend, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long t = __hip_atomic_fetch_add(&V.ctl[2], 1ULL, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == gridDim.x - 1) {
+          const unsigned long long tot = __hip_atomic_load(&V.ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          if (V.host_slot) __hip_atomic_store(V.host_slot, (uint32_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(&V.ctl[1], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&V.ctl[2], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    } else {
+      npend = __syncthreads_or(pend);
+    }
+    if (npend) {
+      if constexpr (GEN == GEN_PF) {
+        // Prefetched mazes (the record written by the side stream's batch, k_pf_*): each wave copies the next
+        // occupancy rows of its pending envs (coalesced, into S.occ and the wave's LDS copy) and writes their f32
+        // map obs (bool map / 255, lidar_localization2d.py:299) from that copy; the env's lane then installs the
+        // reset state (start cell, streams after the reset's draws, map index: :293-315) and publishes the new
+        // generation (release: the side stream's select reads the streams after acquiring it)
+        uint64_t *mrow = reinterpret_cast<uint64_t *>(s_dyn) + (size_t)wave * MAX_MAP_ROWS * 2;
+        const int m = P.h, wpr = P.wpr;
+        const int words = m * wpr;
+        uint32_t g0 = 0;
+        bool ready = false;
+        if (pend) {
+          g0 = V.gen[my_e];
+          ready = V.pf_gen[my_e] == g0;
+        }
+        for (int j = 0; j < LPW; j++) {
+          if (!__shfl((int)(pend && ready), j)) continue;  // wave-uniform
+          const int e = base + j * W + wave;
+          const uint64_t *src = V.occ + (size_t)e * words;
+          uint64_t *dst = S.occ + (size_t)e * words;
+          for (int q = lane; q < words; q += 64) {
+            const uint64_t v = src[q];
+            dst[q] = v;
+            mrow[q] = v;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          if (O.map_obs) bitmap_map_obs<64>(mrow, m, P.w, wpr, O.map_obs + (size_t)e * m * P.w, lane);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();  // mrow is rewritten by the next env
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (pend) {
+          float px = 0.5f, py = 0.5f;
+          if (ready) {
+            const uint32_t sc = V.start[my_e];
+            if (sc == ~0u) {
+              atomicOr(O.err, APG_ERR_MAPGEN);
+            } else {
+              px = __fadd_rn((float)(sc & 255u), 0.5f);
+              py = __fadd_rn((float)(sc >> 8), 0.5f);
+            }
+            *reinterpret_cast<Pcg64 *>(&S.rng[my_e]) = V.rng[my_e];
+            *reinterpret_cast<Pcg64 *>(&S.it_rng[my_e]) = V.it[my_e];
+            const uint64_t midx = V.idx[my_e];
+            S.map_idx[my_e] = midx;
+            if (O.map_idx) oat(O.map_idx, P.row, my_e, 1) = midx;
+          } else {
+            atomicOr(O.err, APG_ERR_PREFETCH);  // the host protocol guarantees a record: never in practice
+          }
+          S.pos[2 * my_e] = px;
+          S.pos[2 * my_e + 1] = py;
+          S.init_pos[2 * my_e] = px;
+          S.init_pos[2 * my_e + 1] = py;
+          S.elapsed[my_e] = 0;
+          S.flags[my_e] = (uint8_t)((f0 & F_AUTORESET) | F_JUST_RESET | F_FIRST);
+          pf_store_gen(&V.gen[my_e], g0 + 1u);
+        }
+      } else if constexpr (GEN == GEN_ROOMS) {
         // R1: the env's streams, its next map index and the map's primitives, generated with the
         // working storage interleaved in LDS (a private-array generator would live in scratch memory)
         using L = RoomsLds<EPB>;
@@ -850,7 +1156,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
 
   // ---------------- phase 0: window origins from the pre-move positions; which envs reset
   if (dir_thread) s_dirs[tid >> 1][tid & 1] = dir_v;
-  constexpr bool kMapObsHere = !(FUSED && GEN == GEN_ROOMS);  // fused rooms resets wrote their map obs in R2
+  constexpr bool kMapObsHere = !(FUSED && (GEN == GEN_ROOMS || GEN == GEN_PF));  // fused resets wrote it in phase R
   if (own) {
     s_x0[tid] = (int)floorf(pf_px) - 15;
     s_y0[tid] = (int)floorf(pf_py) - 15;
@@ -1102,6 +1408,9 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   // (an LDS atomic per beam iteration serialized the waves' pre-tests), then the entries, grouped by beam
   uint32_t wbits = 0;
   int wtot = 0;  // wave-uniform
+  if (!P.pretest) {  // every (env, beam) walks: queue entry i is (beam i / EPB, env slot i % EPB), implicitly
+    if (tid == 0) s_cnt[1] = EPB * P.beams;
+  } else
   for (int beam = tid / EPB, it = 0; beam < P.beams; beam += T / EPB, it++) {
     bool walk = false;
     if (e < P.n) {
@@ -1144,8 +1453,9 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
     start = __shfl(start, 0);
     if (start >= nq) break;
     const int i = start + lane;
-    if (i < nq) {
-      const int ent = s_queue[i], qe = ent & 255, beam = ent >> 8;
+    const int ent = P.pretest ? (i < nq ? (int)s_queue[i] : 0) : (i / EPB) << 8 | (i & (EPB - 1));
+    const int qe = ent & 255, beam = ent >> 8;
+    if (i < nq && (P.pretest || base + qe < P.n)) {
       const float qpx = s_pos[qe][0], qpy = s_pos[qe][1];
       const float qx = __fadd_rn(qpx, s_dirs[beam][0]), qy = __fadd_rn(qpy, s_dirs[beam][1]);
       s_lid[qe * LS + beam] = beam_value(lidar_scan_walk(rows_of(qe, qpx, qx), qpx, qpy, qx, qy).dist);
@@ -1391,25 +1701,22 @@ int launch_reset_gen(const Geo &g, const apg_lidar_state *st, uint64_t seed, int
 
 // k_maze over n mazes (MZ_MAPS: occ / idx; MZ_RESET: the state's envs, all or the pending autoresets).
 // Dynamic LDS: the lanes' DFS state, at least one paint bitmap.
-int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, int n, uint64_t *occ, uint8_t *scratch,
-                int mode, uint64_t seed, int use_seed, int all, uint64_t *out_map_idx, float *map_obs, uint32_t *err,
-                hipStream_t s) {
-  if (!scratch) return fail(APG_E_INVALID, "maze maps need the maze scratch buffer (stack)");
-  const MazeGeom m = maze_geom(g.h, g.w);
-  if (m.ncx > 127 || m.ncy > 127) return fail(APG_E_INVALID, "maze maps must be at most 255 x 255");
+// Lanes (mazes) per one-wave k_maze / k_pf_dfs workgroup for n mazes; APG_MAZE_LANES overrides (tuning A/B only:
+// the mazes do not depend on it)
+int maze_lanes(int n) {
   int lanes = gen_lanes(n);
-  static int forced = -1;  // APG_MAZE_LANES (tuning A/B only: the mazes do not depend on it)
+  static int forced = -1;
   if (forced < 0) {
     const char *e = getenv("APG_MAZE_LANES");
     forced = e ? atoi(e) : 0;
   }
   if (forced > 0 && forced <= 64) lanes = forced;
-  const size_t dyn = maze_wg_lds_bytes(g.h, g.w);  // laid out for 64 lanes whatever `lanes` is
-  const bool onew = m.ncx <= 63;
-  const void *kern = onew ? (const void *)k_maze<true> : (const void *)k_maze<false>;
-  if (int rc = opt_in_lds(kern, dyn)) return rc;
-  // stream groups per maze: APG_MAZE_STREAM_GROUPS (tests: fewer, so the DFS steps the LCG past them; the
-  // mazes do not depend on it) is clamped to [MZ_ITEM_GROUPS, maze_stream_groups], a multiple of MZ_ITEM_GROUPS
+  return lanes;
+}
+
+// Stream groups per maze: APG_MAZE_STREAM_GROUPS (tests: fewer, so the DFS steps the LCG past them; the mazes do not
+// depend on it) is clamped to [MZ_ITEM_GROUPS, maze_stream_groups], a multiple of MZ_ITEM_GROUPS
+int maze_ng(const Geo &g) {
   static int forced_ng = -1;
   if (forced_ng < 0) {
     const char *e = getenv("APG_MAZE_STREAM_GROUPS");
@@ -1417,6 +1724,21 @@ int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, in
   }
   int ng = maze_stream_groups(g.h, g.w);
   if (forced_ng > 0) ng = std::max(MZ_ITEM_GROUPS, std::min(ng, forced_ng / MZ_ITEM_GROUPS * MZ_ITEM_GROUPS));
+  return ng;
+}
+
+int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, int n, uint64_t *occ, uint8_t *scratch,
+                int mode, uint64_t seed, int use_seed, int all, uint64_t *out_map_idx, float *map_obs, uint32_t *err,
+                hipStream_t s, uint32_t *pf_gen_main = nullptr) {
+  if (!scratch) return fail(APG_E_INVALID, "maze maps need the maze scratch buffer (stack)");
+  const MazeGeom m = maze_geom(g.h, g.w);
+  if (m.ncx > 127 || m.ncy > 127) return fail(APG_E_INVALID, "maze maps must be at most 255 x 255");
+  const int lanes = maze_lanes(n);
+  const size_t dyn = maze_wg_lds_bytes(g.h, g.w);  // laid out for 64 lanes whatever `lanes` is
+  const bool onew = m.ncx <= 63;
+  const void *kern = onew ? (const void *)k_maze<true> : (const void *)k_maze<false>;
+  if (int rc = opt_in_lds(kern, dyn)) return rc;
+  const int ng = maze_ng(g);
   if (ng / MZ_ITEM_GROUPS > MZ_MAX_ITEMS) return fail(APG_E_INVALID, "maze stream too long");
   hipLaunchKernelGGL(k_maze_stream, dim3(grid_for(n, MZS_MAZES)), dim3(MZS_THREADS), 0, s, g, st, idx, n, scratch, mode,
                      seed, use_seed, all, ng);
@@ -1429,7 +1751,8 @@ int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, in
                        use_seed, all, err, lanes, ng);
   if (int rc = check_launch("k_maze")) return rc;
   hipLaunchKernelGGL(k_maze_paint, dim3(grid_for(n, MP_ENVS)), dim3(MP_THREADS), (size_t)g.h * g.wpr * sizeof(uint64_t),
-                     s, g, st, idx, n, occ, scratch, mode, seed, use_seed, all, ng, out_map_idx, map_obs, err);
+                     s, g, st, idx, n, occ, scratch, mode, seed, use_seed, all, ng, out_map_idx, map_obs, err,
+                     pf_gen_main);
   return check_launch("k_maze_paint");
 }
 
@@ -1479,7 +1802,14 @@ bool big_rooms(const apg_lidar_config *c) {
 
 int step_gen(const Geo &g) {
   if (g.is_static) return GEN_NONE;
-  return GEN_ROOMS;  // mazes: k_maze (autoresets) + the unfused step kernel
+  return GEN_ROOMS;  // mazes: GEN_PF (prefetched), or k_maze (autoresets) + the unfused step kernel
+}
+
+// Mazes whose next maps can be prefetched and installed by the fused step kernel: rows <= MAX_MAP_ROWS (one wave's
+// LDS row copy, k_pf_paint's one row per thread), two row words, the staged-window step instance.
+bool pf_supported(const apg_lidar_config *c) {
+  return c->map_kind == APG_MAP_MAZE && !c->is_static && c->height <= MAX_MAP_ROWS && c->width <= 128 &&
+         (int)ceilf(c->lidar_range) <= MAX_WIN_RANGE;
 }
 
 int cu_count() {
@@ -1508,30 +1838,35 @@ int step_epb(int n) {
 
 template <int GEN, bool FUSED, int EPB, bool GR = false>
 int launch_step_t(const StepParams &P, const Geo &g, const apg_lidar_state *st, const float *act, const float *pred,
-                  const apg_lidar_outputs *out, hipStream_t s, const BinomTable &bt) {
+                  const apg_lidar_outputs *out, hipStream_t s, const BinomTable &bt, const PfView &V) {
   size_t lds = step_lds_bytes(EPB, P.beams);
   if (FUSED && GEN == GEN_ROOMS && RoomsLds<EPB>::bytes > lds) lds = RoomsLds<EPB>::bytes;
+  if (FUSED && GEN == GEN_PF) lds = std::max(lds, (size_t)(4 * EPB / 64) * MAX_MAP_ROWS * 2 * sizeof(uint64_t));
   auto kern = P.row ? k_lidar_step<GEN, FUSED, EPB, GR, true> : k_lidar_step<GEN, FUSED, EPB, GR, false>;
   if (int rc = opt_in_lds((const void *)kern, lds)) return rc;
-  hipLaunchKernelGGL(kern, dim3(grid_for(P.n, EPB)), dim3(4 * EPB), lds, s, P, g, *st, act, pred, *out, bt);
+  hipLaunchKernelGGL(kern, dim3(grid_for(P.n, EPB)), dim3(4 * EPB), lds, s, P, g, *st, act, pred, *out, bt, V);
   return check_launch("k_lidar_step");
 }
 
+// pf: the prefetch view (its host_slot set) when the autoresets install prefetched mazes (GEN_PF), else NULL
 template <int EPB>
 int launch_step_epb(const StepParams &P, const Geo &g, const apg_lidar_state *st, const float *act, const float *pred,
-                    const apg_lidar_outputs *out, hipStream_t s, bool fused) {
+                    const apg_lidar_outputs *out, hipStream_t s, bool fused, const PfView *pf) {
   const BinomTable bt = make_binom_table();
+  PfView V{};
+  if (pf) V = *pf;
   if (P.R > MAX_WIN_RANGE) {  // scans longer than the staged window covers: rows from global memory (EPB 64)
-    if (!fused) return launch_step_t<GEN_NONE, false, 64, true>(P, g, st, act, pred, out, s, bt);
+    if (!fused) return launch_step_t<GEN_NONE, false, 64, true>(P, g, st, act, pred, out, s, bt, V);
     switch (step_gen(g)) {
-      case GEN_ROOMS: return launch_step_t<GEN_ROOMS, true, 64, true>(P, g, st, act, pred, out, s, bt);
-      default: return launch_step_t<GEN_NONE, true, 64, true>(P, g, st, act, pred, out, s, bt);
+      case GEN_ROOMS: return launch_step_t<GEN_ROOMS, true, 64, true>(P, g, st, act, pred, out, s, bt, V);
+      default: return launch_step_t<GEN_NONE, true, 64, true>(P, g, st, act, pred, out, s, bt, V);
     }
   }
-  if (!fused) return launch_step_t<GEN_NONE, false, EPB>(P, g, st, act, pred, out, s, bt);
+  if (!fused) return launch_step_t<GEN_NONE, false, EPB>(P, g, st, act, pred, out, s, bt, V);
+  if (pf) return launch_step_t<GEN_PF, true, EPB == 128 ? 256 : EPB>(P, g, st, act, pred, out, s, bt, V);
   switch (step_gen(g)) {
-    case GEN_ROOMS: return launch_step_t<GEN_ROOMS, true, EPB>(P, g, st, act, pred, out, s, bt);
-    default: return launch_step_t<GEN_NONE, true, EPB>(P, g, st, act, pred, out, s, bt);
+    case GEN_ROOMS: return launch_step_t<GEN_ROOMS, true, EPB>(P, g, st, act, pred, out, s, bt, V);
+    default: return launch_step_t<GEN_NONE, true, EPB>(P, g, st, act, pred, out, s, bt, V);
   }
 }
 
@@ -1545,7 +1880,8 @@ __global__ __launch_bounds__(256) void k_episode_stats(StepParams P, const float
 }
 
 int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *act,
-                       const float *pred, const apg_lidar_outputs *out, hipStream_t s, bool fused) {
+                       const float *pred, const apg_lidar_outputs *out, hipStream_t s, bool fused,
+                       const PfView *pf = nullptr) {
   StepParams P;
   P.n = cfg->num_envs;
   P.h = cfg->height;
@@ -1563,6 +1899,12 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   // of its scans, plus two rows for the walk's one-crossing-ahead row reads past the segment's end
   P.wlo = std::max(0, 15 - (P.R + 5) - 2);
   P.whi = std::min(MAX_WIN_ROWS, 15 + (P.R + 5) + 2 + 1);
+  static int forced_pt = -2;  // APG_STEP_PRETEST=0|1 (tuning A/B only: the outputs do not depend on it)
+  if (forced_pt == -2) {
+    const char *e = getenv("APG_STEP_PRETEST");
+    forced_pt = e ? atoi(e) : -1;
+  }
+  P.pretest = forced_pt >= 0 ? forced_pt : (cfg->map_kind == APG_MAP_MAZE ? 0 : 1);
   P.lidar16 = (P.beams & 3) == 0 && (reinterpret_cast<uintptr_t>(out->lidar) & 15) == 0;
   P.range = cfg->lidar_range;
   P.loss_scale = cfg->loss_scale;
@@ -1570,13 +1912,167 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   const Geo g = make_geo(cfg);
   int rc;
   switch (step_epb(P.n)) {
-    case 256: rc = launch_step_epb<256>(P, g, st, act, pred, out, s, fused); break;
-    case 128: rc = launch_step_epb<128>(P, g, st, act, pred, out, s, fused); break;
-    default: rc = launch_step_epb<64>(P, g, st, act, pred, out, s, fused); break;
+    case 256: rc = launch_step_epb<256>(P, g, st, act, pred, out, s, fused, pf); break;
+    case 128: rc = launch_step_epb<128>(P, g, st, act, pred, out, s, fused, pf); break;
+    default: rc = launch_step_epb<64>(P, g, st, act, pred, out, s, fused, pf); break;
   }
   if (rc || !P.log_stats || P.step_limit <= PW_PTR_MAX_N) return rc;
   hipLaunchKernelGGL(k_episode_stats, dim3(grid_for(P.n, 256)), dim3(256), 0, s, P, st->stats_hist, *out);
   return check_launch("k_episode_stats");
+}
+
+// One prefetch batch on the prefetcher's side stream (k_pf_select .. k_pf_paint), after `after` (an event of the
+// env's stream): the next mazes of every env whose record is stale by then.
+int pf_batch_kernels(const apg_lidar_config *cfg, const apg_lidar_state *st, const apg_lidar_outputs *out,
+                     hipStream_t side) {
+  const Geo g = make_geo(cfg);
+  const int n = g.n;
+  PfView V = pf_view(st->prefetch, n, g.h, g.wpr);
+  uint8_t *scratch = reinterpret_cast<uint8_t *>(st->stack);
+  const MazeGeom m = maze_geom(g.h, g.w);
+  const int ng = maze_ng(g), lanes = maze_lanes(n);
+  if (!scratch) return fail(APG_E_INVALID, "maze prefetch needs the maze scratch buffer (stack)");
+  if (ng / MZ_ITEM_GROUPS > MZ_MAX_ITEMS) return fail(APG_E_INVALID, "maze stream too long");
+  const size_t dyn = maze_wg_lds_bytes(g.h, g.w);
+  const bool onew = m.ncx <= 63;
+  const void *kern = onew ? (const void *)k_pf_dfs<true> : (const void *)k_pf_dfs<false>;
+  if (int rc = opt_in_lds(kern, dyn)) return rc;
+  if (hipMemsetAsync(&V.ctl[0], 0, sizeof(unsigned long long), side) != hipSuccess)
+    return fail(APG_E_LAUNCH, "hipMemsetAsync (prefetch count)");
+  hipLaunchKernelGGL(k_pf_select, dim3(grid_for(n, 256)), dim3(256), 0, side, n, *st, V);
+  if (int rc = check_launch("k_pf_select")) return rc;
+  hipLaunchKernelGGL(k_pf_stream, dim3(grid_for(n, MZS_MAZES)), dim3(MZS_THREADS), 0, side, g, V, scratch, ng);
+  if (int rc = check_launch("k_pf_stream")) return rc;
+  if (onew)
+    hipLaunchKernelGGL(k_pf_dfs<true>, dim3(grid_for(n, lanes)), dim3(64), dyn, side, g, V, scratch, out->err, lanes, ng);
+  else
+    hipLaunchKernelGGL(k_pf_dfs<false>, dim3(grid_for(n, lanes)), dim3(64), dyn, side, g, V, scratch, out->err, lanes,
+                       ng);
+  if (int rc = check_launch("k_pf_dfs")) return rc;
+  hipLaunchKernelGGL(k_pf_paint, dim3(grid_for(n, MP_ENVS)), dim3(MP_THREADS), (size_t)g.h * g.wpr * sizeof(uint64_t),
+                     side, g, V, scratch, ng, out->err);
+  return check_launch("k_pf_paint");
+}
+
+}  // namespace
+
+// The host side of the map prefetch (apgym_capi.h).  Steps are numbered from the last reset (step 0: every env
+// reset); step c's kernel writes its reset count to host_ring[c % R] and c's completion event is main_ev[c % R].
+struct apg_lidar_prefetcher {
+  struct Batch {
+    int64_t rmin, s;  // covers the resets of steps rmin .. s (rmin: the first of them)
+    hipEvent_t ev;    // recorded on the side stream after the batch
+  };
+  int device = -1;
+  int n = 0, h = 0, w = 0, L = 0, R = 0;
+  hipStream_t side = nullptr;
+  uint32_t *host_ring = nullptr, *dev_ring = nullptr;
+  std::vector<hipEvent_t> main_ev;
+  std::deque<Batch> batches;
+  std::vector<hipEvent_t> spare;
+  int64_t c = 0;            // step calls since the last reset
+  int64_t observed = 0;     // reset counts read for steps <= observed
+  int64_t pending_rmin = -1;  // first observed reset step not in a batch yet (-1: none)
+  bool dirty = true;        // no reset yet, or steps ran outside the protocol (stream capture)
+  int64_t stats[4] = {0, 0, 0, 0};
+};
+
+namespace {
+
+hipEvent_t pf_take_event(apg_lidar_prefetcher *p) {
+  if (!p->spare.empty()) {
+    hipEvent_t e = p->spare.back();
+    p->spare.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  return e;
+}
+
+// completed batches off the front of the list (their events back to the spares)
+void pf_retire(apg_lidar_prefetcher *p) {
+  while (!p->batches.empty() && hipEventQuery(p->batches.front().ev) == hipSuccess) {
+    p->spare.push_back(p->batches.front().ev);
+    p->batches.pop_front();
+  }
+}
+
+// a batch after `after` (an event of the env's stream) covering the resets of steps rmin .. s
+int pf_launch(apg_lidar_prefetcher *p, const apg_lidar_config *cfg, const apg_lidar_state *st,
+              const apg_lidar_outputs *out, hipEvent_t after, int64_t rmin, int64_t s) {
+  if (hipStreamWaitEvent(p->side, after, 0) != hipSuccess) return fail(APG_E_LAUNCH, "hipStreamWaitEvent (prefetch)");
+  if (int rc = pf_batch_kernels(cfg, st, out, p->side)) return rc;
+  hipEvent_t ev = pf_take_event(p);
+  if (!ev || hipEventRecord(ev, p->side) != hipSuccess) return fail(APG_E_LAUNCH, "hipEventRecord (prefetch)");
+  p->batches.push_back({rmin, s, ev});
+  p->pending_rmin = -1;
+  p->stats[0]++;
+  return APG_OK;
+}
+
+// read the reset count of step o (its completion event has been seen)
+void pf_observe(apg_lidar_prefetcher *p, int64_t o) {
+  const uint32_t cnt = *reinterpret_cast<volatile uint32_t *>(&p->host_ring[o % p->R]);
+  p->stats[2] += cnt;
+  if (cnt && p->pending_rmin < 0) p->pending_rmin = o;
+  p->observed = o;
+}
+
+// Before step c (p->c already incremented) on the env's stream `s`: observe the finished steps' reset counts,
+// launch a batch for new resets, and make `s` wait for the batches covering the resets at steps <= c - L - 1.
+int pf_before_step(apg_lidar_prefetcher *p, const apg_lidar_config *cfg, const apg_lidar_state *st,
+                   const apg_lidar_outputs *out, hipStream_t s) {
+  const int64_t c = p->c;
+  if (p->dirty) {  // the records may be stale for any env: one batch after everything queued so far, waited for
+    hipEvent_t mark = p->main_ev[(c - 1 + p->R) % p->R];
+    if (hipEventRecord(mark, s) != hipSuccess) return fail(APG_E_LAUNCH, "hipEventRecord (prefetch)");
+    if (int rc = pf_launch(p, cfg, st, out, mark, 0, c - 1)) return rc;
+    if (hipStreamWaitEvent(s, p->batches.back().ev, 0) != hipSuccess)
+      return fail(APG_E_LAUNCH, "hipStreamWaitEvent (prefetch)");
+    p->stats[1]++;
+    p->observed = c - 1;
+    p->pending_rmin = -1;
+    p->dirty = false;
+    return APG_OK;
+  }
+  while (p->observed < c - 1) {  // non-blocking: steps the GPU has finished
+    const hipError_t q = hipEventQuery(p->main_ev[(p->observed + 1) % p->R]);
+    if (q == hipErrorNotReady) break;
+    if (q != hipSuccess) return fail(APG_E_LAUNCH, "hipEventQuery (prefetch)");
+    pf_observe(p, p->observed + 1);
+  }
+  const int64_t d = c - p->L - 1;  // resets at steps <= d may autoreset again at step c
+  while (p->observed < d) {  // the GPU is more than a whole episode behind: block on the step's event
+    if (hipEventSynchronize(p->main_ev[(p->observed + 1) % p->R]) != hipSuccess)
+      return fail(APG_E_LAUNCH, "hipEventSynchronize (prefetch)");
+    pf_observe(p, p->observed + 1);
+  }
+  if (p->pending_rmin >= 0) {
+    if (int rc = pf_launch(p, cfg, st, out, p->main_ev[p->observed % p->R], p->pending_rmin, p->observed)) return rc;
+  }
+  pf_retire(p);
+  // the last batch holding a reset at a step <= d (the side stream is in order: it implies the earlier ones)
+  const apg_lidar_prefetcher::Batch *need = nullptr;
+  for (const auto &b : p->batches)
+    if (b.rmin <= d) need = &b;
+  if (need) {
+    if (hipStreamWaitEvent(s, need->ev, 0) != hipSuccess) return fail(APG_E_LAUNCH, "hipStreamWaitEvent (prefetch)");
+    p->stats[1]++;
+  }
+  return APG_OK;
+}
+
+apg_lidar_prefetcher *prefetcher_of(const apg_lidar_config *cfg, const apg_lidar_state *st) {
+  if (!st->prefetcher || !st->prefetch || !pf_supported(cfg)) return nullptr;
+  auto *p = reinterpret_cast<apg_lidar_prefetcher *>(st->prefetcher);
+  if (p->n != cfg->num_envs || p->h != cfg->height || p->w != cfg->width || p->L != cfg->step_limit) return nullptr;
+  return p;
+}
+
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
 }
 
 }  // namespace
@@ -1598,6 +2094,7 @@ int apg_lidar_query_sizes(const apg_lidar_config *cfg, apg_lidar_state_sizes *o)
   o->scratch_bytes = 0;  // reserved (rooms maps are painted from primitives, no scratch plane)
   o->stack_bytes = g.kind == APG_MAP_MAZE ? (size_t)g.frames * (g.is_static ? 1 : (size_t)g.n) * sizeof(uint16_t) : 0;
   // (maze scratch: apg_maze.hpp's carve log + spilled DFS frames, maze_frames u16 per map)
+  o->prefetch_bytes = pf_supported(cfg) ? pf_layout(g.n, g.h, g.wpr).bytes : 0;
   return APG_OK;
 }
 
@@ -1618,10 +2115,33 @@ int apg_lidar_reset(const apg_lidar_config *cfg, const apg_lidar_state *st, uint
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   Geo g = make_geo(cfg);
-  if ((rc = launch_reset(g, st, seed, use_seed, 1, out, s))) return rc;
+  apg_lidar_prefetcher *p = prefetcher_of(cfg, st);
+  if (p && !p->batches.empty() && hipStreamWaitEvent(s, p->batches.back().ev, 0) != hipSuccess)
+    return fail(APG_E_LAUNCH, "hipStreamWaitEvent (prefetch)");  // the batches use the maze scratch too
+  if (g.kind == APG_MAP_MAZE && !g.is_static) {
+    uint32_t *gen = st->prefetch && pf_supported(cfg) ? pf_view(st->prefetch, g.n, g.h, g.wpr).gen : nullptr;
+    rc = launch_maze(g, *st, nullptr, g.n, nullptr, reinterpret_cast<uint8_t *>(st->stack), MZ_RESET, seed, use_seed,
+                     1, out->map_idx, out->map_obs, out->err, s, gen);
+  } else {
+    rc = launch_reset(g, st, seed, use_seed, 1, out, s);
+  }
+  if (rc) return rc;
   apg_lidar_outputs o2 = *out;
   if (g.kind == APG_MAP_MAZE && !g.is_static) o2.map_obs = nullptr;  // written by k_maze
-  return launch_step_kernel(cfg, st, nullptr, nullptr, &o2, s, false);
+  if ((rc = launch_step_kernel(cfg, st, nullptr, nullptr, &o2, s, false))) return rc;
+  if (p && !capturing(s)) {  // step 0: every env reset; its next maps are prefetched from here
+    for (auto &b : p->batches) p->spare.push_back(b.ev);  // the env's stream waited for them above
+    p->batches.clear();
+    p->c = 0;
+    p->observed = 0;
+    p->pending_rmin = -1;
+    if (hipEventRecord(p->main_ev[0], s) != hipSuccess) return fail(APG_E_LAUNCH, "hipEventRecord (prefetch)");
+    if ((rc = pf_launch(p, cfg, st, out, p->main_ev[0], 0, 0))) return rc;
+    p->dirty = false;
+  } else if (p) {
+    p->dirty = true;
+  }
+  return APG_OK;
 }
 
 int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
@@ -1635,18 +2155,33 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
   if (cfg->sparse && !out->weight) return fail(APG_E_INVALID, "sparse needs the weight buffer");
   hipStream_t s = (hipStream_t)stream;
   // rooms / static maps: one launch per step, the fused step kernel performs the NEXT_STEP autoresets itself;
-  // mazes: k_maze resets the envs with an autoreset pending (its waves exit at once when there are none),
+  // mazes with a prefetcher: one launch per step, the fused step kernel installs the prefetched next maps;
+  // other mazes: k_maze resets the envs with an autoreset pending (its waves exit at once when there are none),
   // then the unfused step kernel
+  apg_lidar_prefetcher *p = prefetcher_of(cfg, st);
+  const bool use_pf = p && !capturing(s);
+  PfView V{};
+  if (use_pf) {
+    p->c++;
+    if ((rc = pf_before_step(p, cfg, st, out, s))) return rc;
+    V = pf_view(st->prefetch, cfg->num_envs, cfg->height, (cfg->width + 63) / 64);
+    V.host_slot = p->dev_ring + p->c % p->R;
+  } else if (p) {
+    p->dirty = true;  // (stream capture) this step generates its mazes synchronously
+  }
   if (ev_begin && hipEventRecord((hipEvent_t)ev_begin, s) != hipSuccess) return fail(APG_E_LAUNCH, "hipEventRecord");
-  if (big_rooms(cfg)) {
+  if (use_pf) {
+    rc = launch_step_kernel(cfg, st, action, prediction, out, s, true, &V);
+  } else if (big_rooms(cfg)) {
     // rooms the fused step kernel's LDS generator does not hold (max_rooms > 17, maps > 128): the pending
     // autoresets in k_lidar_reset, then the unfused step kernel (it writes their map obs)
     rc = launch_reset_gen<GEN_ROOMS>(make_geo(cfg), st, 0, 0, 0, out, s);
     if (rc == APG_OK) rc = launch_step_kernel(cfg, st, action, prediction, out, s, false);
   } else if (cfg->map_kind == APG_MAP_MAZE && !cfg->is_static) {
     const Geo g = make_geo(cfg);
+    uint32_t *gen = st->prefetch && pf_supported(cfg) ? pf_view(st->prefetch, g.n, g.h, g.wpr).gen : nullptr;
     rc = launch_maze(g, *st, nullptr, g.n, nullptr, reinterpret_cast<uint8_t *>(st->stack), MZ_RESET, 0, 0, 0,
-                     out->map_idx, out->map_obs, out->err, s);
+                     out->map_idx, out->map_obs, out->err, s, gen);
     apg_lidar_outputs o2 = *out;
     o2.map_obs = nullptr;  // written by k_maze
     if (rc == APG_OK) rc = launch_step_kernel(cfg, st, action, prediction, &o2, s, false);
@@ -1655,7 +2190,67 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
   }
   if (rc == APG_OK && ev_end && hipEventRecord((hipEvent_t)ev_end, s) != hipSuccess)
     return fail(APG_E_LAUNCH, "hipEventRecord");
+  if (rc == APG_OK && use_pf && hipEventRecord(p->main_ev[p->c % p->R], s) != hipSuccess)
+    return fail(APG_E_LAUNCH, "hipEventRecord (prefetch)");
   return rc;
+}
+
+int apg_lidar_prefetcher_create(const apg_lidar_config *cfg, apg_lidar_prefetcher **out) {
+  int rc = validate(cfg);
+  if (rc) return rc;
+  if (!out) return fail(APG_E_INVALID, "null output");
+  if (!pf_supported(cfg))
+    return fail(APG_E_INVALID, "map prefetch needs dynamic maze maps of <= 128 x 128 cells and lidar_range <= 10");
+  auto *p = new apg_lidar_prefetcher();
+  p->n = cfg->num_envs;
+  p->h = cfg->height;
+  p->w = cfg->width;
+  p->L = cfg->step_limit;
+  p->R = cfg->step_limit + 2;
+  int least = 0, greatest = 0;
+  bool ok = hipGetDevice(&p->device) == hipSuccess && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+            hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, least) == hipSuccess;
+  void *ring = nullptr;
+  ok = ok && hipHostMalloc(&ring, (size_t)p->R * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess;
+  if (ok) {
+    p->host_ring = static_cast<uint32_t *>(ring);
+    memset(p->host_ring, 0, (size_t)p->R * sizeof(uint32_t));
+    void *dptr = nullptr;
+    ok = hipHostGetDevicePointer(&dptr, ring, 0) == hipSuccess;
+    p->dev_ring = static_cast<uint32_t *>(dptr);
+  }
+  p->main_ev.assign(p->R, nullptr);
+  for (int i = 0; ok && i < p->R; i++) ok = hipEventCreateWithFlags(&p->main_ev[i], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    apg_lidar_prefetcher_destroy(p);
+    return fail(APG_E_LAUNCH, "prefetcher: stream / pinned ring / event creation failed");
+  }
+  *out = p;
+  return APG_OK;
+}
+
+int apg_lidar_prefetcher_destroy(apg_lidar_prefetcher *p) {
+  if (!p) return APG_OK;
+  int dev = -1;
+  hipGetDevice(&dev);
+  if (p->device >= 0) hipSetDevice(p->device);
+  if (p->side) hipStreamSynchronize(p->side);
+  for (auto &b : p->batches) hipEventDestroy(b.ev);
+  for (auto e : p->spare) hipEventDestroy(e);
+  for (auto e : p->main_ev)
+    if (e) hipEventDestroy(e);
+  if (p->side) hipStreamDestroy(p->side);
+  if (p->host_ring) hipHostFree(p->host_ring);
+  if (dev >= 0) hipSetDevice(dev);
+  delete p;
+  return APG_OK;
+}
+
+int apg_lidar_prefetcher_stats(const apg_lidar_prefetcher *p, int64_t out[4]) {
+  if (!p || !out) return fail(APG_E_INVALID, "null prefetcher / output");
+  for (int i = 0; i < 3; i++) out[i] = p->stats[i];
+  out[3] = p->c;
+  return APG_OK;
 }
 
 int apg_lidar_step(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,

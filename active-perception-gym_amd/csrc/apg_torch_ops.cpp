@@ -23,6 +23,7 @@
 #include <torch/library.h>
 
 #include <cstddef>
+#include <cstdint>
 #include <cstring>
 #include <vector>
 
@@ -65,10 +66,12 @@ struct LidarEnv : torch::CustomClassHolder {
   at::Device dev = at::Device(at::kCUDA, 0);
 
   // ints: num_envs, height, width, map_kind, is_static, static_map_index, beams, step_limit, max_rooms,
-  // door_width, log_stats, sparse, out_row_bytes; reals: lidar_range, loss_scale, loss_offset, branching_prob
+  // door_width, log_stats, sparse, out_row_bytes, prefetcher handle (apg_lidar_prefetcher_create's pointer or 0:
+  // owned by the Python env); reals: lidar_range, loss_scale, loss_offset, branching_prob.  The state buffers end
+  // with the prefetch buffer and a 0-element placeholder for the prefetcher field.
   LidarEnv(std::vector<int64_t> ints, std::vector<double> reals, std::vector<at::Tensor> state,
            std::vector<at::Tensor> outputs) {
-    TORCH_CHECK(ints.size() == 13 && reals.size() == 4, "LidarEnv: 13 ints and 4 reals expected");
+    TORCH_CHECK(ints.size() == 14 && reals.size() == 4, "LidarEnv: 14 ints and 4 reals expected");
     cfg.num_envs = (int32_t)ints[0];
     cfg.height = (int32_t)ints[1];
     cfg.width = (int32_t)ints[2];
@@ -88,6 +91,7 @@ struct LidarEnv : torch::CustomClassHolder {
     cfg.branching_prob = reals[3];
     fill_ptrs(st, state, "LidarEnv state");
     fill_ptrs(out, outputs, "LidarEnv outputs");
+    st.prefetcher = reinterpret_cast<void *>(static_cast<uintptr_t>(ints[13]));
     for (auto &t : state)
       if (t.defined() && t.numel() > 0) dev = t.device();
     keep = state;
@@ -102,16 +106,17 @@ struct ImageEnv : torch::CustomClassHolder {
   std::vector<at::Tensor> keep;
   at::Device dev = at::Device(at::kCUDA, 0);
 
-  // ints: the 16 int32 fields of apg_image_config up to env_offset, pool_len, log_stats, sparse;
+  // ints: the 16 int32 fields of apg_image_config up to env_offset, pool_len, log_stats, sparse, out_row_bytes;
   // reals: sensor_scale, max_step[2], cell[2], ce_scale, ce_offset, mse_scale, mse_offset
   ImageEnv(std::vector<int64_t> ints, std::vector<double> reals, std::vector<at::Tensor> state,
            std::vector<at::Tensor> outputs) {
-    TORCH_CHECK(ints.size() == 19 && reals.size() == 9, "ImageEnv: 19 ints and 9 reals expected");
+    TORCH_CHECK(ints.size() == 20 && reals.size() == 9, "ImageEnv: 20 ints and 9 reals expected");
     int32_t *f = &cfg.num_envs;  // num_envs .. env_offset: 16 consecutive int32 fields
     for (int i = 0; i < 16; i++) f[i] = (int32_t)ints[i];
     cfg.pool_len = ints[16];
     cfg.log_stats = (int32_t)ints[17];
     cfg.sparse = (int32_t)ints[18];
+    cfg.out_row_bytes = (int32_t)ints[19];
     cfg.sensor_scale = reals[0];
     cfg.max_step[0] = reals[1];
     cfg.max_step[1] = reals[2];

@@ -77,6 +77,7 @@ extern "C" {
 #define APG_ERR_MAPGEN 4u         /* internal map-generation bound exceeded */
 #define APG_ERR_OOB_Y 8u          /* "One of the requested xi is out of bounds in dimension 0" */
 #define APG_ERR_OOB_X 16u         /* "One of the requested xi is out of bounds in dimension 1" */
+#define APG_ERR_PREFETCH 32u      /* a maze autoreset found no prefetched map (prefetch protocol violated) */
 
 #define APG_MAP_ROOMS 0
 #define APG_MAP_MAZE 1
@@ -131,6 +132,10 @@ typedef struct apg_lidar_state {
   uint64_t *map_idx;   /* [N]   dataset index of the current map */
   const float *beam_dirs; /* [beams][2] lidar_directions (f32, computed by the host like the reference) */
   float *stats_hist;   /* [2][step_limit][N] per-step euclidean_distance, mse of the episode (log_stats) */
+  uint8_t *prefetch;   /* prefetch_bytes (apg_lidar_query_sizes) of zeroed device memory, or NULL: the next map of
+                          every env, generated ahead of its autoreset (mazes up to 128 rows) */
+  void *prefetcher;    /* apg_lidar_prefetcher_create() handle owning the side stream that fills `prefetch`, or
+                          NULL (then mazes are generated synchronously by the autoreset step) */
 } apg_lidar_state;
 
 typedef struct apg_lidar_outputs {
@@ -157,6 +162,7 @@ typedef struct apg_lidar_outputs {
 typedef struct apg_lidar_state_sizes {
   size_t occ_bytes, scratch_bytes, stack_bytes; /* bytes of the variable-size buffers (scratch_bytes: reserved, 0) */
   int32_t wpr, maze_frames;
+  size_t prefetch_bytes;                        /* apg_lidar_state.prefetch (0: the configuration has no prefetch) */
 } apg_lidar_state_sizes;
 
 const char *apg_version(void);
@@ -183,6 +189,26 @@ int apg_lidar_step(const apg_lidar_config *cfg, const apg_lidar_state *st, const
 int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
                             const float *prediction, const apg_lidar_outputs *out, apg_stream_t stream,
                             void *ev_begin, void *ev_end);
+
+/* ---------------------------------------------------------------- map prefetch (dynamic mazes)
+ * The reference builds each sub-env's DataLoader(prefetch=True, prefetch_buffer_size=128): a background thread
+ * generates the next maps while the env steps (ap_gym/envs/lidar_localization2d.py:130-131, 296-298;
+ * ap_gym/envs/dataset/buffered_iterator.py:11-61).  Here every env's next maze (map index, occupancy rows, start
+ * cell and its streams after that reset, all independent of the actions) is generated on a low-priority side
+ * stream right after the env's reset, into apg_lidar_state.prefetch, and the fused step kernel's autoreset only
+ * copies it in (occupancy rows, f32 map obs, state).  The prefetcher is the host side of that protocol, driven by
+ * apg_lidar_reset / apg_lidar_step on the env's stream: after a step with autoresets (it reads the per-step reset
+ * count the step kernel writes to pinned host memory, without synchronizing) it launches a prefetch batch on the
+ * side stream, and before step c it makes the step's stream wait for the batches covering every reset at steps
+ * <= c - step_limit - 1 (the earliest an env can reset again), so an autoreset never waits on a map unless the
+ * side stream fell that far behind.  Create it after apg_lidar_init on the env's device; one prefetcher per env
+ * state; not thread-safe.  Steps captured into a hipGraph (stream capture) generate their mazes synchronously. */
+typedef struct apg_lidar_prefetcher apg_lidar_prefetcher;
+int apg_lidar_prefetcher_create(const apg_lidar_config *cfg, apg_lidar_prefetcher **out);
+int apg_lidar_prefetcher_destroy(apg_lidar_prefetcher *p); /* synchronizes its side stream first */
+/* per-prefetcher counters: [0] batches launched, [1] steps whose main stream had to wait for a batch that was still
+ * running, [2] resets observed, [3] step calls since the last reset (diagnostics, host memory) */
+int apg_lidar_prefetcher_stats(const apg_lidar_prefetcher *p, int64_t out[4]);
 
 /* u16 units of maze scratch per map (apg_lidar_state.stack / apg_map_generate's stack) for an h x w maze;
  * replaces the reference's recursion stack of carve() (floor_map_dataset_maze.py:31-45). */
@@ -269,6 +295,12 @@ typedef struct apg_image_config {
   int32_t log_stats;          /* 1: the registered ids' vector log wrapper statistics */
   int32_t sparse;             /* 1: the -sparse ids (SparsifyVectorWrapper, sparsify_wrapper.py:23-92):
                                  reward = base_reward - loss * terminated */
+  int32_t out_row_bytes;      /* 0: dense outputs.  > 0 (a multiple of 8): packed rows — the per-env outputs glimpse,
+                                 glimpse_pos, time_step, target_glimpse, reward, base_reward, target, label_target,
+                                 loss_f64, loss_f32, stats (as [N][4]) and stats_idx (as [N][2]) of env e are at their
+                                 pointer + e * out_row_bytes, i.e. the pointers are field offsets into one
+                                 [N][out_row_bytes] buffer that a sharded run all-gathers as is (ABI 0.2; the row
+                                 must hold the enabled fields: apg_image_* reject a smaller one) */
 } apg_image_config;
 
 typedef struct apg_image_state {

@@ -487,6 +487,79 @@ def test_torch_backend_matches_numpy_backend(gpu, env_id):
     e_t.check_errors()
 
 
+def _torch_outputs(env):
+    out = {k: v.clone() for k, v in env.device_outputs().items()}
+    for k in ("pos", "map_idx_out", "stats", "stats_len", "elapsed"):
+        out[k] = env._t[k].clone()
+    return out
+
+
+@pytest.mark.parametrize("size,beams,n,limit", [(21, 8, 512, 7), (63, 16, 256, 3), (127, 64, 64, 5)])
+def test_maze_prefetch_matches_synchronous_generation(gpu, size, beams, n, limit):
+    """The maze prefetch (next maps generated on the side stream, installed by the fused step kernel) gives the
+    outputs of synchronous generation bit for bit: many autoresets, a NaN-delayed env whose episode ends at a
+    step no other env resets at, reset() and reset(seed) mid-episode, and a captured graph (synchronous steps)
+    followed by eager steps."""
+    import torch
+
+    import ap_gym_amd as ap
+
+    ds = ap.FloorMapDatasetMaze(size, size)
+    kw = dict(num_envs=n, dataset=ds, lidar_beam_count=beams, device=gpu, array_backend="torch",
+              max_episode_steps=limit, log_stats=True)
+    pf = ap.LIDARLocalization2DVectorEnv(prefetch=True, **kw)
+    sy = ap.LIDARLocalization2DVectorEnv(prefetch=False, **kw)
+    assert pf._prefetcher and not sy._prefetcher
+    g = torch.Generator(device=gpu).manual_seed(5)
+
+    def step_both(a, p):
+        pf.step({"action": a, "prediction": p})
+        sy.step({"action": a, "prediction": p})
+        o1, o2 = _torch_outputs(pf), _torch_outputs(sy)
+        for k in o1:
+            assert torch.equal(o1[k], o2[k]), k
+
+    def rand():
+        return torch.rand((n, 2), generator=g, device=gpu) * 2 - 1, torch.rand((n, 2), generator=g, device=gpu) * 2 - 1
+
+    pf.reset(seed=11)
+    sy.reset(seed=11)
+    for t in range(4 * (limit + 1) + 3):
+        a, p = rand()
+        if t == limit + 3:  # env 3's step is refused: its episode (and its resets) shift by one step
+            a[3, 0] = float("nan")
+        step_both(a, p)
+        if t == limit + 3:
+            for e in (pf, sy):
+                with pytest.raises(ValueError, match="NaN values detected in action."):
+                    e.check_errors()
+    for e in (pf, sy):
+        e.reset()  # streams continue
+    for t in range(limit + 4):
+        step_both(*rand())
+    for e in (pf, sy):
+        e.reset(seed=12)
+    for t in range(limit // 2):
+        step_both(*rand())
+    # a captured step (the synchronous path) replayed across an autoreset, then eager steps again
+    a_s, p_s = rand()
+    graphs = [e.capture_step_graph(a_s, p_s) for e in (pf, sy)]
+    for t in range(limit + 2):
+        for gr in graphs:
+            gr.replay()
+        o1, o2 = _torch_outputs(pf), _torch_outputs(sy)
+        for k in o1:
+            assert torch.equal(o1[k], o2[k]), k
+    for t in range(2 * (limit + 1) + 1):
+        step_both(*rand())
+    for e in (pf, sy):
+        e.check_errors()
+    st = pf.prefetch_stats()
+    assert st["batches"] >= 5 and st["resets"] > 0
+    pf.close()
+    sy.close()
+
+
 @pytest.mark.parametrize("kind", ["rooms", "maze"])
 def test_numpy_backend_copy_semantics(gpu, kind):
     """copy=None (numpy backend -> True, SyncVectorEnv's default): observations returned at step t keep their
@@ -516,7 +589,7 @@ def test_numpy_backend_copy_semantics(gpu, kind):
             assert np.array_equal(o[k], snap[k]), k
     assert not held[-1][0]["map"].flags.writeable
     assert not np.array_equal(held[0][1]["map"], held[-1][1]["map"])  # the maps did change at the resets
-    assert oa["map"] is obs0_a["map"]  # copy=False: one mirror, rewritten in place
+    assert np.shares_memory(oa["map"], obs0_a["map"])  # copy=False: one mirror, rewritten in place
     env.close()
     alias.close()
 

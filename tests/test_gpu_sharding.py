@@ -30,7 +30,7 @@ def _make(kind, num_envs, env_offset=0, num_envs_total=None, **kw):
     ds = ap.SyntheticImageClassificationDataset(64, (32, 32, 3), 10, 3, seed=3)
     cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=(8, 8), step_limit=8)
     return ap.ImageLocalizationVectorEnv(num_envs, cfg, device="cuda:0", array_backend="torch",
-                                         num_envs_total=num_envs_total or num_envs, env_offset=env_offset)
+                                         num_envs_total=num_envs_total or num_envs, env_offset=env_offset, **kw)
 
 
 def _steps(kind):
@@ -114,7 +114,7 @@ def _worker(rank, world, port, kind, outdir, backend="gloo"):
     senv = ShardedVectorEnv(lambda num_envs, env_offset, **kw: _make(kind, num_envs, env_offset, N_TOTAL, **kw),
                             N_TOTAL, rank, world, beams=16 if kind == "lidar" else None, gather=True,
                             gather_glimpse=True)
-    assert senv._packed == (kind == "lidar")  # LIDAR: the kernel writes the all-gather's send rows
+    assert senv._packed  # the step kernels write the all-gather's send rows (LIDAR and image envs)
     lo, n = senv.offset, senv.local_num_envs
     obs0, info0 = senv.reset(seed=5)
     rows = []
@@ -198,6 +198,49 @@ def test_packed_output_rows_equal_dense(gpu, log_stats, sparse):
                 m = envs[0]._t["reset_mask"]
                 x, y = x[m], y[m]
             assert torch.equal(x.cpu(), y.cpu()), f"step {t}: {k}"
+    for e in envs:
+        e.check_errors()
+        e.close()
+
+
+@pytest.mark.parametrize("kind,log_stats,sparse", [("cls", True, False), ("cls", False, True), ("loc", True, False),
+                                                   ("loc", False, False)])
+def test_image_packed_output_rows_equal_dense(gpu, kind, log_stats, sparse):
+    """Image envs with packed_outputs=True (the fused step kernel, the reset path and the autoreset glimpses write
+    [N, row] rows for the all-gather) vs the dense outputs, across two batch autoresets."""
+    import torch
+
+    import ap_gym_amd as ap
+
+    ch = 3 if kind == "loc" else 1
+    ds = ap.SyntheticImageClassificationDataset(64, (32, 32, ch) if ch == 3 else (28, 28), 10, ch, seed=3)
+    cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=(8, 8) if kind == "loc" else (5, 5), step_limit=6)
+    cls = ap.ImageLocalizationVectorEnv if kind == "loc" else ap.ImageClassificationVectorEnv
+    envs = [cls(N_TOTAL, cfg, device="cuda:0", array_backend="torch", log_stats=log_stats, sparse=sparse,
+                packed_outputs=p) for p in (False, True)]
+    assert envs[1].output_rows is not None and envs[0].output_rows is None
+    names = ["glimpse", "glimpse_pos", "time_step", "reward", "base_reward"] + (
+        ["target_glimpse", "target_out", "loss_f32"] if kind == "loc" else ["label_target", "loss_f64"]) + (
+        ["stats"] + (["stats_idx"] if kind == "cls" else []) if log_stats else [])
+
+    def check(t):
+        for k in names:
+            assert torch.equal(envs[0]._t[k].cpu(), envs[1]._t[k].cpu()), f"step {t}: {k}"
+
+    for e in envs:
+        e.reset(seed=21)
+    check(-1)
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    for t in range(15):
+        a = torch.rand((N_TOTAL, 2), device="cuda:0", generator=g) * 2 - 1
+        p = (torch.randn((N_TOTAL, 10), device="cuda:0", generator=g) if kind == "cls"
+             else torch.rand((N_TOTAL, 2), device="cuda:0", generator=g) * 2 - 1)
+        outs = [e.step({"action": a, "prediction": p}) for e in envs]
+        check(t)
+        if log_stats and "stats" in outs[0][4]:
+            s0, s1 = outs[0][4]["stats"]["scalar"], outs[1][4]["stats"]["scalar"]
+            for key in s0:
+                assert torch.equal(s0[key].cpu(), s1[key].cpu()), (t, key)
     for e in envs:
         e.check_errors()
         e.close()

@@ -262,7 +262,7 @@ def test_torch_ops_library_registers_the_ops():
     for name in ("lidar_reset", "lidar_step", "image_reset", "image_step"):
         assert callable(getattr(ops, name)), name
     assert torch.classes.apgym.LidarEnv is not None and torch.classes.apgym.ImageEnv is not None
-    with pytest.raises(RuntimeError, match="13 ints"):
+    with pytest.raises(RuntimeError, match="14 ints"):
         torch.classes.apgym.LidarEnv([1], [0.0], [], [])
 
 

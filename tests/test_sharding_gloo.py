@@ -147,3 +147,184 @@ def test_two_rank_gather_equals_unsharded(tmp_path, oracle_mod, packed):
         saw_reset |= bool(full.truncated.any() or full.terminated.any())
     assert saw_reset  # the trace crosses the TimeLimit autoreset
     full.close()
+
+
+# ---------------------------------------------------------------------------------------- image envs
+# Each rank runs the numpy restatement of the whole batch (the image envs draw every batch from one stream, so a
+# shard draws the whole batch and keeps its slice, as the device env does with num_envs_total / env_offset) and
+# hands over its slice in the torch output contract of the image envs — densely (the copying path) or in the
+# packed output rows of image_env.image_output_row_layout (the zero-copy path).
+IMG_N, IMG_STEPS, IMG_LIMIT, IMG_SENSOR = 8, 21, 8, (5, 5)
+
+
+def _img_pool():
+    rng = np.random.default_rng(3)
+    return rng.integers(0, 256, (32, 16, 16, 1)).astype(np.uint8), rng.integers(0, 10, 32).astype(np.int32)
+
+
+def _img_actions(kind):
+    rng = np.random.default_rng(2)
+    a = rng.uniform(-1, 1, (IMG_STEPS, IMG_N, 2)).astype(np.float32)
+    p = (rng.standard_normal((IMG_STEPS, IMG_N, 10)) if kind == "cls"
+         else rng.uniform(-1, 1, (IMG_STEPS, IMG_N, 2))).astype(np.float32)
+    return a, p
+
+
+class _ImageOracleShard:
+    def __init__(self, kind, num_envs, env_offset, packed_outputs=False):
+        from ap_gym_amd import _native as N
+        from ap_gym_amd.image_env import image_output_row_layout, image_row_views
+        from oracle import image_oracle as io
+
+        pool, labels = _img_pool()
+        self.kname, self.lo, self.n = kind, env_offset, num_envs
+        self.kind = N.APG_IMAGE_CLASSIFY if kind == "cls" else N.APG_IMAGE_LOCALIZE
+        self.single_observation_space = {"glimpse": np.zeros(IMG_SENSOR + (1,), np.float32)}  # .shape only
+        self.e = io.ImageVectorEnvOracle(kind, pool, labels, 10, 1, IMG_N, IMG_SENSOR, step_limit=IMG_LIMIT)
+        self.copy = False
+        self._prev_done = False
+        self.output_rows = self.output_layout = None
+        if packed_outputs:
+            self.output_layout, row = image_output_row_layout(self.kind, IMG_SENSOR, 1, log_stats=True)
+            self.output_rows = torch.zeros((num_envs, row), dtype=torch.uint8)
+            self.v = image_row_views(self.output_rows, self.output_layout)
+
+    def _metric_names(self):
+        return ("correct_label_prob", "accuracy") if self.kname == "cls" else ("euclidean_distance", "mse")
+
+    def _sl(self, x):
+        return torch.from_numpy(np.ascontiguousarray(np.asarray(x)[self.lo:self.lo + self.n]))
+
+    def _obs(self, o):
+        out = {k: self._sl(o[k]) for k in ("glimpse", "glimpse_pos", "time_step")}
+        if "target_glimpse" in o:
+            out["target_glimpse"] = self._sl(o["target_glimpse"])
+        return out
+
+    def reset(self, *, seed=None, options=None):
+        o, info = self.e.reset(seed)
+        self._prev_done = False
+        obs = self._obs(o)
+        if self.output_rows is not None:
+            for k in obs:
+                self.v[k].copy_(obs[k])
+        return obs, {"index": self._sl(info["index"])}
+
+    def step(self, action):
+        # the other shards' envs step with zeros: an env's outputs depend only on its own action / prediction
+        a = np.zeros((IMG_N, 2), np.float32)
+        p = np.zeros((IMG_N,) + tuple(action["prediction"].shape[1:]), np.float32)
+        a[self.lo:self.lo + self.n] = action["action"].numpy()
+        p[self.lo:self.lo + self.n] = action["prediction"].numpy()
+        o, r, te, tr, info = self.e.step(a, p)
+        self._prev_done = bool(te.any())
+        obs = self._obs(o)
+        tgt = info["prediction"]["target"]
+        loss = info["prediction"]["loss"]
+        ti = {"index": self._sl(info["index"]), "base_reward": self._sl(np.asarray(info["base_reward"], np.float32)),
+              "prediction": {"target": self._sl(tgt if self.kname == "cls" else np.asarray(tgt, np.float32)),
+                             "loss": self._sl(np.asarray(loss, np.float64 if self.kname == "cls" else np.float32))}}
+        if "stats" in info:
+            ti["stats"] = {"vector": {}, "_vector": self._sl(info["stats"]["_vector"]), "np": info["stats"]}
+        if self.output_rows is not None:
+            v = self.v
+            for k in obs:
+                v[k].copy_(obs[k])
+            v["reward"].copy_(self._sl(np.asarray(r, np.float64)))
+            v["base_reward"].copy_(ti["base_reward"])
+            if self.kname == "cls":
+                v["label_target"].copy_(ti["prediction"]["target"])
+                v["loss_f64"].copy_(ti["prediction"]["loss"])
+            else:
+                v["target_out"].copy_(ti["prediction"]["target"])
+                v["loss_f32"].copy_(ti["prediction"]["loss"])
+            if "stats" in info:
+                sc = info["stats"]["scalar"]
+                nm = self._metric_names()
+                for j, key in enumerate((f"final_{nm[0]}", f"final_{nm[1]}", f"avg_{nm[0]}", f"avg_{nm[1]}")):
+                    v["stats"][j].copy_(self._sl(sc[key]))
+                if self.kname == "cls":
+                    v["stats_idx"][0].copy_(self._sl(sc["first_correct"]))
+                    v["stats_idx"][1].copy_(self._sl(sc["last_incorrect"]))
+        return obs, self._sl(np.asarray(r, np.float64)), self._sl(te), self._sl(tr), ti
+
+    def close(self):
+        pass
+
+
+def _img_worker(rank, world, port, outdir, kind, packed):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ap_gym_amd.sharding import ShardedVectorEnv
+
+    def make(num_envs, env_offset, packed_outputs=False):
+        return _ImageOracleShard(kind, num_envs, env_offset, packed_outputs)
+
+    senv = ShardedVectorEnv(make, IMG_N, rank, world, gather=True, gather_glimpse=True)
+    assert senv._packed == packed or not packed
+    if not packed:  # the copying path: a factory without packed_outputs
+        senv = ShardedVectorEnv(lambda num_envs, env_offset: _ImageOracleShard(kind, num_envs, env_offset), IMG_N, rank,
+                                world, gather=True, gather_glimpse=True)
+        assert not senv._packed
+    acts, preds = _img_actions(kind)
+    lo, n = senv.offset, senv.local_num_envs
+    obs, info = senv.reset(seed=7)
+    out = {}
+    if packed:  # (the copying path gathers step outputs only)
+        out["reset_glimpse"] = obs["glimpse"].numpy().copy()
+        out["reset_index"] = info["index"].numpy().copy()
+    for t in range(IMG_STEPS):
+        obs, rew, term, trunc, info = senv.step({"action": torch.from_numpy(acts[t, lo:lo + n]),
+                                                 "prediction": torch.from_numpy(preds[t, lo:lo + n])})
+        for k in ("glimpse", "glimpse_pos", "time_step", "target_glimpse"):
+            if k in obs:
+                out[f"{k}_{t}"] = obs[k].numpy().copy()
+        out[f"reward_{t}"] = rew.numpy().copy()
+        out[f"term_{t}"] = term.numpy().copy()
+        out[f"base_{t}"] = info["base_reward"].numpy().copy()
+        out[f"target_{t}"] = info["prediction"]["target"].numpy().copy()
+        out[f"loss_{t}"] = info["prediction"]["loss"].numpy().copy()
+        out[f"index_{t}"] = info["index"].numpy().copy()
+        if packed and "stats" in info:
+            for key, val in info["stats"]["scalar"].items():
+                out[f"stats_{t}_{key}"] = val.numpy().copy()
+    np.savez(os.path.join(outdir, f"img_rank{rank}.npz"), **out)
+    senv.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("packed", [False, True], ids=["copying", "packed_rows"])
+@pytest.mark.parametrize("kind", ["cls", "loc"])
+def test_two_rank_image_gather_equals_unsharded(tmp_path, kind, packed):
+    from oracle import image_oracle as io
+
+    mp.start_processes(_img_worker, args=(2, _free_port(), str(tmp_path), kind, packed), nprocs=2, join=True,
+                       start_method="spawn")
+    r0, r1 = np.load(tmp_path / "img_rank0.npz"), np.load(tmp_path / "img_rank1.npz")
+    assert sorted(r0.files) == sorted(r1.files)
+    for k in r0.files:
+        assert np.array_equal(r0[k], r1[k], equal_nan=True), k  # every rank holds the full batch
+    pool, labels = _img_pool()
+    full = io.ImageVectorEnvOracle(kind, pool, labels, 10, 1, IMG_N, IMG_SENSOR, step_limit=IMG_LIMIT)
+    o, info = full.reset(7)
+    if packed:
+        assert np.array_equal(r0["reset_glimpse"], o["glimpse"])
+        assert np.array_equal(r0["reset_index"], info["index"])
+    acts, preds = _img_actions(kind)
+    ends = 0
+    for t in range(IMG_STEPS):
+        o, r, te, tr, info = full.step(acts[t], preds[t])
+        for k in ("glimpse", "glimpse_pos", "time_step", "target_glimpse"):
+            if k in o:
+                assert np.array_equal(r0[f"{k}_{t}"], o[k]), (k, t)
+        assert np.array_equal(r0[f"reward_{t}"], np.asarray(r, np.float64)), t
+        assert np.array_equal(r0[f"term_{t}"], te), t
+        assert np.array_equal(r0[f"base_{t}"], np.asarray(info["base_reward"], np.float32)), t
+        assert np.array_equal(r0[f"target_{t}"], np.asarray(info["prediction"]["target"]).astype(r0[f"target_{t}"].dtype))
+        assert np.array_equal(r0[f"index_{t}"], info["index"]), t
+        if packed and "stats" in info:
+            ends += 1
+            for key, val in info["stats"]["scalar"].items():
+                if not key.startswith("_"):
+                    assert np.array_equal(r0[f"stats_{t}_{key}"], val), (t, key)
+    assert not packed or ends == 2
