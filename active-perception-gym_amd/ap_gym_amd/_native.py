@@ -100,7 +100,7 @@ class ImageConfig(ctypes.Structure):
 class ImageState(ctypes.Structure):
     _fields_ = [(n, _vp) for n in ("pool", "pool_labels", "unique_grid", "index", "label", "inverted", "pos",
                                    "target", "rng", "scratch_i64", "scratch_f64", "top_k", "rng_work",
-                                   "stats_hist")]
+                                   "stats_hist", "ahead_i64", "ahead_f64", "rng_saved")]
 
 
 class ImageOutputs(ctypes.Structure):
@@ -170,6 +170,8 @@ SYMBOLS = [
                                        ctypes.POINTER(ImageOutputs), _vp]),
     ("apg_image_step", ctypes.c_int, [ctypes.POINTER(ImageConfig), ctypes.POINTER(ImageState), _vp, _vp,
                                       ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ImageOutputs), _vp]),
+    ("apg_image_draw_ahead", ctypes.c_int, [ctypes.POINTER(ImageConfig), ctypes.POINTER(ImageState), _vp]),
+    ("apg_image_discard_ahead", ctypes.c_int, [ctypes.POINTER(ImageConfig), ctypes.POINTER(ImageState), _vp]),
     ("apg_image_glimpse", ctypes.c_int, [ctypes.POINTER(ImageConfig), _vp, _vp, _vp, ctypes.c_int, ctypes.c_int32,
                                          _vp, _vp, _vp]),
     ("apg_image_unique_top_k", ctypes.c_int, [ctypes.POINTER(ImageConfig), _vp, _vp, _vp, ctypes.c_int32,

@@ -123,7 +123,8 @@ class _ImageVectorEnv(VectorEnv):
     def __init__(self, num_envs: int, image_perception_config: ImagePerceptionConfig,
                  render_mode: str = "rgb_array", device=None, copy: bool = False, strict_errors: bool = False,
                  array_backend: str = "numpy", num_envs_total: int | None = None, env_offset: int = 0,
-                 log_stats: bool = False, sparse: bool = False, render_envs=None, packed_outputs: bool = False):
+                 log_stats: bool = False, sparse: bool = False, render_envs=None, packed_outputs: bool = False,
+                 draw_ahead: bool = True):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -254,7 +255,11 @@ class _ImageVectorEnv(VectorEnv):
             stats_hist=(t.zeros((n, 2, int(cfg.step_limit)), dtype=t.float32, device=dev) if self.log_stats
                         else None),
             stats=t.zeros((4, n), dtype=t.float32, device=dev) if self.log_stats else None,
-            stats_idx=t.zeros((2, n), dtype=t.int32, device=dev) if self.log_stats else None)
+            stats_idx=t.zeros((2, n), dtype=t.int32, device=dev) if self.log_stats else None,
+            # the next batch autoreset's draws, made ahead on a side stream (apg_image_draw_ahead)
+            ahead_i64=t.zeros(2 * nt, dtype=t.int64, device=dev),
+            ahead_f64=t.zeros(4 * nt, dtype=t.float64, device=dev),
+            rng_saved=t.zeros((3, 5), dtype=t.int64, device=dev))
         # packed_outputs: the per-env outputs are field views of one [n, row] buffer (ShardedVectorEnv's send)
         self.output_rows = None
         if row_bytes:
@@ -262,7 +267,8 @@ class _ImageVectorEnv(VectorEnv):
             T.update(image_row_views(self.output_rows, self.output_layout))
         self._state = N.ImageState(*[N.ptr(T[k_]) for k_ in ("pool", "pool_labels", "unique_grid", "index", "label",
                                                               "inverted", "pos", "target", "rng", "scratch_i64",
-                                                              "scratch_f64", "top_k", "rng_work", "stats_hist")])
+                                                              "scratch_f64", "top_k", "rng_work", "stats_hist",
+                                                              "ahead_i64", "ahead_f64", "rng_saved")])
         self._out = N.ImageOutputs(*[N.ptr(T[k_]) for k_ in ("glimpse", "glimpse_pos", "time_step", "target_glimpse",
                                                               "reward", "base_reward", "target_out", "label_target",
                                                               "loss_f64", "loss_f32", "err", "stats", "stats_idx")])
@@ -284,10 +290,17 @@ class _ImageVectorEnv(VectorEnv):
              c.mse_scale, c.mse_offset],
             N.op_buffers([T[k_] for k_ in ("pool", "pool_labels", "unique_grid", "index", "label", "inverted", "pos",
                                            "target", "rng", "scratch_i64", "scratch_f64", "top_k", "rng_work",
-                                           "stats_hist")], dev),
+                                           "stats_hist", "ahead_i64", "ahead_f64", "rng_saved")], dev),
             N.op_buffers([T[k_] for k_ in ("glimpse", "glimpse_pos", "time_step", "target_glimpse", "reward",
                                            "base_reward", "target_out", "label_target", "loss_f64", "loss_f32", "err",
                                            "stats", "stats_idx")], dev))
+        # The next batch's draws depend only on the module / iterator / env streams, never on actions, so they are
+        # made right after each batch reset on a low-priority side stream (the reference draws them inside the
+        # autoreset step): that step then installs them in the fused step kernel, one launch instead of five.
+        self.draw_ahead = bool(draw_ahead)
+        self._ahead_stream = t.cuda.Stream(dev, priority=0) if self.draw_ahead else None
+        self._ahead_event = t.cuda.Event() if self.draw_ahead else None
+        self._ahead = False  # draws made ahead and not yet installed
         self._err_host = t.zeros(1, dtype=t.int32).pin_memory()
         self._err_event = t.cuda.Event()
         self._err_pending = False
@@ -379,13 +392,21 @@ class _ImageVectorEnv(VectorEnv):
         L = N.lib()
         if seed is None and not self._seeded:
             seed = int(np.random.SeedSequence().entropy) & ((1 << 63) - 1)
+        if seed is not None and (not isinstance(seed, (int, np.integer)) or int(seed) < 0 or int(seed) >= 2**64):
+            raise ValueError("seed must be a non-negative int below 2**64")
+        if self._ahead:  # the batch is replaced here: the streams go back to before the draws made ahead
+            import torch
+
+            torch.cuda.current_stream(self.device).wait_event(self._ahead_event)
+            N.check(L.apg_image_discard_ahead(ctypes.byref(self._cfg), ctypes.byref(self._state), self._stream()),
+                    "apg_image_discard_ahead")
+            self._ahead = False
         if seed is not None:
-            if not isinstance(seed, (int, np.integer)) or int(seed) < 0 or int(seed) >= 2**64:
-                raise ValueError("seed must be a non-negative int below 2**64")
             N.check(L.apg_image_seed(ctypes.byref(self._cfg), ctypes.byref(self._state), int(seed), self._stream()),
                     "apg_image_seed")
             self._seeded = True
         self._ops.image_reset(self._h)
+        self._launch_draw_ahead()
         self._t_step = 0
         self._prev_done = False
         self._visits = [[] for _ in self.render_envs]  # module.reset clears the overlay (:184-186)
@@ -425,20 +446,28 @@ class _ImageVectorEnv(VectorEnv):
             a_t = N.as_device_f32(a, self._dev, 2 * n, (n, 2), name="action")
             p_t = N.as_device_f32(p, self._dev, pdim * n, (n, pdim), name="prediction")
         resetting = self._prev_done
+        flags = 0
+        if resetting:
+            flags = 1
+            if self._ahead:  # install the draws made ahead (the step's stream waits for the side stream)
+                torch.cuda.current_stream(self.device).wait_event(self._ahead_event)
+                flags |= 2
+                self._ahead = False
         self._track_render(p_np if numpy_mode else p_t, resetting)
         ev = self._kernel_events
         if ev is not None:  # bench timing: hipEvents on the launch stream right around the step's launches
             N.event_record(ev[0], N.current_stream_ptr(self._dev))
         if self.use_torch_op:
-            self._step_op(self._h, a_t, p_t, int(self._t_step), bool(resetting))
+            self._step_op(self._h, a_t, p_t, int(self._t_step), flags)
         elif N.wrong_current_device(self._dev):  # the op's DeviceGuard, for the direct call
             with torch.cuda.device(self._dev):
-                self._c_step(a_t, p_t, resetting)
+                self._c_step(a_t, p_t, flags)
         else:
-            self._c_step(a_t, p_t, resetting)
+            self._c_step(a_t, p_t, flags)
         if ev is not None:
             N.event_record(ev[1], N.current_stream_ptr(self._dev))
         if resetting:
+            self._launch_draw_ahead()  # the next batch's draws, while this episode steps
             self._t_step = 0
             terminated = False
         else:
@@ -455,11 +484,26 @@ class _ImageVectorEnv(VectorEnv):
         Python step), on their stream (bench.py's live timing).  None disables."""
         self._kernel_events = None if begin is None else (begin, end)
 
-    def _c_step(self, a_t, p_t, resetting):
+    def _launch_draw_ahead(self):
+        """The next batch autoreset's draws (apg_image_draw_ahead) on the side stream, after the work queued so far
+        on the env's stream (the reset that just replaced the batch)."""
+        if not self.draw_ahead:
+            return
+        import torch
+
+        main = torch.cuda.current_stream(self.device)
+        self._ahead_stream.wait_stream(main)
+        with torch.cuda.stream(self._ahead_stream):
+            N.check(N.lib().apg_image_draw_ahead(ctypes.byref(self._cfg), ctypes.byref(self._state),
+                                                 self._ahead_stream.cuda_stream), "apg_image_draw_ahead")
+        self._ahead_event.record(self._ahead_stream)
+        self._ahead = True
+
+    def _c_step(self, a_t, p_t, flags):
         if self._c_args is None:
             self._c_args = (ctypes.byref(self._cfg), ctypes.byref(self._state), ctypes.byref(self._out))
         cfg, st, out = self._c_args
-        rc = N.lib().apg_image_step(cfg, st, a_t.data_ptr(), p_t.data_ptr(), int(self._t_step), 1 if resetting else 0,
+        rc = N.lib().apg_image_step(cfg, st, a_t.data_ptr(), p_t.data_ptr(), int(self._t_step), flags,
                                     out, N.current_stream_ptr(self._dev))
         if rc:
             N.check(rc, "apg_image_step")

@@ -602,7 +602,17 @@ struct EnvArgs {
   float time_value;
   float loss_weight;  // 1, or for the -sparse ids terminated.astype(float32) (one value: episodes end together)
   const float *copy_target;  // localize, steps without a target refresh: prediction_target = target.copy() here
+  // the batch autoreset with its draws made ahead (apg_image_draw_ahead), k_image_gather and k_loc_target folded
+  // into the step kernel: draws of env e at d = offset + e; NULL: the draws (if any) are installed already
+  const int64_t *ahead_idx, *ahead_inv;
+  const double *ahead_pos, *ahead_tgt;
+  const int32_t *pool_labels;
+  int invert, offset;
+  int64_t *index_st;
+  int32_t *label_st, *inverted_st;
+  float *target_st;
 };
+
 
 // scipy.special.log_softmax(row)[target] in float32 (x_max zeroed when not finite); -> -value
 APG_DEV float ce_f32(const float *row, int k, int target) {
@@ -687,6 +697,36 @@ struct EnvIn {
   float p0, p1, t0, t1;  // localization: prediction, target before the autoreset update
   int32_t label;         // classification
 };
+// The batch autoreset of env e from the draws made ahead (k_image_gather + k_loc_target): the new data point,
+// its label (inverted when drawn so), start position, and (localize) the pre-update target as this step's
+// prediction target, the refreshed target into the state.  Returns the new image's pool index.
+APG_DEV int64_t install_ahead(const EnvArgs &a, int e, const apg_image_outputs &out, double *pos, EnvIn &in) {
+  const int d = a.offset + e;
+  const int64_t idx = a.ahead_idx[d];
+  a.index_st[e] = idx;
+  int32_t l = a.pool_labels[idx];
+  if (a.invert) {
+    const int32_t inv = a.ahead_inv[d] == 1 ? 1 : 0;  // integers(0, 2, N) == 1
+    a.inverted_st[e] = inv;
+    if (inv) l = a.k - l - 1;
+  }
+  a.label_st[e] = l;
+  in.label = l;
+  in.px = a.ahead_pos[2 * d];
+  in.py = a.ahead_pos[2 * d + 1];
+  pos[2 * e] = in.px;
+  pos[2 * e + 1] = in.py;
+  if (a.kind == APG_IMAGE_LOCALIZE) {  // prediction_target = target.copy(); target[prev_done] = uniform draws
+    in.t0 = a.target_st[2 * e];
+    in.t1 = a.target_st[2 * e + 1];
+    ro(out.target, a.row, e, 2, 0) = in.t0;
+    ro(out.target, a.row, e, 2, 1) = in.t1;
+    a.target_st[2 * e] = (float)a.ahead_tgt[2 * d];
+    a.target_st[2 * e + 1] = (float)a.ahead_tgt[2 * d + 1];
+  }
+  return idx;
+}
+
 template <int KIND>
 APG_DEV EnvIn load_env_in(const EnvArgs &a, int e, const float *__restrict__ act, const float *__restrict__ pred,
                           const int32_t *label, const double *pos, const apg_image_outputs &out) {
@@ -973,8 +1013,16 @@ __attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fuse
     in = EnvIn{};
     if (r < nu) {
       const int e = u0 + r;
-      in = load_env_in<KIND>(a, e, act, pred, label, pos, out);
-      s_base[r] = index[e] * g.img_elems;
+      if (a.ahead_idx) {  // the batch autoreset, its draws made ahead: installed here (k_image_gather folded in)
+        if constexpr (KIND == APG_IMAGE_LOCALIZE) {
+          in.p0 = pred[2 * e];
+          in.p1 = pred[2 * e + 1];
+        }
+        s_base[r] = install_ahead(a, e, out, pos, in) * g.img_elems;
+      } else {
+        in = load_env_in<KIND>(a, e, act, pred, label, pos, out);
+        s_base[r] = index[e] * g.img_elems;
+      }
       double px = in.px, py = in.py;
       if (!a.resetting) move_pos(a, in.a0, in.a1, px, py);  // the autoreset step observes the new batch in place
       s_npos[r][0] = px;
@@ -1714,23 +1762,39 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
   if (c->log_stats && (!st->stats_hist || !out->stats || (c->kind == APG_IMAGE_CLASSIFY && !out->stats_idx)))
     return fail(APG_E_INVALID, "log_stats needs stats_hist, stats (and stats_idx) buffers");
   hipStream_t s = (hipStream_t)stream;
-  const int n = c->num_envs;
+  const int n = c->num_envs, nt = c->num_envs_total;
+  const bool ahead = (prev_done & 2) != 0;
+  prev_done &= 1;
+  if (ahead && (!prev_done || !st->ahead_i64 || !st->ahead_f64))
+    return fail(APG_E_INVALID, "draws made ahead are installed by a batch autoreset step with the ahead buffers");
   int rc;
-  if (c->kind == APG_IMAGE_LOCALIZE) {
+  // tuning knobs, read once: APG_IMAGE_UNFUSED (two launches per step), APG_GLIMPSE_GENERIC, APG_CLS_LANES8
+  static const bool unfused = getenv("APG_IMAGE_UNFUSED") != nullptr, generic = getenv("APG_GLIMPSE_GENERIC") != nullptr,
+                    lanes8 = getenv("APG_CLS_LANES8") != nullptr;
+  const GlimpseGeo g = env_geo(c);
+  const bool fusable = !unfused && !generic && !lanes8 && g.s0 <= GS_MAX_SIDE && g.s1 <= GS_MAX_SIDE &&
+                       (c->kind == APG_IMAGE_LOCALIZE || c->num_classes <= CLS1_MAX_K);
+  const bool fold = ahead && fusable;  // the fused step kernel installs the draws made ahead itself
+  if (c->kind == APG_IMAGE_LOCALIZE && prev_done && !fold) {
     // prediction_target = target.copy(); target[prev_done] = np_random.uniform(-1, 1, (k, 2)) as f32
-    if (prev_done) {
+    const double *draw = ahead ? st->ahead_f64 + 2 * (size_t)nt : st->scratch_f64;
+    if (!ahead) {
       const double low[2] = {-1.0, -1.0}, range[2] = {2.0, 2.0};
-      if ((rc = launch_uniform(st->rng + 0, c->num_envs_total, 2, low, range, st->scratch_f64, s, st->rng_work)))
-        return rc;
+      if ((rc = launch_uniform(st->rng + 0, nt, 2, low, range, st->scratch_f64, s, st->rng_work))) return rc;
     }
-    if (prev_done) {  // otherwise the copy is folded into k_image_env_loc
-      hipLaunchKernelGGL(k_loc_target, dim3(grid_for(n, 256)), dim3(256), 0, s, n, c->env_offset, prev_done,
-                         st->scratch_f64, st->target, out->target, c->out_row_bytes);
-      if ((rc = check_launch("k_loc_target"))) return rc;
-    }
+    // (steps without a refresh fold the copy into the env kernels)
+    hipLaunchKernelGGL(k_loc_target, dim3(grid_for(n, 256)), dim3(256), 0, s, n, c->env_offset, prev_done, draw,
+                       st->target, out->target, c->out_row_bytes);
+    if ((rc = check_launch("k_loc_target"))) return rc;
   }
-  if (prev_done && (rc = module_reset(c, st, out, s))) return rc;
-  EnvArgs a;
+  if (prev_done && !ahead && (rc = module_reset(c, st, out, s))) return rc;
+  if (prev_done && ahead && !fold) {  // the draws made ahead, installed as module_reset's gather would
+    hipLaunchKernelGGL(k_image_gather, dim3(grid_for(n, 256)), dim3(256), 0, s, n, c->env_offset, st->pool_labels,
+                       st->ahead_i64, c->invert_labels, st->ahead_i64 + nt, st->ahead_f64, c->num_classes,
+                       st->index, st->label, st->inverted, st->pos);
+    if ((rc = check_launch("k_image_gather"))) return rc;
+  }
+  EnvArgs a{};
   a.n = n;
   a.kind = c->kind;
   a.k = c->num_classes;
@@ -1749,12 +1813,19 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
   a.loss_weight = !c->sparse ? 1.0f : (!prev_done && t_new >= c->step_limit ? 1.0f : 0.0f);
   a.copy_target = c->kind == APG_IMAGE_LOCALIZE && !prev_done ? st->target : nullptr;
   a.row = c->out_row_bytes;
-  // tuning knobs, read once: APG_IMAGE_UNFUSED (two launches per step), APG_GLIMPSE_GENERIC, APG_CLS_LANES8
-  static const bool unfused = getenv("APG_IMAGE_UNFUSED") != nullptr, generic = getenv("APG_GLIMPSE_GENERIC") != nullptr,
-                    lanes8 = getenv("APG_CLS_LANES8") != nullptr;
-  const GlimpseGeo g = env_geo(c);
-  const bool fusable = !unfused && !generic && !lanes8 && g.s0 <= GS_MAX_SIDE && g.s1 <= GS_MAX_SIDE &&
-                       (c->kind == APG_IMAGE_LOCALIZE || c->num_classes <= CLS1_MAX_K);
+  if (fold) {
+    a.ahead_idx = st->ahead_i64;
+    a.ahead_inv = st->ahead_i64 + nt;
+    a.ahead_pos = st->ahead_f64;
+    a.ahead_tgt = st->ahead_f64 + 2 * (size_t)nt;
+    a.pool_labels = st->pool_labels;
+    a.invert = c->invert_labels;
+    a.offset = c->env_offset;
+    a.index_st = st->index;
+    a.label_st = st->label;
+    a.inverted_st = st->inverted;
+    a.target_st = st->target;
+  }
   if (fusable) {
     const int per = g.s0 * g.s1;
     // The env wave pays off for classification (its env step is the long serial tail: exp, log, pairwise
@@ -1819,6 +1890,35 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
   if ((rc = check_launch("k_image_env"))) return rc;
   // the target glimpse only changes with the target or the images, i.e. on the autoreset step
   return observe(c, st, out, s, prev_done != 0);
+}
+
+int apg_image_draw_ahead(const apg_image_config *c, const apg_image_state *st, apg_stream_t stream) {
+  if (int rc = validate(c)) return rc;
+  if (!st->ahead_i64 || !st->ahead_f64 || !st->rng_saved) return fail(APG_E_INVALID, "null ahead buffers");
+  hipStream_t s = (hipStream_t)stream;
+  const int nt = c->num_envs_total;
+  if (hipMemcpyAsync(st->rng_saved, st->rng, 3 * sizeof(apg_pcg64), hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return fail(APG_E_LAUNCH, "hipMemcpyAsync (streams before the draws made ahead)");
+  int rc;
+  // module_reset's draws in its order: next(DatasetBatchIterator), label inversions, start positions
+  if ((rc = launch_integers(st->rng + 2, nt, 0, (uint64_t)c->pool_len, st->ahead_i64, st->rng_work, s))) return rc;
+  if (c->invert_labels && (rc = launch_integers(st->rng + 1, nt, 0, 2, st->ahead_i64 + nt, st->rng_work, s))) return rc;
+  const double low[2] = {-1.0, -1.0}, range[2] = {2.0, 2.0};
+  if ((rc = launch_uniform(st->rng + 1, nt, 2, low, range, st->ahead_f64, s, st->rng_work))) return rc;
+  // ImageLocalizationVectorEnv's target refresh on the autoreset step: np_random.uniform(-1, 1, (N, 2))
+  if (c->kind == APG_IMAGE_LOCALIZE &&
+      (rc = launch_uniform(st->rng + 0, nt, 2, low, range, st->ahead_f64 + 2 * (size_t)nt, s, st->rng_work)))
+    return rc;
+  return APG_OK;
+}
+
+int apg_image_discard_ahead(const apg_image_config *c, const apg_image_state *st, apg_stream_t stream) {
+  if (int rc = validate(c)) return rc;
+  if (!st->rng_saved) return fail(APG_E_INVALID, "null rng_saved");
+  if (hipMemcpyAsync(st->rng, st->rng_saved, 3 * sizeof(apg_pcg64), hipMemcpyDeviceToDevice, (hipStream_t)stream) !=
+      hipSuccess)
+    return fail(APG_E_LAUNCH, "hipMemcpyAsync (restore the streams)");
+  return APG_OK;
 }
 
 int apg_image_glimpse(const apg_image_config *c, const void *pool, const int64_t *index, const void *pos,

@@ -9,7 +9,7 @@
 //   torch.ops.apgym.lidar_reset(LidarEnv env, int seed, bool use_seed) -> ()
 //   torch.ops.apgym.lidar_step(LidarEnv env, Tensor action, Tensor prediction) -> ()
 //   torch.ops.apgym.image_reset(ImageEnv env) -> ()
-//   torch.ops.apgym.image_step(ImageEnv env, Tensor action, Tensor prediction, int t, bool prev_done) -> ()
+//   torch.ops.apgym.image_step(ImageEnv env, Tensor action, Tensor prediction, int t, int prev_done) -> ()
 //
 // Replaces, like the C ABI below it (include/apgym_capi.h): SyncVectorEnv.reset/step over
 // TimeLimit(LIDARLocalization2DEnv) (ap_gym/envs/lidar_localization2d.py:293-389) and
@@ -157,15 +157,16 @@ void image_reset(const c10::intrusive_ptr<ImageEnv> &e) {
   check(apg_image_reset(&e->cfg, &e->st, &e->out, stream_of(e->dev)), "apg_image_reset");
 }
 
+// prev_done: bit 0 the previous step terminated the batch, bit 1 its draws were made ahead (apg_image_step)
 void image_step(const c10::intrusive_ptr<ImageEnv> &e, const at::Tensor &action, const at::Tensor &prediction,
-                int64_t t, bool prev_done) {
+                int64_t t, int64_t prev_done) {
   const c10::DeviceGuard guard(e->dev);
   const int64_t n = e->cfg.num_envs;
   check_io(action, e->dev, 2 * n, "action");
   const int64_t pw = e->cfg.kind == APG_IMAGE_CLASSIFY ? (int64_t)e->cfg.num_classes : 2;
   check_io(prediction, e->dev, pw * n, "prediction");
   check(apg_image_step(&e->cfg, &e->st, action.data_ptr<float>(), prediction.data_ptr<float>(), (int32_t)t,
-                       prev_done ? 1 : 0, &e->out, stream_of(e->dev)),
+                       (int32_t)prev_done, &e->out, stream_of(e->dev)),
         "apg_image_step");
 }
 
@@ -180,6 +181,6 @@ TORCH_LIBRARY(apgym, m) {
   m.def("lidar_step(__torch__.torch.classes.apgym.LidarEnv env, Tensor action, Tensor prediction) -> ()", lidar_step);
   m.def("image_reset(__torch__.torch.classes.apgym.ImageEnv env) -> ()", image_reset);
   m.def("image_step(__torch__.torch.classes.apgym.ImageEnv env, Tensor action, Tensor prediction, int t, "
-        "bool prev_done) -> ()",
+        "int prev_done) -> ()",
         image_step);
 }

@@ -319,6 +319,9 @@ typedef struct apg_image_state {
   int64_t *rng_work;          /* apg_rng_fill_work_elems(N, max(pool_len, top_k, 2)) int64 */
   float *stats_hist;          /* [N][2][step_limit] per-step metrics of the episode (log_stats):
                                  classify: correct_label_prob; localize: euclidean_distance, mse */
+  int64_t *ahead_i64;         /* [2][N_total] the next batch's index and inversion draws (apg_image_draw_ahead) or NULL */
+  double *ahead_f64;          /* [2][N_total][2] the next batch's start positions and (localize) refreshed targets */
+  apg_pcg64 *rng_saved;       /* [3] the streams before the draws made ahead (apg_image_discard_ahead) */
 } apg_image_state;
 
 typedef struct apg_image_outputs {
@@ -348,11 +351,21 @@ int apg_image_seed(const apg_image_config *cfg, const apg_image_state *st, uint6
 int apg_image_reset(const apg_image_config *cfg, const apg_image_state *st, const apg_image_outputs *out,
                     apg_stream_t stream);
 
-/* One vector step.  t = time step before the step, prev_done = the previous step terminated all
- * envs (the module then resets instead of moving; the host tracks both, they are batch-global). */
+/* One vector step.  t = time step before the step; prev_done bit 0 = the previous step terminated all envs (the
+ * module then resets instead of moving; the host tracks both, they are batch-global), bit 1 = that reset's draws
+ * were made ahead by apg_image_draw_ahead (the step then only installs them: one launch). */
 int apg_image_step(const apg_image_config *cfg, const apg_image_state *st, const float *action,
                    const float *prediction, int32_t t, int32_t prev_done, const apg_image_outputs *out,
                    apg_stream_t stream);
+
+/* The next batch autoreset's draws, made ahead (typically on a second stream right after a reset, while the episode
+ * steps; they depend only on the streams, not on actions): DatasetBatchIterator indices, label inversions, start
+ * positions (image_perception_module.py:120-139, dataset_iterator.py:52-57) and, localize, the refreshed targets
+ * (image_localization.py:151-158), into ahead_i64 / ahead_f64, advancing the streams as the autoreset step would;
+ * the streams before them are kept in rng_saved.  The stream of the step that consumes them must wait for them. */
+int apg_image_draw_ahead(const apg_image_config *cfg, const apg_image_state *st, apg_stream_t stream);
+/* Undo apg_image_draw_ahead (restores the streams from rng_saved): before a reset() that replaces the batch. */
+int apg_image_discard_ahead(const apg_image_config *cfg, const apg_image_state *st, apg_stream_t stream);
 
 /* Glimpses of npos positions per env: pos (f64 or f32, pos_is_f32) [N][npos][2] -> out
  * [N][npos][sensor_h][sensor_w][C]; index[N] selects the pool image of each env. */

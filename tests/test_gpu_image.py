@@ -542,3 +542,58 @@ def test_tuning_knobs_do_not_change_results(gpu, tmp_path, knobs):
     assert set(base.files) == set(got.files)
     for key in base.files:
         assert np.array_equal(base[key], got[key]), key
+
+
+@pytest.mark.parametrize("kind,invert,backend", [("cls", True, "torch"), ("loc", False, "torch"), ("cls", False, "numpy"),
+                                                 ("loc", False, "numpy")])
+def test_draw_ahead_matches_drawing_at_the_autoreset(gpu, kind, invert, backend):
+    """The next batch's draws made ahead on the side stream (apg_image_draw_ahead, installed by the fused step
+    kernel) give the outputs of drawing them in the autoreset step, across autoresets, a reset() (the streams are
+    restored from before the draws made ahead) and a reset(seed)."""
+    import torch
+
+    import ap_gym_amd as ap
+
+    ch = 3 if kind == "loc" else 1
+    ds = ap.SyntheticImageClassificationDataset(64, (32, 32, 3) if ch == 3 else (28, 28), 10, ch, seed=3)
+    cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=(8, 8) if kind == "loc" else (5, 5), step_limit=5,
+                                   randomly_invert_labels=invert)
+    cls = ap.ImageLocalizationVectorEnv if kind == "loc" else ap.ImageClassificationVectorEnv
+    n = 300
+    envs = [cls(n, cfg, array_backend=backend, draw_ahead=d) for d in (True, False)]
+    assert envs[0]._ahead_stream is not None and envs[1]._ahead_stream is None
+    rng = np.random.default_rng(6)
+
+    def same(x, y, what):
+        if isinstance(x, dict):
+            assert x.keys() == y.keys(), what
+            for k in x:
+                same(x[k], y[k], f"{what}/{k}")
+        elif isinstance(x, torch.Tensor):
+            assert torch.equal(x.cpu(), y.cpu()), what
+        else:
+            assert np.array_equal(np.asarray(x), np.asarray(y), equal_nan=True), what
+
+    def run(steps):
+        for t in range(steps):
+            a = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+            p = (rng.standard_normal((n, 10)) if kind == "cls" else rng.uniform(-1, 1, (n, 2))).astype(np.float32)
+            if backend == "torch":
+                a, p = torch.from_numpy(a).to(gpu), torch.from_numpy(p).to(gpu)
+            out = [e.step({"action": a, "prediction": p}) for e in envs]
+            for i, what in enumerate(("obs", "reward", "terminated", "truncated", "info")):
+                same(out[0][i], out[1][i], f"step {t} {what}")
+
+    for e in envs:
+        e.reset(seed=4)
+    run(14)  # two batch autoresets
+    outs = [e.reset() for e in envs]  # mid-episode reset(): the batch drawn from the restored streams
+    same(outs[0][0], outs[1][0], "reset obs")
+    same(outs[0][1], outs[1][1], "reset info")
+    run(8)
+    outs = [e.reset(seed=9) for e in envs]
+    same(outs[0][0], outs[1][0], "reset(seed) obs")
+    run(7)
+    for e in envs:
+        e.check_errors()
+        e.close()

@@ -51,7 +51,7 @@ for _ in range(2):
     loop("as_tensor+reshape+contig x2", lambda t: (
         torch.as_tensor(acts[t % 8], dtype=torch.float32, device=dev).reshape(n, 2).contiguous(),
         torch.as_tensor(preds[t % 8], dtype=torch.float32, device=dev).reshape(n, 10).contiguous()))
-    loop("raw op", lambda t: env._ops.image_step(env._h, acts[t % 8], preds[t % 8], 1, False))
+    loop("raw op", lambda t: env._ops.image_step(env._h, acts[t % 8], preds[t % 8], 1, 0))
     loop("_torch_step", lambda t: env._torch_step(False, False))
     loop("check_errors(block=False)", lambda t: env.check_errors(block=False))
 print("ok")
