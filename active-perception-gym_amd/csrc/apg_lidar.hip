@@ -309,10 +309,13 @@ enum : int { MZ_MAPS = 0, MZ_RESET = 1 };
 // apg_lidar_state.prefetch holds, per env, the result of its NEXT reset computed ahead (the reference's
 // DataLoader prefetch thread, lidar_localization2d.py:130-131, buffered_iterator.py:11-61): map index, occupancy
 // rows, start cell, and the env / iterator streams after those draws.  Ownership: gen[] (resets done) is written
-// only by the step / reset kernels on the env's stream; every other field only by the prefetch batch on the side
-// stream.  A record is valid for the env's current episode when pf_gen[e] == gen[e].  The batch selects the envs
-// whose record is stale (acquire of gen, release in the consuming step kernel: their streams are read after it),
-// the step kernel consumes a record only after its stream waited for the batch that wrote it.
+// only by the step / reset kernels on the env's stream; every other field by the prefetch batch on the side
+// stream (and by the synchronous reset kernels, which run ordered against the batches by events).  A record is
+// valid for the env's current episode when pf_gen[e] == gen[e].  Its streams are the env's current streams from
+// the moment its reset installs them (S.rng = rng), so a batch draws the next reset from the record alone and reads
+// nothing the concurrently running step kernel writes except gen, which that kernel stores after its reads of the
+// record (a coherent relaxed atomic: the batch overwrites a record only once it sees the reset that consumed it).
+// The step kernel consumes a record only after its stream waited for the batch that wrote it.
 struct PfLayout {
   size_t gen, pf_gen, sel_gen, start, list, ctl, idx, rng, it, occ, bytes;
 };
@@ -362,12 +365,13 @@ PfView pf_view(uint8_t *base, int n, int h, int wpr) {
   return v;
 }
 static_assert(sizeof(Pcg64) == sizeof(apg_pcg64), "prefetch records hold apg_pcg64 streams");
-APG_DEV uint32_t pf_load_gen(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
-APG_DEV void pf_store_gen(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT); }
+// relaxed, agent scope: coherent across the XCDs' L2s without the L2 write-back of a release fence
+APG_DEV uint32_t pf_load_gen(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+APG_DEV void pf_store_gen(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
-// Batch kernel 1: the envs whose record is stale (pf_gen != gen), their streams copied into the records (the
-// only read of the env state by the batch), appended to the list.  ctl[0] was zeroed before the launch.
-__global__ __launch_bounds__(256) void k_pf_select(int n, apg_lidar_state S, PfView V) {
+// Batch kernel 1: the envs whose record is stale (pf_gen != gen), appended to the list.  ctl[0] was zeroed before
+// the launch.
+__global__ __launch_bounds__(256) void k_pf_select(int n, PfView V) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   bool sel = false;
   uint32_t g = 0;
@@ -382,8 +386,6 @@ __global__ __launch_bounds__(256) void k_pf_select(int n, apg_lidar_state S, PfV
   if (lane == __ffsll((long long)m) - 1) base = atomicAdd(&V.ctl[0], (unsigned long long)__popcll(m));
   base = __shfl(base, __ffsll((long long)m) - 1);
   if (sel) {
-    V.rng[e] = *reinterpret_cast<const Pcg64 *>(&S.rng[e]);
-    V.it[e] = *reinterpret_cast<const Pcg64 *>(&S.it_rng[e]);
     V.sel_gen[e] = g;
     V.list[base + __popcll(m & ((1ULL << lane) - 1ULL))] = (uint32_t)e;
   }
@@ -490,7 +492,7 @@ __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_stat
                                                            uint64_t *occ, const uint8_t *scratch, int mode,
                                                            uint64_t seed, int use_seed, int all, int ng,
                                                            uint64_t *out_map_idx, float *map_obs, uint32_t *err,
-                                                           uint32_t *pf_gen_main) {
+                                                           PfView pv) {
   __shared__ uint16_t s_list[MP_ENVS];
   __shared__ int s_cnt, s_wsum[MP_THREADS / 64], s_hit[2];
   extern __shared__ uint64_t s_bm[];  // one maze's rows
@@ -569,7 +571,11 @@ __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_stat
       *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
       S.map_idx[e] = midx;
       if (out_map_idx) oat(out_map_idx, g.row, e, 1) = midx;
-      if (pf_gen_main) pf_store_gen(&pf_gen_main[e], pf_gen_main[e] + 1u);  // a prefetched next map is stale now
+      if (pv.gen) {  // the record's streams follow the env's; a prefetched next map is stale now
+        pv.rng[e] = rng;
+        pv.it[e] = it;
+        pf_store_gen(&pv.gen[e], pv.gen[e] + 1u);
+      }
     }
     __syncthreads();  // s_hit / the bitmap are reused by the next maze
   }
@@ -941,11 +947,12 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       // the step's reset count to the prefetcher (pinned host word): every workgroup adds its count, the last one
       // to finish this point (ticket) publishes the total and rearms the counters for the next step
       npend = __syncthreads_count(pend);
-      if (tid == 0) {
+      if (tid == 0) {  // (coherent relaxed atomics, ordered by a vmcnt wait instead of a release fence's L2 flush)
         if (npend) __hip_atomic_fetch_add(&V.ctl[1], (unsigned long long)npend, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long t = __hip_atomic_fetch_add(&V.ctl[2], 1ULL, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the count is added before the ticket is taken
+        const unsigned long long t = __hip_atomic_fetch_add(&V.ctl[2], 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (t == gridDim.x - 1) {
-          const unsigned long long tot = __hip_atomic_load(&V.ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          const unsigned long long tot = __hip_atomic_load(&V.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (V.host_slot) __hip_atomic_store(V.host_slot, (uint32_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           __hip_atomic_store(&V.ctl[1], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(&V.ctl[2], 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1729,7 +1736,7 @@ int maze_ng(const Geo &g) {
 
 int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, int n, uint64_t *occ, uint8_t *scratch,
                 int mode, uint64_t seed, int use_seed, int all, uint64_t *out_map_idx, float *map_obs, uint32_t *err,
-                hipStream_t s, uint32_t *pf_gen_main = nullptr) {
+                hipStream_t s, const PfView *pv = nullptr) {
   if (!scratch) return fail(APG_E_INVALID, "maze maps need the maze scratch buffer (stack)");
   const MazeGeom m = maze_geom(g.h, g.w);
   if (m.ncx > 127 || m.ncy > 127) return fail(APG_E_INVALID, "maze maps must be at most 255 x 255");
@@ -1752,7 +1759,7 @@ int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, in
   if (int rc = check_launch("k_maze")) return rc;
   hipLaunchKernelGGL(k_maze_paint, dim3(grid_for(n, MP_ENVS)), dim3(MP_THREADS), (size_t)g.h * g.wpr * sizeof(uint64_t),
                      s, g, st, idx, n, occ, scratch, mode, seed, use_seed, all, ng, out_map_idx, map_obs, err,
-                     pf_gen_main);
+                     pv ? *pv : PfView{});
   return check_launch("k_maze_paint");
 }
 
@@ -1939,7 +1946,7 @@ int pf_batch_kernels(const apg_lidar_config *cfg, const apg_lidar_state *st, con
   if (int rc = opt_in_lds(kern, dyn)) return rc;
   if (hipMemsetAsync(&V.ctl[0], 0, sizeof(unsigned long long), side) != hipSuccess)
     return fail(APG_E_LAUNCH, "hipMemsetAsync (prefetch count)");
-  hipLaunchKernelGGL(k_pf_select, dim3(grid_for(n, 256)), dim3(256), 0, side, n, *st, V);
+  hipLaunchKernelGGL(k_pf_select, dim3(grid_for(n, 256)), dim3(256), 0, side, n, V);
   if (int rc = check_launch("k_pf_select")) return rc;
   hipLaunchKernelGGL(k_pf_stream, dim3(grid_for(n, MZS_MAZES)), dim3(MZS_THREADS), 0, side, g, V, scratch, ng);
   if (int rc = check_launch("k_pf_stream")) return rc;
@@ -2119,9 +2126,10 @@ int apg_lidar_reset(const apg_lidar_config *cfg, const apg_lidar_state *st, uint
   if (p && !p->batches.empty() && hipStreamWaitEvent(s, p->batches.back().ev, 0) != hipSuccess)
     return fail(APG_E_LAUNCH, "hipStreamWaitEvent (prefetch)");  // the batches use the maze scratch too
   if (g.kind == APG_MAP_MAZE && !g.is_static) {
-    uint32_t *gen = st->prefetch && pf_supported(cfg) ? pf_view(st->prefetch, g.n, g.h, g.wpr).gen : nullptr;
+    const bool pf = st->prefetch && pf_supported(cfg);
+    const PfView pv = pf ? pf_view(st->prefetch, g.n, g.h, g.wpr) : PfView{};
     rc = launch_maze(g, *st, nullptr, g.n, nullptr, reinterpret_cast<uint8_t *>(st->stack), MZ_RESET, seed, use_seed,
-                     1, out->map_idx, out->map_obs, out->err, s, gen);
+                     1, out->map_idx, out->map_obs, out->err, s, pf ? &pv : nullptr);
   } else {
     rc = launch_reset(g, st, seed, use_seed, 1, out, s);
   }
@@ -2179,9 +2187,10 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
     if (rc == APG_OK) rc = launch_step_kernel(cfg, st, action, prediction, out, s, false);
   } else if (cfg->map_kind == APG_MAP_MAZE && !cfg->is_static) {
     const Geo g = make_geo(cfg);
-    uint32_t *gen = st->prefetch && pf_supported(cfg) ? pf_view(st->prefetch, g.n, g.h, g.wpr).gen : nullptr;
+    const bool pf = st->prefetch && pf_supported(cfg);
+    const PfView pv = pf ? pf_view(st->prefetch, g.n, g.h, g.wpr) : PfView{};
     rc = launch_maze(g, *st, nullptr, g.n, nullptr, reinterpret_cast<uint8_t *>(st->stack), MZ_RESET, 0, 0, 0,
-                     out->map_idx, out->map_obs, out->err, s, gen);
+                     out->map_idx, out->map_obs, out->err, s, pf ? &pv : nullptr);
     apg_lidar_outputs o2 = *out;
     o2.map_obs = nullptr;  // written by k_maze
     if (rc == APG_OK) rc = launch_step_kernel(cfg, st, action, prediction, &o2, s, false);

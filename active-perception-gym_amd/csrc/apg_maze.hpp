@@ -415,15 +415,16 @@ APG_DEV int maze_dfs(const Pcg64 &r0, const uint8_t *stream, int ng, bool active
       arow += dy * RB;
       const int slot = carve ? sp : sp - 1;
       char *rb = ring + ((slot >> 2) & (MZ_RING / 4 - 1)) * (4 * MZ_LANES) + (slot & 3);
-      if (carve) {
-        *rb = (char)(pidx | (from << 5));
-        __hip_atomic_fetch_or(reinterpret_cast<uint64_t *>(vis + arow + (cx >> 6) * 8 * MZ_LANES), 1ULL << (cx & 63),
-                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        *reinterpret_cast<uint16_t *>(logb + (lg >> 1) * (4 * MZ_LANES) + (lg & 1) * 2) =
-            (uint16_t)((uint32_t)cx | ((uint32_t)cy << 7) | (d << 14));
-      }
-      uint32_t fb = 0u;
-      if (back) fb = (uint8_t)*rb;
+      // The carve's three LDS writes are issued unconditionally (no lane-divergent branch): without a carve the
+      // frame byte lands in the free slot above the top (sp - 1 is read instead: slot sp), the visited word is
+      // OR-ed with 0 and the log entry lands in the free entry lg, which the next carve overwrites
+      char *wb = ring + ((sp >> 2) & (MZ_RING / 4 - 1)) * (4 * MZ_LANES) + (sp & 3);
+      const uint32_t fb = (uint8_t)*rb;  // the parent frame (used on a return)
+      *wb = (char)(pidx | (from << 5));
+      __hip_atomic_fetch_or(reinterpret_cast<uint64_t *>(vis + arow + (cx >> 6) * 8 * MZ_LANES),
+                            carve ? 1ULL << (cx & 63) : 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      *reinterpret_cast<uint16_t *>(logb + (lg >> 1) * (4 * MZ_LANES) + (lg & 1) * 2) =
+          (uint16_t)((uint32_t)cx | ((uint32_t)cy << 7) | (d << 14));
       lg += carve ? 1 : 0;
       sp += carve ? 1 : (back ? -1 : 0);
       const uint32_t child = from;

@@ -44,7 +44,7 @@ stream = N.stream_handle(dev)
 cfg_p, st_p, out_p = ctypes.byref(env._cfg), ctypes.byref(env._state), ctypes.byref(env._out)
 a_ptr, p_ptr = [N.ptr(acts[t]) for t in range(8)], [N.ptr(preds[t]) for t in range(8)]
 for _ in range(2):
-    loop("raw op .default", lambda t: env._step_op(env._h, acts[t % 8], preds[t % 8], 1, False))
+    loop("raw op .default", lambda t: env._step_op(env._h, acts[t % 8], preds[t % 8], 1, 0))
     loop("C ABI via ctypes", lambda t: L.apg_image_step(cfg_p, st_p, a_ptr[t % 8], p_ptr[t % 8], 1, 0, out_p, stream))
 for _ in range(2):
     loop("env.step", lambda t: env.step({"action": acts[t % 8], "prediction": preds[t % 8]}))
