@@ -113,8 +113,9 @@ def cpu_baseline(beams: int, size: int, kind: str, num_envs: int | None, steps: 
 # image workloads (BASELINE.json configs 4, 5): per-GPU envs, pool, classes, sensor, kind
 IMAGE_WORKLOADS = {
     "mnist": dict(name="MNIST-v0 ImageClassificationVectorEnv", kind="cls", envs=65536, shape=(28, 28),
-                  pool=60000, classes=10, sensor=(5, 5)),
-    "tinyimagenet-loc": dict(name="TinyImageNetLoc-v0 ImageLocalizationVectorEnv", kind="loc", envs=32768,
+                  pool=60000, classes=10, sensor=(5, 5)),  # BASELINE config 4: 65536 envs on one GPU (weak)
+    # BASELINE config 5: 32768 envs in total, sharded over the GPUs (strong, like the maze config)
+    "tinyimagenet-loc": dict(name="TinyImageNetLoc-v0 ImageLocalizationVectorEnv", kind="loc", envs_total=32768,
                              shape=(64, 64, 3), pool=100000, classes=200, sensor=(12, 12)),
 }
 
@@ -155,8 +156,9 @@ def run_image(args, world, rank, dev):
     import ap_gym_amd as apg
 
     w = IMAGE_WORKLOADS[args.workload]
-    n_local = args.num_envs or w["envs"]
-    n_total = n_local * world
+    plan = shard_plan(args, world)
+    n_local, n_total = plan["num_envs_per_gpu"], plan["num_envs_total"]
+    log_stats = not args.no_log_stats
     c = 1 if len(w["shape"]) == 2 else w["shape"][-1]
     pool_len = args.pool_len or w["pool"]
     ds = apg.SyntheticImageClassificationDataset(pool_len, w["shape"], w["classes"], c, seed=0)
@@ -165,7 +167,8 @@ def run_image(args, world, rank, dev):
     from ap_gym_amd.sharding import ShardedVectorEnv
 
     senv = ShardedVectorEnv(lambda num_envs, env_offset: cls(num_envs, cfg, device=dev, array_backend="torch",
-                                                             num_envs_total=n_total, env_offset=env_offset),
+                                                             num_envs_total=n_total, env_offset=env_offset,
+                                                             log_stats=log_stats),
                             n_total, rank, world, gather=args.gather, time_gather=True)
     env = senv.env
     ring = 17
@@ -215,7 +218,7 @@ def run_image(args, world, rank, dev):
         elapsed, step_ms, reset_ms, gather_ms = (float(x) for x in tt)
     if rank == 0:
         bpe = image_bytes_per_env_step(w["kind"], w["classes"], w["sensor"], c)
-        shape = {"num_envs": n_local, "sensor": list(w["sensor"]), "classes": w["classes"]}
+        shape = {"num_envs": n_local, "sensor": list(w["sensor"]), "classes": w["classes"], "log_stats": log_stats}
         # the step kernel's time: the rocprof duration table of these sources at this shape when there is one
         # (the events around a launch the GPU is not backed up behind include the host's launch latency, and
         # then exceed the wall time per step), else the events
@@ -237,11 +240,12 @@ def run_image(args, world, rank, dev):
             "metric": "env-steps/sec (vectorized step) at 1/2/4/8 MI355X + achieved HBM GB/s",
             "value": n_total * args.steps / elapsed, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64 bilinear / f32 outputs",
+            "scaling": plan["scaling"], "vs_baseline": None, "dtype": "f64 bilinear / f32 outputs",
             "data": f"synthetic uint8 pool {pool_len}x{'x'.join(map(str, w['shape']))} (default_rng(0)); "
                     "uniform actions, normal logits / uniform predictions generated on device",
             "config": {"workload": w["name"], "num_envs_per_gpu": n_local, "num_envs_total": n_total,
                        "sensor": list(w["sensor"]), "classes": w["classes"], "step_limit": 16,
+                       "log_stats": log_stats,
                        "reset_ms": reset_ms, "parallelism": f"env-shard x{world}" + (" + all-gather" if senv.gather
                                                                                         else ""),
                        "gather_ms": gather_ms if senv.gather else None},
@@ -586,22 +590,75 @@ def self_launch(n: int) -> None:
         raise SystemExit(bad[0])
 
 
+def shard_plan(args, world: int) -> dict:
+    """The per-rank work of a workload at `world` ranks, as run_lidar / run_image size it: envs per rank, total
+    envs, the scaling mode, and with --gather the packed output row every rank all-gathers per step (the row
+    layouts the step kernels write: lidar_env.lidar_output_row_layout / image_env.image_output_row_layout)."""
+    from ap_gym_amd import _native as N
+
+    if args.workload in IMAGE_WORKLOADS:
+        from ap_gym_amd.image_env import image_output_row_layout
+
+        w = IMAGE_WORKLOADS[args.workload]
+        c = 1 if len(w["shape"]) == 2 else w["shape"][-1]
+        kind = N.APG_IMAGE_CLASSIFY if w["kind"] == "cls" else N.APG_IMAGE_LOCALIZE
+        row = image_output_row_layout(kind, w["sensor"], c, not args.no_log_stats)[1]
+        name = w["name"]
+    else:
+        from ap_gym_amd.lidar_env import lidar_output_row_layout
+
+        w = LIDAR_WORKLOADS[args.workload]
+        row = lidar_output_row_layout(args.beams or w["beams"], True)[1]  # make_vec logs stats
+        name = w["env_id"]
+    if args.num_envs:
+        n_local = args.num_envs
+    elif "envs_total" in w:
+        if w["envs_total"] % world:
+            raise SystemExit(f"{args.workload}: {w['envs_total']} envs do not split over {world} ranks")
+        n_local = w["envs_total"] // world
+    else:
+        n_local = w["envs"]
+    return {"workload": name, "num_envs_per_gpu": n_local, "num_envs_total": n_local * world,
+            "scaling": "strong" if "envs_total" in w else "weak", "row_bytes": row if args.gather else None,
+            "gather_bytes_per_rank_step": row * n_local * (world - 1) if args.gather else 0,
+            "parallelism": f"env-shard x{world}" + (" + all-gather" if args.gather else "")}
+
+
 def run_dry(args, world, rank):
-    """--dry-run: the multi-rank plumbing of the bench (rendezvous, barrier-bracketed timing, max over
-    ranks, one JSON line from rank 0) over gloo on CPU, without envs."""
+    """--dry-run: the multi-rank plumbing of the bench over gloo on CPU, without envs or a GPU: rendezvous, the
+    workload's shard plan (envs per rank, seed offsets, packed row size), barrier-bracketed timing of `steps`
+    rounds, max over ranks, one JSON line from rank 0.  With --gather every round all-gathers the full-size
+    [envs per rank, row] byte buffers the step kernels would write and checks every rank's block arrived."""
     import torch
     import torch.distributed as dist
 
+    plan = shard_plan(args, world)
+    n_local = plan["num_envs_per_gpu"]
     if world > 1:
         dist.init_process_group("gloo")
         dist.barrier()
+    send = parts = None
+    if args.gather:
+        send = torch.empty((n_local, plan["row_bytes"]), dtype=torch.uint8)
+        send[:, 0] = rank
+        send[:, 8:16].view(torch.int64)[:, 0] = torch.arange(rank * n_local, (rank + 1) * n_local)  # env index
+        parts = [torch.empty_like(send) for _ in range(world)]
     t0 = time.perf_counter()
-    x = torch.ones(1024)
     for _ in range(args.steps):
-        x = x * 1.0
+        if args.gather:
+            if world > 1:
+                dist.all_gather(parts, send)
+            else:
+                parts[0].copy_(send)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if args.gather:
+        got = torch.cat(parts)
+        ok = bool((got[:, 0] == torch.arange(world).repeat_interleave(n_local)).all()) and bool(
+            (got[:, 8:16].contiguous().view(torch.int64)[:, 0] == torch.arange(world * n_local)).all())
+        if not ok:
+            raise SystemExit(f"rank {rank}: gathered rows out of order")
     tt = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -609,8 +666,8 @@ def run_dry(args, world, rank):
         print(json.dumps({"metric": "dry-run", "value": args.steps / float(tt[0]), "unit": "steps/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": float(tt[0]) * 1e3 / args.steps, "higher_is_better": True,
-                          "scaling": "weak", "vs_baseline": None, "dtype": "none", "data": "none",
-                          "config": {"workload": "dry-run", "ranks": world}}), flush=True)
+                          "scaling": plan["scaling"], "vs_baseline": None, "dtype": "none",
+                          "data": "none (gloo on CPU)", "config": dict(plan, ranks=world)}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -642,6 +699,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend of multi-rank runs (nccl = RCCL; gloo for rehearsals with "
                          "several ranks on one GPU)")
+    ap.add_argument("--no-log-stats", action="store_true",
+                    help="image workloads: the bare env class without the episode statistics make_vec's log "
+                         "wrapper adds (the default measures the drop-in make_vec configuration, log_stats=True)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: ranks rendezvous over gloo, time a barrier, rank 0 prints "
                          "the JSON line")

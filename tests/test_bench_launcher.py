@@ -30,6 +30,40 @@ def _run(args, timeout):
 def test_self_launch_dry_run_two_ranks():
     out = _run(["--gpus", "2", "--dry-run", "--steps", "5", "--warmup", "1"], 120)
     assert out["n_gpus"] == 2 and out["config"]["ranks"] == 2 and out["steps"] == 5
+    assert out["config"]["num_envs_per_gpu"] == 65536 and out["scaling"] == "weak"  # config 2: per-GPU envs
+
+
+def test_dry_run_eight_ranks_tinyimagenet_gather():
+    """BASELINE config 5 at 8 ranks: 32768 envs split 8 ways, each rank all-gathers the full-size packed rows
+    (reward, glimpse + target glimpse, glimpse_pos, time_step, base_reward, target, loss, stats) of the others."""
+    from ap_gym_amd import _native as N
+    from ap_gym_amd.image_env import image_output_row_layout
+
+    out = _run(["--gpus", "8", "--dry-run", "--workload", "tinyimagenet-loc", "--gather", "--steps", "2",
+                "--warmup", "0"], 300)
+    cfg = out["config"]
+    row = image_output_row_layout(N.APG_IMAGE_LOCALIZE, (12, 12), 3, True)[1]
+    assert out["n_gpus"] == 8 and cfg["ranks"] == 8 and out["scaling"] == "strong"
+    assert cfg["num_envs_per_gpu"] == 4096 and cfg["num_envs_total"] == 32768
+    assert cfg["row_bytes"] == row and cfg["gather_bytes_per_rank_step"] == 7 * 4096 * row
+    assert cfg["parallelism"] == "env-shard x8 + all-gather"
+
+
+def test_dry_run_eight_ranks_maze127():
+    """BASELINE config 3 at 8 ranks: 262144 envs split 8 ways, no data-path collective."""
+    out = _run(["--gpus", "8", "--dry-run", "--workload", "maze127", "--steps", "2", "--warmup", "0"], 300)
+    cfg = out["config"]
+    assert out["n_gpus"] == 8 and out["scaling"] == "strong"
+    assert cfg["workload"] == "LIDARLocMaze-v0" and cfg["num_envs_per_gpu"] == 32768
+    assert cfg["num_envs_total"] == 262144 and cfg["gather_bytes_per_rank_step"] == 0
+    assert cfg["parallelism"] == "env-shard x8"
+
+
+def test_dry_run_rejects_an_uneven_split():
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--workload", "maze127",
+                        "--gpus", "1"], capture_output=True, text=True, timeout=120, cwd=ROOT,
+                       env=dict(os.environ, WORLD_SIZE="3", RANK="0"))
+    assert p.returncode != 0 and "do not split over 3 ranks" in p.stderr
 
 
 @pytest.mark.gpu

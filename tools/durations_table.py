@@ -54,7 +54,8 @@ def main():
         shape = {"num_envs": cfg["num_envs_per_gpu"], "beams": cfg["beams"], "map": int(cfg["map"].split("x")[0])}
     else:
         family = "image"
-        shape = {"num_envs": cfg["num_envs_per_gpu"], "sensor": cfg["sensor"], "classes": cfg["classes"]}
+        shape = {"num_envs": cfg["num_envs_per_gpu"], "sensor": cfg["sensor"], "classes": cfg["classes"],
+                 "log_stats": cfg.get("log_stats", False)}
     print(json.dumps({"workload": wl, "kernel_family": family, "source_sha": bench.kernel_source_sha(family),
                       "shape": shape, "per_class": per, "bench_cmd_shape": {"steps": b["steps"], "warmup": b["warmup"]},
                       "note": "rocprofv3 --kernel-trace dispatch durations (end - start) per class"}, indent=1,

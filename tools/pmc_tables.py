@@ -102,7 +102,8 @@ def main():
         hbm_b = {cls: hbm(p) for cls, p in per.items()}
     else:
         family = "image"
-        shape = {"num_envs": cfg["num_envs_per_gpu"], "sensor": cfg["sensor"], "classes": cfg["classes"]}
+        shape = {"num_envs": cfg["num_envs_per_gpu"], "sensor": cfg["sensor"], "classes": cfg["classes"],
+                 "log_stats": cfg.get("log_stats", False)}
         steps = b["steps"]
         fused = [cls for cls in counts if cls.startswith("k_image_step_fused")]
         # an ordinary step is one k_image_step_fused launch; otherwise the kernels launched on every step
