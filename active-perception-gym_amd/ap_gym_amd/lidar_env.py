@@ -729,7 +729,9 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         if not self.copy:
             return m
         if changed or self._map_snapshot is None:
-            self._map_snapshot = m.copy()
+            # torch's CPU copy runs on the intra-op thread pool (numpy's m.copy() is one thread: 3-4x slower at
+            # the 1 GB of a cfg-2 episode end)
+            self._map_snapshot = self._map_host.clone().numpy()
             self._map_snapshot.flags.writeable = False
         return self._map_snapshot
 

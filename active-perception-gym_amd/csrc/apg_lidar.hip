@@ -467,7 +467,7 @@ __global__ __launch_bounds__(64) void k_maze(Geo g, apg_lidar_state S, const uin
   const bool active = mine && (mode != MZ_RESET || all || (S.flags[i] & F_AUTORESET));
   if (__ballot(active) == 0ULL) return;
   char *lds = reinterpret_cast<char *>(s_mz);
-  maze_table_init(lds, lane);
+  maze_table_init<ONEW>(lds, lane);
   __syncthreads();
   Pcg64 mr{};
   if (active) {  // get_data_point: default_rng(idx) (its increment; the stream: k_maze_stream)
@@ -642,7 +642,7 @@ __global__ __launch_bounds__(64) void k_pf_dfs(Geo g, PfView V, uint8_t *scratch
   const MazeGeom m = maze_geom(g.h, g.w);
   const size_t sb = maze_scratch_bytes(g.h, g.w), lb = maze_log_bytes(g.h, g.w);
   char *lds = reinterpret_cast<char *>(s_mz);
-  maze_table_init(lds, lane);
+  maze_table_init<ONEW>(lds, lane);
   __syncthreads();
   Pcg64 mr{};
   if (active) mr = seed_pcg64(V.idx[e]);

@@ -37,7 +37,7 @@ constexpr int MZ_RING = 64;    // frames held in LDS (a multiple of MZ_CHUNK)
 constexpr int MZ_CHUNK = 32;   // frames per spill / reload
 constexpr int MZ_PERIOD = 16;  // DFS iterations between memory phases (ring headroom below)
 constexpr int MZ_LOGBUF = 24;  // log entries buffered in LDS per lane (< 8 left over + MZ_PERIOD new)
-constexpr uint32_t MZ_LOG_PAD = 0xFFFFu;  // padding entry (x = 127 is never a cell: ncx <= 127)
+constexpr uint32_t MZ_LOG_PAD = 0xFFFFu;  // padding entry (x = 127, resp. 63 in the ncx <= 63 format: never a cell)
 static_assert(MZ_RING - MZ_PERIOD - MZ_CHUNK >= 0, "ring headroom");
 static_assert(MZ_LOGBUF >= 7 + MZ_PERIOD && MZ_LOGBUF % 8 == 0, "log buffer: leftover group + one period");
 
@@ -263,35 +263,71 @@ __host__ __device__ inline size_t maze_scratch_bytes(int h, int w) {
 }
 
 // LDS of one k_maze workgroup (always laid out for 64 lanes, so every stride is a compile-time immediate):
-//   [0, 512)        the permutation table: per index 16 B = the map "eligible directions (4 bits, by
-//                   direction) -> eligible positions (4 bits, by permutation position)" as 16 nibbles, then
-//                   the permutation (2 bits per position) | its inverse << 8
-//   MZ_V            visited rows, u64 [ncy][cw][64 lanes], with the bits of columns >= ncx set (the
-//                   column bounds cost nothing; the row bounds are two compares)
+//   [0, 512)        the permutation table (maze_table_init)
+//   MZ_V            visited rows, u64 [rows][cw][64 lanes], with the bits of columns >= ncx set (the column
+//                   bounds cost nothing).  Mazes of ncx <= 63 (one word per row, maze_dfs_rows) also have an
+//                   all-visited pad row below row 0 and above row ncy - 1, so the row bounds cost nothing
+//                   either; wider mazes (maze_dfs_words) bound rows with two compares
 //   ring, log       u32 [MZ_RING / 4][64], u32 [MZ_LOGBUF / 2][64]
+// 127 x 127 (ncy = 63): 512 + 65 * 512 + 4096 + 3072 = 40960 B, four one-wave workgroups per CU.
 constexpr int MZ_LANES = 64, MZ_V = 512;
+__host__ __device__ inline bool maze_onew(const MazeGeom &m) { return m.ncx <= 63; }
 __host__ __device__ inline int maze_row_bytes(const MazeGeom &m) { return m.cw * 8 * MZ_LANES; }
-__host__ __device__ inline int maze_ring_off(const MazeGeom &m) { return MZ_V + m.ncy * maze_row_bytes(m); }
+__host__ __device__ inline int maze_vis_off(const MazeGeom &m) {  // row 0
+  return MZ_V + (maze_onew(m) ? maze_row_bytes(m) : 0);
+}
+__host__ __device__ inline int maze_ring_off(const MazeGeom &m) {
+  return MZ_V + (m.ncy + (maze_onew(m) ? 2 : 0)) * maze_row_bytes(m);
+}
 __host__ __device__ inline int maze_log_off(const MazeGeom &m) { return maze_ring_off(m) + MZ_RING * MZ_LANES; }
 __host__ __device__ inline size_t maze_wg_lds_bytes(int h, int w) {
   const MazeGeom m = maze_geom(h, w);
   return (size_t)maze_log_off(m) + MZ_LOGBUF * 2 * MZ_LANES;
 }
 
-// the permutation table (thread t < 24 writes entry t; the caller synchronizes)
+// The permutation table (thread t < 32 writes entry t; the caller synchronizes).
+// ONEW (maze_dfs_rows): entry c = j3 | j2 << 2 | j1 << 4 (the shuffle's three draws; j2 = 3 never occurs) holds
+//   x, y  for each visited mask V (bit 0: column - 1, bit 1: row + 1, bit 2: column + 1, bit 3: row - 1) the
+//         unvisited permutation positions, 4 bits at bits 4V..
+//   z     the permutation (direction of position k at bits 2k)
+//   w     for each direction r the positions after r's, (0xF << (position of r + 1)) & 0xF at bits 4r (where a
+//         frame resumes when its child r returns)
+// otherwise (maze_dfs_words): entry pidx = j3 * 6 + j2 * 2 + j1 holds the map "eligible directions (by
+//   direction) -> eligible positions" as 16 nibbles, then the permutation | its inverse << 8.
+template <bool ONEW>
 APG_DEV void maze_table_init(char *lds, int t) {
-  if (t >= 24) return;
-  const uint32_t perm = mz_perm_of((uint32_t)t);
-  uint32_t inv = 0;
-  uint64_t pm = 0;
-  for (int j = 0; j < 4; j++) inv |= (uint32_t)j << (2 * ((perm >> (2 * j)) & 3u));
-  for (uint32_t E = 0; E < 16; E++) {
-    uint32_t v = 0;
-    for (int j = 0; j < 4; j++) v |= ((E >> ((perm >> (2 * j)) & 3u)) & 1u) << j;
-    pm |= (uint64_t)v << (4 * E);
-  }
   uint4 *e = reinterpret_cast<uint4 *>(lds) + t;
-  *e = make_uint4((uint32_t)pm, (uint32_t)(pm >> 32), perm | (inv << 8), 0u);
+  if constexpr (ONEW) {
+    if (t >= 32) return;
+    const uint32_t j3 = t & 3, j2 = (t >> 2) & 3, j1 = t >> 4;
+    if (j2 == 3) {
+      *e = make_uint4(0u, 0u, 0u, 0u);
+      return;
+    }
+    const uint32_t perm = mz_perm_of(j3 * 6 + j2 * 2 + j1);
+    constexpr uint32_t vbit[4] = {2, 0, 1, 3};  // direction (+x, -x, +y, -y) -> bit of the visited mask
+    uint64_t pm = 0;
+    for (uint32_t V = 0; V < 16; V++) {
+      uint32_t v = 0;
+      for (int j = 0; j < 4; j++) v |= (((V >> vbit[(perm >> (2 * j)) & 3u]) & 1u) ^ 1u) << j;
+      pm |= (uint64_t)v << (4 * V);
+    }
+    uint32_t after = 0;
+    for (int j = 0; j < 4; j++) after |= ((0xFu << (j + 1)) & 0xFu) << (4 * ((perm >> (2 * j)) & 3u));
+    *e = make_uint4((uint32_t)pm, (uint32_t)(pm >> 32), perm, after);
+  } else {
+    if (t >= 24) return;
+    const uint32_t perm = mz_perm_of((uint32_t)t);
+    uint32_t inv = 0;
+    uint64_t pm = 0;
+    for (int j = 0; j < 4; j++) inv |= (uint32_t)j << (2 * ((perm >> (2 * j)) & 3u));
+    for (uint32_t E = 0; E < 16; E++) {
+      uint32_t v = 0;
+      for (int j = 0; j < 4; j++) v |= ((E >> ((perm >> (2 * j)) & 3u)) & 1u) << j;
+      pm |= (uint64_t)v << (4 * E);
+    }
+    *e = make_uint4((uint32_t)pm, (uint32_t)(pm >> 32), perm | (inv << 8), 0u);
+  }
 }
 
 // L1-bypassing load (agent scope): a reloaded chunk may have been read before, then re-spilled
@@ -299,23 +335,272 @@ APG_DEV uint64_t mz_load_coherent(const uint64_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The DFS of one maze per lane.  Every lane of the wave must call it (wave-uniform memory phases); lanes
-// with active == false only take part in them.  `lds` is the workgroup's dynamic LDS (table initialized),
-// `spill` / `logg` / `stream` this maze's global scratch (16-byte aligned; the stream of ng groups written by
-// k_maze_stream), r0 the maze's seeded generator (its increment steps the LCG past the stream).  ONEW: ncx
-// <= 63 (one vis word per row, the left neighbour of column 0 reads the pad bit 63).  Returns the log length
-// in entries (a multiple of 8, the tail padded); `bad` is set when a draw does not fit in a full window
-// (30 rejected halves in one permutation: never in practice) and that maze is abandoned.
-template <bool ONEW>
-APG_DEV int maze_dfs(const Pcg64 &r0, const uint8_t *stream, int ng, bool active, const MazeGeom &m, double bp,
-                     char *lds, int lane, uint8_t *spill, uint32_t *logg, bool &bad) {
+// The DFS's frame stack and carve log outside the iterations: frames sp - 1 .. lo in the LDS ring (older ones
+// spilled, the chunk below the ring in pd when pend), lg entries in the LDS log buffer, logpos flushed.
+struct MzStack {
+  int sp, lo, lg, logpos;
+  bool pend;
+  uint32_t pd[MZ_CHUNK / 4];
+};
+
+// The wave-uniform memory phase between MZ_PERIOD iterations: window refill, ring spill / reload, log flush,
+// prefetch of the chunk below the ring, the next stream groups staged.  Everything this lane stored in the previous
+// phase is complete before any reload is issued (vmcnt(0): issued MZ_PERIOD iterations ago).
+// U16LOG: the log buffer holds entry e of this lane at logb + e * 2 * MZ_LANES (maze_dfs_rows); otherwise two
+// entries per lane dword, dword i at logb + i * 4 * MZ_LANES.
+template <bool U16LOG>
+APG_DEV void maze_memory_phase(MzWin &W, MzStack &K, bool done, bool more, const uint8_t *stream, int ng,
+                               const Pcg64 &r0, double bp, char *ring, char *logb, uint8_t *spill, uint32_t *logg) {
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  if (!done) mz_win_refill(W, stream, ng, r0.i_hi, r0.i_lo, bp);  // the staged groups into the window
+  const int cnt = K.sp - K.lo;
+  uint32_t *ringw = reinterpret_cast<uint32_t *>(ring);
+  // (a) the chunk below the ring back into it, once there is room for it and a period of pushes
+  if (K.pend && cnt <= MZ_RING - MZ_PERIOD - MZ_CHUNK) {
+    const int w0 = ((K.lo - MZ_CHUNK) >> 2) & (MZ_RING / 4 - 1);
+#pragma unroll
+    for (int i = 0; i < MZ_CHUNK / 4; i++) ringw[(w0 + i) * MZ_LANES] = K.pd[i];
+    K.lo -= MZ_CHUNK;
+    K.pend = false;
+  } else if (cnt > MZ_RING - MZ_PERIOD) {
+    // (b) spill the oldest chunk; it stays in registers as the chunk below the ring
+    const int w0 = (K.lo >> 2) & (MZ_RING / 4 - 1);
+#pragma unroll
+    for (int i = 0; i < MZ_CHUNK / 4; i++) K.pd[i] = ringw[(w0 + i) * MZ_LANES];
+    uint4 *dst = reinterpret_cast<uint4 *>(spill + K.lo);
+#pragma unroll
+    for (int i = 0; i < MZ_CHUNK / 16; i++)
+      dst[i] = make_uint4(K.pd[4 * i], K.pd[4 * i + 1], K.pd[4 * i + 2], K.pd[4 * i + 3]);
+    K.lo += MZ_CHUNK;
+    K.pend = true;
+  }
+  // (c) the log buffer out in whole groups of 8 entries (16-byte stores); the rest moves to the front.
+  // After the last period the tail is padded to a whole group.
+  auto entry = [&](int e) -> uint16_t & {
+    return *reinterpret_cast<uint16_t *>(U16LOG ? logb + e * (2 * MZ_LANES) : logb + (e >> 1) * (4 * MZ_LANES) + (e & 1) * 2);
+  };
+  if (!more && (K.lg & 7)) {
+    for (int e = K.lg; e < ((K.lg + 7) & ~7); e++) entry(e) = (uint16_t)MZ_LOG_PAD;
+    K.lg = (K.lg + 7) & ~7;
+  }
+  if (K.lg >= 8) {
+    const int g = K.lg >> 3;  // groups: 1..3
+    uint4 *dst = reinterpret_cast<uint4 *>(logg) + (K.logpos >> 3);
+    if constexpr (U16LOG) {
+      auto group = [&](int q) {
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) w[i] = (uint32_t)entry(8 * q + 2 * i) | ((uint32_t)entry(8 * q + 2 * i + 1) << 16);
+        dst[q] = make_uint4(w[0], w[1], w[2], w[3]);
+      };
+      group(0);
+      if (g > 1) group(1);
+      if (g > 2) group(2);
+      // the leftover (< 8 entries) to the front
+#pragma unroll
+      for (int i = 0; i < 7; i++) {
+        const int src = 8 * g + i;
+        if (src < MZ_LOGBUF) entry(i) = entry(src);
+      }
+    } else {
+      uint32_t *logw = reinterpret_cast<uint32_t *>(logb);  // log dword i at logw[i * MZ_LANES]
+      dst[0] = make_uint4(logw[0], logw[MZ_LANES], logw[2 * MZ_LANES], logw[3 * MZ_LANES]);
+      if (g > 1) dst[1] = make_uint4(logw[4 * MZ_LANES], logw[5 * MZ_LANES], logw[6 * MZ_LANES], logw[7 * MZ_LANES]);
+      if (g > 2) dst[2] = make_uint4(logw[8 * MZ_LANES], logw[9 * MZ_LANES], logw[10 * MZ_LANES], logw[11 * MZ_LANES]);
+      // the leftover (< 8 entries = 4 dwords) to the front
+      const int w0 = 4 * g;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t v = logw[(w0 + i < MZ_LOGBUF / 2 ? w0 + i : 0) * MZ_LANES];
+        if (w0 + i < MZ_LOGBUF / 2) logw[i * MZ_LANES] = v;
+      }
+    }
+    K.logpos += 8 * g;
+    K.lg -= 8 * g;
+  }
+  // (d) prefetch the chunk below the ring (used at a later phase; the wait for it is the vmcnt(0) above)
+  if (!K.pend && K.lo > 0) {
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(spill + K.lo - MZ_CHUNK);
+#pragma unroll
+    for (int i = 0; i < MZ_CHUNK / 8; i++) {
+      const uint64_t v = mz_load_coherent(src + i);
+      K.pd[2 * i] = (uint32_t)v;
+      K.pd[2 * i + 1] = (uint32_t)(v >> 32);
+    }
+    K.pend = true;
+  }
+  if (!done) mz_win_stage(W, stream, ng, W.e >> 5);  // the groups after the window, for the next phase
+}
+
+// The first window (a synchronous load), the groups after it staged, and the start cell's permutation (drawn
+// fresh: no buffered half).  Returns false when the draw does not fit a full window (never in practice).
+APG_DEV bool maze_dfs_start(MzWin &W, const Pcg64 &r0, const uint8_t *stream, int ng, double bp, uint32_t &pidx) {
+  mz_win_stage(W, stream, ng, 0);
+  mz_win_refill(W, stream, ng, r0.i_hi, r0.i_lo, bp);
+  mz_win_stage(W, stream, ng, W.e >> 5);
+  const MzPerm pr = mz_perm_draw(W, W.h0, 0);
+  if (!pr.ok) return false;
+  pidx = pr.pidx;
+  W.has32 = (uint32_t)(pr.q & 1);
+  W.b2 = W.has32 ? (uint32_t)(W.h0 >> (4 * (pr.p - 1) + 2)) & 3u : 0u;
+  mz_win_shift(W, pr.p);
+  return true;
+}
+
+// maze_dfs for mazes of ncx <= 63 (one visited word per row; every maze up to 127 x 127).  The iteration is
+// issue-bound (one wave per SIMD: one instruction per 4 cycles), so it is written for the fewest instructions:
+//  * the cell is one index pos = cy * 64 + cx; a move adds {+1, -1, +64, -64}[direction] (a byte table);
+//  * the rows the next iteration tests (row cy and column cx's words of rows cy +- 1; pad rows stand in for
+//    rows -1 and ncy) are read right after this iteration's move and carve, so their LDS latency overlaps the
+//    rest of the iteration; the parent frame is read at the top, the table entries of both possible next frames
+//    (parent, drawn child) as soon as their indices are known;
+//  * log entries are pos | direction << 13 (cy <= 126: 13 bits of pos), buffered as one u16 per lane and entry;
+//  * the body is straight-line (selects; the long-permutation fallback, probability < 4^-14 per draw, is the only
+//    lane-divergent branch): the wave executes every path any lane takes.  Loop-carried flags are integers.
+template <bool BP1>
+APG_DEV int maze_dfs_rows(const Pcg64 &r0, const uint8_t *stream, int ng, bool active, const MazeGeom &m, double bp,
+                          char *lds, int lane, uint8_t *spill, uint32_t *logg, bool &bad) {
+  constexpr int RB = 8 * MZ_LANES;                    // bytes per vis row (all lanes)
+  constexpr uint32_t MZ_DELTA = 0xC040FF01u;          // direction (+x, -x, +y, -y) -> pos delta (int8 each)
   MzWin W{};
-  const int CW = ONEW ? 1 : m.cw;
+  char *vis = lds + maze_vis_off(m) + lane * 8;       // row 0 of this lane; rows -1 and ncy are the pads
+  char *ring = lds + maze_ring_off(m) + lane * 4;
+  char *logb = lds + maze_log_off(m) + lane * 2;      // entry e at logb + e * 2 * MZ_LANES
+  const uint64_t pad = m.ncx >= 64 ? 0ULL : ~((1ULL << m.ncx) - 1ULL);
+  for (int r = -1; r <= m.ncy; r++)
+    *reinterpret_cast<uint64_t *>(vis + r * RB) = (r < 0 || r == m.ncy) ? ~0ULL : (r == 0 ? pad | 1ULL : pad);
+  const uint4 *tab = reinterpret_cast<const uint4 *>(lds);
+
+  MzStack K{};
+  int pos = 0;
+  // frame = code | from << 5 (the ring byte); rflag / rchild: the frame was just returned to from child
+  // direction rchild (its resume positions come from its table entry, read at the end of the iteration)
+  uint32_t done = active ? 0u : 1u, badf = 0u, first = 1u, frame = 0u, kmask = 0xFu, rflag = 0u, rchild = 0u;
+  uint64_t Rc = pad | 1ULL;                              // row cy
+  uint32_t Wu = m.ncy > 1 ? (uint32_t)pad : ~0u, Wd = ~0u;  // column cx's word of rows cy + 1, cy - 1
+  if (active) {
+    uint32_t pidx = 0;
+    if (maze_dfs_start(W, r0, stream, ng, bp, pidx)) {
+      frame = (pidx / 6u) | (((pidx % 6u) >> 1) << 2) | ((pidx & 1u) << 4);
+    } else {
+      bad = true;
+      done = 1u;
+    }
+  }
+  uint4 T = tab[frame];  // the current frame's table entry
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing in flight at the loop entry
+  for (;;) {
+    for (int it = 0; it < MZ_PERIOD; it++) {
+      // ---- the parent frame (slot sp - 1), for a return
+      const int ps = K.sp - 1;
+      const uint32_t fb = (uint8_t)ring[((ps >> 2) & (MZ_RING / 4 - 1)) * (4 * MZ_LANES) + (ps & 3)];
+      // ---- visited mask of the neighbours: columns cx - 1 .. cx + 1 of row cy (a 64-bit rotation by cx - 1;
+      // column -1 is the pad bit 63), column cx of rows cy +- 1
+      const int cx = pos & 63;
+      const uint32_t n = (uint32_t)(cx - 1);  // cx = 0: 0xFFFFFFFF, the rotation by 63
+      const bool nlo = n < 32u;
+      const uint32_t rc = __builtin_amdgcn_alignbit(nlo ? (uint32_t)(Rc >> 32) : (uint32_t)Rc,
+                                                    nlo ? (uint32_t)Rc : (uint32_t)(Rc >> 32), n);
+      // 4 * the visited mask: the nibble of the table's map
+      const uint32_t V4 = ((rc & 5u) << 2) | (__builtin_amdgcn_ubfe(Wu, (uint32_t)pos, 1u) << 3) |
+                          (__builtin_amdgcn_ubfe(Wd, (uint32_t)pos, 1u) << 5);
+      // ---- the unvisited permutation positions not tried yet, the first one, its direction
+      kmask = rflag ? __builtin_amdgcn_ubfe(T.w, 4u * rchild, 4u) : kmask;
+      const uint32_t pm = (uint32_t)((((uint64_t)T.y << 32) | T.x) >> V4) & kmask;
+      const uint32_t j = (uint32_t)__builtin_ctz(pm | 0x10u);
+      const uint32_t d = (T.z >> (2u * j)) & 3u;
+      // ---- the draws (maze.py:42, 33): rng.random() when the branch is not the frame's first (always below
+      // branching_prob >= 1: BP1), then the child's permutation from the outputs after it.  X = the halves
+      // next_uint32 returns (the buffered one first).
+      const uint32_t hasE = pm != 0u ? 1u : 0u;
+      const uint32_t dneed = hasE & (first ^ 1u);
+      const uint32_t want = BP1 ? hasE : hasE & (first | (W.d & 1u));
+      const uint64_t hs = W.h0 >> (4u * dneed);
+      const uint64_t X = (hs << (2u * W.has32)) | W.b2;
+      const uint32_t xl = (uint32_t)X;
+      const uint32_t kept = ~(xl & (xl >> 1)) & 0x55555554u;  // bit 2i (i >= 1): half i is not 3
+      uint32_t i2x2, j21;
+      if (__builtin_expect(kept != 0u, 1)) {
+        i2x2 = (uint32_t)__builtin_ctz(kept);
+        j21 = __builtin_amdgcn_alignbit((uint32_t)(X >> 32), xl, i2x2) & 7u;
+      } else {  // 15 rejected halves: the rest of X
+        const uint64_t k64 = ~(X & (X >> 1)) & 0x5555555555555554ULL;
+        i2x2 = (uint32_t)__builtin_ctzll(k64 | (1ULL << 62));
+        j21 = (uint32_t)(X >> i2x2) & 7u;
+      }
+      const uint32_t q = (i2x2 >> 1) + 2u - W.has32;  // halves taken from outputs
+      const uint32_t p = (q + 1u) >> 1;               // outputs
+      const uint32_t nhas = q & 1u;
+      const uint32_t nb2 = nhas ? (uint32_t)(hs >> (4u * p - 2u)) & 3u : 0u;
+      const int lim = W.avail < 15 ? W.avail : 15;  // a draw must fit the window (and its 64-bit X)
+      const int need = (int)(dneed + (want ? p : 0u));
+      const uint32_t go = (done == 0u && need <= lim) ? 1u : 0u;
+      // a permutation of > 28 rejected halves (never in practice): the maze is abandoned and reported
+      const uint32_t stuck = (go | done) == 0u && W.avail >= 15 ? 1u : 0u;
+      badf |= stuck;
+      done |= stuck;
+      const uint32_t carve = want & go;
+      const uint32_t ret = go & (hasE ^ 1u) & (K.sp > K.lo ? 1u : 0u);  // sp == lo > 0: parent chunk not back yet
+      done |= go & (hasE ^ 1u) & (K.sp == 0 ? 1u : 0u);                  // carve(starting_pos) returned
+      // ---- the window past this iteration's draws
+      {
+        const int used = go ? need : 0;
+        const uint32_t s = 4u * (uint32_t)used;
+        W.h0 = (W.h0 >> s) | ((W.h1 << 1) << (63u - s));
+        W.h1 >>= s;
+        if constexpr (!BP1) W.d >>= used;
+        W.avail -= used;
+      }
+      W.has32 = carve ? nhas : W.has32;
+      W.b2 = carve ? nb2 : W.b2;
+      // ---- one move: into d (carve), or back against the entry direction (return); the carve's LDS writes,
+      // issued unconditionally (without a carve: the frame byte lands in the free slot above the top, the visited
+      // word is OR-ed with 0, the log entry lands in the free entry lg)
+      const uint32_t from = frame >> 5;
+      const uint32_t mv = carve ? d : (from ^ 1u);
+      pos += (carve | ret) ? __builtin_amdgcn_sbfe((int)MZ_DELTA, 8u * mv, 8u) : 0;
+      char *row = vis + (pos >> 6) * RB;
+      char *wrow = row + ((pos >> 3) & 4);  // column cx's word
+      ring[((K.sp >> 2) & (MZ_RING / 4 - 1)) * (4 * MZ_LANES) + (K.sp & 3)] = (char)frame;
+      __hip_atomic_fetch_or(reinterpret_cast<uint32_t *>(wrow), carve << (pos & 31), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_WAVEFRONT);
+      *reinterpret_cast<uint16_t *>(logb + K.lg * (2 * MZ_LANES)) = (uint16_t)((uint32_t)pos | (d << 13));
+      K.lg += (int)carve;
+      K.sp += carve ? 1 : (ret ? -1 : 0);
+      // ---- the next frame: the child (fresh), the parent (resumes after the child's position: rflag), or this
+      // one (after a skipped branch, BP1 never: the positions after j)
+      kmask = carve ? 0xFu : ((!BP1 && (go & hasE)) ? (0x1Eu << j) & 0xFu : kmask);
+      rflag = ret;
+      rchild = from;
+      {  // (a bit blend: a select chain here compiles to lane-divergent branches)
+        const uint32_t mc = 0u - carve, mr = 0u - ret;
+        frame = (mc & ((j21 << 2) | (xl & 3u) | (d << 5))) | (mr & fb) | (~(mc | mr) & frame);
+      }
+      first = (carve | ret) ? carve : first;
+      // ---- the next iteration's rows (after the carve's visited bit) and table entry
+      Rc = *reinterpret_cast<const uint64_t *>(row);
+      Wu = *reinterpret_cast<const uint32_t *>(wrow + RB);
+      Wd = *reinterpret_cast<const uint32_t *>(wrow - RB);
+      T = tab[frame & 31u];
+    }
+    const bool more = __ballot(done == 0u) != 0ULL;
+    maze_memory_phase<true>(W, K, done != 0u, more, stream, ng, r0, bp, ring, logb, spill, logg);
+    if (!more) break;
+  }
+  if (badf) bad = true;
+  return K.logpos;
+}
+
+// maze_dfs for mazes of ncx > 63 (cw visited words per row): the current cell's rows are read from LDS each
+// iteration, the row bounds are two compares.  Same iteration as maze_dfs_rows otherwise (pidx table entries).
+APG_DEV int maze_dfs_words(const Pcg64 &r0, const uint8_t *stream, int ng, bool active, const MazeGeom &m, double bp,
+                           char *lds, int lane, uint8_t *spill, uint32_t *logg, bool &bad) {
+  MzWin W{};
+  const int CW = m.cw;
   const int RB = CW * 8 * MZ_LANES;  // bytes per vis row (all lanes)
-  char *vis = lds + MZ_V + lane * 8;
+  char *vis = lds + maze_vis_off(m) + lane * 8;
   char *ring = lds + maze_ring_off(m) + lane * 4;
   char *logb = lds + maze_log_off(m) + lane * 4;
-  uint32_t *logw = reinterpret_cast<uint32_t *>(logb);  // log dword i at logw[i * MZ_LANES]
   // visited rows: pad bits of the columns >= ncx, cell (1, 1) visited
   for (int r = 0; r < m.ncy; r++)
     for (int kk = 0; kk < CW; kk++) {
@@ -327,60 +612,38 @@ APG_DEV int maze_dfs(const Pcg64 &r0, const uint8_t *stream, int ng, bool active
     }
   const uint4 *tab = reinterpret_cast<const uint4 *>(lds);
 
-  int cx = 0, cy = 0, sp = 0, lo = 0, k = 0, lg = 0, logpos = 0;
+  MzStack K{};
+  int cx = 0, cy = 0, k = 0;
   int arow = 0;  // byte offset of the current cell's vis row
   uint32_t from = 0, pidx = 0, pinfo = 0;
   uint64_t pmt = 0;
-  bool first = true, done = !active, pend = false;
-  uint32_t pd[MZ_CHUNK / 4];
-#pragma unroll
-  for (int i = 0; i < MZ_CHUNK / 4; i++) pd[i] = 0u;
+  bool first = true, done = !active;
   auto load_perm = [&](uint32_t p) {
     const uint4 t = tab[p];
     pmt = (uint64_t)t.x | ((uint64_t)t.y << 32);
     pinfo = t.z;
   };
-  if (active) {  // the first window (a synchronous load), the groups after it staged, the first permutation
-    mz_win_stage(W, stream, ng, 0);
-    mz_win_refill(W, stream, ng, r0.i_hi, r0.i_lo, bp);
-    mz_win_stage(W, stream, ng, W.e >> 5);
-    const MzPerm pr = mz_perm_draw(W, W.h0, 0);
-    if (pr.ok) {
-      pidx = pr.pidx;
-      W.has32 = (uint32_t)(pr.q & 1);
-      W.b2 = (uint32_t)(W.h0 >> (4 * (pr.p - 1) + 2)) & 3u;
-      mz_win_shift(W, pr.p);
+  if (active) {
+    if (maze_dfs_start(W, r0, stream, ng, bp, pidx)) {
       load_perm(pidx);
     } else {
       bad = true;
       done = true;
     }
   }
-  // nothing in flight at the loop entry: otherwise the compiler's wait for the first window sits inside the
-  // loop, where it also catches every memory phase's prefetches in the iteration after it
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing in flight at the loop entry
   for (;;) {
     for (int it = 0; it < MZ_PERIOD; it++) {
       if (done) continue;
-      // eligible directions of the current cell: in bounds (pad bits, row compares) and not visited.  The
-      // body is kept branch-light (selects, not nested ifs): the wave executes every path any lane takes.
+      // eligible directions of the current cell: in bounds (pad bits, row compares) and not visited
       const uint64_t *vr = reinterpret_cast<const uint64_t *>(vis + arow);
-      uint32_t E;
-      if constexpr (ONEW) {
-        // rows -1 and ncy read other LDS (the table / the ring): masked by the compares
-        const uint64_t rc = ~vr[0], ru = ~vr[MZ_LANES], rd = ~vr[-MZ_LANES];
-        E = (uint32_t)((rc >> ((cx + 1) & 63)) & 1ULL) | ((uint32_t)((rc >> ((cx - 1) & 63)) & 1ULL) << 1) |
-            (((uint32_t)(ru >> cx) & (uint32_t)(cy + 1 < m.ncy) & 1u) << 2) |
-            (((uint32_t)(rd >> cx) & (uint32_t)(cy > 0) & 1u) << 3);
-      } else {
-        const int wc = CW * MZ_LANES, kx = cx >> 6, kr = (cx + 1) >> 6, kl = (cx - 1) >> 6;
-        const uint64_t ru = ~vr[(cy + 1 < m.ncy ? wc : 0) + kx * MZ_LANES], rd = ~vr[(cy > 0 ? -wc : 0) + kx * MZ_LANES];
-        const uint64_t rr = ~vr[(kr < CW ? kr : kx) * MZ_LANES], rl = ~vr[(cx > 0 ? kl : kx) * MZ_LANES];
-        E = ((uint32_t)(rr >> ((cx + 1) & 63)) & (uint32_t)(kr < CW) & 1u) |
-            (((uint32_t)(rl >> ((cx - 1) & 63)) & (uint32_t)(cx > 0) & 1u) << 1) |
-            (((uint32_t)(ru >> (cx & 63)) & (uint32_t)(cy + 1 < m.ncy) & 1u) << 2) |
-            (((uint32_t)(rd >> (cx & 63)) & (uint32_t)(cy > 0) & 1u) << 3);
-      }
+      const int wc = CW * MZ_LANES, kx = cx >> 6, kr = (cx + 1) >> 6, kl = (cx - 1) >> 6;
+      const uint64_t ru = ~vr[(cy + 1 < m.ncy ? wc : 0) + kx * MZ_LANES], rd = ~vr[(cy > 0 ? -wc : 0) + kx * MZ_LANES];
+      const uint64_t rr = ~vr[(kr < CW ? kr : kx) * MZ_LANES], rl = ~vr[(cx > 0 ? kl : kx) * MZ_LANES];
+      const uint32_t E = ((uint32_t)(rr >> ((cx + 1) & 63)) & (uint32_t)(kr < CW) & 1u) |
+                         (((uint32_t)(rl >> ((cx - 1) & 63)) & (uint32_t)(cx > 0) & 1u) << 1) |
+                         (((uint32_t)(ru >> (cx & 63)) & (uint32_t)(cy + 1 < m.ncy) & 1u) << 2) |
+                         (((uint32_t)(rd >> (cx & 63)) & (uint32_t)(cy > 0) & 1u) << 3);
       // the eligible permutation positions >= k
       const uint32_t pm = (uint32_t)(pmt >> (4 * E)) & (0xFu << k) & 0xFu;
       const int j = __builtin_ctz(pm | 0x10u);
@@ -400,8 +663,8 @@ APG_DEV int maze_dfs(const Pcg64 &r0, const uint8_t *stream, int ng, bool active
         done = true;
       }
       const bool carve = want && go;
-      const bool back = go && pm == 0u && sp > lo;  // sp == lo > 0: the parent's chunk arrives at the next phase
-      done = done || (go && pm == 0u && sp == 0);   // carve(starting_pos) returned
+      const bool back = go && pm == 0u && K.sp > K.lo;  // sp == lo > 0: the parent's chunk arrives at the next phase
+      done = done || (go && pm == 0u && K.sp == 0);     // carve(starting_pos) returned
       W.has32 = carve ? (uint32_t)(pr.q & 1) : W.has32;
       W.b2 = carve ? (uint32_t)(hs >> (4 * (pr.p - 1) + 2)) & 3u : W.b2;
       mz_win_shift(W, go ? need : 0);
@@ -413,20 +676,18 @@ APG_DEV int maze_dfs(const Pcg64 &r0, const uint8_t *stream, int ng, bool active
       cx += dx;
       cy += dy;
       arow += dy * RB;
-      const int slot = carve ? sp : sp - 1;
+      const int slot = carve ? K.sp : K.sp - 1;
       char *rb = ring + ((slot >> 2) & (MZ_RING / 4 - 1)) * (4 * MZ_LANES) + (slot & 3);
-      // The carve's three LDS writes are issued unconditionally (no lane-divergent branch): without a carve the
-      // frame byte lands in the free slot above the top (sp - 1 is read instead: slot sp), the visited word is
-      // OR-ed with 0 and the log entry lands in the free entry lg, which the next carve overwrites
-      char *wb = ring + ((sp >> 2) & (MZ_RING / 4 - 1)) * (4 * MZ_LANES) + (sp & 3);
+      // the carve's three LDS writes, issued unconditionally (see maze_dfs_rows)
+      char *wb = ring + ((K.sp >> 2) & (MZ_RING / 4 - 1)) * (4 * MZ_LANES) + (K.sp & 3);
       const uint32_t fb = (uint8_t)*rb;  // the parent frame (used on a return)
       *wb = (char)(pidx | (from << 5));
       __hip_atomic_fetch_or(reinterpret_cast<uint64_t *>(vis + arow + (cx >> 6) * 8 * MZ_LANES),
                             carve ? 1ULL << (cx & 63) : 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-      *reinterpret_cast<uint16_t *>(logb + (lg >> 1) * (4 * MZ_LANES) + (lg & 1) * 2) =
+      *reinterpret_cast<uint16_t *>(logb + (K.lg >> 1) * (4 * MZ_LANES) + (K.lg & 1) * 2) =
           (uint16_t)((uint32_t)cx | ((uint32_t)cy << 7) | (d << 14));
-      lg += carve ? 1 : 0;
-      sp += carve ? 1 : (back ? -1 : 0);
+      K.lg += carve ? 1 : 0;
+      K.sp += carve ? 1 : (back ? -1 : 0);
       const uint32_t child = from;
       pidx = carve ? pr.pidx : (back ? fb & 31u : pidx);
       from = carve ? d : (back ? fb >> 5 : from);
@@ -434,69 +695,27 @@ APG_DEV int maze_dfs(const Pcg64 &r0, const uint8_t *stream, int ng, bool active
       load_perm(pidx);  // (the same entry again when nothing moved)
       k = carve ? 0 : (back ? (int)((pinfo >> (8 + 2 * child)) & 3u) + 1 : k);
     }
-    // ---- memory phase (wave-uniform).  Everything this lane stored in the previous phase is complete
-    // before any reload is issued below (vmcnt(0): issued MZ_PERIOD iterations ago).
     const bool more = __ballot(!done) != 0ULL;
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    if (!done) mz_win_refill(W, stream, ng, r0.i_hi, r0.i_lo, bp);  // the staged groups into the window
-    const int cnt = sp - lo;
-    uint32_t *ringw = reinterpret_cast<uint32_t *>(ring);
-    // (a) the chunk below the ring back into it, once there is room for it and a period of pushes
-    if (pend && cnt <= MZ_RING - MZ_PERIOD - MZ_CHUNK) {
-      const int w0 = ((lo - MZ_CHUNK) >> 2) & (MZ_RING / 4 - 1);
-#pragma unroll
-      for (int i = 0; i < MZ_CHUNK / 4; i++) ringw[(w0 + i) * MZ_LANES] = pd[i];
-      lo -= MZ_CHUNK;
-      pend = false;
-    } else if (cnt > MZ_RING - MZ_PERIOD) {
-      // (b) spill the oldest chunk; it stays in registers as the chunk below the ring
-      const int w0 = (lo >> 2) & (MZ_RING / 4 - 1);
-#pragma unroll
-      for (int i = 0; i < MZ_CHUNK / 4; i++) pd[i] = ringw[(w0 + i) * MZ_LANES];
-      uint4 *dst = reinterpret_cast<uint4 *>(spill + lo);
-#pragma unroll
-      for (int i = 0; i < MZ_CHUNK / 16; i++) dst[i] = make_uint4(pd[4 * i], pd[4 * i + 1], pd[4 * i + 2], pd[4 * i + 3]);
-      lo += MZ_CHUNK;
-      pend = true;
-    }
-    // (c) the log buffer out in whole groups of 8 entries (16-byte stores); the rest moves to the front.
-    // After the last period the tail is padded to a whole group.
-    if (!more && (lg & 7)) {
-      for (int e = lg; e < ((lg + 7) & ~7); e++)
-        *reinterpret_cast<uint16_t *>(logb + (e >> 1) * (4 * MZ_LANES) + (e & 1) * 2) = (uint16_t)MZ_LOG_PAD;
-      lg = (lg + 7) & ~7;
-    }
-    if (lg >= 8) {
-      const int g = lg >> 3;  // groups: 1..3
-      uint4 *dst = reinterpret_cast<uint4 *>(logg) + (logpos >> 3);
-      dst[0] = make_uint4(logw[0], logw[MZ_LANES], logw[2 * MZ_LANES], logw[3 * MZ_LANES]);
-      if (g > 1) dst[1] = make_uint4(logw[4 * MZ_LANES], logw[5 * MZ_LANES], logw[6 * MZ_LANES], logw[7 * MZ_LANES]);
-      if (g > 2) dst[2] = make_uint4(logw[8 * MZ_LANES], logw[9 * MZ_LANES], logw[10 * MZ_LANES], logw[11 * MZ_LANES]);
-      // the leftover (< 8 entries = 4 dwords) to the front
-      const int w0 = 4 * g;
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const uint32_t v = logw[(w0 + i < MZ_LOGBUF / 2 ? w0 + i : 0) * MZ_LANES];
-        if (w0 + i < MZ_LOGBUF / 2) logw[i * MZ_LANES] = v;
-      }
-      logpos += 8 * g;
-      lg -= 8 * g;
-    }
-    // (d) prefetch the chunk below the ring (used at a later phase; the wait for it is the vmcnt(0) above)
-    if (!pend && lo > 0) {
-      const uint64_t *src = reinterpret_cast<const uint64_t *>(spill + lo - MZ_CHUNK);
-#pragma unroll
-      for (int i = 0; i < MZ_CHUNK / 8; i++) {
-        const uint64_t v = mz_load_coherent(src + i);
-        pd[2 * i] = (uint32_t)v;
-        pd[2 * i + 1] = (uint32_t)(v >> 32);
-      }
-      pend = true;
-    }
-    if (!done) mz_win_stage(W, stream, ng, W.e >> 5);  // the groups after the window, for the next phase
+    maze_memory_phase<false>(W, K, done, more, stream, ng, r0, bp, ring, logb, spill, logg);
     if (!more) break;
   }
-  return logpos;
+  return K.logpos;
+}
+
+// The DFS of one maze per lane.  Every lane of the wave must call it (wave-uniform memory phases); lanes
+// with active == false only take part in them.  `lds` is the workgroup's dynamic LDS (maze_table_init<ONEW>
+// done), `spill` / `logg` / `stream` this maze's global scratch (16-byte aligned; the stream of ng groups written
+// by k_maze_stream), r0 the maze's seeded generator (its increment steps the LCG past the stream).  ONEW: ncx
+// <= 63.  Returns the log length in entries (a multiple of 8, the tail padded); `bad` is set when a draw does
+// not fit in a full window (a permutation of ~30 rejected halves: never in practice) and that maze is abandoned.
+template <bool ONEW>
+APG_DEV int maze_dfs(const Pcg64 &r0, const uint8_t *stream, int ng, bool active, const MazeGeom &m, double bp,
+                     char *lds, int lane, uint8_t *spill, uint32_t *logg, bool &bad) {
+  if constexpr (ONEW) {
+    if (bp >= 1.0) return maze_dfs_rows<true>(r0, stream, ng, active, m, bp, lds, lane, spill, logg, bad);
+    return maze_dfs_rows<false>(r0, stream, ng, active, m, bp, lds, lane, spill, logg, bad);
+  }
+  else return maze_dfs_words(r0, stream, ng, active, m, bp, lds, lane, spill, logg, bad);
 }
 
 // Paint a maze's occupancy rows from its log into the LDS bitmap bm[h][wpr] (all walls, then the start cell
@@ -532,8 +751,10 @@ APG_DEV void maze_paint(const MazeGeom &m, int wpr, const uint32_t *logg, int nl
     for (int t = 0; t < 8; t++) {
       const uint32_t e = (wv[t >> 1] >> (16 * (t & 1))) & 0xFFFFu;
       if (8 * q + t >= nlog || e == MZ_LOG_PAD) continue;
-      const int x = 2 * (int)(e & 127u) + 1, y = 2 * (int)((e >> 7) & 127u) + 1;
-      const uint32_t d = e >> 14;
+      // entries: cx | cy << 7 | d << 14 (maze_dfs_words), pos | d << 13 with pos = cy * 64 + cx (maze_dfs_rows)
+      const bool onew = maze_onew(m);
+      const int x = 2 * (int)(e & (onew ? 63u : 127u)) + 1, y = 2 * (int)((e >> (onew ? 6 : 7)) & 127u) + 1;
+      const uint32_t d = (e >> (onew ? 13 : 14)) & 3u;
       const int px = x - ((d == 0u) - (d == 1u)), py = y - ((d == 2u) - (d == 3u));  // passage cell
       if (py == y) {  // same row: one or two words
         const int k0 = x >> 6, k1 = px >> 6;
