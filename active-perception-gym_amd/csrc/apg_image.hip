@@ -601,16 +601,17 @@ struct EnvArgs {
   float mse_scale, mse_offset;
   float time_value;
   float loss_weight;  // 1, or for the -sparse ids terminated.astype(float32) (one value: episodes end together)
-  const float *copy_target;  // localize, steps without a target refresh: prediction_target = target.copy() here
+  int copy_target;  // localize, steps without a target refresh: prediction_target = target.copy() here
+  float *target_st;  // the state's targets (localize)
   // the batch autoreset with its draws made ahead (apg_image_draw_ahead), k_image_gather and k_loc_target folded
-  // into the step kernel: draws of env e at d = offset + e; NULL: the draws (if any) are installed already
-  const int64_t *ahead_idx, *ahead_inv;
-  const double *ahead_pos, *ahead_tgt;
+  // into the step kernel: draws of env e at d = offset + e, the index / inversion draws at ahead_i64[d] /
+  // [nt + d], the start / target draws at ahead_f64[2 d] / [2 nt + 2 d]; NULL: the draws (if any) are installed
+  // already.  (Few fields: the kernel's SGPR budget holds the arguments without spilling.)
+  const int64_t *ahead_i64;
+  const double *ahead_f64;
   const int32_t *pool_labels;
-  int invert, offset;
-  int64_t *index_st;
-  int32_t *label_st, *inverted_st;
-  float *target_st;
+  int32_t *inverted_st;
+  int invert, offset, nt;
 };
 
 
@@ -700,20 +701,21 @@ struct EnvIn {
 // The batch autoreset of env e from the draws made ahead (k_image_gather + k_loc_target): the new data point,
 // its label (inverted when drawn so), start position, and (localize) the pre-update target as this step's
 // prediction target, the refreshed target into the state.  Returns the new image's pool index.
-APG_DEV int64_t install_ahead(const EnvArgs &a, int e, const apg_image_outputs &out, double *pos, EnvIn &in) {
+APG_DEV int64_t install_ahead(const EnvArgs &a, int e, const apg_image_outputs &out, double *pos, EnvIn &in,
+                              int64_t *index_st, int32_t *label_st) {
   const int d = a.offset + e;
-  const int64_t idx = a.ahead_idx[d];
-  a.index_st[e] = idx;
+  const int64_t idx = a.ahead_i64[d];
+  index_st[e] = idx;
   int32_t l = a.pool_labels[idx];
   if (a.invert) {
-    const int32_t inv = a.ahead_inv[d] == 1 ? 1 : 0;  // integers(0, 2, N) == 1
+    const int32_t inv = a.ahead_i64[(size_t)a.nt + d] == 1 ? 1 : 0;  // integers(0, 2, N) == 1
     a.inverted_st[e] = inv;
     if (inv) l = a.k - l - 1;
   }
-  a.label_st[e] = l;
+  label_st[e] = l;
   in.label = l;
-  in.px = a.ahead_pos[2 * d];
-  in.py = a.ahead_pos[2 * d + 1];
+  in.px = a.ahead_f64[2 * d];
+  in.py = a.ahead_f64[2 * d + 1];
   pos[2 * e] = in.px;
   pos[2 * e + 1] = in.py;
   if (a.kind == APG_IMAGE_LOCALIZE) {  // prediction_target = target.copy(); target[prev_done] = uniform draws
@@ -721,8 +723,8 @@ APG_DEV int64_t install_ahead(const EnvArgs &a, int e, const apg_image_outputs &
     in.t1 = a.target_st[2 * e + 1];
     ro(out.target, a.row, e, 2, 0) = in.t0;
     ro(out.target, a.row, e, 2, 1) = in.t1;
-    a.target_st[2 * e] = (float)a.ahead_tgt[2 * d];
-    a.target_st[2 * e + 1] = (float)a.ahead_tgt[2 * d + 1];
+    a.target_st[2 * e] = (float)a.ahead_f64[2 * ((size_t)a.nt + d)];
+    a.target_st[2 * e + 1] = (float)a.ahead_f64[2 * ((size_t)a.nt + d) + 1];
   }
   return idx;
 }
@@ -740,8 +742,8 @@ APG_DEV EnvIn load_env_in(const EnvArgs &a, int e, const float *__restrict__ act
   if constexpr (KIND == APG_IMAGE_LOCALIZE) {
     in.p0 = pred[2 * e];
     in.p1 = pred[2 * e + 1];
-    in.t0 = a.copy_target ? a.copy_target[2 * e] : ro(out.target, a.row, e, 2, 0);
-    in.t1 = a.copy_target ? a.copy_target[2 * e + 1] : ro(out.target, a.row, e, 2, 1);
+    in.t0 = a.copy_target ? a.target_st[2 * e] : ro(out.target, a.row, e, 2, 0);
+    in.t1 = a.copy_target ? a.target_st[2 * e + 1] : ro(out.target, a.row, e, 2, 1);
   } else {
     in.label = label[e];
   }
@@ -1013,12 +1015,13 @@ __attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fuse
     in = EnvIn{};
     if (r < nu) {
       const int e = u0 + r;
-      if (a.ahead_idx) {  // the batch autoreset, its draws made ahead: installed here (k_image_gather folded in)
+      if (a.ahead_i64) {  // the batch autoreset, its draws made ahead: installed here (k_image_gather folded in)
         if constexpr (KIND == APG_IMAGE_LOCALIZE) {
           in.p0 = pred[2 * e];
           in.p1 = pred[2 * e + 1];
         }
-        s_base[r] = install_ahead(a, e, out, pos, in) * g.img_elems;
+        s_base[r] = install_ahead(a, e, out, pos, in, const_cast<int64_t *>(index), const_cast<int32_t *>(label)) *
+                    g.img_elems;
       } else {
         in = load_env_in<KIND>(a, e, act, pred, label, pos, out);
         s_base[r] = index[e] * g.img_elems;
@@ -1811,20 +1814,17 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
   a.t_new = t_new;
   a.time_value = (float)(((double)t_new / (double)c->step_limit) * 2.0 - 1.0);
   a.loss_weight = !c->sparse ? 1.0f : (!prev_done && t_new >= c->step_limit ? 1.0f : 0.0f);
-  a.copy_target = c->kind == APG_IMAGE_LOCALIZE && !prev_done ? st->target : nullptr;
+  a.copy_target = c->kind == APG_IMAGE_LOCALIZE && !prev_done ? 1 : 0;
+  a.target_st = st->target;
   a.row = c->out_row_bytes;
   if (fold) {
-    a.ahead_idx = st->ahead_i64;
-    a.ahead_inv = st->ahead_i64 + nt;
-    a.ahead_pos = st->ahead_f64;
-    a.ahead_tgt = st->ahead_f64 + 2 * (size_t)nt;
+    a.ahead_i64 = st->ahead_i64;
+    a.ahead_f64 = st->ahead_f64;
+    a.nt = (int)nt;
     a.pool_labels = st->pool_labels;
     a.invert = c->invert_labels;
     a.offset = c->env_offset;
-    a.index_st = st->index;
-    a.label_st = st->label;
     a.inverted_st = st->inverted;
-    a.target_st = st->target;
   }
   if (fusable) {
     const int per = g.s0 * g.s1;

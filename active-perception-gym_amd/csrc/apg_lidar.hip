@@ -495,7 +495,7 @@ __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_stat
                                                            PfView pv) {
   __shared__ uint16_t s_list[MP_ENVS];
   __shared__ int s_cnt, s_wsum[MP_THREADS / 64], s_hit[2];
-  extern __shared__ uint64_t s_bm[];  // one maze's rows
+  extern __shared__ uint64_t s_bm[];  // one maze's rows, then bitmap_map_obs's linear bitmap
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e0 = blockIdx.x * MP_ENVS;
   if (tid == 0) s_cnt = 0;
   __syncthreads();
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_stat
       __syncthreads();  // the bitmap is read before the next maze paints it
       continue;
     }
-    if (map_obs) bitmap_map_obs<MP_THREADS>(s_bm, g.h, g.w, g.wpr, map_obs + (size_t)e * g.h * g.w, tid);
+    if (map_obs) bitmap_map_obs<MP_THREADS>(s_bm, g.h, g.w, g.wpr, map_obs + (size_t)e * g.h * g.w, tid, s_bm + words);
     // free cells per row, their inclusive scan (rows <= MP_THREADS = 256: one per thread), the row holding the pick
     int fr = 0;
     if (tid < g.h) {
@@ -790,6 +790,8 @@ struct StepShape {
   static_assert(LPW == 16, "16 envs per wave in the env-major phases");
 };
 constexpr int MAX_MAP_ROWS = 128;
+// GEN_PF phase R, per wave: an env's occupancy rows (<= 128 x 2 words), then bitmap_map_obs's linear bitmap
+constexpr int PF_WAVE_WORDS = MAX_MAP_ROWS * 2 + (MAX_MAP_ROWS * 128 + 63) / 64 + 1;
 
 // Row y of a rooms map painted from its primitives (rooms_paint's result, one row at a time): border
 // | walls & ~doors.  Word k covers columns [64k, 64k + 64); the primitives are pr[i * st].
@@ -968,7 +970,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         // map obs (bool map / 255, lidar_localization2d.py:299) from that copy; the env's lane then installs the
         // reset state (start cell, streams after the reset's draws, map index: :293-315) and publishes the new
         // generation (release: the side stream's select reads the streams after acquiring it)
-        uint64_t *mrow = reinterpret_cast<uint64_t *>(s_dyn) + (size_t)wave * MAX_MAP_ROWS * 2;
+        uint64_t *mrow = reinterpret_cast<uint64_t *>(s_dyn) + (size_t)wave * PF_WAVE_WORDS;  // rows, linear bitmap
         const int m = P.h, wpr = P.wpr;
         const int words = m * wpr;
         uint32_t g0 = 0;
@@ -990,7 +992,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          if (O.map_obs) bitmap_map_obs<64>(mrow, m, P.w, wpr, O.map_obs + (size_t)e * m * P.w, lane);
+          if (O.map_obs) bitmap_map_obs<64>(mrow, m, P.w, wpr, O.map_obs + (size_t)e * m * P.w, lane, mrow + words);
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();  // mrow is rewritten by the next env
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1757,7 +1759,8 @@ int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, in
     hipLaunchKernelGGL(k_maze<false>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, st, idx, n, scratch, mode, seed,
                        use_seed, all, err, lanes, ng);
   if (int rc = check_launch("k_maze")) return rc;
-  hipLaunchKernelGGL(k_maze_paint, dim3(grid_for(n, MP_ENVS)), dim3(MP_THREADS), (size_t)g.h * g.wpr * sizeof(uint64_t),
+  hipLaunchKernelGGL(k_maze_paint, dim3(grid_for(n, MP_ENVS)), dim3(MP_THREADS),
+                     ((size_t)g.h * g.wpr + bitmap_lin_words(g.h, g.w)) * sizeof(uint64_t),
                      s, g, st, idx, n, occ, scratch, mode, seed, use_seed, all, ng, out_map_idx, map_obs, err,
                      pv ? *pv : PfView{});
   return check_launch("k_maze_paint");
@@ -1848,7 +1851,7 @@ int launch_step_t(const StepParams &P, const Geo &g, const apg_lidar_state *st, 
                   const apg_lidar_outputs *out, hipStream_t s, const BinomTable &bt, const PfView &V) {
   size_t lds = step_lds_bytes(EPB, P.beams);
   if (FUSED && GEN == GEN_ROOMS && RoomsLds<EPB>::bytes > lds) lds = RoomsLds<EPB>::bytes;
-  if (FUSED && GEN == GEN_PF) lds = std::max(lds, (size_t)(4 * EPB / 64) * MAX_MAP_ROWS * 2 * sizeof(uint64_t));
+  if (FUSED && GEN == GEN_PF) lds = std::max(lds, (size_t)(4 * EPB / 64) * PF_WAVE_WORDS * sizeof(uint64_t));
   auto kern = P.row ? k_lidar_step<GEN, FUSED, EPB, GR, true> : k_lidar_step<GEN, FUSED, EPB, GR, false>;
   if (int rc = opt_in_lds((const void *)kern, lds)) return rc;
   hipLaunchKernelGGL(kern, dim3(grid_for(P.n, EPB)), dim3(4 * EPB), lds, s, P, g, *st, act, pred, *out, bt, V);

@@ -773,46 +773,67 @@ APG_DEV void maze_paint(const MazeGeom &m, int wpr, const uint32_t *logg, int nl
   sync();
 }
 
+// Words of the row-major linear bitmap bitmap_map_obs builds (bit c = cell c = y * w + x), + 1 zero word.
+__host__ __device__ inline int bitmap_lin_words(int h, int w) { return (h * w + 63) / 64 + 1; }
+
 // The f32 map observation of a painted bitmap (bool map / 255, lidar_localization2d.py:299) into dst[h * w],
-// by NT cooperating threads (t = 0 .. NT - 1, NT >= 8): 16-byte non-temporal stores over the 16-byte-aligned
-// body of the map's floats (a wave-store of dwords per row left the kernel store-issue bound), scalar stores
-// for the unaligned head and tail.  Cell c = y * w + x of float4 q is found once per store and then stepped.
+// by NT cooperating threads (t = 0 .. NT - 1, NT >= 8; the caller synchronizes NT = 64 as a wave, NT > 64 with
+// __syncthreads around the call).  The bitmap's rows are first re-laid as one row-major bit string in `lin`
+// (bitmap_lin_words; cells c .. c + 3 are then four consecutive bits, read by 16 lanes at once), then the
+// 16-byte-aligned body of the map's floats goes out in 16-byte non-temporal stores (4 cells each; a wave-store of
+// dwords per row left the kernel store-issue bound), the unaligned head and tail in scalar stores.
 template <int NT = 64>
-APG_DEV void bitmap_map_obs(const uint64_t *bm, int h, int w, int wpr, float *dst, int lane) {
+APG_DEV void bitmap_map_obs(const uint64_t *bm, int h, int w, int wpr, float *dst, int lane, uint64_t *lin) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   const float wall = 1.0f / 255.0f;
-  const int cells = h * w;
+  const int cells = h * w, nlin = bitmap_lin_words(h, w);
+  // bits [x, x + k) (k <= 64) of row y
+  auto row_bits = [&](int y, int x, int k) -> uint64_t {
+    const uint64_t *r = bm + y * wpr;
+    const int q = x >> 6, o = x & 63;
+    const uint64_t lo = r[q], hi = q + 1 < wpr ? r[q + 1] : 0ULL;
+    const uint64_t v = (lo >> o) | ((hi << 1) << (63 - o));
+    return k >= 64 ? v : v & ((1ULL << k) - 1ULL);
+  };
+  for (int i = lane; i < nlin; i += NT) {
+    uint64_t v = 0;
+    int c = 64 * i;
+    if (c < cells) {
+      int y = c / w, x = c - y * w, filled = 0;
+      while (filled < 64 && y < h) {
+        const int k = min(64 - filled, w - x);
+        v |= row_bits(y, x, k) << filled;
+        filled += k;
+        x = 0;
+        y++;
+      }
+    }
+    lin[i] = v;
+  }
+  if constexpr (NT == 64) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
   const int head = (int)(((16u - ((unsigned)(uintptr_t)dst & 15u)) & 15u) >> 2);  // floats before a 16-B boundary
   const int nbody = (cells - head) >> 2;
-  const float invw = 1.0f / (float)w;
-  auto cell_of = [&](int c, int &y, int &x) {
-    y = (int)((float)c * invw);
-    if (y * w > c) y--;
-    if ((y + 1) * w <= c) y++;
-    x = c - y * w;
-  };
-  auto bit = [&](int y, int x) { return (uint32_t)(bm[y * wpr + (x >> 6)] >> (x & 63)) & 1u; };
   for (int q = lane; q < nbody; q += NT) {
-    int y, x;
-    cell_of(head + 4 * q, y, x);
+    const int c = head + 4 * q, wi = c >> 6;
+    const uint32_t o = (uint32_t)c & 63u;
+    const uint32_t nib = (uint32_t)((lin[wi] >> o) | ((lin[wi + 1] << 1) << (63u - o))) & 15u;
     f4 v;
-    float *vv = reinterpret_cast<float *>(&v);
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      vv[i] = bit(y, x) ? wall : 0.0f;
-      x++;
-      const bool wrap = x >= w;
-      x = wrap ? 0 : x;
-      y += wrap ? 1 : 0;
-    }
+    v.x = (nib & 1u) ? wall : 0.0f;
+    v.y = (nib & 2u) ? wall : 0.0f;
+    v.z = (nib & 4u) ? wall : 0.0f;
+    v.w = (nib & 8u) ? wall : 0.0f;
     __builtin_nontemporal_store(v, reinterpret_cast<f4 *>(dst + head) + q);
   }
   const int tail0 = head + 4 * nbody;
   if (lane < head || (lane >= 4 && lane - 4 < cells - tail0)) {
     const int c = lane < head ? lane : tail0 + lane - 4;
-    int y, x;
-    cell_of(c, y, x);
-    dst[c] = bit(y, x) ? wall : 0.0f;
+    dst[c] = ((lin[c >> 6] >> (c & 63)) & 1ULL) ? wall : 0.0f;
   }
 }
 

@@ -188,28 +188,35 @@ def run_image(args, world, rank, dev):
         senv.step(inputs[t % ring])
     senv.gather_ms()
     ev = HipEvents(args.steps)
+    stepper = senv.step if senv.gather else env.step
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    # the timed window (`value`): K plain steps, no hipEvents between the launches
     t0 = time.perf_counter()
-    timed = [t for t in range(args.steps) if t % args.event_every == args.event_every - 1]  # steps with hipEvents
-    stepper = senv.step if senv.gather else env.step
     for t in range(args.steps):
-        # hipEvents right around the step's kernel launches (inside env.step), on sampled steps
-        if t % args.event_every == args.event_every - 1:
-            env.set_kernel_timing_events(*ev.pair(t))
-            stepper(inputs[(args.warmup + t) % ring])
-            env.set_kernel_timing_events(None)
-        else:
-            stepper(inputs[(args.warmup + t) % ring])
-    env.set_kernel_timing_events(None)
+        stepper(inputs[(args.warmup + t) % ring])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     env.check_errors()
-    step_ms = sum(ev.elapsed_ms(i) for i in timed) / len(timed)
     gather_ms = senv.gather_ms() or 0.0
+    # the kernel-time pass (roofline, not `value`): K more steps, hipEvents right around the step's kernel launches
+    # (inside env.step) on every event_every-th
+    timed = [t for t in range(args.steps) if t % args.event_every == args.event_every - 1]  # steps with hipEvents
+    for t in range(args.steps):
+        if t % args.event_every == args.event_every - 1:
+            env.set_kernel_timing_events(*ev.pair(t))
+            stepper(inputs[(args.warmup + args.steps + t) % ring])
+            env.set_kernel_timing_events(None)
+        else:
+            stepper(inputs[(args.warmup + args.steps + t) % ring])
+    env.set_kernel_timing_events(None)
+    torch.cuda.synchronize(dev)
+    env.check_errors()
+    step_ms = sum(ev.elapsed_ms(i) for i in timed) / len(timed)
+    senv.gather_ms()
     ev.close()
     if world > 1:
         tt = torch.tensor([elapsed, step_ms, reset_ms, gather_ms], dtype=torch.float64,
@@ -440,19 +447,28 @@ def run_lidar(args, world, rank, dev):
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    # the timed window (`value`): K plain steps, no hipEvents between the launches
     t0 = time.perf_counter()
     first_timed = steps_done + 1
-    timed = [t for t in range(args.steps) if t % args.event_every == args.event_every - 1]  # steps with hipEvents
     for t in range(args.steps):
-        step(ev.pair(t) if t % args.event_every == args.event_every - 1 else (None, None))
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    env.check_errors()
+    gather_ms = senv.gather_ms() or 0.0
+    # the kernel-time pass (roofline, not `value`): K more steps, hipEvents around the step's launches on every
+    # event_every-th (an event pair adds stream packets and +6..9 us of wall to its step)
+    first_ev = steps_done + 1
+    timed = [t for t in range(args.steps) if t % args.event_every == args.event_every - 1]  # steps with hipEvents
+    for t in range(args.steps):
+        step(ev.pair(t) if t % args.event_every == args.event_every - 1 else (None, None))
+    torch.cuda.synchronize(dev)
     env.set_kernel_timing_events(None)
     env.check_errors()
     per_step = [ev.elapsed_ms(i) for i in timed]
-    gather_ms = senv.gather_ms() or 0.0
+    senv.gather_ms()
     kernel_ms = sum(per_step) / len(per_step)
     median_ms = statistics.median(per_step)
     # reset steps (1-based step index t with t % 101 == 0: synchronized episodes) in the timed window
@@ -493,8 +509,8 @@ def run_lidar(args, world, rank, dev):
         step_b = BYTES_PER_ENV_STEP(beams) * n_local
         # a reset step also writes each env's map obs (f32) and its bit-packed occupancy rows
         reset_b = step_b + (MAP_OBS_BYTES(msize) + msize * ((msize + 63) // 64) * 8) * n_local
-        # the launches the kernel time averages over: the timed steps that carried events
-        reset_ev = sum(1 for t in timed if (first_timed + t) % EPISODE_PERIOD == 0)
+        # the launches the kernel time averages over: the kernel-time pass's steps that carried events
+        reset_ev = sum(1 for t in timed if (first_ev + t) % EPISODE_PERIOD == 0)
         bytes_per_launch = (step_b * (len(timed) - reset_ev) + reset_b * reset_ev) / len(timed)
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
         shape = {"num_envs": n_local, "beams": beams, "map": msize}
@@ -689,10 +705,10 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=101)
     ap.add_argument("--cpu-threads", type=int, default=None, help="OpenMP threads of the multi-thread CPU row")
     ap.add_argument("--event-every", type=int, default=4,
-                    help="record the kernel's hipEvents on every N-th timed step (steps N-1, 2N-1, ...: not the "
-                         "first launch after the synchronize): each event pair adds two stream packets between "
-                         "kernels, measured +6..9 us of wall per step on MI355X (tools/host_overhead.py), so "
-                         "sampling keeps `value` unperturbed")
+                    help="kernel-time pass after the timed window: record the kernel's hipEvents on every N-th "
+                         "step (steps N-1, 2N-1, ...: not the first launch after the synchronize); the timed "
+                         "window itself carries no events (an event pair adds two stream packets between kernels, "
+                         "+6..9 us of wall per step on MI355X, tools/host_overhead.py)")
     ap.add_argument("--array-backend", default="torch", choices=["torch", "numpy"],
                     help="LIDAR workloads: torch = device tensors in/out (the hot path, default); numpy = the "
                          "drop-in default of make_vec (host arrays, one packed D2H copy per step)")

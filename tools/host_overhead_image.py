@@ -15,7 +15,7 @@ n, K = 65536, 400
 dev = torch.device("cuda:0")
 ds = ap.SyntheticImageClassificationDataset(60000, (28, 28), 10, 1, seed=0)
 cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=(5, 5), step_limit=16)
-env = ap.ImageClassificationVectorEnv(n, cfg, device=dev, array_backend="torch")
+env = ap.ImageClassificationVectorEnv(n, cfg, device=dev, array_backend="torch", log_stats="--no-stats" not in sys.argv)
 env.reset(seed=0)
 acts = torch.rand((8, n, 2), device=dev) * 2 - 1
 preds = torch.randn((8, n, 10), device=dev)

@@ -89,7 +89,7 @@ __global__ __launch_bounds__(64) void k_paint(int n, int h, int w, const uint8_t
     maze_paint(m, wpr, reinterpret_cast<const uint32_t *>(scratch + (size_t)e * sb), nlog[e], s_mz, lane);
     for (int y = lane; y < h; y += 64)
       for (int k = 0; k < wpr; k++) occ[((size_t)e * h + y) * wpr + k] = s_mz[y * wpr + k];
-    if (mo) bitmap_map_obs(s_mz, h, w, wpr, mo + (size_t)e * h * w, lane);
+    if (mo) bitmap_map_obs(s_mz, h, w, wpr, mo + (size_t)e * h * w, lane, s_mz + h * wpr);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -117,7 +117,7 @@ int main(int argc, char **argv) {
   CHECK(hipMalloc(&hash, (size_t)2 * n * sizeof(uint64_t)));
   CHECK(hipMalloc(&occ, (size_t)n * size * wpr * 8));
   const size_t lds = maze_wg_lds_bytes(size, size);
-  const size_t lds_p = (size_t)size * wpr * 8;
+  const size_t lds_p = ((size_t)size * wpr + bitmap_lin_words(size, size)) * 8;
   CHECK(hipFuncSetAttribute((const void *)k_dfs<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   CHECK(hipFuncSetAttribute((const void *)k_dfs<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int occ0 = 0, occ1 = 0;
