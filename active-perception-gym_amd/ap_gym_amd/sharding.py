@@ -108,6 +108,7 @@ class ShardedVectorEnv:
         self._send = self._recv = None
         self._views = None
         self._index_full = None  # image envs: the gathered info["index"] (changes only with the batch)
+        self._done_full = None  # image envs: gathered terminated / truncated / sparse weight constants
         self.time_gather = time_gather
         self.gather_events: list = []  # (begin, end) torch.cuda.Event pairs around each all-gather
 
@@ -263,12 +264,19 @@ class ShardedVectorEnv:
         cls = "label_target" in v
         target = v["label_target"] if cls else v["target_out"]
         loss = v["loss_f64"] if cls else v["loss_f32"]
-        tflag, fflag = bool(term[0]), bool(trunc[0])  # the whole batch terminates together
-        g_term = torch.full((n,), tflag, dtype=torch.bool, device=target.device)
-        g_trunc = torch.full((n,), fflag, dtype=torch.bool, device=target.device)
+        # the whole batch terminates together, never truncated, and the env knows when on the host (no device
+        # read: bool(term[0]) synchronized every gathered step); the gathered flags are constant tensors
+        tflag = bool(getattr(self.env, "_prev_done", False)) if hasattr(self.env, "_prev_done") else bool(term[0])
+        if self._done_full is None:
+            dev = target.device
+            self._done_full = (torch.zeros(n, dtype=torch.bool, device=dev), torch.ones(n, dtype=torch.bool, device=dev),
+                               torch.zeros(n, dtype=torch.float32, device=dev),
+                               torch.ones(n, dtype=torch.float32, device=dev))
+        g_term = self._c(self._done_full[1 if tflag else 0])
+        g_trunc = self._c(self._done_full[0])
         pt = info["prediction"]["target"]
         if isinstance(pt, dict):  # -sparse ids: weight = terminated as float32
-            target = {"target": target, "weight": g_term.to(torch.float32)}
+            target = {"target": target, "weight": self._c(self._done_full[3 if tflag else 2])}
         ginfo = {"index": self._c(self._index_full), "base_reward": v["base_reward"],
                  "prediction": {"target": target, "loss": loss}, "local_obs": obs}
         if "stats" in info:  # the vector log wrapper's scalars of the whole batch from the rows; the per-step

@@ -166,9 +166,10 @@ def run_image(args, world, rank, dev):
     cls = apg.ImageClassificationVectorEnv if w["kind"] == "cls" else apg.ImageLocalizationVectorEnv
     from ap_gym_amd.sharding import ShardedVectorEnv
 
-    senv = ShardedVectorEnv(lambda num_envs, env_offset: cls(num_envs, cfg, device=dev, array_backend="torch",
-                                                             num_envs_total=n_total, env_offset=env_offset,
-                                                             log_stats=log_stats),
+    # (**kw: packed_outputs=True when gathering: the step kernel writes the all-gather's rows itself)
+    senv = ShardedVectorEnv(lambda num_envs, env_offset, **kw: cls(num_envs, cfg, device=dev, array_backend="torch",
+                                                                   num_envs_total=n_total, env_offset=env_offset,
+                                                                   log_stats=log_stats, **kw),
                             n_total, rank, world, gather=args.gather, time_gather=True)
     env = senv.env
     ring = 17
@@ -192,7 +193,8 @@ def run_image(args, world, rank, dev):
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    # the timed window (`value`): K plain steps, no hipEvents between the launches
+    # the timed window (`value`): K plain steps, no hipEvents between the launches (nor around the all-gathers)
+    senv.time_gather = False
     t0 = time.perf_counter()
     for t in range(args.steps):
         stepper(inputs[(args.warmup + t) % ring])
@@ -201,9 +203,9 @@ def run_image(args, world, rank, dev):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     env.check_errors()
-    gather_ms = senv.gather_ms() or 0.0
-    # the kernel-time pass (roofline, not `value`): K more steps, hipEvents right around the step's kernel launches
-    # (inside env.step) on every event_every-th
+    # the kernel-time pass (roofline and gather_ms, not `value`): K more steps, hipEvents right around the step's
+    # kernel launches (inside env.step) on every event_every-th, and around every all-gather
+    senv.time_gather = True
     timed = [t for t in range(args.steps) if t % args.event_every == args.event_every - 1]  # steps with hipEvents
     for t in range(args.steps):
         if t % args.event_every == args.event_every - 1:
@@ -216,7 +218,7 @@ def run_image(args, world, rank, dev):
     torch.cuda.synchronize(dev)
     env.check_errors()
     step_ms = sum(ev.elapsed_ms(i) for i in timed) / len(timed)
-    senv.gather_ms()
+    gather_ms = senv.gather_ms() or 0.0
     ev.close()
     if world > 1:
         tt = torch.tensor([elapsed, step_ms, reset_ms, gather_ms], dtype=torch.float64,
@@ -255,6 +257,7 @@ def run_image(args, world, rank, dev):
                        "log_stats": log_stats,
                        "reset_ms": reset_ms, "parallelism": f"env-shard x{world}" + (" + all-gather" if senv.gather
                                                                                         else ""),
+                       "packed_rows": bool(senv._packed),
                        "gather_ms": gather_ms if senv.gather else None},
             "roofline": {"bound": bound, "bound_basis": basis, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -447,7 +450,8 @@ def run_lidar(args, world, rank, dev):
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    # the timed window (`value`): K plain steps, no hipEvents between the launches
+    # the timed window (`value`): K plain steps, no hipEvents between the launches (nor around the all-gathers)
+    senv.time_gather = False
     t0 = time.perf_counter()
     first_timed = steps_done + 1
     for t in range(args.steps):
@@ -457,9 +461,10 @@ def run_lidar(args, world, rank, dev):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     env.check_errors()
-    gather_ms = senv.gather_ms() or 0.0
-    # the kernel-time pass (roofline, not `value`): K more steps, hipEvents around the step's launches on every
-    # event_every-th (an event pair adds stream packets and +6..9 us of wall to its step)
+    # the kernel-time pass (roofline and gather_ms, not `value`): K more steps, hipEvents around the step's
+    # launches on every event_every-th (an event pair adds stream packets and +6..9 us of wall to its step) and
+    # around every all-gather
+    senv.time_gather = True
     first_ev = steps_done + 1
     timed = [t for t in range(args.steps) if t % args.event_every == args.event_every - 1]  # steps with hipEvents
     for t in range(args.steps):
@@ -468,7 +473,7 @@ def run_lidar(args, world, rank, dev):
     env.set_kernel_timing_events(None)
     env.check_errors()
     per_step = [ev.elapsed_ms(i) for i in timed]
-    senv.gather_ms()
+    gather_ms = senv.gather_ms() or 0.0
     kernel_ms = sum(per_step) / len(per_step)
     median_ms = statistics.median(per_step)
     # reset steps (1-based step index t with t % 101 == 0: synchronized episodes) in the timed window
@@ -545,6 +550,7 @@ def run_lidar(args, world, rank, dev):
                        "num_envs_total": n_total,
                        "beams": beams, "map": f"{msize}x{msize} {w['kind']}", "max_episode_steps": 100,
                        "reset_ms": reset_ms, "note": w["note"], "gather_ms": gather_ms if senv.gather else None,
+                       "packed_rows": bool(senv._packed),
                        "parallelism": f"env-shard x{world}" + (" + all-gather" if senv.gather else "")},
             "roofline": {"bound": bound, "bound_basis": basis, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -573,6 +579,21 @@ def run_lidar(args, world, rank, dev):
     senv.close()
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+class stdout_to_stderr:
+    """File descriptor 1 pointed at stderr inside the block (native libraries write there directly)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
 
 
 def free_port() -> int:
@@ -744,10 +765,14 @@ def main():
     if world == 1 and args.gather:  # one GPU: a one-rank group still runs the all-gather's collective code path
         os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
     if world > 1 or args.gather:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+        # RCCL prints its version banner on stdout when the communicator comes up (eagerly here: device_id):
+        # keep stdout for the one JSON line
+        with stdout_to_stderr():
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=dev)
+                dist.barrier()
+            else:
+                dist.init_process_group("gloo")
     if args.workload in IMAGE_WORKLOADS:
         return run_image(args, world, rank, dev)
     return run_lidar(args, world, rank, dev)
