@@ -131,8 +131,8 @@ int validate(const apg_lidar_config *c) {
     return fail(APG_E_INVALID, "unknown map kind");
   }
   if (c->beams <= 0 || c->beams > 4096) return fail(APG_E_INVALID, "beams must be in [1, 4096]");
-  if (!(c->lidar_range > 0.0f) || c->lidar_range > 28.0f)
-    return fail(APG_E_INVALID, "lidar_range must be in (0, 28] (32-column scan windows)");
+  if (!(c->lidar_range > 0.0f) || c->lidar_range > 60.0f)
+    return fail(APG_E_INVALID, "lidar_range must be in (0, 60] (64-column scan windows)");
   if (c->step_limit <= 0) return fail(APG_E_INVALID, "step_limit must be positive");
   if (c->log_stats && c->step_limit > PW_DEEP_MAX_N) return fail(APG_E_INVALID, "log_stats needs step_limit <= 15368");
   if (c->out_row_bytes < 0 || (c->out_row_bytes & 7)) return fail(APG_E_INVALID, "out_row_bytes must be a multiple of 8");

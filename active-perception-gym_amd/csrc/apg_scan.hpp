@@ -12,8 +12,9 @@
 // Algorithm: a DDA walk over grid-line crossings in segment order.  The loop body is branch-free
 // except for node bookkeeping: the crossing order comes from the exact orientation predicate
 // (filter, exact fallback only on near-ties), and the closure cells of each crossing are read as
-// a 2x2 bit quad from two 32-column occupancy rows (`rows.row(y)` = cells [x0, x0+32) of map row
-// y, zero outside the map).  GEOS's crossing coordinate is computed only for nodes that start a
+// a 2x2 bit quad from two occupancy row words (`rows.row(y)` = cells [x0, x0 + width) of map row y, zero
+// outside the map; Rows::word = uint32_t for the LDS window of the step kernel, uint64_t for rows read from
+// global memory, so a segment may span width - 3 columns).  GEOS's crossing coordinate is computed only for nodes that start a
 // line piece.
 #pragma once
 #include "apg_device.hpp"
@@ -40,8 +41,8 @@ template <class Rows>
 APG_DEV unsigned quad_status(const Rows &rows, int i0, int di, int j0, int dj) {
   const unsigned m = di ? 3u : 1u;
   const int sh = i0 - rows.x0;
-  const unsigned b0 = (rows.row(j0) >> sh) & m;
-  const unsigned b1 = (rows.row(j0 + dj) >> sh) & m;
+  const unsigned b0 = (unsigned)(rows.row(j0) >> sh) & m;
+  const unsigned b1 = (unsigned)(rows.row(j0 + dj) >> sh) & m;
   return ((b0 | b1) != 0u ? 1u : 0u) | ((b0 == m && b1 == m) ? 2u : 0u);
 }
 
@@ -56,9 +57,10 @@ template <class Rows>
 APG_DEV bool scan_may_hit(const Rows &rows, float fpx, float fpy, float fqx, float fqy, int hmax = 8) {
   const int i0 = (int)ceilf(fminf(fpx, fqx)) - 1, i1 = (int)floorf(fmaxf(fpx, fqx));
   const int j0 = (int)ceilf(fminf(fpy, fqy)) - 1, j1 = (int)floorf(fmaxf(fpy, fqy));
-  const int wdt = i1 - i0 + 1;  // <= lidar range + 2 < 32
-  const uint32_t mask = ((1u << wdt) - 1u) << (i0 - rows.x0);
-  return (rows.or_rows(j0, j1, hmax) & mask) != 0u;
+  using W = typename Rows::word;
+  const int wdt = i1 - i0 + 1;  // <= lidar range + 2 < the word width
+  const W mask = ((W(1) << wdt) - W(1)) << (i0 - rows.x0);
+  return (rows.or_rows(j0, j1, hmax) & mask) != W(0);
 }
 
 APG_DEV ScanOut scan_empty(float fpx, float fpy, float fqx, float fqy) {
@@ -137,10 +139,11 @@ APG_DEV ScanOut scan_runs_result(const Rows &rows, float fpx, float fpy, float f
 // only: SCAN_POINT / SCAN_MULTIPOINT at distance 0 (the first point is p when p is one).  Returns false
 // (the caller runs the general walk) when a crossing turns out to be a lattice point or the segment is
 // collinear with a grid line; the exact orientation decides near-ties as in the general walk.
+template <class W>
 struct FastWalk {
   float px, py, qx, qy, sxy;
   int sx, sy, ux, vy, sd, force, a, b, xoff, left;
-  uint32_t r_c, r_o, r_p;
+  W r_c, r_o, r_p;
   bool cur0, cur, bail;
   int n_runs, n_x, na, nb;
 
@@ -172,7 +175,7 @@ struct FastWalk {
     sd = sy > 0 ? 1 : -1;
     xoff = ux + rows.x0;  // the current column is a - ux: its bit in a window row is a - xoff
     r_c = rows.row(cy), r_o = rows.row(cy + sd), r_p = rows.row(cy + 2 * sd);
-    cur0 = (r_c >> (cx - rows.x0)) & 1u;
+    cur0 = ((unsigned)(r_c >> (cx - rows.x0)) & 1u) != 0u;
     cur = cur0;
     n_runs = cur ? 1 : 0;
     n_x = 0, na = 0, nb = 0;  // the first run's entry crossing: lines (na, nb) ahead of it, x-line or not
@@ -211,7 +214,9 @@ struct FastWalk {
     r_o = takex ? r_o : r_p;
     const int ry = b - vy + 2 * sd;  // unchanged after an x-crossing; consumed a crossing later at the earliest
     r_p = kWrap ? rows.row(ry) : rows.row_nw(ry);
-    const bool in = __builtin_amdgcn_ubfe(r_c, (unsigned)(a - xoff), 1u) != 0u;
+    bool in;
+    if constexpr (sizeof(W) == 4) in = __builtin_amdgcn_ubfe(r_c, (unsigned)(a - xoff), 1u) != 0u;
+    else in = ((unsigned)(r_c >> (a - xoff)) & 1u) != 0u;
     const bool rise = act && in && !cur;
     const bool first = rise && n_runs == 0;
     n_x = first ? (int)takex : n_x;
@@ -230,12 +235,12 @@ struct FastWalk {
 
 template <class Rows>
 APG_DEV bool lidar_scan_fast(const Rows &rows, float fpx, float fpy, float fqx, float fqy, ScanOut &o) {
-  FastWalk w;
+  FastWalk<typename Rows::word> w;
   if (!w.init(rows, fpx, fpy, fqx, fqy)) return false;
   for (int left = w.left; left > 0; left--) {  // single exit: a lattice crossing is checked after the loop
     int c = w.order();
     if (w.undecided(c)) c = w.order_exact();
-    w.step<false>(rows, c, true);
+    w.template step<false>(rows, c, true);
   }
   if (w.bail) return false;
   o = w.result(rows);
@@ -342,7 +347,8 @@ APG_DEV ScanOut lidar_scan_general(const Rows &rows, float fpx, float fpy, float
   // shift when a y-crossing moves the walk to the next row; the row after them is read one crossing
   // ahead, so the loop never waits on a just-issued LDS read.
   const int sd = sy > 0 ? 1 : -1;
-  uint32_t r_c = rows.row(cy), r_o = rows.row(cy + sd), r_p = rows.row(cy + 2 * sd);
+  using W = typename Rows::word;
+  W r_c = rows.row(cy), r_o = rows.row(cy + sd), r_p = rows.row(cy + 2 * sd);
   if (!colv && !colh) {
     // generic segment (not along a grid line): quads are [a-1, a] x cy (x-crossing), cx x [b-1, b]
     // (y-crossing) or the 2 x 2 block at lattice point (a, b); the crossing order is the orientation
@@ -363,9 +369,9 @@ APG_DEV ScanOut lidar_scan_general(const Rows &rows, float fpx, float fpy, float
       const bool takex = c <= 0, takey = c >= 0;
       const int i0 = takex ? a - 1 : cx;
       const int sh = i0 - rows.x0;
-      const uint32_t r0 = (takey && sy < 0) ? r_o : r_c;  // rows.row(j0), j0 = takey ? b - 1 : cy
-      const uint32_t r1 = (takey && sy > 0) ? r_o : r_c;  // rows.row(j0 + dj)
-      const unsigned q0 = (r0 >> sh) & 3u, q1 = (r1 >> sh) & 3u, m = takex ? 3u : 1u;
+      const W r0 = (takey && sy < 0) ? r_o : r_c;  // rows.row(j0), j0 = takey ? b - 1 : cy
+      const W r1 = (takey && sy > 0) ? r_o : r_c;  // rows.row(j0 + dj)
+      const unsigned q0 = (unsigned)(r0 >> sh) & 3u, q1 = (unsigned)(r1 >> sh) & 3u, m = takex ? 3u : 1u;
       const bool onb = ((q0 | q1) & m) != 0u && ((q0 & q1 & m) != m);
       // status of the next open interval: cell (ncx, ncy) at offset (u, v) in the quad
       const unsigned u = takex ? ux : 0u, v = takey ? vy : 0u;
@@ -398,9 +404,9 @@ APG_DEV ScanOut lidar_scan_general(const Rows &rows, float fpx, float fpy, float
       const int j0 = takey ? b - 1 : (colh ? ipy - 1 : cy);
       const bool di = takex || colv;
       const int sh = i0 - rows.x0;
-      const uint32_t r0 = takey ? (sy > 0 ? r_c : r_o) : (colh ? r_o : r_c);  // rows.row(j0)
-      const uint32_t r1 = (takey && sy > 0) ? r_o : r_c;                      // rows.row(j0 + dj)
-      const unsigned q0 = (r0 >> sh) & 3u, q1 = (r1 >> sh) & 3u, m = di ? 3u : 1u;
+      const W r0 = takey ? (sy > 0 ? r_c : r_o) : (colh ? r_o : r_c);  // rows.row(j0)
+      const W r1 = (takey && sy > 0) ? r_o : r_c;                      // rows.row(j0 + dj)
+      const unsigned q0 = (unsigned)(r0 >> sh) & 3u, q1 = (unsigned)(r1 >> sh) & 3u, m = di ? 3u : 1u;
       const bool onb = ((q0 | q1) & m) != 0u && ((q0 & q1 & m) != m);
       const int ncx = cx + (takex ? sx : 0), ncy = cy + (takey ? sy : 0);
       // status of the next open interval from the same quad: cell (ncx, ncy) (+ its collinear twin)
@@ -530,6 +536,7 @@ APG_DEV uint32_t extract_window_row(const uint64_t *row, int wpr, int x0) {
 }
 
 struct RowsWindow {  // 32-row x 32-column window staged in LDS (rows [y0, y0+32)); callers keep
+  typedef uint32_t word;
   const uint32_t *win;  // every access inside the window (see k_lidar_step), so no bounds test
   int x0, y0, nrows;
   APG_DEV uint32_t row(int y) const { return win[(unsigned)(y - y0) & 31u]; }
@@ -552,16 +559,24 @@ struct RowsWindow {  // 32-row x 32-column window staged in LDS (rows [y0, y0+32
   }
 };
 
-struct RowsGlobal {  // bit rows in global memory, read through a 32-column window at x0
+// bits [x0, x0+64) of a bit row (zero outside [0, 64*wpr))
+APG_DEV uint64_t extract_window_row64(const uint64_t *row, int wpr, int x0) {
+  const int q = x0 >> 6, o = x0 & 63;  // floor division: x0 may be negative
+  const uint64_t lo = (q >= 0 && q < wpr) ? row[q] : 0ULL, hi = (q + 1 >= 0 && q + 1 < wpr) ? row[q + 1] : 0ULL;
+  return (lo >> o) | ((hi << 1) << (63 - o));
+}
+
+struct RowsGlobal {  // bit rows in global memory, read through a 64-column window at x0 (segments up to 61 long)
+  typedef uint64_t word;
   const uint64_t *occ;
   int h, wpr, x0;
-  APG_DEV uint32_t row(int y) const {
-    if ((unsigned)y >= (unsigned)h) return 0u;
-    return extract_window_row(occ + (size_t)y * wpr, wpr, x0);
+  APG_DEV uint64_t row(int y) const {
+    if ((unsigned)y >= (unsigned)h) return 0ULL;
+    return extract_window_row64(occ + (size_t)y * wpr, wpr, x0);
   }
-  APG_DEV uint32_t row_nw(int y) const { return row(y); }
-  APG_DEV uint32_t or_rows(int j0, int j1, int) const {
-    uint32_t acc = 0u;
+  APG_DEV uint64_t row_nw(int y) const { return row(y); }
+  APG_DEV uint64_t or_rows(int j0, int j1, int) const {
+    uint64_t acc = 0ULL;
     for (int j = j0; j <= j1; j++) acc |= row(j);
     return acc;
   }

@@ -359,10 +359,13 @@ def test_vector_env_matches_oracle(gpu, oracle_mod, kind, size, beams, n, steps,
 @pytest.mark.parametrize("kind,size,static,beams,lidar_range,n", [("rooms", 64, False, 16, 12.0, 512),
                                                                    ("maze", 63, False, 32, 20.0, 256),
                                                                    ("rooms", 32, True, 8, 10.5, 256),
-                                                                   ("rooms", 64, False, 8, 28.0, 128)])
+                                                                   ("rooms", 64, False, 8, 28.0, 128),
+                                                                   ("rooms", 64, False, 8, 40.0, 128),
+                                                                   ("maze", 63, False, 16, 60.0, 128),
+                                                                   ("rooms", 128, False, 16, 45.5, 128)])
 def test_long_range_matches_oracle(gpu, oracle_mod, kind, size, static, beams, lidar_range, n):
-    """lidar_range > 10 (the step kernel's rows-from-global-memory instance): observations, rewards and
-    terminations of 110 steps (one autoreset) against the oracle env."""
+    """lidar_range > 10 (the step kernel's rows-from-global-memory instance, 64-column row windows: ranges up to
+    60): observations, rewards and terminations of 110 steps (one autoreset) against the oracle env."""
     import ap_gym_amd as ap
 
     env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_ds(ap, kind, size), lidar_beam_count=beams,

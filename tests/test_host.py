@@ -47,15 +47,15 @@ def test_capi_validation_without_gpu():
     cfg.height = cfg.width = 128  # even maze sizes are rejected like FloorMapDatasetMaze
     assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == -1
     assert b"odd" in N.lib().apg_last_error()
-    # the envelope: mazes up to 255 x 255, lidar_range up to 28
+    # the envelope: mazes up to 255 x 255, lidar_range up to 60
     cfg.height, cfg.width = 255, 101
     assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0 and sz.wpr == 2
     cfg.height = cfg.width = 257
     assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == -1
     cfg.height = cfg.width = 127
-    cfg.lidar_range = 28.0
+    cfg.lidar_range = 60.0
     assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0
-    cfg.lidar_range = 28.5
+    cfg.lidar_range = 60.5
     assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == -1
     cfg.lidar_range = 5.0
     # packed output rows must hold every enabled field (the Python row layout's size is the minimum)
