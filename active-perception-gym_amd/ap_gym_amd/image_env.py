@@ -89,8 +89,9 @@ def image_output_row_layout(kind: int, sensor: tuple, channels: int, log_stats: 
     f64, f32, i32 = torch.float64, torch.float32, torch.int32
     g = (int(sensor[0]), int(sensor[1]), int(channels))
     cls = kind == N.APG_IMAGE_CLASSIFY
-    fields = [("reward", f64, ())] + ([("loss_f64", f64, ())] if cls else []) + [("glimpse", f32, g)] + (
-        [] if cls else [("target_glimpse", f32, g)]) + [
+    # (the localization target glimpse is not in the row: it changes only with the batch, so a sharded run
+    # gathers it on reset / autoreset steps only)
+    fields = [("reward", f64, ())] + ([("loss_f64", f64, ())] if cls else []) + [("glimpse", f32, g)] + [
         ("glimpse_pos", f32, (2,)), ("time_step", f32, ()), ("base_reward", f32, ())] + (
         [("label_target", i32, ())] if cls else [("target_out", f32, (2,)), ("loss_f32", f32, ())]) + (
         [("stats", f32, (4,))] if log_stats else []) + ([("stats_idx", i32, (2,))] if log_stats and cls else [])

@@ -18,9 +18,9 @@ gloo on CPU — for consumers that need the full batch (the north star's obs/rew
          fields are strided views of the receive buffer: no packing or unpacking copies.  The per-reset map
          observation (4*H*W bytes per env) and the per-step stats history stay sharded: they are returned
          as info["local_obs"] / the local env's buffers.
-  image  likewise packed_outputs=True: the fused step kernel writes reward, loss, glimpse (+ target glimpse), glimpse
-         position, time step, base reward, target and the episode statistics into the row
-         (image_env.image_output_row_layout); info["index"] changes only with the batch, so it is gathered on
+  image  likewise packed_outputs=True: the fused step kernel writes reward, loss, glimpse, glimpse position, time step,
+         base reward, target and the episode statistics into the row (image_env.image_output_row_layout);
+         info["index"] and the localization target glimpse change only with the batch, so they are gathered on
          reset and autoreset steps only, and terminated / truncated are the same for the whole batch (episodes
          end together), so they are not gathered at all
 (image_classification.py:117-151 and image_localization.py:131-181 are the outputs gathered).
@@ -109,6 +109,7 @@ class ShardedVectorEnv:
         self._views = None
         self._index_full = None  # image envs: the gathered info["index"] (changes only with the batch)
         self._done_full = None  # image envs: gathered terminated / truncated / sparse weight constants
+        self._tg_full = None  # image localization: the gathered target glimpses (change only with the batch)
         self.time_gather = time_gather
         self.gather_events: list = []  # (begin, end) torch.cuda.Event pairs around each all-gather
 
@@ -170,6 +171,16 @@ class ShardedVectorEnv:
                                            device=local_index.device)
         return self._all_gather_into(self._index_full, local_index.contiguous())
 
+    def _gathered_target_glimpse(self, local):
+        """Image localization: the target glimpses of the whole batch, gathered when the batch changes (reset,
+        autoreset); not part of the packed rows."""
+        import torch
+
+        if self._tg_full is None:
+            self._tg_full = torch.zeros((self.world * self.local_num_envs, *local.shape[1:]), dtype=local.dtype,
+                                        device=local.device)
+        return self._all_gather_into(self._tg_full, local.contiguous())
+
     def _pack(self, fields: dict):
         import torch
 
@@ -224,6 +235,8 @@ class ShardedVectorEnv:
         v = self._gathered_rows()
         if not self._lidar:
             gobs = self._image_obs(v)
+            if "target_glimpse" in obs:
+                gobs["target_glimpse"] = self._c(self._gathered_target_glimpse(obs["target_glimpse"]))
             if "inverted_label" in obs:
                 gobs["inverted_label"] = obs["inverted_label"]  # (local: drawn per shard like the index)
             return gobs, {"index": self._c(self._gathered_index(info["index"])), "local_obs": obs,
@@ -292,6 +305,10 @@ class ShardedVectorEnv:
             ginfo["stats"] = {"scalar": scalar, "_scalar": done, "vector": info["stats"]["vector"],
                               "_vector": info["stats"]["_vector"]}
         gobs = self._image_obs(v)
+        if "target_glimpse" in obs:  # gathered when the batch changed (this step's autoreset), else the last one
+            if resetting or self._tg_full is None:
+                self._gathered_target_glimpse(obs["target_glimpse"])
+            gobs["target_glimpse"] = self._c(self._tg_full)
         if "inverted_label" in obs:
             gobs["inverted_label"] = obs["inverted_label"]
         return gobs, v["reward"], g_term, g_trunc, ginfo

@@ -1449,13 +1449,13 @@ __global__ void k_loss_mse(const float *pred, const float *target, int n, int d,
 int grid_for(int64_t n, int threads) { return (int)((n + threads - 1) / threads); }
 
 // Bytes of a packed output row (apg_image_config.out_row_bytes): reward (f64), the glimpse, glimpse_pos, time_step,
-// base_reward; classification: loss_f64, label_target; localization: target_glimpse, target, loss_f32; stats (4 f32)
+// base_reward; classification: loss_f64, label_target; localization: target, loss_f32; stats (4 f32)
 // with log_stats, stats_idx (2 i32) for classification
 int image_min_row_bytes(const apg_image_config *c) {
   const int64_t glimpse = 4LL * c->sensor_h * c->sensor_w * c->channels;
   int64_t b = 8 + glimpse + 8 + 4 + 4;
   if (c->kind == APG_IMAGE_CLASSIFY) b += 8 + 4 + (c->log_stats ? 8 : 0);
-  else b += glimpse + 8 + 4;
+  else b += 8 + 4;  // (the target glimpse stays dense)
   if (c->log_stats) b += 16;
   b = (b + 7) & ~7LL;
   return b > 0x7fffffff ? 0x7fffffff : (int)b;
@@ -1724,7 +1724,9 @@ static int observe(const apg_image_config *c, const apg_image_state *st, const a
   const GlimpseGeo g = env_geo(c);
   int rc = launch_glimpse<double>(g, st->pool, st->index, st->pos, c->num_envs, 1, out->glimpse, out->err, s);
   if (rc || c->kind != APG_IMAGE_LOCALIZE || !target_changed) return rc;
-  return launch_glimpse<float>(g, st->pool, st->index, st->target, c->num_envs, 1, out->target_glimpse, out->err, s);
+  // the target glimpse is never part of a packed row (dense pitch)
+  return launch_glimpse<float>(make_geo(c), st->pool, st->index, st->target, c->num_envs, 1, out->target_glimpse,
+                               out->err, s);
 }
 
 int apg_image_reset(const apg_image_config *c, const apg_image_state *st, const apg_image_outputs *out,
@@ -1871,7 +1873,7 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
     if ((rc = check_launch("k_image_step_fused"))) return rc;
     // the target glimpse only changes with the target and the images, i.e. on the autoreset step
     if (!prev_done || c->kind != APG_IMAGE_LOCALIZE) return APG_OK;
-    return launch_glimpse<float>(g, st->pool, st->index, st->target, n, 1, out->target_glimpse, out->err, s);
+    return launch_glimpse<float>(make_geo(c), st->pool, st->index, st->target, n, 1, out->target_glimpse, out->err, s);
   }
   if (c->kind == APG_IMAGE_CLASSIFY && c->num_classes <= CLS1_MAX_K && !lanes8) {
     const size_t lds = (size_t)CLS1_ENVS * (c->num_classes + 2) * sizeof(float);

@@ -296,11 +296,12 @@ typedef struct apg_image_config {
   int32_t sparse;             /* 1: the -sparse ids (SparsifyVectorWrapper, sparsify_wrapper.py:23-92):
                                  reward = base_reward - loss * terminated */
   int32_t out_row_bytes;      /* 0: dense outputs.  > 0 (a multiple of 8): packed rows — the per-env outputs glimpse,
-                                 glimpse_pos, time_step, target_glimpse, reward, base_reward, target, label_target,
-                                 loss_f64, loss_f32, stats (as [N][4]) and stats_idx (as [N][2]) of env e are at their
+                                 glimpse_pos, time_step, reward, base_reward, target, label_target, loss_f64,
+                                 loss_f32, stats (as [N][4]) and stats_idx (as [N][2]) of env e are at their
                                  pointer + e * out_row_bytes, i.e. the pointers are field offsets into one
                                  [N][out_row_bytes] buffer that a sharded run all-gathers as is (ABI 0.2; the row
-                                 must hold the enabled fields: apg_image_* reject a smaller one) */
+                                 must hold the enabled fields: apg_image_* reject a smaller one).  target_glimpse
+                                 stays dense [N][G0][G1][C] either way: it changes only with the batch */
 } apg_image_config;
 
 typedef struct apg_image_state {

@@ -207,7 +207,8 @@ class _ImageOracleShard:
         obs = self._obs(o)
         if self.output_rows is not None:
             for k in obs:
-                self.v[k].copy_(obs[k])
+                if k in self.v:  # (the target glimpse is not in the row)
+                    self.v[k].copy_(obs[k])
         return obs, {"index": self._sl(info["index"])}
 
     def step(self, action):
@@ -229,7 +230,8 @@ class _ImageOracleShard:
         if self.output_rows is not None:
             v = self.v
             for k in obs:
-                v[k].copy_(obs[k])
+                if k in v:  # (the target glimpse is not in the row)
+                    v[k].copy_(obs[k])
             v["reward"].copy_(self._sl(np.asarray(r, np.float64)))
             v["base_reward"].copy_(ti["base_reward"])
             if self.kname == "cls":
