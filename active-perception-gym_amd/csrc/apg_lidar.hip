@@ -117,16 +117,16 @@ int min_row_bytes(const apg_lidar_config *c) {
 int validate(const apg_lidar_config *c) {
   if (!c) return fail(APG_E_INVALID, "null config");
   if (c->num_envs <= 0) return fail(APG_E_INVALID, "num_envs must be positive");
-  if (c->height < 3 || c->width < 3 || c->height > 255 || c->width > 255)
-    return fail(APG_E_INVALID, "map size must be within [3, 255]");
+  if (c->height < 3 || c->width < 3) return fail(APG_E_INVALID, "map size must be at least 3");
   if (c->map_kind == APG_MAP_ROOMS) {
+    if (c->height > 511 || c->width > 511) return fail(APG_E_INVALID, "rooms maps must be at most 511 x 511");
     if (c->height != c->width) return fail(APG_E_INVALID, "rooms maps must be square");
-    if (c->max_rooms < 1 || c->max_rooms > ROOMS_MAX) return fail(APG_E_INVALID, "max_rooms must be in [1, 32]");
+    if (c->max_rooms < 1 || c->max_rooms > ROOMS_MAX) return fail(APG_E_INVALID, "max_rooms must be in [1, 64]");
     if (c->door_width < 1) return fail(APG_E_INVALID, "door_width must be positive");
   } else if (c->map_kind == APG_MAP_MAZE) {
     if ((c->height % 2) == 0 || (c->width % 2) == 0)
       return fail(APG_E_INVALID, "Width and height must be odd.");
-    if (c->height > 255 || c->width > 255) return fail(APG_E_INVALID, "maze maps must be at most 255 x 255");
+    if (c->height > 511 || c->width > 511) return fail(APG_E_INVALID, "maze maps must be at most 511 x 511");
   } else {
     return fail(APG_E_INVALID, "unknown map kind");
   }
@@ -482,6 +482,71 @@ __global__ __launch_bounds__(64) void k_maze(Geo g, apg_lidar_state S, const uin
   if (active) *reinterpret_cast<int *>(mine_scr + maze_stream_off(g.h, g.w) + maze_stream_state_off(ng) + 16) = nlog;
 }
 
+// Mazes past the LDS layout of k_maze (maze_big: maps wider or taller than 255, up to 511): the reference's carve()
+// recursion (floor_map_dataset_maze.py:24-55) one thread per maze, as an explicit frame stack in the maze scratch
+// (frame: cell x | y << 9 | permutation index << 18 | next position << 23 | first << 26), the visited bits beside
+// it, the draws straight from default_rng(idx): rng.permutation(directions) as numpy's shuffle (random_interval 3,
+// 2, 1 on next_uint32) on entering a cell, rng.random() for a non-first eligible branch.  The occupancy rows are
+// carved in place (all walls first); k_maze_paint (prepainted) then writes the map obs and the start cell.  Slow
+// (global memory, one lane per maze) but exact: these sizes are off the benched configurations.
+__global__ __launch_bounds__(64) void k_maze_big(Geo g, apg_lidar_state S, const uint64_t *idx, int n, uint64_t *occ,
+                                                 uint8_t *scratch, int mode, uint64_t seed, int use_seed, int all) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  if (mode == MZ_RESET && !all && !(S.flags[i] & F_AUTORESET)) return;
+  Pcg64 rng, it;
+  Pcg64 r = seed_pcg64(maze_index(S, idx, i, mode, seed, use_seed, rng, it));
+  const MazeGeom m = maze_geom(g.h, g.w);
+  const int words = g.h * g.wpr;
+  uint64_t *rows = (mode == MZ_RESET ? S.occ : occ) + (size_t)i * words;
+  uint8_t *scr = scratch + (size_t)i * maze_scratch_bytes(g.h, g.w);
+  uint64_t *vis = reinterpret_cast<uint64_t *>(scr);
+  uint32_t *stk = reinterpret_cast<uint32_t *>(scr + maze_big_vis_bytes(g.h, g.w));
+  for (int q = 0; q < words; q++) {  // all walls
+    const int lo = 64 * (q % g.wpr);
+    rows[q] = g.w - lo >= 64 ? ~0ULL : ((1ULL << (g.w - lo)) - 1ULL);
+  }
+  for (int q = 0; q < m.ncy * m.cw; q++) vis[q] = 0ULL;
+  auto open_cell = [&](int x, int y) { rows[y * g.wpr + (x >> 6)] &= ~(1ULL << (x & 63)); };
+  auto visited = [&](int cx, int cy) { return (vis[cy * m.cw + (cx >> 6)] >> (cx & 63)) & 1ULL; };
+  auto visit = [&](int cx, int cy) { vis[cy * m.cw + (cx >> 6)] |= 1ULL << (cx & 63); };
+  auto draw_perm = [&]() {  // numpy shuffle of the 4 directions: swap(3, j3), swap(2, j2), swap(1, j1)
+    const uint32_t j3 = random_interval_small(r, 3u), j2 = random_interval_small(r, 2u), j1 = random_interval_small(r, 1u);
+    return j3 * 6u + j2 * 2u + j1;
+  };
+  auto pack = [](uint32_t cx, uint32_t cy, uint32_t p, uint32_t k, uint32_t first) {
+    return cx | (cy << 9) | (p << 18) | (k << 23) | (first << 26);
+  };
+  open_cell(1, 1);  // maze[1, 1] = 0 (maze.py:51)
+  visit(0, 0);
+  stk[0] = pack(0u, 0u, draw_perm(), 0u, 1u);
+  int sp = 1;
+  while (sp > 0) {
+    const uint32_t f = stk[sp - 1];
+    const int cx = (int)(f & 511u), cy = (int)((f >> 9) & 511u);
+    const uint32_t p = (f >> 18) & 31u, k = (f >> 23) & 7u;
+    uint32_t first = (f >> 26) & 1u;
+    if (k >= 4u) {  // every direction tried: return to the parent
+      sp--;
+      continue;
+    }
+    const uint32_t d = (mz_perm_of(p) >> (2u * k)) & 3u;
+    const int dx = (d == 0u) - (d == 1u), dy = (d == 2u) - (d == 3u);
+    const int nx = cx + dx, ny = cy + dy;
+    bool carve = false;
+    if (nx >= 0 && nx < m.ncx && ny >= 0 && ny < m.ncy && !visited(nx, ny))  // 0 < next < dims - 1, maze[next] == 1
+      carve = first || next_double(r) < g.bp;  // maze.py:42
+    if (carve) first = 0u;
+    stk[sp - 1] = pack((uint32_t)cx, (uint32_t)cy, p, k + 1u, first);
+    if (carve) {
+      open_cell(2 * cx + 1 + dx, 2 * cy + 1 + dy);  // the passage, then the cell
+      open_cell(2 * nx + 1, 2 * ny + 1);
+      visit(nx, ny);
+      stk[sp++] = pack((uint32_t)nx, (uint32_t)ny, draw_perm(), 0u, 1u);  // carve(next_pos)
+    }
+  }
+}
+
 // After k_maze's DFS, at full occupancy: a workgroup per MP_ENVS consecutive envs lists the mazes k_maze
 // generated and, one maze at a time with all its threads, paints the occupancy rows from the carve log
 // (maze_paint), writes them out (occ, or S.occ), and for MZ_RESET writes the map obs (bool map / 255,
@@ -492,7 +557,7 @@ __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_stat
                                                            uint64_t *occ, const uint8_t *scratch, int mode,
                                                            uint64_t seed, int use_seed, int all, int ng,
                                                            uint64_t *out_map_idx, float *map_obs, uint32_t *err,
-                                                           PfView pv) {
+                                                           PfView pv, int prepainted) {
   __shared__ uint16_t s_list[MP_ENVS];
   __shared__ int s_cnt, s_wsum[MP_THREADS / 64], s_hit[2];
   extern __shared__ uint64_t s_bm[];  // one maze's rows, then bitmap_map_obs's linear bitmap
@@ -508,22 +573,31 @@ __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_stat
   for (int k = 0; k < cnt; k++) {
     const int e = e0 + s_list[k];
     const uint8_t *scr = scratch + (size_t)e * sb;
-    const int nlog = *reinterpret_cast<const int *>(scr + maze_stream_off(g.h, g.w) + maze_stream_state_off(ng) + 16);
-    maze_paint<MP_THREADS>(m, g.wpr, reinterpret_cast<const uint32_t *>(scr), nlog, s_bm, tid);
     uint64_t *dst = (mode == MZ_RESET ? S.occ : occ) + (size_t)e * words;
-    for (int q = tid; q < (int)words; q += MP_THREADS) dst[q] = s_bm[q];
+    if (prepainted) {  // k_maze_big wrote the rows: into the LDS bitmap
+      for (int q = tid; q < (int)words; q += MP_THREADS) s_bm[q] = dst[q];
+      __syncthreads();
+    } else {
+      const int nlog = *reinterpret_cast<const int *>(scr + maze_stream_off(g.h, g.w) + maze_stream_state_off(ng) + 16);
+      maze_paint<MP_THREADS>(m, g.wpr, reinterpret_cast<const uint32_t *>(scr), nlog, s_bm, tid);
+      for (int q = tid; q < (int)words; q += MP_THREADS) dst[q] = s_bm[q];
+    }
     if (mode != MZ_RESET) {
       __syncthreads();  // the bitmap is read before the next maze paints it
       continue;
     }
     if (map_obs) bitmap_map_obs<MP_THREADS>(s_bm, g.h, g.w, g.wpr, map_obs + (size_t)e * g.h * g.w, tid, s_bm + words);
-    // free cells per row, their inclusive scan (rows <= MP_THREADS = 256: one per thread), the row holding the pick
-    int fr = 0;
-    if (tid < g.h) {
+    // free cells per row, their inclusive scan (rpt consecutive rows per thread: maps up to 2 * MP_THREADS rows),
+    // the row holding the pick
+    const int rpt = (g.h + MP_THREADS - 1) / MP_THREADS;
+    auto row_free = [&](int y) {
       int oc = 0;
-      for (int kk = 0; kk < g.wpr; kk++) oc += __popcll(s_bm[tid * g.wpr + kk]);
-      fr = g.w - oc;
-    }
+      for (int kk = 0; kk < g.wpr; kk++) oc += __popcll(s_bm[y * g.wpr + kk]);
+      return g.w - oc;
+    };
+    int fr = 0;
+    for (int rr = 0; rr < rpt; rr++)
+      if (tid * rpt + rr < g.h) fr += row_free(tid * rpt + rr);
     const int incl_w = wave_inclusive_scan(fr, lane);
     if (lane == 63) s_wsum[wave] = incl_w;
     if (tid == 0) s_hit[0] = -1;
@@ -538,18 +612,26 @@ __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_stat
     Pcg64 rng, it;
     const uint64_t midx = maze_index(S, idx, e, mode, seed, use_seed, rng, it);
     const long long pick = nfree > 0 ? (long long)integers(rng, 0, nfree) : -1;  // every thread: same draw
-    if (tid < g.h && pick >= excl && pick < incl) {
-      int k2 = (int)(pick - excl), hx = -1;
+    if (tid * rpt < g.h && pick >= excl && pick < incl) {
+      int k2 = (int)(pick - excl), hx = -1, hy = tid * rpt;
+      for (int rr = 0; rr < rpt; rr++) {  // the row of this thread's rows that holds the pick
+        const int y = tid * rpt + rr, c = y < g.h ? row_free(y) : 0;
+        if (k2 < c) {
+          hy = y;
+          break;
+        }
+        k2 -= c;
+      }
       for (int kk = 0; kk < g.wpr && hx < 0; kk++) {
         const int lo = 64 * kk;
         const uint64_t valid = g.w - lo >= 64 ? ~0ULL : ((1ULL << (g.w - lo)) - 1ULL);
-        const uint64_t fm = ~s_bm[tid * g.wpr + kk] & valid;
+        const uint64_t fm = ~s_bm[hy * g.wpr + kk] & valid;
         const int c = __popcll(fm);
         if (k2 < c) hx = lo + select_bit(fm, k2);
         else k2 -= c;
       }
       s_hit[0] = hx;
-      s_hit[1] = tid;
+      s_hit[1] = hy;
     }
     __syncthreads();
     if (tid == 0) {
@@ -795,22 +877,20 @@ constexpr int PF_WAVE_WORDS = MAX_MAP_ROWS * 2 + (MAX_MAP_ROWS * 128 + 63) / 64 
 
 // Row y of a rooms map painted from its primitives (rooms_paint's result, one row at a time): border
 // | walls & ~doors.  Word k covers columns [64k, 64k + 64); the primitives are pr[i * st].
-APG_DEV uint64_t rooms_row_word(const uint32_t *pr, int st, int m, int y, int k) {
+APG_DEV uint64_t rooms_row_word(const uint32_t *pr, int st, int m, int dw, int y, int k) {
   const int nw = (int)(pr[0] & 255u), nd = (int)(pr[0] >> 8);
   uint64_t v = (y == 0 || y == m - 1) ? span_mask(0, m, k) : (span_mask(0, 1, k) | span_mask(m - 1, 1, k));
   for (int i = 0; i < nw; i++) {
-    const uint32_t wl = pr[(1 + i) * st];
-    const int fixed = (int)((wl >> 16) & 255u), s0 = (int)((wl >> 8) & 255u), len = (int)(wl & 255u);
-    if (wl >> 31) {
-      if (y >= s0 && y < s0 + len && (fixed >> 6) == k) v |= 1ULL << (fixed & 63);
-    } else if (fixed == y) {
-      v |= span_mask(s0, len, k);
+    const Wall wl = wall_of(pr[(1 + i) * st]);
+    if (wl.vertical) {
+      if (y >= wl.start && y < wl.start + wl.len && (wl.fixed >> 6) == k) v |= 1ULL << (wl.fixed & 63);
+    } else if (wl.fixed == y) {
+      v |= span_mask(wl.start, wl.len, k);
     }
   }
   for (int i = 0; i < nd; i++) {
-    const uint32_t d = pr[(17 + i) * st];
-    const int r0 = (int)(d >> 24), c0 = (int)((d >> 16) & 255u), hh = (int)((d >> 8) & 255u), ww = (int)(d & 255u);
-    if (y >= r0 && y < r0 + hh) v &= ~span_mask(c0, ww, k);
+    const Door d = door_of(pr[(17 + i) * st], dw);
+    if (y >= d.r0 && y < d.r0 + d.hh) v &= ~span_mask(d.c0, d.ww, k);
   }
   return v;
 }
@@ -1069,7 +1149,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
             if (y < m) {
               int occ = 0;
               for (int k = 0; k < wpr; k++) {
-                const uint64_t v = rooms_row_word(pr, EPB, m, y, k);
+                const uint64_t v = rooms_row_word(pr, EPB, m, g.door_width, y, k);
                 rw[rr][k] = v;
                 dst[y * wpr + k] = v;
                 mrow[y * 2 + k] = v;
@@ -1741,7 +1821,16 @@ int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, in
                 hipStream_t s, const PfView *pv = nullptr) {
   if (!scratch) return fail(APG_E_INVALID, "maze maps need the maze scratch buffer (stack)");
   const MazeGeom m = maze_geom(g.h, g.w);
-  if (m.ncx > 127 || m.ncy > 127) return fail(APG_E_INVALID, "maze maps must be at most 255 x 255");
+  const size_t paint_lds = ((size_t)g.h * g.wpr + bitmap_lin_words(g.h, g.w)) * sizeof(uint64_t);
+  if (maze_big(g.h, g.w)) {  // maps past 255: one thread per maze, then the prepainted finish
+    hipLaunchKernelGGL(k_maze_big, dim3(grid_for(n, 64)), dim3(64), 0, s, g, st, idx, n, occ, scratch, mode, seed,
+                       use_seed, all);
+    if (int rc = check_launch("k_maze_big")) return rc;
+    if (mode != MZ_RESET) return APG_OK;
+    hipLaunchKernelGGL(k_maze_paint, dim3(grid_for(n, MP_ENVS)), dim3(MP_THREADS), paint_lds, s, g, st, idx, n, occ,
+                       scratch, mode, seed, use_seed, all, 0, out_map_idx, map_obs, err, pv ? *pv : PfView{}, 1);
+    return check_launch("k_maze_paint");
+  }
   const int lanes = maze_lanes(n);
   const size_t dyn = maze_wg_lds_bytes(g.h, g.w);  // laid out for 64 lanes whatever `lanes` is
   const bool onew = m.ncx <= 63;
@@ -1759,10 +1848,8 @@ int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, in
     hipLaunchKernelGGL(k_maze<false>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, st, idx, n, scratch, mode, seed,
                        use_seed, all, err, lanes, ng);
   if (int rc = check_launch("k_maze")) return rc;
-  hipLaunchKernelGGL(k_maze_paint, dim3(grid_for(n, MP_ENVS)), dim3(MP_THREADS),
-                     ((size_t)g.h * g.wpr + bitmap_lin_words(g.h, g.w)) * sizeof(uint64_t),
-                     s, g, st, idx, n, occ, scratch, mode, seed, use_seed, all, ng, out_map_idx, map_obs, err,
-                     pv ? *pv : PfView{});
+  hipLaunchKernelGGL(k_maze_paint, dim3(grid_for(n, MP_ENVS)), dim3(MP_THREADS), paint_lds, s, g, st, idx, n, occ,
+                     scratch, mode, seed, use_seed, all, ng, out_map_idx, map_obs, err, pv ? *pv : PfView{}, 0);
   return check_launch("k_maze_paint");
 }
 

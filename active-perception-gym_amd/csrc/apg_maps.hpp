@@ -8,7 +8,7 @@
 
 namespace apg {
 
-constexpr int ROOMS_MAX = 32;  // max_rooms of the generator (binomial draws of n = mrl - 2 < ROOMS_MAX)
+constexpr int ROOMS_MAX = 64;  // max_rooms of the generator (binomial draws of n = mrl - 2 < ROOMS_MAX)
 struct BinomTable {  // random_binomial_inversion constants for n = 0..ROOMS_MAX-1 at p = 0.3 (host libm)
   double qn[ROOMS_MAX];
   int32_t bound[ROOMS_MAX];
@@ -115,10 +115,35 @@ struct Bits {  // bit-packed rows in global memory
 
 // Rooms: a view task is numpy's room[...] slice: element (i, j) is map cell
 //   t == 0: (y0 + i, x0 + j)      t == 1: (y0 + j, x0 + i)
-// packed as y0 | x0 << 8 | t << 16 | n0 << 17 | n1 << 25 | max_rooms << 33
+// packed as y0 | x0 << 9 | t << 18 | n0 << 19 | n1 << 28 | max_rooms << 37 (maps up to 511)
 APG_DEV uint64_t pack_task(int y0, int x0, int t, int n0, int n1, int mr) {
-  return (uint64_t)y0 | ((uint64_t)x0 << 8) | ((uint64_t)t << 16) | ((uint64_t)n0 << 17) |
-         ((uint64_t)n1 << 25) | ((uint64_t)mr << 33);
+  return (uint64_t)y0 | ((uint64_t)x0 << 9) | ((uint64_t)t << 18) | ((uint64_t)n0 << 19) |
+         ((uint64_t)n1 << 28) | ((uint64_t)mr << 37);
+}
+
+// Primitives (9-bit coordinates: maps up to 511).  wall: vertical << 31 | fixed << 18 | start << 9 | len, the cells
+// (fixed, start .. start + len) of a row (vertical = 0) or column; door: r0 << 23 | c0 << 14 | vertical << 13, the
+// block of rows [r0, r0 + hh) and columns [c0, c0 + ww) with (hh, ww) = (2 dw - 1, dw) across a row wall and
+// (dw, 2 dw - 1) across a column wall (dw = door_width).  The transpose flips `vertical` (and swaps r0, c0).
+APG_DEV uint32_t wall_prim(uint32_t vertical, int fixed, int start, int len) {
+  return (vertical << 31) | ((uint32_t)fixed << 18) | ((uint32_t)start << 9) | (uint32_t)len;
+}
+struct Wall {
+  bool vertical;
+  int fixed, start, len;
+};
+APG_DEV Wall wall_of(uint32_t wl) {
+  return {(wl >> 31) != 0u, (int)((wl >> 18) & 511u), (int)((wl >> 9) & 511u), (int)(wl & 511u)};
+}
+APG_DEV uint32_t door_prim(uint32_t vertical, int r0, int c0) {
+  return ((uint32_t)r0 << 23) | ((uint32_t)c0 << 14) | (vertical << 13);
+}
+struct Door {
+  int r0, c0, hh, ww;
+};
+APG_DEV Door door_of(uint32_t d, int dw) {
+  const bool v = (d >> 13) & 1u;
+  return {(int)(d >> 23), (int)((d >> 14) & 511u), v ? dw : 2 * dw - 1, v ? 2 * dw - 1 : dw};
 }
 
 // The reference paints walls (`room[wp] = where(room[wp] != -1, 1, -1)`) and doors (`= -1`) into an
@@ -126,7 +151,7 @@ APG_DEV uint64_t pack_task(int y0, int x0, int t, int n0, int n1, int mr) {
 // covered by some wall segment, and covered by no door block: paint order never matters.  So the
 // generator only records the segments and blocks (in map coordinates, W.P) and paints rows at the
 // end, with the final 50% transpose applied to the primitives instead of the bitmap.
-//   wall: vertical << 31 | fixed << 16 | start << 8 | len (len <= 255); door: r0 << 24 | c0 << 16 | h << 8 | w
+//   (wall_prim / door_prim above)
 APG_DEV int rooms_primitives(Pcg64 &r, int m, int max_rooms, int door_width, const BinomTable &bt,
                              const RoomsWork &W) {
   const int min_size = door_width + 2;
@@ -136,8 +161,8 @@ APG_DEV int rooms_primitives(Pcg64 &r, int m, int max_rooms, int door_width, con
   W.S(sp++) = pack_task(1, 1, 0, m - 2, m - 2, max_rooms);
   while (sp > 0) {
     const uint64_t tk = W.S(--sp);
-    const int y0 = (int)(tk & 255), x0 = (int)((tk >> 8) & 255), t = (int)((tk >> 16) & 1);
-    const int n0 = (int)((tk >> 17) & 255), n1 = (int)((tk >> 25) & 255), mr = (int)((tk >> 33) & 255);
+    const int y0 = (int)(tk & 511), x0 = (int)((tk >> 9) & 511), t = (int)((tk >> 18) & 1);
+    const int n0 = (int)((tk >> 19) & 511), n1 = (int)((tk >> 28) & 511), mr = (int)((tk >> 37) & 255);
     int64_t mrl = pyfloordiv(n0 - min_size, min_size + 1) + 1;
     if (mr < mrl) mrl = mr;
     if (mrl <= 1) continue;
@@ -156,15 +181,13 @@ APG_DEV int rooms_primitives(Pcg64 &r, int m, int max_rooms, int door_width, con
       const int dp = (int)integers(r, 0, n1 - door_width);
       if (wp - (door_width - 1) < 0 || wp + (door_width - 1) >= n0 || dp + door_width > n1) return -3;
       // wall: the whole view row wp; door: view rows wp-dw+1 .. wp+dw-1, columns dp .. dp+dw-1
-      const int lo = wp - (door_width - 1), span = 2 * door_width - 1;
+      const int lo = wp - (door_width - 1);
       if (t == 0) {
-        W.P(1 + nw++) = ((uint32_t)(y0 + wp) << 16) | ((uint32_t)x0 << 8) | (uint32_t)n1;
-        W.P(1 + W.maxw + nd++) = ((uint32_t)(y0 + lo) << 24) | ((uint32_t)(x0 + dp) << 16) | ((uint32_t)span << 8) |
-                         (uint32_t)door_width;
+        W.P(1 + nw++) = wall_prim(0u, y0 + wp, x0, n1);
+        W.P(1 + W.maxw + nd++) = door_prim(0u, y0 + lo, x0 + dp);
       } else {
-        W.P(1 + nw++) = (1u << 31) | ((uint32_t)(x0 + wp) << 16) | ((uint32_t)y0 << 8) | (uint32_t)n1;
-        W.P(1 + W.maxw + nd++) = ((uint32_t)(y0 + dp) << 24) | ((uint32_t)(x0 + lo) << 16) | ((uint32_t)door_width << 8) |
-                         (uint32_t)span;
+        W.P(1 + nw++) = wall_prim(1u, x0 + wp, y0, n1);
+        W.P(1 + W.maxw + nd++) = door_prim(1u, y0 + dp, x0 + lo);
       }
     }
     // children room[s:e+1].T, depth-first in order => push in reverse (acc = acc_{k-1} here)
@@ -183,8 +206,7 @@ APG_DEV int rooms_primitives(Pcg64 &r, int m, int max_rooms, int door_width, con
     for (int i = 0; i < nw; i++) W.P(1 + i) ^= 1u << 31;
     for (int i = 0; i < nd; i++) {
       const uint32_t d = W.P(1 + W.maxw + i);
-      W.P(1 + W.maxw + i) =
-          (((d >> 16) & 255u) << 24) | (((d >> 24) & 255u) << 16) | ((d & 255u) << 8) | ((d >> 8) & 255u);
+      W.P(1 + W.maxw + i) = door_prim(((d >> 13) & 1u) ^ 1u, (int)((d >> 14) & 511u), (int)(d >> 23));
     }
   }
   W.P(0) = (uint32_t)nw | ((uint32_t)nd << 8);
@@ -201,26 +223,24 @@ APG_DEV uint64_t span_mask(int s, int l, int k) {
 
 // Paint rows [m][wpr] = border | walls & ~doors, one primitive at a time (each primitive is read
 // once; the row words are read-modify-written, so `rows` should be LDS: see k_lidar_reset).
-APG_DEV void rooms_paint(const RoomsWork &W, int m, int wpr, uint64_t *rows) {
+APG_DEV void rooms_paint(const RoomsWork &W, int m, int wpr, int dw, uint64_t *rows) {
   const int nw = (int)(W.P(0) & 255u), nd = (int)(W.P(0) >> 8);
   for (int y = 0; y < m; y++)
     for (int k = 0; k < wpr; k++)
       rows[y * wpr + k] = (y == 0 || y == m - 1) ? span_mask(0, m, k) : (span_mask(0, 1, k) | span_mask(m - 1, 1, k));
   for (int i = 0; i < nw; i++) {
-    const uint32_t wl = W.P(1 + i);
-    const int fixed = (int)((wl >> 16) & 255u), st = (int)((wl >> 8) & 255u), len = (int)(wl & 255u);
-    if (wl >> 31) {  // vertical: column `fixed`, rows [st, st + len)
-      const uint64_t bit = 1ULL << (fixed & 63);
-      for (int y = st; y < st + len; y++) rows[y * wpr + (fixed >> 6)] |= bit;
+    const Wall wl = wall_of(W.P(1 + i));
+    if (wl.vertical) {  // column `fixed`, rows [start, start + len)
+      const uint64_t bit = 1ULL << (wl.fixed & 63);
+      for (int y = wl.start; y < wl.start + wl.len; y++) rows[y * wpr + (wl.fixed >> 6)] |= bit;
     } else {
-      for (int k = 0; k < wpr; k++) rows[fixed * wpr + k] |= span_mask(st, len, k);
+      for (int k = 0; k < wpr; k++) rows[wl.fixed * wpr + k] |= span_mask(wl.start, wl.len, k);
     }
   }
   for (int i = 0; i < nd; i++) {
-    const uint32_t d = W.P(1 + W.maxw + i);
-    const int r0 = (int)(d >> 24), c0 = (int)((d >> 16) & 255u), hh = (int)((d >> 8) & 255u), ww = (int)(d & 255u);
-    for (int y = r0; y < r0 + hh; y++)
-      for (int k = 0; k < wpr; k++) rows[y * wpr + k] &= ~span_mask(c0, ww, k);
+    const Door d = door_of(W.P(1 + W.maxw + i), dw);
+    for (int y = d.r0; y < d.r0 + d.hh; y++)
+      for (int k = 0; k < wpr; k++) rows[y * wpr + k] &= ~span_mask(d.c0, d.ww, k);
   }
 }
 
@@ -233,7 +253,7 @@ APG_DEV int rooms_generate(Pcg64 &r, uint64_t *occ, int wpr, int m, int max_room
   uint32_t prim[rooms_prim_words(MR)];
   const RoomsWork W{stk, cap, size, cut, prim, 1, MR + 7, MR - 1};
   const int rc = rooms_primitives(r, m, max_rooms, door_width, bt, W);
-  rooms_paint(W, m, wpr, occ);
+  rooms_paint(W, m, wpr, door_width, occ);
   return rc;
 }
 

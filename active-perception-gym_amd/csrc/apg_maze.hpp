@@ -258,7 +258,18 @@ __host__ __device__ inline size_t maze_stream_off(int h, int w) {
   const size_t cells = (size_t)((w - 1) / 2) * ((h - 1) / 2);
   return (maze_log_bytes(h, w) + cells + MZ_CHUNK + 15) & ~(size_t)15;
 }
+// Mazes with more than 127 odd cells per row or column (maps wider or taller than 255; up to 511): their DFS state
+// does not fit the LDS layout below, so k_maze_big carves them one thread per maze with the visited bits
+// (u64 [ncy][cw]) and the frame stack (u32 per frame) in this scratch, writing the occupancy rows directly.
+__host__ __device__ inline bool maze_big(int h, int w) { return (w - 1) / 2 > 127 || (h - 1) / 2 > 127; }
+__host__ __device__ inline size_t maze_big_vis_bytes(int h, int w) {
+  return ((size_t)((h - 1) / 2) * (size_t)(((w - 1) / 2 + 63) / 64) * 8 + 15) & ~(size_t)15;
+}
 __host__ __device__ inline size_t maze_scratch_bytes(int h, int w) {
+  if (maze_big(h, w)) {
+    const size_t cells = (size_t)((w - 1) / 2) * ((h - 1) / 2);
+    return (maze_big_vis_bytes(h, w) + 4 * (cells + 1) + 63) & ~(size_t)63;
+  }
   return (maze_stream_off(h, w) + maze_stream_bytes(maze_stream_groups(h, w)) + 63) & ~(size_t)63;
 }
 

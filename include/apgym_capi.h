@@ -92,13 +92,13 @@ typedef struct apg_pcg64 {
 
 typedef struct apg_lidar_config {
   int32_t num_envs;
-  int32_t height, width;        /* map size in cells, 3 .. 255 each; rooms maps must be square, mazes odd */
+  int32_t height, width;        /* map size in cells, 3 .. 511 each; rooms maps must be square, mazes odd */
   int32_t map_kind;             /* APG_MAP_ROOMS | APG_MAP_MAZE */
   int32_t is_static;            /* 1: one map for all envs (static_map=True) */
   int32_t static_map_index;     /* dataset index of the static map */
   int32_t beams;                /* lidar_beam_count */
   int32_t step_limit;           /* TimeLimit max_episode_steps (issue_termination=True) */
-  int32_t max_rooms, door_width;/* FloorMapDatasetRooms parameters */
+  int32_t max_rooms, door_width;/* FloorMapDatasetRooms parameters (max_rooms 1 .. 64) */
   float lidar_range;
   float loss_scale, loss_offset;/* normalized MSE affine, as float32 (NEP 50) */
   double branching_prob;        /* FloorMapDatasetMaze parameter */

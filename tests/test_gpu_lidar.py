@@ -77,7 +77,8 @@ def test_device_maps_match_oracle_random_idx(gpu, oracle_mod, kind, size, count)
 
 @pytest.mark.parametrize("h,w,bp,count", [(21, 21, 0.5, 512), (21, 35, 0.0, 512), (63, 63, 0.3, 256),
                                            (127, 127, 0.7, 64), (3, 3, 1.0, 16), (127, 9, 1.0, 64),
-                                           (255, 255, 1.0, 32), (255, 101, 0.6, 32)])
+                                           (255, 255, 1.0, 32), (255, 101, 0.6, 32), (301, 301, 1.0, 16),
+                                           (257, 9, 0.5, 32), (11, 511, 1.0, 16), (301, 275, 0.4, 8)])
 def test_device_maze_branching_matches_oracle(gpu, oracle_mod, h, w, bp, count):
     """branching_prob < 1 (rng.random() draws decide later branches; mazes need not be perfect, so the
     stream consumption differs from the bp = 1 mazes the stream length is sized for) and odd rectangles."""
@@ -117,7 +118,8 @@ def test_device_maze_stream_overflow_matches_oracle(gpu, oracle_mod, tmp_path):
 
 
 @pytest.mark.parametrize("size,max_rooms,door_width", [(128, 17, 3), (128, 10, 3), (96, 17, 2), (48, 6, 4),
-                                                       (160, 24, 3), (200, 32, 2), (255, 17, 3), (64, 24, 2)])
+                                                       (160, 24, 3), (200, 32, 2), (255, 17, 3), (64, 24, 2),
+                                                       (320, 48, 3), (511, 64, 2), (300, 40, 6), (257, 33, 1)])
 def test_device_rooms_parameters_match_oracle(gpu, oracle_mod, size, max_rooms, door_width):
     import ap_gym_amd as ap
 
@@ -309,6 +311,7 @@ def test_vector_env_matches_reference_trace(gpu, name):
                                                             ("maze", 21, 8, 1024, 120, False),
                                                             ("maze", 127, 64, 64, 40, False),
                                                             ("maze", 255, 32, 32, 110, False),
+                                                            ("maze", 301, 32, 16, 110, False),
                                                             ("rooms", 32, 16, 512, 120, False),
                                                             ("rooms", 64, 32, 1024, 120, True)])
 def test_vector_env_matches_oracle(gpu, oracle_mod, kind, size, beams, n, steps, sparse):
@@ -389,7 +392,7 @@ def test_long_range_matches_oracle(gpu, oracle_mod, kind, size, static, beams, l
     env.close()
 
 
-@pytest.mark.parametrize("size,max_rooms,n", [(160, 24, 256), (130, 10, 256), (64, 24, 512)])
+@pytest.mark.parametrize("size,max_rooms,n", [(160, 24, 256), (130, 10, 256), (64, 24, 512), (320, 48, 32)])
 def test_large_rooms_env_matches_oracle(gpu, oracle_mod, size, max_rooms, n):
     """Rooms maps past the fused step kernel's generator (maps > 128, max_rooms > 17: the autoresets run
     in k_lidar_reset before the unfused step kernel): 110 steps (one autoreset) against the oracle env."""

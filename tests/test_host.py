@@ -47,11 +47,27 @@ def test_capi_validation_without_gpu():
     cfg.height = cfg.width = 128  # even maze sizes are rejected like FloorMapDatasetMaze
     assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == -1
     assert b"odd" in N.lib().apg_last_error()
-    # the envelope: mazes up to 255 x 255, lidar_range up to 60
+    # the envelope: mazes up to 511 x 511 (past 255: k_maze_big), rooms up to 255,
+    # lidar_range up to 60
     cfg.height, cfg.width = 255, 101
     assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0 and sz.wpr == 2
-    cfg.height = cfg.width = 257
+    cfg.height = cfg.width = 301
+    assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0 and sz.wpr == 5
+    # k_maze_big's scratch: visited bits (150 rows x 3 words) + a u32 frame per cell and one more, 64-B rounded
+    assert sz.maze_frames * 2 == (150 * 3 * 8 + 4 * (150 * 150 + 1) + 63) // 64 * 64
+    cfg.height = cfg.width = 513
     assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == -1
+    cfg.map_kind = N.APG_MAP_ROOMS
+    cfg.height = cfg.width = 320
+    cfg.max_rooms, cfg.door_width = 48, 3
+    assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0 and sz.wpr == 5
+    cfg.max_rooms = 65
+    assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == -1
+    cfg.max_rooms = 48
+    cfg.height = cfg.width = 512
+    assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == -1
+    assert b"rooms" in N.lib().apg_last_error()
+    cfg.map_kind = N.APG_MAP_MAZE
     cfg.height = cfg.width = 127
     cfg.lidar_range = 60.0
     assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0
