@@ -64,20 +64,6 @@ constexpr int MAX_STAGED_BEAMS = 64;          // lidar rows staged in LDS for co
 // from p lands within ~1e-4 of it (f32 rounding of p + dir), i.e. within a few hundred f32 steps
 constexpr int EMPTY_TAB = 1024;
 
-BinomTable make_binom_table() {
-  BinomTable t;
-  t.p = 0.3;
-  t.q = 1.0 - t.p;
-  for (int n = 0; n < ROOMS_MAX; n++) {
-    // random_binomial_inversion's cached constants, evaluated with the host libm like numpy
-    double np_ = n * t.p;
-    t.qn[n] = std::exp(n * std::log(t.q));
-    double b = np_ + 10.0 * std::sqrt(np_ * t.q + 1);
-    t.bound[n] = (int32_t)(n < b ? n : b);
-  }
-  return t;
-}
-
 struct Geo {
   int n, h, w, wpr, is_static, kind, max_rooms, door_width, frames, row;
   double bp;
@@ -187,7 +173,8 @@ APG_DEV void copy_out_maps(const uint64_t *s_maps, unsigned long long done, size
 
 template <int MR>
 __global__ __launch_bounds__(64) void k_map_generate_rooms(Geo g, const uint64_t *idx, int n, uint64_t *occ,
-                                                           uint32_t *err, BinomTable bt, int lanes) {
+                                                           uint32_t *err, int lanes) {
+  const BinomTable &bt = c_binom;
   extern __shared__ uint64_t s_rows[];  // [lanes][h * wpr]
   const int lane = threadIdx.x;
   const int i = blockIdx.x * lanes + lane;
@@ -281,8 +268,9 @@ APG_DEV uint8_t reset_one(const Geo &g, const apg_lidar_state &S, int e, uint8_t
 // Waves with nothing to reset exit after one flag load.
 template <int GEN, int MR = 17>
 __global__ __launch_bounds__(64) void k_lidar_reset(Geo g, apg_lidar_state S, uint64_t seed, int use_seed,
-                                                    int all, uint64_t *out_map_idx, uint32_t *err, BinomTable bt,
+                                                    int all, uint64_t *out_map_idx, uint32_t *err,
                                                     int lanes) {
+  const BinomTable &bt = c_binom;
   extern __shared__ uint64_t s_rows[];  // rooms: [lanes][h * wpr]
   const int lane = threadIdx.x;
   const int e = blockIdx.x * lanes + lane;
@@ -875,13 +863,13 @@ constexpr int MAX_MAP_ROWS = 128;
 // GEN_PF phase R, per wave: an env's occupancy rows (<= 128 x 2 words), then bitmap_map_obs's linear bitmap
 constexpr int PF_WAVE_WORDS = MAX_MAP_ROWS * 2 + (MAX_MAP_ROWS * 128 + 63) / 64 + 1;
 
-// Row y of a rooms map painted from its primitives (rooms_paint's result, one row at a time): border
+// Row y of a rooms map painted from its (narrow) primitives (rooms_paint's result, one row at a time): border
 // | walls & ~doors.  Word k covers columns [64k, 64k + 64); the primitives are pr[i * st].
-APG_DEV uint64_t rooms_row_word(const uint32_t *pr, int st, int m, int dw, int y, int k) {
+APG_DEV uint64_t rooms_row_word(const uint32_t *pr, int st, int m, int y, int k) {
   const int nw = (int)(pr[0] & 255u), nd = (int)(pr[0] >> 8);
   uint64_t v = (y == 0 || y == m - 1) ? span_mask(0, m, k) : (span_mask(0, 1, k) | span_mask(m - 1, 1, k));
   for (int i = 0; i < nw; i++) {
-    const Wall wl = wall_of(pr[(1 + i) * st]);
+    const Wall wl = RoomsFmt<false>::wall_of(pr[(1 + i) * st]);
     if (wl.vertical) {
       if (y >= wl.start && y < wl.start + wl.len && (wl.fixed >> 6) == k) v |= 1ULL << (wl.fixed & 63);
     } else if (wl.fixed == y) {
@@ -889,7 +877,7 @@ APG_DEV uint64_t rooms_row_word(const uint32_t *pr, int st, int m, int dw, int y
     }
   }
   for (int i = 0; i < nd; i++) {
-    const Door d = door_of(pr[(17 + i) * st], dw);
+    const Door d = RoomsFmt<false>::door_of(pr[(17 + i) * st]);
     if (y >= d.r0 && y < d.r0 + d.hh) v &= ~span_mask(d.c0, d.ww, k);
   }
   return v;
@@ -921,7 +909,8 @@ template <int GEN, bool FUSED, int EPB, bool GR = false, bool ROWP = false>
 __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(StepParams P_in, Geo g, apg_lidar_state S,
                                                                  const float *__restrict__ act,
                                                                  const float *__restrict__ pred,
-                                                                 apg_lidar_outputs O, BinomTable bt, PfView V) {
+                                                                 apg_lidar_outputs O, PfView V) {
+  const BinomTable &bt = c_binom;
   using SS = StepShape<EPB>;
   constexpr int T = SS::T, W = SS::W, LPW = SS::LPW;
   StepParams P = P_in;
@@ -1122,7 +1111,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
                              reinterpret_cast<int16_t *>(s_raw + L::size) + my_el,
                              reinterpret_cast<int16_t *>(s_raw + L::cut) + my_el, s_prims + my_el, EPB, ROOMS_STACK,
                              16};  // ROOMS_PRIM_WORDS: 17 rooms (larger max_rooms: k_lidar_reset + unfused step)
-          const int rc = rooms_primitives(map_rng, g.h, g.max_rooms, g.door_width, bt, wk);
+          const int rc = rooms_primitives<false>(map_rng, g.h, g.max_rooms, g.door_width, bt, wk);
           if (rc != 0) atomicOr(O.err, APG_ERR_MAPGEN);
         }
         // R2 reads only the primitives its own wave wrote in R1 (wave w owns the envs j * W + w): a wave
@@ -1149,7 +1138,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
             if (y < m) {
               int occ = 0;
               for (int k = 0; k < wpr; k++) {
-                const uint64_t v = rooms_row_word(pr, EPB, m, g.door_width, y, k);
+                const uint64_t v = rooms_row_word(pr, EPB, m, y, k);
                 rw[rr][k] = v;
                 dst[y * wpr + k] = v;
                 mrow[y * 2 + k] = v;
@@ -1694,7 +1683,8 @@ __global__ __launch_bounds__(RT_THREADS) void k_lidar_render_track(StepParams P,
 }
 
 __global__ void k_rng_draws(const uint64_t *seeds, int m, int kind, int64_t a, int64_t b, int n,
-                            double *out, BinomTable bt) {
+                            double *out) {
+  const BinomTable &bt = c_binom;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   Pcg64 r = seed_pcg64(seeds[i]);
@@ -1776,7 +1766,7 @@ int launch_reset_mr(const Geo &g, const apg_lidar_state *st, uint64_t seed, int 
   size_t dyn;
   if (int rc = gen_lds(k_lidar_reset<GEN, MR>, GEN, g, lanes, dyn)) return rc;
   hipLaunchKernelGGL((k_lidar_reset<GEN, MR>), dim3(grid_for(g.n, lanes)), dim3(64), dyn, s, g, *st, seed, use_seed,
-                     all, out->map_idx, out->err, make_binom_table(), lanes);
+                     all, out->map_idx, out->err, lanes);
   return check_launch("k_lidar_reset");
 }
 
@@ -1877,10 +1867,10 @@ int launch_map_generate_any(const Geo &g, const uint64_t *idx, int n, uint64_t *
   if (int rc = gen_lds(kern, GEN_ROOMS, g, lanes, dyn)) return rc;
   if (big)
     hipLaunchKernelGGL(k_map_generate_rooms<ROOMS_MAX>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, idx, n, occ, err,
-                       make_binom_table(), lanes);
+                       lanes);
   else
     hipLaunchKernelGGL(k_map_generate_rooms<17>, dim3(grid_for(n, lanes)), dim3(64), dyn, s, g, idx, n, occ, err,
-                       make_binom_table(), lanes);
+                       lanes);
   return check_launch("k_map_generate");
 }
 
@@ -1935,13 +1925,13 @@ int step_epb(int n) {
 
 template <int GEN, bool FUSED, int EPB, bool GR = false>
 int launch_step_t(const StepParams &P, const Geo &g, const apg_lidar_state *st, const float *act, const float *pred,
-                  const apg_lidar_outputs *out, hipStream_t s, const BinomTable &bt, const PfView &V) {
+                  const apg_lidar_outputs *out, hipStream_t s, const PfView &V) {
   size_t lds = step_lds_bytes(EPB, P.beams);
   if (FUSED && GEN == GEN_ROOMS && RoomsLds<EPB>::bytes > lds) lds = RoomsLds<EPB>::bytes;
   if (FUSED && GEN == GEN_PF) lds = std::max(lds, (size_t)(4 * EPB / 64) * PF_WAVE_WORDS * sizeof(uint64_t));
   auto kern = P.row ? k_lidar_step<GEN, FUSED, EPB, GR, true> : k_lidar_step<GEN, FUSED, EPB, GR, false>;
   if (int rc = opt_in_lds((const void *)kern, lds)) return rc;
-  hipLaunchKernelGGL(kern, dim3(grid_for(P.n, EPB)), dim3(4 * EPB), lds, s, P, g, *st, act, pred, *out, bt, V);
+  hipLaunchKernelGGL(kern, dim3(grid_for(P.n, EPB)), dim3(4 * EPB), lds, s, P, g, *st, act, pred, *out, V);
   return check_launch("k_lidar_step");
 }
 
@@ -1949,21 +1939,20 @@ int launch_step_t(const StepParams &P, const Geo &g, const apg_lidar_state *st, 
 template <int EPB>
 int launch_step_epb(const StepParams &P, const Geo &g, const apg_lidar_state *st, const float *act, const float *pred,
                     const apg_lidar_outputs *out, hipStream_t s, bool fused, const PfView *pf) {
-  const BinomTable bt = make_binom_table();
   PfView V{};
   if (pf) V = *pf;
   if (P.R > MAX_WIN_RANGE) {  // scans longer than the staged window covers: rows from global memory (EPB 64)
-    if (!fused) return launch_step_t<GEN_NONE, false, 64, true>(P, g, st, act, pred, out, s, bt, V);
+    if (!fused) return launch_step_t<GEN_NONE, false, 64, true>(P, g, st, act, pred, out, s, V);
     switch (step_gen(g)) {
-      case GEN_ROOMS: return launch_step_t<GEN_ROOMS, true, 64, true>(P, g, st, act, pred, out, s, bt, V);
-      default: return launch_step_t<GEN_NONE, true, 64, true>(P, g, st, act, pred, out, s, bt, V);
+      case GEN_ROOMS: return launch_step_t<GEN_ROOMS, true, 64, true>(P, g, st, act, pred, out, s, V);
+      default: return launch_step_t<GEN_NONE, true, 64, true>(P, g, st, act, pred, out, s, V);
     }
   }
-  if (!fused) return launch_step_t<GEN_NONE, false, EPB>(P, g, st, act, pred, out, s, bt, V);
-  if (pf) return launch_step_t<GEN_PF, true, EPB == 128 ? 256 : EPB>(P, g, st, act, pred, out, s, bt, V);
+  if (!fused) return launch_step_t<GEN_NONE, false, EPB>(P, g, st, act, pred, out, s, V);
+  if (pf) return launch_step_t<GEN_PF, true, EPB == 128 ? 256 : EPB>(P, g, st, act, pred, out, s, V);
   switch (step_gen(g)) {
-    case GEN_ROOMS: return launch_step_t<GEN_ROOMS, true, EPB>(P, g, st, act, pred, out, s, bt, V);
-    default: return launch_step_t<GEN_NONE, true, EPB>(P, g, st, act, pred, out, s, bt, V);
+    case GEN_ROOMS: return launch_step_t<GEN_ROOMS, true, EPB>(P, g, st, act, pred, out, s, V);
+    default: return launch_step_t<GEN_NONE, true, EPB>(P, g, st, act, pred, out, s, V);
   }
 }
 
@@ -2422,7 +2411,7 @@ int apg_rng_draws(const uint64_t *seeds, int m, int kind, int64_t a, int64_t b, 
   if (m <= 0 || n <= 0 || kind < 0 || kind > 5) return fail(APG_E_INVALID, "bad rng draw arguments");
   if (kind == 5 && (a < 0 || a > 15)) return fail(APG_E_INVALID, "binomial n must be in [0, 15]");
   hipLaunchKernelGGL(k_rng_draws, dim3(grid_for(m, 64)), dim3(64), 0, (hipStream_t)stream, seeds, m, kind, a, b,
-                     n, out, make_binom_table());
+                     n, out);
   return check_launch("k_rng_draws");
 }
 

@@ -366,3 +366,26 @@ def test_lidar_output_block_layout():
             tv["reward"][0] = -1.25
             assert nv["lidar"][-1, -1] == 2.5 and nv["reward"][0] == -1.25
             assert all(v.is_contiguous() for v in tv.values()) and all(v.flags.c_contiguous for v in nv.values())
+
+
+def test_binomial_constant_table_matches_host_libm():
+    """csrc/apg_binom_table.hpp (the rooms generator's random_binomial_inversion constants in constant memory) is
+    what tools/gen_binom_table.py computes with this host's libm, numpy's own evaluation of qn and bound."""
+    import os
+    import re
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tools"))
+    from gen_binom_table import table
+
+    text = open(os.path.join(root, "active-perception-gym_amd", "csrc", "apg_binom_table.hpp")).read()
+
+    def macro(name):
+        m = re.search(r"#define " + name + r" \\\n((?:.*\\\n)*.*)\n", text)
+        return [v.strip() for v in m.group(1).replace("\\", "").split(",") if v.strip()]
+
+    p, q, qn, bound = table()
+    assert [float.fromhex(v) for v in macro("APG_BINOM_QN")] == qn
+    assert [int(v) for v in macro("APG_BINOM_BOUND")] == bound
+    assert len(qn) == 64 and qn[1] == 0.7 and bound[:3] == [0, 1, 2]
