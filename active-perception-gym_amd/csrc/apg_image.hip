@@ -419,12 +419,12 @@ struct Axis {  // one sampling coordinate: pool offset of its grid interval (row
 // Separable glimpse of `nu` units (env x position) starting at unit u0, in two passes over a workgroup:
 // gs_axes computes every unit's row and column grid intervals / weights once (into LDS s_ax, plus the
 // pool offset of its image), gs_pixels then evaluates one pixel per thread from them.
-template <class PosAt>
+template <int GT = GS_THREADS, class PosAt>
 APG_DEV uint32_t gs_axes(const GlimpseGeo &g, const int64_t *index, PosAt pos_at, int u0, int nu, int npos,
                          FastDiv side_div, Axis *s_ax, int64_t *s_base) {
   const int side = g.s0 + g.s1;
   uint32_t bad = 0;
-  for (int q = threadIdx.x; q < nu * side; q += GS_THREADS) {
+  for (int q = threadIdx.x; q < nu * side; q += GT) {
     const int u = (int)side_div.div((uint32_t)q), k = q - u * side;
     const bool row = k < g.s0;
     const int t = row ? k : k - g.s0;
@@ -451,7 +451,7 @@ struct U8Taps {
   int o0, o1;
 };
 
-template <bool F32, int PC, int C>
+template <bool F32, int PC, int C, int GT = GS_THREADS>
 APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, FastDiv per_div, FastDiv s1_div,
                          const Axis *s_ax, const int64_t *s_base, const float *s_lut, float *out) {
   const int side = g.s0 + g.s1;
@@ -482,7 +482,7 @@ APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, 
   };
   if constexpr (F32) {
     const float *im = static_cast<const float *>(pool);
-    for (int q = threadIdx.x; q < total; q += GS_THREADS) {
+    for (int q = threadIdx.x; q < total; q += GT) {
       int u, i, j;
       coords(q, u, i, j);
       const Axis ay = s_ax[u * side + i], axx = s_ax[u * side + g.s0 + j];
@@ -527,7 +527,7 @@ APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, 
       }
       return t;
     };
-    for (int q = threadIdx.x; q < total; q += GS_THREADS) {
+    for (int q = threadIdx.x; q < total; q += GT) {
       const U8Taps cur = fetch(q);
       int u, i, j;
       coords(q, u, i, j);
@@ -982,16 +982,18 @@ APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const EnvIn &in, doub
 // start positions, as observe() does.  KIND:
 // APG_IMAGE_LOCALIZE, or APG_IMAGE_CLASSIFY with K <= CLS1_MAX_K (logits staged in LDS with coalesced loads,
 // one thread per env as k_image_env_cls1).
-// ENVW: the workgroup is GS_THREADS glimpse threads plus one env wave.  The env wave loads the env inputs,
+// ENVW: the workgroup is GT glimpse threads plus one env wave.  The env wave loads the env inputs,
 // moves the units (positions into LDS for the axes), and after the second barrier runs the env steps while
 // the glimpse waves compute the pixels: the serial per-env tail (exp / log / stats / move) overlaps the
-// glimpse instead of following it.  Without ENVW the first GS_THREADS threads do both in turn.
+// glimpse instead of following it.  Without ENVW the first GT threads do both in turn.  GT: 256, or 448 for the
+// env-wave instances (eight waves per workgroup: four workgroups fill a CU's 32 wave slots, so a grid of up to
+// 1024 workgroups is resident at once with each glimpse thread on fewer pixels).
 #ifndef APG_FUSED_MIN_WAVES
 #define APG_FUSED_MIN_WAVES 8  // <= 64 VGPRs: every workgroup of the grid resident at once
 #endif
 constexpr int ENV_WAVE = 64;
-template <int KIND, bool F32, int PC, int C, bool ENVW>
-__global__ __launch_bounds__(ENVW ? GS_THREADS + ENV_WAVE : GS_THREADS)
+template <int KIND, bool F32, int PC, int C, bool ENVW, int GT = GS_THREADS>
+__global__ __launch_bounds__(ENVW ? GT + ENV_WAVE : GT)
 __attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fused(EnvArgs a, GlimpseGeo g, const void *pool, const int64_t *index, const float *__restrict__ act,
                    const float *__restrict__ pred, const int32_t *label, double *pos, apg_image_outputs out,
                    float *hist, int upb, FastDiv per_div, FastDiv s1_div, FastDiv side_div, FastDiv k_div) {
@@ -1040,30 +1042,30 @@ __attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fuse
       loc_env(a, u0 + r, in, pos, out, hist);
   };
   if constexpr (ENVW) {
-    if (tid >= GS_THREADS) {  // the env wave (wave-uniform branch; it takes part in both barriers)
+    if (tid >= GT) {  // the env wave (wave-uniform branch; it takes part in both barriers)
       EnvIn in;
-      env_inputs(tid - GS_THREADS, ENV_WAVE, in);
+      env_inputs(tid - GT, ENV_WAVE, in);
       __syncthreads();
       __syncthreads();
-      env_step(tid - GS_THREADS, in);
+      env_step(tid - GT, in);
       return;
     }
-    if (!APG_U8_ARITH) for (int v = tid; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
+    if (!APG_U8_ARITH) for (int v = tid; v < 256; v += GT) s_lut[v] = u8_value((unsigned)v);
     __syncthreads();
     const uint32_t bad =
-        gs_axes(g, nullptr, [&](int u, int c) { return s_npos[u][c]; }, u0, nu, 1, side_div, s_ax, s_base);
+        gs_axes<GT>(g, nullptr, [&](int u, int c) { return s_npos[u][c]; }, u0, nu, 1, side_div, s_ax, s_base);
     __syncthreads();
-    gs_pixels_t<F32, PC, C>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
+    gs_pixels_t<F32, PC, C, GT>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
     if (bad) atomicOr(out.err, bad);
   } else {
-    if (!APG_U8_ARITH) for (int v = tid; v < 256; v += GS_THREADS) s_lut[v] = u8_value((unsigned)v);
+    if (!APG_U8_ARITH) for (int v = tid; v < 256; v += GT) s_lut[v] = u8_value((unsigned)v);
     EnvIn in;
-    env_inputs(tid, GS_THREADS, in);
+    env_inputs(tid, GT, in);
     __syncthreads();
     const uint32_t bad =
-        gs_axes(g, nullptr, [&](int u, int c) { return s_npos[u][c]; }, u0, nu, 1, side_div, s_ax, s_base);
+        gs_axes<GT>(g, nullptr, [&](int u, int c) { return s_npos[u][c]; }, u0, nu, 1, side_div, s_ax, s_base);
     __syncthreads();
-    gs_pixels_t<F32, PC, C>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
+    gs_pixels_t<F32, PC, C, GT>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
     env_step(tid, in);
     if (bad) atomicOr(out.err, bad);
   }
@@ -1843,11 +1845,19 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
     const FastDiv pd = make_fastdiv((uint32_t)per), sd = make_fastdiv((uint32_t)g.s1),
                   sid = make_fastdiv((uint32_t)(g.s0 + g.s1)), kd = make_fastdiv((uint32_t)std::max(1, c->num_classes));
     // one instance per env kind and pool format (u8 / f32, pool channels, glimpse channels)
-    const dim3 block_e(GS_THREADS + ENV_WAVE);
+    // glimpse threads of the env-wave instances: 448 (eight-wave workgroups) unless APG_IMAGE_GT=256 (A/B knob;
+    // results do not depend on it)
+    static const int gt_knob = getenv("APG_IMAGE_GT") ? atoi(getenv("APG_IMAGE_GT")) : 448;
+    const bool gt448 = gt_knob == 448;
+    const dim3 block_e((gt448 ? 448 : GS_THREADS) + ENV_WAVE);
     // one instance per env kind and pool format (u8 / f32, pool channels, glimpse channels)
 #define APG_FUSED(K, F, P, C)                                                                                    \
   do {                                                                                                           \
-    if (envw)                                                                                                    \
+    if (envw && gt448)                                                                                           \
+      hipLaunchKernelGGL((k_image_step_fused<K, F, P, C, true, 448>), grid, block_e, dyn, s, a, g, st->pool,     \
+                         st->index, action, prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, sd, sid, \
+                         kd);                                                                                    \
+    else if (envw)                                                                                               \
       hipLaunchKernelGGL((k_image_step_fused<K, F, P, C, true>), grid, block_e, dyn, s, a, g, st->pool, st->index, \
                          action, prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, sd, sid, kd);    \
     else                                                                                                         \
