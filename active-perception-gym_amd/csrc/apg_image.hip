@@ -1006,7 +1006,9 @@ __attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fuse
   float *s_logit = reinterpret_cast<float *>(s_ax + (size_t)upb * (g.s0 + g.s1));
   // env inputs of unit u by thread r of `nr` (the env wave, or the first GS_THREADS threads): logits staged,
   // inputs loaded, image offset and the move (the env step repeats it for its outputs) into LDS for the axes
-  auto env_inputs = [&](int r, int nr, EnvIn &in) {
+  // (classify) the units' logits staged in LDS for the env step: off the move's path, so the env wave stages them
+  // between the two barriers while the glimpse waves compute the axes
+  auto stage_logits = [&](int r, int nr) {
     if constexpr (KIND == APG_IMAGE_CLASSIFY) {
       const int k = a.k, stride = cls1_stride(k);
       for (int q = r; q < nu * k; q += nr) {
@@ -1014,6 +1016,8 @@ __attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fuse
         s_logit[row * stride + (q - row * k)] = pred[(size_t)u0 * k + q];
       }
     }
+  };
+  auto env_inputs = [&](int r, int nr, EnvIn &in) {
     in = EnvIn{};
     if (r < nu) {
       const int e = u0 + r;
@@ -1046,6 +1050,7 @@ __attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fuse
       EnvIn in;
       env_inputs(tid - GT, ENV_WAVE, in);
       __syncthreads();
+      stage_logits(tid - GT, ENV_WAVE);
       __syncthreads();
       env_step(tid - GT, in);
       return;
@@ -1061,6 +1066,7 @@ __attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fuse
     if (!APG_U8_ARITH) for (int v = tid; v < 256; v += GT) s_lut[v] = u8_value((unsigned)v);
     EnvIn in;
     env_inputs(tid, GT, in);
+    stage_logits(tid, GT);
     __syncthreads();
     const uint32_t bad =
         gs_axes<GT>(g, nullptr, [&](int u, int c) { return s_npos[u][c]; }, u0, nu, 1, side_div, s_ax, s_base);
