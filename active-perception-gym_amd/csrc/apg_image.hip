@@ -1838,12 +1838,13 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
   }
   if (fusable) {
     const int per = g.s0 * g.s1;
-    // The env wave pays off for classification (its env step is the long serial tail: exp, log, pairwise
-    // sum), with the workgroup's units at its 64 lanes; localization's short tail does not repay a fifth wave
-    // (MI355X, fused step: MNIST 11.6 vs 13.8 us, TinyImageNetLoc 29.7 vs 28.0 us).  APG_IMAGE_ENV_WAVE=0|1
-    // overrides (A/B knob; results do not depend on it).
+    // The env wave (the workgroup's units at its 64 lanes) runs the serial per-env tail beside the glimpse waves:
+    // with 448 glimpse threads it pays off for both kinds (MI355X, fused step rocprof medians: MNIST 13.08 ->
+    // 12.46 us, TinyImageNetLoc 31.15 -> 30.3 us; with 256 glimpse threads localization's short tail did not
+    // repay the extra wave, 29.7 vs 28.0 us in round 3).  APG_IMAGE_ENV_WAVE=0|1 overrides (A/B knob; results
+    // do not depend on it).
     static const int envw_knob = getenv("APG_IMAGE_ENV_WAVE") ? atoi(getenv("APG_IMAGE_ENV_WAVE")) : -1;
-    const bool envw = envw_knob >= 0 ? envw_knob != 0 : c->kind == APG_IMAGE_CLASSIFY;
+    const bool envw = envw_knob >= 0 ? envw_knob != 0 : true;
     const int upb = envw ? std::min(ENV_WAVE, glimpse_units_per_block(per, 8)) : glimpse_units_per_block(per, 4);
     size_t dyn = (size_t)upb * (g.s0 + g.s1) * sizeof(Axis);
     if (c->kind == APG_IMAGE_CLASSIFY) dyn += (size_t)upb * (c->num_classes + 2) * sizeof(float);
