@@ -540,10 +540,7 @@ __global__ __launch_bounds__(64) void k_maze_big(Geo g, apg_lidar_state S, const
 // (maze_paint), writes them out (occ, or S.occ), and for MZ_RESET writes the map obs (bool map / 255,
 // lidar_localization2d.py:299), draws the start cell like place_start (reset :304: the pick-th free cell in
 // row-major order, pick = integers(0, nfree) on the env's stream) and resets the env's state.
-#ifndef APG_MP_ENVS
-#define APG_MP_ENVS 4  // mazes per k_maze_paint / k_pf_paint workgroup (64: 4.80 ms, 16: 4.51, 8: 4.49, 4: 4.44 at cfg 3)
-#endif
-constexpr int MP_THREADS = 256, MP_ENVS = APG_MP_ENVS;
+constexpr int MP_THREADS = 256, MP_ENVS = 64;
 __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_state S, const uint64_t *idx, int n,
                                                            uint64_t *occ, const uint8_t *scratch, int mode,
                                                            uint64_t seed, int use_seed, int all, int ng,
