@@ -16,7 +16,8 @@ from .circle_square import (  # noqa: F401
     CircleSquareHideAndSeekVectorWrapper,
     DoubleCircleSquareDataset,
 )
-from .floor_map import FloorMapDataset, FloorMapDatasetMaze, FloorMapDatasetRooms  # noqa: F401
+from .floor_map import (ArrayFloorMapDataset, FloorMapDataset, FloorMapDatasetMaze, FloorMapDatasetRooms,  # noqa: F401
+                        ForeignFloorMapView, PoolFloorMapDataset)
 from .image_dataset import (  # noqa: F401
     ArrayImageClassificationDataset,
     HuggingfaceImageClassificationDataset,

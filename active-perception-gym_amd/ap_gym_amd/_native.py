@@ -26,8 +26,10 @@ APG_ERR_MAPGEN = 4
 APG_ERR_OOB_Y = 8
 APG_ERR_OOB_X = 16
 APG_ERR_PREFETCH = 32
+APG_ERR_NO_FREE_CELL = 64
 APG_MAP_ROOMS = 0
 APG_MAP_MAZE = 1
+APG_MAP_POOL = 2
 APG_DRAW_UNIFORM = 0
 APG_DRAW_INTEGERS = 1
 APG_IMAGE_CLASSIFY = 0
@@ -60,12 +62,13 @@ class LidarConfig(ctypes.Structure):
                 ("beams", ctypes.c_int32), ("step_limit", ctypes.c_int32), ("max_rooms", ctypes.c_int32),
                 ("door_width", ctypes.c_int32), ("lidar_range", ctypes.c_float), ("loss_scale", ctypes.c_float),
                 ("loss_offset", ctypes.c_float), ("branching_prob", ctypes.c_double), ("log_stats", ctypes.c_int32),
-                ("sparse", ctypes.c_int32), ("out_row_bytes", ctypes.c_int32)]
+                ("sparse", ctypes.c_int32), ("out_row_bytes", ctypes.c_int32), ("pool_len", ctypes.c_int32)]
 
 
 class LidarState(ctypes.Structure):
     _fields_ = [(n, _vp) for n in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng", "occ", "scratch", "stack",
-                                   "map_idx", "beam_dirs", "stats_hist", "prefetch", "prefetcher")]
+                                   "map_idx", "beam_dirs", "stats_hist", "prefetch", "prefetcher", "pool_occ",
+                                   "pool_free")]
 
 
 class LidarOutputs(ctypes.Structure):

@@ -35,6 +35,9 @@ class FloorMapDataset:
     def native_params(self) -> dict:
         raise NotImplementedError
 
+    def host_pool(self):
+        raise NotImplementedError  # pool datasets only (PoolFloorMapDataset)
+
     def get_data_point_batch(self, idx, device="cuda") -> np.ndarray:
         return generate_maps(self, np.asarray(idx, dtype=np.uint64), device=device)
 
@@ -74,6 +77,115 @@ class FloorMapDatasetMaze(FloorMapDataset):
 
     def native_params(self):
         return dict(max_rooms=10, door_width=3, branching_prob=self.branching_prob)
+
+
+class PoolFloorMapDataset(FloorMapDataset):
+    """A finite floor-map dataset whose maps the LIDAR envs hold in HBM as one resident pool (APG_MAP_POOL):
+    bit rows u64[len][H][ceil(W/64)] plus each map's free-cell count, uploaded once per device and shared by
+    every env built on the dataset.  An episode's map is pool map `integers(0, len(dataset))` of the env's
+    DatasetIterator stream (dataset_iterator.py:26-32), the static map pool map `static_map_index`
+    (lidar_localization2d.py:177-178) -- the reference's own draws, so any finite FloorMapDataset
+    (floor_map_dataset.py:10-22) runs on the GPU path.  Subclasses provide `map_array(i)` (bool [H, W])."""
+
+    map_kind = N.APG_MAP_POOL
+    FETCH_CHUNK = 1024
+
+    def native_params(self) -> dict:
+        return dict(max_rooms=10, door_width=3, branching_prob=1.0)  # unused by pool maps
+
+    def map_array(self, idx: int) -> np.ndarray:
+        raise NotImplementedError
+
+    def get_data_point(self, idx, device=None) -> np.ndarray:
+        return np.array(self.map_array(int(idx)), dtype=bool)
+
+    def get_data_point_batch(self, idx, device=None) -> np.ndarray:
+        return np.stack([self.get_data_point(int(i)) for i in np.asarray(idx).reshape(-1)])
+
+    def host_pool(self) -> tuple[np.ndarray, np.ndarray]:
+        """(bits u64 [len, H, wpr], free-cell counts i32 [len]) of every map, checked like __set_map
+        (lidar_localization2d.py:279: shape (map_height, map_width)); maps must be boolean arrays (the reference
+        indexes its coordinate grids with them, :282-284)."""
+        n = len(self)
+        if n < 1 or n > 2**31 - 1:
+            raise ValueError(f"pool maps: the dataset must hold 1 .. 2**31 - 1 maps, got {n}")
+        h, w = self.map_height, self.map_width
+        wpr = (w + 63) // 64
+        bits = np.zeros((n, h, wpr * 8), np.uint8)
+        free = np.zeros(n, np.int32)
+        for lo in range(0, n, self.FETCH_CHUNK):
+            for i in range(lo, min(n, lo + self.FETCH_CHUNK)):
+                m = np.asarray(self.map_array(i))
+                if m.shape != (h, w):
+                    raise ValueError(f"map {i} has shape {m.shape}, expected (map_height, map_width) = {(h, w)}")
+                if m.dtype != np.bool_:
+                    raise TypeError(f"map {i} has dtype {m.dtype}: floor maps are boolean arrays (True = wall)")
+                bits[i, :, :(w + 7) // 8] = np.packbits(m, axis=-1, bitorder="little")
+                free[i] = h * w - int(np.count_nonzero(m))
+        return bits.view("<u8").reshape(n, h, wpr), free
+
+    def device_pool(self, device):
+        """(pool_occ int64 [len, H, wpr], pool_free int32 [len]) on `device`, uploaded on first use."""
+        import torch
+
+        dev = torch.device(device)
+        cache = self.__dict__.setdefault("_device_pools", {})
+        key = str(dev)
+        if key not in cache:
+            bits, free = self.host_pool()
+            cache[key] = (torch.as_tensor(bits.view(np.int64), device=dev).contiguous(),
+                          torch.as_tensor(free, device=dev))
+        return cache[key]
+
+
+class ArrayFloorMapDataset(PoolFloorMapDataset):
+    """Maps given as one array, bool [M, H, W] (True = wall): a pool dataset for ap_gym_amd users."""
+
+    def __init__(self, maps):
+        m = np.asarray(maps)
+        if m.ndim != 3 or m.dtype != np.bool_:
+            raise ValueError("maps must be a bool array [num_maps, height, width]")
+        self._maps = np.ascontiguousarray(m)
+        super().__init__(m.shape[2], m.shape[1])
+
+    def __len__(self):
+        return int(self._maps.shape[0])
+
+    def map_array(self, idx: int) -> np.ndarray:
+        return self._maps[idx]
+
+
+class ForeignFloorMapView(PoolFloorMapDataset):
+    """Any object with the reference's FloorMapDataset interface (`map_width`, `map_height`, `load`, `__len__`,
+    `get_data_point`) -- e.g. a user subclass of ap_gym.envs.floor_map.FloorMapDataset
+    (floor_map_dataset.py:10-22) -- seen as a pool dataset: `get_data_point(i)` is called once for every index
+    and the maps are frozen on the device.  The reference env calls `get_data_point(idx)` at every draw, so a
+    dataset that randomizes per fetch or does not fit in device memory behaves differently here (every draw of
+    index i sees the first fetch); parity for such datasets is unpinned."""
+
+    def __init__(self, inner):
+        self.inner = inner
+        super().__init__(int(inner.map_width), int(inner.map_height))
+
+    def load(self):
+        if hasattr(self.inner, "load"):
+            self.inner.load()
+
+    def __len__(self):
+        return int(len(self.inner))
+
+    def map_array(self, idx: int) -> np.ndarray:
+        return np.asarray(self.inner.get_data_point(idx))
+
+
+def as_floor_map_dataset(ds):
+    """`ds` itself when the LIDAR envs can use it directly (procedural or pool), else a ForeignFloorMapView."""
+    if isinstance(ds, FloorMapDataset):
+        return ds
+    for attr in ("map_width", "map_height", "get_data_point"):
+        if not hasattr(ds, attr):
+            raise TypeError(f"dataset {type(ds).__name__} is not a FloorMapDataset (no {attr})")
+    return ForeignFloorMapView(ds)
 
 
 def unpack_occupancy(occ_words: np.ndarray, h: int, w: int) -> np.ndarray:

@@ -46,7 +46,7 @@ from typing import Any
 import numpy as np
 
 from . import _native as N
-from .floor_map import FloorMapDataset, FloorMapDatasetMaze, FloorMapDatasetRooms
+from .floor_map import FloorMapDataset, FloorMapDatasetMaze, FloorMapDatasetRooms, as_floor_map_dataset
 from .loss_fn import WeightedLossFn, affine_f32, regression_loss
 from .spaces import ActivePerceptionActionSpace, Box, Dict, ImageSpace, batch_space
 from .vector_env import VectorEnv
@@ -196,6 +196,9 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             raise ValueError(f"Invalid render mode: {render_mode}")
         if dataset is None:
             dataset = FloorMapDatasetRooms()
+        # any other FloorMapDataset (a reference subclass included) runs from a resident map pool (APG_MAP_POOL)
+        dataset = as_floor_map_dataset(dataset)
+        dataset.load()  # lidar_localization2d.py:176
         self.num_envs = int(num_envs)
         self.dataset = dataset
         self.render_mode = render_mode
@@ -227,6 +230,12 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
 
         # ---- native configuration
         p = dataset.native_params()
+        pool_occ = pool_free = None
+        if dataset.map_kind == N.APG_MAP_POOL:  # every map of the dataset, once per device
+            pool_occ, pool_free = dataset.device_pool(self.device)
+            if self.static_map and not 0 <= int(static_map_index) < len(dataset):
+                raise IndexError(f"static_map_index {static_map_index} is out of range for a dataset of "
+                                 f"{len(dataset)} maps")
         scale, offset = affine_f32(inner_loss)
         self.output_layout, row_bytes = lidar_output_row_layout(self.lidar_beam_count, self.log_stats, self.sparse)
         if not packed_outputs:
@@ -237,7 +246,8 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
                                   max_rooms=p["max_rooms"], door_width=p["door_width"],
                                   lidar_range=float(np.float32(lidar_range)), loss_scale=scale, loss_offset=offset,
                                   branching_prob=p["branching_prob"], log_stats=int(self.log_stats),
-                                  sparse=int(self.sparse), out_row_bytes=row_bytes)
+                                  sparse=int(self.sparse), out_row_bytes=row_bytes,
+                                  pool_len=len(dataset) if pool_occ is not None else 0)
         L = N.lib()
         sizes = N.LidarSizes()
         N.check(L.apg_lidar_query_sizes(ctypes.byref(self._cfg), ctypes.byref(sizes)), "apg_lidar_query_sizes")
@@ -279,6 +289,7 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             # reference's DataLoader(prefetch=True) thread (lidar_localization2d.py:130-131, 296-298)
             prefetch=(t.zeros(sizes.prefetch_bytes, dtype=t.uint8, device=dev)
                       if prefetch and sizes.prefetch_bytes else None),
+            pool_occ=pool_occ, pool_free=pool_free,
         )
         # packed_outputs: the per-env outputs are field views of one [n, row] buffer (ShardedVectorEnv's send)
         self.output_rows = None
@@ -301,7 +312,8 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             self._prefetcher = h_pf.value
         self._state = N.LidarState(*[N.ptr(T[k]) for k in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng",
                                                             "occ", "scratch", "stack", "map_idx", "beam_dirs",
-                                                            "stats_hist", "prefetch")], self._prefetcher)
+                                                            "stats_hist", "prefetch")], self._prefetcher,
+                                    N.ptr(T["pool_occ"]), N.ptr(T["pool_free"]))
         self._out = N.LidarOutputs(N.ptr(T["lidar"]), N.ptr(T["odometry"]), N.ptr(T["time_step"]),
                                    N.ptr(T["map_obs"]), N.ptr(T["reward"]), N.ptr(T["terminated"]),
                                    N.ptr(T["truncated"]), N.ptr(T["base_reward"]), N.ptr(T["target"]),
@@ -319,10 +331,11 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         self._c_args = None
         self._h = t.classes.apgym.LidarEnv(
             [c.num_envs, c.height, c.width, c.map_kind, c.is_static, c.static_map_index, c.beams, c.step_limit,
-             c.max_rooms, c.door_width, c.log_stats, c.sparse, c.out_row_bytes, self._prefetcher or 0],
+             c.max_rooms, c.door_width, c.log_stats, c.sparse, c.out_row_bytes, self._prefetcher or 0, c.pool_len],
             [c.lidar_range, c.loss_scale, c.loss_offset, c.branching_prob],
             N.op_buffers([T[k] for k in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng", "occ", "scratch",
-                                         "stack", "map_idx", "beam_dirs", "stats_hist", "prefetch")] + [None], dev),
+                                         "stack", "map_idx", "beam_dirs", "stats_hist", "prefetch")] + [None] +
+                         [T["pool_occ"], T["pool_free"]], dev),
             N.op_buffers([T[k] for k in ("lidar", "odometry", "time_step", "map_obs", "reward", "terminated",
                                          "truncated", "base_reward", "target", "loss", "info_mask", "map_idx_out",
                                          "reset_mask", "err", "stats", "stats_len", "weight")], dev))
@@ -496,6 +509,8 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             raise ValueError(NAN_PREDICTION_MSG)
         if bits & N.APG_ERR_MAPGEN:
             raise N.ApgError("map generation exceeded an internal bound")
+        if bits & N.APG_ERR_NO_FREE_CELL:  # numpy's integers(0, 0) in reset (lidar_localization2d.py:302-303)
+            raise ValueError("high <= 0")
         if bits & N.APG_ERR_PREFETCH:
             raise N.ApgError("an autoreset found no prefetched map (prefetch protocol violated)")
 
@@ -803,7 +818,8 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             pass
 
     def __repr__(self):
-        kind = "maze" if isinstance(self.dataset, FloorMapDatasetMaze) else "rooms"
+        kind = ("maze" if isinstance(self.dataset, FloorMapDatasetMaze) else
+                "rooms" if isinstance(self.dataset, FloorMapDatasetRooms) else f"pool[{len(self.dataset)}]")
         return (f"LIDARLocalization2DVectorEnv(num_envs={self.num_envs}, {kind} "
                 f"{self.dataset.map_width}x{self.dataset.map_height}, static={self.static_map}, "
                 f"beams={self.lidar_beam_count}, device={self.device})")

@@ -9,6 +9,7 @@ Outputs (git-ignored; they travel to the GPU box with the gpurun snapshot):
 
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -20,7 +21,7 @@ OUT = os.path.join(OUT_DIR, "libapgym_hip.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 SOURCES = ["apg_lidar.hip", "apg_image.hip", "apg_circle_square.hip", "apg_light_dark.hip"]
 HEADERS = ["apg_device.hpp", "apg_maps.hpp", "apg_scan.hpp", "apg_rng.hpp", "apg_host.hpp", "apg_pairwise.hpp",
-           "apg_ziggurat.hpp", "apg_maze.hpp"]
+           "apg_ziggurat.hpp", "apg_maze.hpp", "apg_binom_table.hpp"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = [
@@ -81,19 +82,45 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+OBJ_DIR = os.path.join(HERE, "build_obj")  # per-source objects (git- and gpurun-ignored)
+
+
 def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str | None = None) -> str:
-    """Build the library; `extra_flags`/`out` make tuning variants (e.g. -DAPG_STEP_PROFILE into tune/)."""
+    """Build the library; `extra_flags`/`out` make tuning variants (e.g. -DAPG_STEP_PROFILE into tune/).
+    Each source compiles to its own object in parallel (the kernels are independent translation units), and only
+    objects older than their source or a shared header are rebuilt; then one link."""
     os.makedirs(OUT_DIR, exist_ok=True)
     variant = out is not None
     out = out or OUT
     if not force and not variant and not _stale():
         return OUT
     os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
-    cmd = [HIPCC, *FLAGS, *extra_flags, "-I", INCLUDE, "-o", out + ".tmp", *[os.path.join(CSRC, s) for s in SOURCES]]
-    if verbose:
-        cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    tag = "" if not extra_flags else "_" + hashlib.sha1(" ".join(extra_flags).encode()).hexdigest()[:10]
+    odir = os.path.join(OBJ_DIR, "default" + tag)
+    os.makedirs(odir, exist_ok=True)
+    compile_flags = [f for f in FLAGS if f != "-shared" and not f.startswith("-Wl,")]
+    shared = [os.path.join(CSRC, f) for f in HEADERS] + [os.path.join(INCLUDE, "apgym_capi.h"), os.path.abspath(__file__)]
+    newest_shared = max(os.path.getmtime(d) for d in shared)
+    procs, objs = [], []
+    for src in SOURCES:
+        spath = os.path.join(CSRC, src)
+        obj = os.path.join(odir, os.path.splitext(src)[0] + ".o")
+        objs.append(obj)
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(spath), newest_shared):
+            continue
+        cmd = [HIPCC, *compile_flags, *extra_flags, "-I", INCLUDE, "-c", "-o", obj + ".tmp", spath]
+        if verbose:
+            cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
+            print(" ".join(cmd))
+        procs.append((subprocess.Popen(cmd), obj))
+    failed = [obj for p, obj in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, f"hipcc -c ({', '.join(os.path.basename(f) for f in failed)})")
+    for _, obj in procs:
+        os.replace(obj + ".tmp", obj)
+    link = [HIPCC, *[f for f in FLAGS if f in ("--offload-arch=gfx950", "-fPIC", "-shared") or f.startswith("-Wl,")],
+            "-o", out + ".tmp", *objs]
+    subprocess.run(link, check=True)
     os.replace(out + ".tmp", out)
     return out
 

@@ -65,7 +65,7 @@ constexpr int MAX_STAGED_BEAMS = 64;          // lidar rows staged in LDS for co
 constexpr int EMPTY_TAB = 1024;
 
 struct Geo {
-  int n, h, w, wpr, is_static, kind, max_rooms, door_width, frames, row;
+  int n, h, w, wpr, is_static, kind, max_rooms, door_width, frames, row, pool_len;
   double bp;
 };
 
@@ -90,6 +90,7 @@ Geo make_geo(const apg_lidar_config *c) {
   g.frames = (int)(maze_scratch_bytes(c->height, c->width) / 2);  // maze scratch, in u16 units
   g.bp = c->branching_prob;
   g.row = c->out_row_bytes;
+  g.pool_len = c->map_kind == APG_MAP_POOL ? c->pool_len : 0;
   return g;
 }
 
@@ -103,8 +104,17 @@ int min_row_bytes(const apg_lidar_config *c) {
 int validate(const apg_lidar_config *c) {
   if (!c) return fail(APG_E_INVALID, "null config");
   if (c->num_envs <= 0) return fail(APG_E_INVALID, "num_envs must be positive");
-  if (c->height < 3 || c->width < 3) return fail(APG_E_INVALID, "map size must be at least 3");
-  if (c->map_kind == APG_MAP_ROOMS) {
+  if (c->map_kind == APG_MAP_POOL) {  // any FloorMapDataset: any H x W
+    if (c->height < 1 || c->width < 1 || c->height > 511 || c->width > 511)
+      return fail(APG_E_INVALID, "pool maps must be 1 .. 511 cells on each side");
+    if (c->pool_len < 1) return fail(APG_E_INVALID, "the map pool must hold at least one map");
+    if (c->is_static && (c->static_map_index < 0 || c->static_map_index >= c->pool_len))
+      return fail(APG_E_INVALID, "static_map_index is outside the map pool");
+  } else if (c->height < 3 || c->width < 3) {
+    return fail(APG_E_INVALID, "map size must be at least 3");
+  }
+  if (c->map_kind == APG_MAP_POOL) {
+  } else if (c->map_kind == APG_MAP_ROOMS) {
     if (c->height > 511 || c->width > 511) return fail(APG_E_INVALID, "rooms maps must be at most 511 x 511");
     if (c->height != c->width) return fail(APG_E_INVALID, "rooms maps must be square");
     if (c->max_rooms < 1 || c->max_rooms > ROOMS_MAX) return fail(APG_E_INVALID, "max_rooms must be in [1, 64]");
@@ -159,7 +169,8 @@ APG_DEV int place_start(Pcg64 &rng, const uint64_t *rows, int h, int w, int wpr,
 // ------------------------------------------------------------------ kernels
 // Map generator of a kernel instance (template parameter GEN): static maps are generated once by
 // apg_lidar_init, so the reset kernel for them only draws start cells.
-enum : int { GEN_NONE = 0, GEN_ROOMS = 1, GEN_PF = 2 };  // mazes: k_maze (synchronous) or prefetched (GEN_PF)
+// GEN_POOL: maps of the resident pool (APG_MAP_POOL, any FloorMapDataset)
+enum : int { GEN_NONE = 0, GEN_ROOMS = 1, GEN_PF = 2, GEN_POOL = 3 };  // mazes: k_maze (synchronous) or prefetched (GEN_PF)
 
 // Rooms maps are painted into the lane's LDS bitmap (row words are read-modify-written once per
 // primitive), then the wave copies its bitmaps out with coalesced stores.
@@ -226,7 +237,7 @@ APG_DEV int select_bit(uint64_t m, int k) {
 template <int GEN, int MR = 17>
 APG_DEV uint8_t reset_one(const Geo &g, const apg_lidar_state &S, int e, uint8_t f, bool use_seed, uint64_t seed,
                           uint64_t *own, uint64_t *out_map_idx, uint32_t *err, const BinomTable &bt) {
-  static_assert(GEN == GEN_NONE || GEN == GEN_ROOMS, "mazes reset in k_maze");
+  static_assert(GEN == GEN_NONE || GEN == GEN_ROOMS || GEN == GEN_POOL, "mazes reset in k_maze");
   Pcg64 rng;
   Pcg64 it;
   if (use_seed) {
@@ -238,7 +249,17 @@ APG_DEV uint8_t reset_one(const Geo &g, const apg_lidar_state &S, int e, uint8_t
   }
   uint64_t midx;
   float px = 0.5f, py = 0.5f;
-  if constexpr (GEN != GEN_NONE) {
+  if constexpr (GEN == GEN_POOL) {
+    // DatasetIterator: integers(0, len(dataset)) (dataset_iterator.py:26-32), then get_data_point(idx) is pool map idx
+    midx = (uint64_t)integers(it, 0, g.pool_len);
+    const size_t words = (size_t)g.h * g.wpr;
+    uint64_t *rows = S.occ + (size_t)e * words;
+    const uint64_t *src = S.pool_occ + midx * words;
+    for (size_t q = 0; q < words; q++) rows[q] = src[q];
+    if (place_start(rng, rows, g.h, g.w, g.wpr, px, py) != 0) atomicOr(err, APG_ERR_NO_FREE_CELL);
+    *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
+    S.map_idx[e] = midx;
+  } else if constexpr (GEN != GEN_NONE) {
     midx = next32(it);  // DatasetIterator: integers(0, len(dataset) = 2**32)
     Pcg64 map_rng = seed_pcg64(midx);  // FloorMapDataset*.get_data_point: default_rng(idx)
     int rc = rooms_generate<MR>(map_rng, own, g.wpr, g.h, g.max_rooms, g.door_width, bt);
@@ -248,7 +269,8 @@ APG_DEV uint8_t reset_one(const Geo &g, const apg_lidar_state &S, int e, uint8_t
     S.map_idx[e] = midx;
   } else {
     midx = S.map_idx[e];
-    if (place_start(rng, S.occ, g.h, g.w, g.wpr, px, py) != 0) atomicOr(err, APG_ERR_MAPGEN);
+    if (place_start(rng, S.occ, g.h, g.w, g.wpr, px, py) != 0)
+      atomicOr(err, g.kind == APG_MAP_POOL ? APG_ERR_NO_FREE_CELL : APG_ERR_MAPGEN);
   }
   S.pos[2 * e] = px;
   S.pos[2 * e + 1] = py;
@@ -1092,6 +1114,85 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           S.flags[my_e] = (uint8_t)((f0 & F_AUTORESET) | F_JUST_RESET | F_FIRST);
           pf_store_gen(&V.gen[my_e], g0 + 1u);
         }
+      } else if constexpr (GEN == GEN_POOL) {
+        // Maps of the resident pool (any FloorMapDataset, APG_MAP_POOL).  The env's lane draws the DatasetIterator
+        // index, integers(0, len(dataset)) (dataset_iterator.py:26-32), and the start-cell pick from the pool map's
+        // free-cell count (lidar_localization2d.py:302-304); then each wave copies the pool rows of its pending envs
+        // into their occupancy (lane = row, coalesced) and finds the pick-th free cell in row-major order on the way.
+        // The f32 map obs (:299) is written from the copied rows by phase 0 like every unfused reset.
+        Pcg64 rng, it;
+        uint64_t midx = 0;
+        long long pick = -1;
+        if (pend) {
+          rng = *reinterpret_cast<const Pcg64 *>(&S.rng[my_e]);
+          it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[my_e]);
+          midx = (uint64_t)integers(it, 0, g.pool_len);
+          const int nfree = S.pool_free[midx];
+          if (nfree > 0) pick = (long long)integers(rng, 0, nfree);
+        }
+        const int wpr = P.wpr;
+        for (int j = 0; j < LPW; j++) {
+          if (!__shfl((int)pend, j)) continue;  // wave-uniform
+          const int el = j * W + wave, e = base + el;
+          const uint64_t mj = ((uint64_t)(uint32_t)__shfl((int)(midx >> 32), j) << 32) | (uint32_t)__shfl((int)midx, j);
+          const long long pj = ((long long)__shfl((int)((unsigned long long)pick >> 32), j) << 32) |
+                               (uint32_t)__shfl((int)pick, j);
+          const uint64_t *src = S.pool_occ + mj * words;
+          uint64_t *dst = S.occ + (size_t)e * words;
+          if (lane == 0) s_start[el] = ~0u;
+          int off = 0;
+          for (int y0 = 0; y0 < P.h; y0 += 64) {
+            const int y = y0 + lane;
+            int fr = 0;
+            if (y < P.h) {
+              int occ = 0;
+              for (int k = 0; k < wpr; k++) {
+                const uint64_t v = src[(size_t)y * wpr + k];
+                dst[(size_t)y * wpr + k] = v;
+                occ += __popcll(v);
+              }
+              fr = P.w - occ;
+            }
+            const int incl = wave_inclusive_scan(fr, lane) + off;
+            const int excl = incl - fr;
+            if (y < P.h && pj >= excl && pj < incl) {  // the pick-th free cell is in this lane's row
+              int k2 = (int)(pj - excl), x = -1;
+              for (int k = 0; k < wpr && x < 0; k++) {
+                const int lo = 64 * k;
+                const uint64_t valid = P.w - lo >= 64 ? ~0ULL : ((1ULL << (P.w - lo)) - 1ULL);
+                const uint64_t fm = ~src[(size_t)y * wpr + k] & valid;
+                const int c = __popcll(fm);
+                if (k2 < c) x = lo + select_bit(fm, k2);
+                else k2 -= c;
+              }
+              s_start[el] = ((uint32_t)y << 16) | (uint32_t)x;
+            }
+            off = __shfl(incl, 63);
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // s_start of the wave's envs
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (pend) {
+          const uint32_t sc = s_start[my_el];
+          float px = 0.5f, py = 0.5f;
+          if (sc == ~0u) {
+            atomicOr(O.err, APG_ERR_NO_FREE_CELL);  // integers(0, 0): numpy's ValueError
+          } else {
+            px = __fadd_rn((float)(sc & 0xFFFFu), 0.5f);
+            py = __fadd_rn((float)(sc >> 16), 0.5f);
+          }
+          S.pos[2 * my_e] = px;
+          S.pos[2 * my_e + 1] = py;
+          S.init_pos[2 * my_e] = px;
+          S.init_pos[2 * my_e + 1] = py;
+          S.elapsed[my_e] = 0;
+          S.flags[my_e] = (uint8_t)((f0 & F_AUTORESET) | F_JUST_RESET | F_FIRST);
+          *reinterpret_cast<Pcg64 *>(&S.rng[my_e]) = rng;
+          *reinterpret_cast<Pcg64 *>(&S.it_rng[my_e]) = it;
+          S.map_idx[my_e] = midx;
+          if (O.map_idx) oat(O.map_idx, P.row, my_e, 1) = midx;
+        }
       } else if constexpr (GEN == GEN_ROOMS) {
         // R1: the env's streams, its next map index and the map's primitives, generated with the
         // working storage interleaved in LDS (a private-array generator would live in scratch memory)
@@ -1762,7 +1863,7 @@ int rooms_lanes(const Geo &g, int n) {
 template <int GEN, int MR>
 int launch_reset_mr(const Geo &g, const apg_lidar_state *st, uint64_t seed, int use_seed, int all,
                     const apg_lidar_outputs *out, hipStream_t s) {
-  const int lanes = GEN == GEN_NONE ? 64 : rooms_lanes(g, g.n);
+  const int lanes = GEN == GEN_ROOMS ? rooms_lanes(g, g.n) : 64;
   size_t dyn;
   if (int rc = gen_lds(k_lidar_reset<GEN, MR>, GEN, g, lanes, dyn)) return rc;
   hipLaunchKernelGGL((k_lidar_reset<GEN, MR>), dim3(grid_for(g.n, lanes)), dim3(64), dyn, s, g, *st, seed, use_seed,
@@ -1846,6 +1947,7 @@ int launch_maze(const Geo &g, const apg_lidar_state &st, const uint64_t *idx, in
 int launch_reset(const Geo &g, const apg_lidar_state *st, uint64_t seed, int use_seed, int all,
                  const apg_lidar_outputs *out, hipStream_t s) {
   if (g.is_static) return launch_reset_gen<GEN_NONE>(g, st, seed, use_seed, all, out, s);
+  if (g.kind == APG_MAP_POOL) return launch_reset_gen<GEN_POOL>(g, st, seed, use_seed, all, out, s);
   if (g.kind == APG_MAP_MAZE)
     return launch_maze(g, *st, nullptr, g.n, nullptr, reinterpret_cast<uint8_t *>(st->stack), MZ_RESET, seed, use_seed,
                        all, out->map_idx, out->map_obs, out->err, s);
@@ -1889,6 +1991,7 @@ bool big_rooms(const apg_lidar_config *c) {
 
 int step_gen(const Geo &g) {
   if (g.is_static) return GEN_NONE;
+  if (g.kind == APG_MAP_POOL) return GEN_POOL;
   return GEN_ROOMS;  // mazes: GEN_PF (prefetched), or k_maze (autoresets) + the unfused step kernel
 }
 
@@ -1919,7 +2022,7 @@ int step_epb(int n) {
     const char *s = getenv("APG_STEP_EPB");
     forced = s ? atoi(s) : 0;
   }
-  if (forced == 64 || forced == 128 || forced == 256) return forced;
+  if (forced == 64 || forced == 256) return forced;  // (128: measured slower in r02, no longer instantiated)
   return (int64_t)n >= (int64_t)256 * cu_count() ? 256 : 64;
 }
 
@@ -1945,13 +2048,15 @@ int launch_step_epb(const StepParams &P, const Geo &g, const apg_lidar_state *st
     if (!fused) return launch_step_t<GEN_NONE, false, 64, true>(P, g, st, act, pred, out, s, V);
     switch (step_gen(g)) {
       case GEN_ROOMS: return launch_step_t<GEN_ROOMS, true, 64, true>(P, g, st, act, pred, out, s, V);
+      case GEN_POOL: return launch_step_t<GEN_POOL, true, 64, true>(P, g, st, act, pred, out, s, V);
       default: return launch_step_t<GEN_NONE, true, 64, true>(P, g, st, act, pred, out, s, V);
     }
   }
   if (!fused) return launch_step_t<GEN_NONE, false, EPB>(P, g, st, act, pred, out, s, V);
-  if (pf) return launch_step_t<GEN_PF, true, EPB == 128 ? 256 : EPB>(P, g, st, act, pred, out, s, V);
+  if (pf) return launch_step_t<GEN_PF, true, EPB>(P, g, st, act, pred, out, s, V);
   switch (step_gen(g)) {
     case GEN_ROOMS: return launch_step_t<GEN_ROOMS, true, EPB>(P, g, st, act, pred, out, s, V);
+    case GEN_POOL: return launch_step_t<GEN_POOL, true, EPB>(P, g, st, act, pred, out, s, V);
     default: return launch_step_t<GEN_NONE, true, EPB>(P, g, st, act, pred, out, s, V);
   }
 }
@@ -1999,7 +2104,6 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
   int rc;
   switch (step_epb(P.n)) {
     case 256: rc = launch_step_epb<256>(P, g, st, act, pred, out, s, fused, pf); break;
-    case 128: rc = launch_step_epb<128>(P, g, st, act, pred, out, s, fused, pf); break;
     default: rc = launch_step_epb<64>(P, g, st, act, pred, out, s, fused, pf); break;
   }
   if (rc || !P.log_stats || P.step_limit <= PW_PTR_MAX_N) return rc;
@@ -2165,7 +2269,7 @@ bool capturing(hipStream_t s) {
 
 extern "C" {
 
-const char *apg_version(void) { return "apgym-mi355x 0.2.0 (gfx950)"; }
+const char *apg_version(void) { return "apgym-mi355x 0.3.0 (gfx950)"; }
 const char *apg_last_error(void) { return g_err; }
 
 int apg_lidar_query_sizes(const apg_lidar_config *cfg, apg_lidar_state_sizes *o) {
@@ -2187,10 +2291,19 @@ int apg_lidar_query_sizes(const apg_lidar_config *cfg, apg_lidar_state_sizes *o)
 int apg_lidar_init(const apg_lidar_config *cfg, const apg_lidar_state *st, apg_stream_t stream) {
   int rc = validate(cfg);
   if (rc) return rc;
+  if (cfg->map_kind == APG_MAP_POOL && (!st->pool_occ || !st->pool_free))
+    return fail(APG_E_INVALID, "pool maps need the pool_occ and pool_free buffers");
   if (!cfg->is_static) return APG_OK;
   // One map for every env: generate dataset[static_map_index] once.
   Geo g = make_geo(cfg);
   hipStream_t s = (hipStream_t)stream;
+  if (cfg->map_kind == APG_MAP_POOL) {  // dataset[static_map_index] is pool map static_map_index
+    const size_t bytes = (size_t)g.h * g.wpr * sizeof(uint64_t);
+    if (hipMemcpyAsync(st->occ, st->pool_occ + (size_t)cfg->static_map_index * g.h * g.wpr, bytes,
+                       hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return fail(APG_E_LAUNCH, "hipMemcpyAsync (static pool map)");
+    return APG_OK;
+  }
   // map_idx[0] already holds static_map_index (the host fills the state before init)
   return launch_map_generate_any(g, (const uint64_t *)st->map_idx, 1, st->occ, st->stack, nullptr, s);
 }
@@ -2199,6 +2312,8 @@ int apg_lidar_reset(const apg_lidar_config *cfg, const apg_lidar_state *st, uint
                     const apg_lidar_outputs *out, apg_stream_t stream) {
   int rc = validate(cfg);
   if (rc) return rc;
+  if (cfg->map_kind == APG_MAP_POOL && (!st->pool_occ || !st->pool_free))
+    return fail(APG_E_INVALID, "pool maps need the pool_occ and pool_free buffers");
   hipStream_t s = (hipStream_t)stream;
   Geo g = make_geo(cfg);
   apg_lidar_prefetcher *p = prefetcher_of(cfg, st);
@@ -2240,6 +2355,8 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
   if (cfg->log_stats && (!st->stats_hist || !out->stats || !out->stats_len))
     return fail(APG_E_INVALID, "log_stats needs stats_hist, stats and stats_len buffers");
   if (cfg->sparse && !out->weight) return fail(APG_E_INVALID, "sparse needs the weight buffer");
+  if (cfg->map_kind == APG_MAP_POOL && (!st->pool_occ || !st->pool_free))
+    return fail(APG_E_INVALID, "pool maps need the pool_occ and pool_free buffers");
   hipStream_t s = (hipStream_t)stream;
   // rooms / static maps: one launch per step, the fused step kernel performs the NEXT_STEP autoresets itself;
   // mazes with a prefetcher: one launch per step, the fused step kernel installs the prefetched next maps;

@@ -78,9 +78,14 @@ extern "C" {
 #define APG_ERR_OOB_Y 8u          /* "One of the requested xi is out of bounds in dimension 0" */
 #define APG_ERR_OOB_X 16u         /* "One of the requested xi is out of bounds in dimension 1" */
 #define APG_ERR_PREFETCH 32u      /* a maze autoreset found no prefetched map (prefetch protocol violated) */
+#define APG_ERR_NO_FREE_CELL 64u  /* a pool map without a free cell was drawn: numpy's integers(0, 0) raises
+                                     ValueError("high <= 0") in reset (lidar_localization2d.py:302-303) */
 
 #define APG_MAP_ROOMS 0
 #define APG_MAP_MAZE 1
+#define APG_MAP_POOL 2 /* maps of any FloorMapDataset, read once into a resident pool (state.pool_occ):
+                          ap_gym/envs/floor_map/floor_map_dataset.py:10-22, drawn per episode as
+                          DatasetIterator does, ap_gym/envs/dataset/dataset_iterator.py:26-32 */
 
 typedef void *apg_stream_t; /* hipStream_t */
 
@@ -92,8 +97,9 @@ typedef struct apg_pcg64 {
 
 typedef struct apg_lidar_config {
   int32_t num_envs;
-  int32_t height, width;        /* map size in cells, 3 .. 511 each; rooms maps must be square, mazes odd */
-  int32_t map_kind;             /* APG_MAP_ROOMS | APG_MAP_MAZE */
+  int32_t height, width;        /* map size in cells, 3 .. 511 each (pool maps 1 .. 511); rooms maps must be square,
+                                   mazes odd; pool maps any H x W */
+  int32_t map_kind;             /* APG_MAP_ROOMS | APG_MAP_MAZE | APG_MAP_POOL */
   int32_t is_static;            /* 1: one map for all envs (static_map=True) */
   int32_t static_map_index;     /* dataset index of the static map */
   int32_t beams;                /* lidar_beam_count */
@@ -115,6 +121,10 @@ typedef struct apg_lidar_config {
                                    16 + 4 * beams + 36 bytes, + 8 with sparse, + 20 with log_stats, rounded up to
                                    a multiple of 8).  Added in ABI 0.2 (apg_version): callers built against 0.1
                                    must zero it. */
+  int32_t pool_len;             /* APG_MAP_POOL: len(dataset), 1 .. 2**31 - 1 maps in state.pool_occ; the episode's
+                                   map is pool map integers(0, pool_len) of the env's DatasetIterator stream
+                                   (dataset_iterator.py:26-32), the static map pool map static_map_index.
+                                   Other kinds: ignored (ABI 0.3) */
 } apg_lidar_config;
 
 /* Persistent per-env state.  Sizes come from apg_lidar_query_sizes(). */
@@ -136,6 +146,11 @@ typedef struct apg_lidar_state {
                           every env, generated ahead of its autoreset (mazes up to 128 rows) */
   void *prefetcher;    /* apg_lidar_prefetcher_create() handle owning the side stream that fills `prefetch`, or
                           NULL (then mazes are generated synchronously by the autoreset step) */
+  const uint64_t *pool_occ;  /* APG_MAP_POOL: [pool_len][H][wpr] bit-packed maps (bit x % 64 of word x / 64 of row
+                                y is map[y, x]; bits past W zero), i.e. dataset.get_data_point(i) for every i;
+                                NULL for the procedural kinds (ABI 0.3) */
+  const int32_t *pool_free;  /* APG_MAP_POOL: [pool_len] free cells of each pool map (the start-cell draw's
+                                integers(0, nfree), lidar_localization2d.py:302-304) */
 } apg_lidar_state;
 
 typedef struct apg_lidar_outputs {

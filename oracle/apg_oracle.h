@@ -57,12 +57,15 @@ float orc_lidar_scan(const uint8_t *map, int h, int w, float px, float py, float
 
 /* Vectorised LIDAR env (SyncVectorEnv of TimeLimit(LIDARLocalization2DEnv) restated). */
 typedef struct orc_lidar_env orc_lidar_env;
-orc_lidar_env *orc_lidar_create(int num_envs, int map_kind /*0 rooms, 1 maze*/, int h, int w,
+orc_lidar_env *orc_lidar_create(int num_envs, int map_kind /*0 rooms, 1 maze, 2 pool*/, int h, int w,
                                 int static_map, int static_map_index, int beams, float lidar_range,
                                 int step_limit, const float *beam_dirs /*[beams][2], scaled*/);
 void orc_lidar_destroy(orc_lidar_env *e);
 /* rooms parameters of the dynamic maps of later resets (defaults 10, 3) */
 void orc_lidar_set_rooms(orc_lidar_env *e, int max_rooms, int door_width);
+/* kind 2: the maps of any finite FloorMapDataset, [pool_len][h][w] 0/1 bytes (borrowed), before reset */
+int orc_lidar_set_pool(orc_lidar_env *e, const uint8_t *maps, int64_t pool_len, int static_map_index);
+int orc_lidar_no_free(const orc_lidar_env *e);
 /* reset(seed=seed): sub-env i seeded with seed+i. Writes obs. */
 void orc_lidar_reset(orc_lidar_env *e, uint64_t seed, float *lidar, float *odometry,
                      float *time_step, float *map_obs /*may be NULL*/, uint64_t *map_idx);

@@ -336,6 +336,8 @@ float orc_lidar_scan(const uint8_t *map, int h, int w, float fpx, float fpy, flo
 struct orc_lidar_env {
   int n, kind, h, w, is_static, beams, step_limit;
   int max_rooms, door_width; /* FloorMapDatasetRooms parameters of the dynamic maps (default 10, 3) */
+  const uint8_t *pool;       /* kind 2: the dataset's maps [pool_len][h][w] (borrowed), any FloorMapDataset */
+  int64_t pool_len;
   float range;
   float *dirs;        /* [beams][2] scaled beam vectors (lidar_directions) */
   orc_pcg64 *rng;     /* env np_random */
@@ -346,6 +348,7 @@ struct orc_lidar_env {
   int32_t *elapsed;
   uint8_t *first_step; /* pos/initial_pos still alias the same ndarray (reset :305) */
   uint8_t *autoreset;
+  int no_free; /* a map without free cells was drawn (sticky) */
 };
 
 orc_lidar_env *orc_lidar_create(int num_envs, int map_kind, int h, int w, int static_map,
@@ -373,15 +376,16 @@ orc_lidar_env *orc_lidar_create(int num_envs, int map_kind, int h, int w, int st
   e->elapsed = (int32_t *)calloc(num_envs, sizeof(int32_t));
   e->first_step = (uint8_t *)calloc(num_envs, 1);
   e->autoreset = (uint8_t *)calloc(num_envs, 1);
-  if (static_map) {
+  if (static_map && map_kind != 2) {
     int r = map_kind == 0 ? orc_rooms_map((uint64_t)static_map_index, h, w, 10, 3, e->maps)
                           : orc_maze_map((uint64_t)static_map_index, h, w, 1.0, e->maps);
     if (r != 0) {
       orc_lidar_destroy(e);
       return NULL;
     }
-    for (int i = 0; i < num_envs; i++) e->map_idx[i] = (uint64_t)static_map_index;
   }
+  if (static_map)
+    for (int i = 0; i < num_envs; i++) e->map_idx[i] = (uint64_t)static_map_index;
   return e;
 }
 
@@ -427,7 +431,13 @@ static void write_obs(orc_lidar_env *e, int i, float *lidar, float *odometry, fl
 }
 
 static void env_reset_one(orc_lidar_env *e, int i) {
-  if (!e->is_static) {
+  if (!e->is_static && e->kind == 2) {
+    /* DatasetIterator.__next__ (dataset_iterator.py:26-32): idx = rng.integers(0, len(dataset)), then
+       dataset.get_data_point(idx) -- the pool's map idx */
+    uint64_t idx = (uint64_t)orc_integers(&e->it_rng[i], 0, e->pool_len);
+    memcpy(e->maps + (size_t)i * e->h * e->w, e->pool + (size_t)idx * e->h * e->w, (size_t)e->h * e->w);
+    e->map_idx[i] = idx;
+  } else if (!e->is_static) {
     uint64_t idx = (uint64_t)orc_next32(&e->it_rng[i]); /* integers(0, 2**32) */
     uint8_t *m = e->maps + (size_t)i * e->h * e->w;
     if (e->kind == 0)
@@ -439,6 +449,14 @@ static void env_reset_one(orc_lidar_env *e, int i) {
   const uint8_t *m = env_map(e, i);
   int64_t nfree = 0;
   for (int k = 0; k < e->h * e->w; k++) nfree += m[k] == 0;
+  if (nfree == 0) { /* numpy raises ValueError("high <= 0") (lidar_localization2d.py:302-303) */
+    e->no_free = 1;
+    e->pos[2 * i] = e->pos[2 * i + 1] = 0.5f;
+    e->init_pos[2 * i] = e->init_pos[2 * i + 1] = 0.5f;
+    e->first_step[i] = 1;
+    e->elapsed[i] = 0;
+    return;
+  }
   int64_t pick = orc_integers(&e->rng[i], 0, nfree);
   int64_t c = -1;
   for (int k = 0; k < e->h * e->w; k++) {
@@ -607,3 +625,19 @@ void orc_lidar_set_rooms(orc_lidar_env *e, int max_rooms, int door_width) {
   e->max_rooms = max_rooms;
   e->door_width = door_width;
 }
+
+/* kind 2 (any finite FloorMapDataset): its maps [pool_len][h][w] (0/1 bytes, borrowed: the caller keeps them alive).
+   Static envs take pool map static_map_index (lidar_localization2d.py:177-178). */
+int orc_lidar_set_pool(orc_lidar_env *e, const uint8_t *maps, int64_t pool_len, int static_map_index) {
+  if (e->kind != 2 || pool_len < 1) return -1;
+  e->pool = maps;
+  e->pool_len = pool_len;
+  if (e->is_static) {
+    if (static_map_index < 0 || static_map_index >= pool_len) return -1;
+    memcpy(e->maps, maps + (size_t)static_map_index * e->h * e->w, (size_t)e->h * e->w);
+  }
+  return 0;
+}
+
+/* 1 once a map without a free cell was drawn (the reference raised ValueError there) */
+int orc_lidar_no_free(const orc_lidar_env *e) { return e->no_free; }

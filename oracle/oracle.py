@@ -47,6 +47,10 @@ def lib():
         L.orc_lidar_step_mt.restype = i32
         L.orc_lidar_step_mt.argtypes = [vp, i32] + [vp] * 14
         L.orc_lidar_get_state.argtypes = [vp, vp, vp, vp, vp]
+        L.orc_lidar_set_pool.restype = i32
+        L.orc_lidar_set_pool.argtypes = [vp, vp, ctypes.c_int64, i32]
+        L.orc_lidar_no_free.restype = i32
+        L.orc_lidar_no_free.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -88,21 +92,32 @@ class OracleLidarVectorEnv:
     """SyncVectorEnv(TimeLimit(LIDARLocalization2DEnv)) restated in C; numpy in/out."""
 
     def __init__(self, num_envs, map_kind="rooms", size=32, static_map=False, static_map_index=0, beams=8,
-                 lidar_range=5, step_limit=100, sparse=False, max_rooms=10, door_width=3):
-        self.n, self.h, self.w, self.beams = num_envs, size, size, beams
+                 lidar_range=5, step_limit=100, sparse=False, max_rooms=10, door_width=3, pool=None):
+        """map_kind "pool": `pool` holds the maps of a finite FloorMapDataset, bool [len, H, W] (any H x W)."""
+        if map_kind == "pool":
+            self._pool = np.ascontiguousarray(np.asarray(pool, dtype=bool).view(np.uint8))
+            size_hw = self._pool.shape[1:]
+        else:
+            size_hw = (size, size)
+        self.n, self.beams = num_envs, beams
+        self.h, self.w = size_hw
+        size = self.h
         self.static = static_map
         self.dirs = beam_directions(beams, lidar_range)
-        self._e = lib().orc_lidar_create(num_envs, 0 if map_kind == "rooms" else 1, size, size, int(static_map),
+        kind = {"rooms": 0, "maze": 1, "pool": 2}[map_kind]
+        self._e = lib().orc_lidar_create(num_envs, kind, self.h, self.w, int(static_map),
                                          static_map_index, beams, float(lidar_range), step_limit, _p(self.dirs))
         if not self._e:
             raise ValueError("invalid map configuration")
+        if kind == 2 and lib().orc_lidar_set_pool(self._e, _p(self._pool), len(self._pool), static_map_index) != 0:
+            raise ValueError("invalid map pool / static_map_index")
         if (max_rooms, door_width) != (10, 3):
             lib().orc_lidar_set_rooms(self._e, max_rooms, door_width)
         n = num_envs
         self.lidar = np.zeros((n, beams), np.float32)
         self.odometry = np.zeros((n, 2), np.float32)
         self.time_step = np.zeros(n, np.float32)
-        self.map = None if static_map else np.zeros((n, size, size), np.float32)
+        self.map = None if static_map else np.zeros((n, self.h, self.w), np.float32)
         self.map_idx = np.zeros(n, np.uint64)
         self.reward = np.zeros(n, np.float64)
         self.terminated = np.zeros(n, np.uint8)
@@ -147,6 +162,10 @@ class OracleLidarVectorEnv:
             self.weight = np.where(m, w.astype(np.float64), 0.0)
             self.reward = np.where(m, r, 0.0)
         return rc
+
+    def no_free_cell(self) -> bool:
+        """A map without free cells was drawn (the reference raised ValueError("high <= 0") there)."""
+        return bool(lib().orc_lidar_no_free(self._e))
 
     def state(self):
         n = self.n

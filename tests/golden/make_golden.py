@@ -183,7 +183,8 @@ def _reset_prediction_info_shim(ap):
     return ResetPredictionInfo
 
 
-def run_lidar_env(name, dataset, static, beams, n_envs, steps, seed, action_mode, sparse=False):
+def run_lidar_env(name, dataset, static, beams, n_envs, steps, seed, action_mode, sparse=False, static_map_index=0,
+                  extra=None):
     lmod = _lidar_module()
     gym = sys.modules["gymnasium"]
     ap = sys.modules["ap_gym"]
@@ -191,7 +192,7 @@ def run_lidar_env(name, dataset, static, beams, n_envs, steps, seed, action_mode
 
     def mk():
         env = lmod.LIDARLocalization2DEnv(dataset=dataset, static_map=static, lidar_beam_count=beams,
-                                          prefetch=False)
+                                          prefetch=False, static_map_index=static_map_index)
         env = ap.TimeLimit(env, max_episode_steps=100, issue_termination=True)
         env = ap.ActiveRegressionLogWrapper(env)
         # the "-sparse" ids (registration.py:115-142): SparsifyWrapper over the registered composition
@@ -269,7 +270,76 @@ def run_lidar_env(name, dataset, static, beams, n_envs, steps, seed, action_mode
          reset_lidar=reset_obs["lidar"], reset_odometry=reset_obs["odometry"],
          reset_time_step=reset_obs["time_step"], reset_map_idx=reset_map_idx,
          reset_map=(np.packbits(reset_obs["map"][..., 0] > 0, axis=-1) if "map" in reset_obs
-                    else np.zeros(0, np.uint8)), **arrays)
+                    else np.zeros(0, np.uint8)), **arrays, **(extra or {}))
+
+
+def fixed_floor_maps(n=37, h=40, w=48, seed=2024, open_every=0):
+    """The maps of the custom-dataset fixtures: walls, blocks and scattered cells; map 7 has 6 free cells.  With
+    open_every = k every k-th map has no border (agents walk off it: early terminations).  Only square maps may be
+    open: for H != W the reference's __get_obs raises IndexError once a scan point passes the map edge
+    (lidar_localization2d.py:254-259 compares (x, y) with map.shape = (h, w))."""
+    rng = np.random.default_rng(seed)
+    maps = np.zeros((n, h, w), bool)
+    for i in range(n):
+        m = maps[i]
+        if not open_every or i % open_every != open_every - 1:
+            m[0, :] = m[-1, :] = m[:, 0] = m[:, -1] = True
+        for _ in range(int(rng.integers(2, 9))):
+            y, x = int(rng.integers(0, h)), int(rng.integers(0, w))
+            if rng.random() < 0.5:  # a wall line
+                if rng.random() < 0.5:
+                    m[y, x:x + int(rng.integers(3, 30))] = True
+                else:
+                    m[y:y + int(rng.integers(3, 30)), x] = True
+            else:  # a block
+                m[y:y + int(rng.integers(1, 8)), x:x + int(rng.integers(1, 8))] = True
+        m |= rng.random((h, w)) < 0.02
+    maps[7] = True
+    maps[7, h // 2:h // 2 + 2, w // 2:w // 2 + 3] = False
+    return maps
+
+
+def make_pool():
+    """LIDAR envs over a user FloorMapDataset subclass (floor_map_dataset.py:10-22): the DatasetIterator draws
+    integers(0, len(dataset)) (dataset_iterator.py:26-32), any H x W."""
+    fm = refload.load("envs.floor_map")
+    maps = fixed_floor_maps()
+
+    class FixedFloorMaps(fm.FloorMapDataset):
+        def __init__(self, m):
+            super().__init__(m.shape[2], m.shape[1])
+            self._m = m
+
+        def _get_length(self):
+            return len(self._m)
+
+        def get_data_point(self, idx):
+            return self._m[int(idx)].copy()
+
+        def get_data_point_batch(self, idx):
+            return self._m[np.asarray(idx)].copy()
+
+    def extra(m):
+        return dict(pool_bits=np.packbits(m, axis=-1), pool_hw=np.array(m.shape[1:]))
+
+    def first_seed(fn, seeds):
+        """fn(seed) for the first seed whose reference run does not raise IndexError: for H != W the reference's
+        __get_obs indexes observation_map with scan points it bounds-checks against the swapped shape
+        (lidar_localization2d.py:254-259), which raises once a non-occluded scan point passes the bottom edge
+        (the "touch plus crossing is no hit" beams pass through the border wall)."""
+        for sd in seeds:
+            try:
+                return fn(sd)
+            except IndexError as e:
+                print("seed", sd, "raised IndexError in the reference:", e)
+        raise RuntimeError("no seed ran through")
+
+    first_seed(lambda sd: run_lidar_env("pool48x40_b16", FixedFloorMaps(maps), False, 16, 8, 110, sd, "wide",
+                                        extra=extra(maps)), range(5, 40))
+    first_seed(lambda sd: run_lidar_env("pool48x40_static_b8", FixedFloorMaps(maps), True, 8, 6, 60, sd, "uniform",
+                                        static_map_index=5, extra=extra(maps)), range(2, 40))
+    open_maps = fixed_floor_maps(23, 36, 36, seed=7, open_every=3)
+    run_lidar_env("pool36_open_b8", FixedFloorMaps(open_maps), False, 8, 12, 110, 11, "wide", extra=extra(open_maps))
 
 
 def make_lidar_env():
@@ -744,7 +814,7 @@ def make_hf():
 SECTIONS = {"rng": make_rng, "maps": make_maps, "loss": make_loss, "scan": make_lidar_scan,
             "lidar": make_lidar_env, "image": make_image_env,
             "sparse": make_sparse_env, "circle_square": make_circle_square,
-            "light_dark": make_light_dark, "render": make_render, "hf": make_hf}
+            "light_dark": make_light_dark, "render": make_render, "hf": make_hf, "pool": make_pool}
 
 
 def main(argv):

@@ -22,10 +22,49 @@ ENV_CASES = {
     "maze21_b8_grid": ("maze", 21, False, 8),
     "maze127_b64": ("maze", 127, False, 64),
     "maze21_b8_sparse": ("maze", 21, False, 8),  # LIDARLocMaze-sparse-v0 (SparsifyWrapper per sub-env)
+    # a user FloorMapDataset subclass (make_golden.make_pool): the resident map pool (APG_MAP_POOL)
+    "pool48x40_b16": ("pool", 0, False, 16),
+    "pool48x40_static_b8": ("pool", 0, True, 8),
+    "pool36_open_b8": ("pool", 0, False, 8),
 }
+POOL_STATIC_INDEX = 5  # make_golden.make_pool's static_map_index
 
 
-def _ds(ap, kind, size):
+class UserFloorMaps:
+    """Stand-in for a user subclass of the reference's FloorMapDataset (floor_map_dataset.py:10-22, not importable
+    on the GPU box): the interface the reference env uses -- map_width / map_height, load, __len__,
+    get_data_point(idx) -> bool [H, W].  The backend sees it through ForeignFloorMapView."""
+
+    def __init__(self, maps):
+        self._m = np.asarray(maps, dtype=bool)
+        self.loads = 0
+
+    @property
+    def map_width(self):
+        return self._m.shape[2]
+
+    @property
+    def map_height(self):
+        return self._m.shape[1]
+
+    def load(self):
+        self.loads += 1
+
+    def __len__(self):
+        return len(self._m)
+
+    def get_data_point(self, idx):
+        return self._m[int(idx)].copy()
+
+
+def pool_maps(d) -> np.ndarray:
+    h, w = (int(x) for x in d["pool_hw"])
+    return np.unpackbits(d["pool_bits"], axis=-1)[..., :w].astype(bool).reshape(-1, h, w)
+
+
+def _ds(ap, kind, size, d=None):
+    if kind == "pool":
+        return UserFloorMaps(pool_maps(d))
     return ap.FloorMapDatasetRooms(size, size) if kind == "rooms" else ap.FloorMapDatasetMaze(size, size)
 
 
@@ -249,9 +288,10 @@ def test_vector_env_matches_reference_trace(gpu, name):
     d = golden(f"lidar_env_{name}.npz")
     n = d["actions"].shape[1]
     sparse = name.endswith("_sparse")
-    env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_ds(ap, kind, size), static_map=static,
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_ds(ap, kind, size, d), static_map=static,
                                           lidar_beam_count=beams, device=gpu, log_stats=True, sparse=sparse,
-                                          sparse_reset_info=sparse)
+                                          sparse_reset_info=sparse,
+                                          static_map_index=POOL_STATIC_INDEX if kind == "pool" and static else 0)
     obs, info = env.reset(seed=int(d["seed"]))
     vec_off = 0
     assert np.array_equal(obs["lidar"], d["reset_lidar"])

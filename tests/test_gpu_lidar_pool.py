@@ -1,0 +1,181 @@
+"""GPU parity of the LIDAR envs over an arbitrary FloorMapDataset (the resident map pool, APG_MAP_POOL).
+
+The reference draws an episode's map as `dataset.get_data_point(rng.integers(0, len(dataset)))`
+(ap_gym/envs/dataset/dataset_iterator.py:26-32, lidar_localization2d.py:293-299), so any finite FloorMapDataset
+subclass (floor_map_dataset.py:10-22) drives the env.  Here the maps are read once into HBM and the step kernel's
+autoreset copies the drawn pool map.  Checked bit for bit against the C oracle (itself pinned to the reference's
+own env over a custom dataset: tests/golden/lidar_env_pool*.npz, test_oracle_golden.py) on seeded inputs, at
+sizes past the fixtures: N = 1024 over 110 steps (TimeLimit crossing), non-square maps with multi-word rows and
+more than 256 rows, long-range scans (global-row walks), static pool maps, tiny maps.
+"""
+
+import numpy as np
+import pytest
+
+from conftest import golden
+from test_gpu_lidar import UserFloorMaps, pool_maps
+
+pytestmark = pytest.mark.gpu
+
+
+def random_pool(n, h, w, seed, open_every=0, density=0.03):
+    """n maps bool [h, w]: border walls (except every open_every-th map), wall lines, blocks, scattered cells;
+    every map keeps free cells."""
+    rng = np.random.default_rng(seed)
+    maps = np.zeros((n, h, w), bool)
+    for i in range(n):
+        m = maps[i]
+        if not open_every or i % open_every:
+            m[0, :] = m[-1, :] = m[:, 0] = m[:, -1] = True
+        for _ in range(int(rng.integers(0, 12))):
+            y, x = int(rng.integers(0, h)), int(rng.integers(0, w))
+            if rng.random() < 0.5:
+                m[y, x:x + int(rng.integers(2, max(3, w // 2)))] = True
+            else:
+                m[y:y + int(rng.integers(2, max(3, h // 2))), x] = True
+        m |= rng.random((h, w)) < density
+        if m.all():
+            m[h // 2, w // 2] = False
+    return maps
+
+
+def _compare(env, ref, obs, rew, term, t, static):
+    assert np.array_equal(obs["lidar"], ref.lidar), t
+    assert np.array_equal(obs["odometry"], ref.odometry), t
+    assert np.array_equal(obs["time_step"], ref.time_step), t
+    assert np.array_equal(rew, ref.reward, equal_nan=True), t
+    assert np.array_equal(term, ref.terminated.astype(bool)), t
+    if not static:
+        assert np.array_equal(obs["map"][..., 0], ref.map), t
+
+
+@pytest.mark.parametrize("case", ["golden48x40_n1024", "wide100x70_r12", "tall300x257", "tiny5x7", "open64"])
+def test_pool_env_matches_oracle(gpu, oracle_mod, case):
+    import ap_gym_amd as ap
+
+    beams, rng_, n, steps, a_scale = 16, 5.0, 1024, 110, 1.5
+    if case == "golden48x40_n1024":  # the fixture's 37 maps at full batch
+        maps = pool_maps(golden("lidar_env_pool48x40_b16.npz"))
+    elif case == "wide100x70_r12":  # H != W, lidar_range > 10: scans read global rows
+        maps, beams, rng_, n = random_pool(300, 70, 100, 1), 32, 12.0, 512
+    elif case == "tall300x257":  # 257 rows (start rows past 255), 5 words per row
+        maps, beams, n = random_pool(17, 257, 300, 2), 8, 64
+    elif case == "tiny5x7":  # maps smaller than the scan window, most beams leave the map
+        maps, beams, n = random_pool(9, 7, 5, 3, open_every=2, density=0.1), 8, 256
+    else:  # square maps with open borders: early terminations, autoresets every few steps
+        maps, n, a_scale = random_pool(64, 64, 64, 4, open_every=2), 1024, 2.5
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=UserFloorMaps(maps), lidar_beam_count=beams,
+                                          lidar_range=rng_, device=gpu)
+    ref = oracle_mod.OracleLidarVectorEnv(n, "pool", 0, False, 0, beams, lidar_range=rng_, pool=maps)
+    obs, info = env.reset(seed=321)
+    ref.reset(321)
+    assert np.array_equal(obs["lidar"], ref.lidar)
+    assert np.array_equal(info["map_idx"], ref.map_idx.astype(np.int64))
+    assert np.array_equal(obs["map"][..., 0], ref.map)
+    rng = np.random.default_rng(17)
+    resets = 0
+    for t in range(steps):
+        a = rng.uniform(-a_scale, a_scale, (n, 2)).astype(np.float32)
+        p = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        ref.step(a, p)
+        _compare(env, ref, obs, rew, term, t, False)
+        if "map_idx" in info:
+            m = info["_map_idx"]
+            resets += int(m.sum())
+            assert np.array_equal(info["map_idx"][m], ref.map_idx.astype(np.int64)[m]), t
+    assert resets >= n  # every env crossed the TimeLimit (and open maps reset earlier)
+    assert not ref.no_free_cell()
+    env.close()
+
+
+@pytest.mark.parametrize("backend", ["numpy", "torch"])
+def test_pool_static_map_matches_oracle(gpu, oracle_mod, backend):
+    import torch
+
+    import ap_gym_amd as ap
+
+    maps, n, idx = random_pool(11, 70, 100, 5), 2048, 3
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=ap.ArrayFloorMapDataset(maps), static_map=True,
+                                          static_map_index=idx, lidar_beam_count=16, device=gpu,
+                                          array_backend=backend)
+    ref = oracle_mod.OracleLidarVectorEnv(n, "pool", 0, True, idx, 16, pool=maps)
+    obs, info = env.reset(seed=5)
+    ref.reset(5)
+    to_np = (lambda x: x.cpu().numpy()) if backend == "torch" else (lambda x: x)
+    assert np.array_equal(to_np(obs["lidar"]), ref.lidar)
+    assert np.all(to_np(info["map_idx"]) == idx)
+    rng = np.random.default_rng(2)
+    for t in range(105):
+        a = rng.uniform(-1.5, 1.5, (n, 2)).astype(np.float32)
+        p = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        if backend == "torch":
+            a, p = torch.as_tensor(a, device=gpu), torch.as_tensor(p, device=gpu)
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        ref.step(to_np(a) if backend == "torch" else a, to_np(p) if backend == "torch" else p)
+        _compare(env, ref, {k: to_np(v) for k, v in obs.items()}, to_np(rew), to_np(term), t, True)
+    env.close()
+
+
+def test_pool_without_free_cell_raises(gpu):
+    """A drawn map without a free cell: numpy's integers(0, 0) raises ValueError("high <= 0") in the reference's
+    reset (lidar_localization2d.py:302-303)."""
+    import ap_gym_amd as ap
+
+    maps = random_pool(3, 9, 9, 6)
+    maps[1] = True
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=4, dataset=ap.ArrayFloorMapDataset(maps), static_map=True,
+                                          static_map_index=1, device=gpu)
+    with pytest.raises(ValueError, match="high <= 0"):
+        env.reset(seed=0)
+    env.close()
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=64, dataset=ap.ArrayFloorMapDataset(maps), device=gpu)
+    with pytest.raises(ValueError, match="high <= 0"):
+        env.reset(seed=0)  # 64 draws from 3 maps: map 1 is drawn
+    env.close()
+
+
+def test_pool_dataset_checks_and_sharing(gpu):
+    """The dataset is loaded like the reference env does (lidar_localization2d.py:176), its maps checked against
+    (map_height, map_width) (:279) and uploaded once per device for every env built on it."""
+    import ap_gym_amd as ap
+
+    maps = random_pool(5, 12, 20, 7)
+    ds = UserFloorMaps(maps)
+    e1 = ap.LIDARLocalization2DVectorEnv(num_envs=8, dataset=ds, device=gpu)
+    view = e1.dataset
+    assert isinstance(view, ap.ForeignFloorMapView) and ds.loads == 1
+    e2 = ap.LIDARLocalization2DVectorEnv(num_envs=8, dataset=view, device=gpu)
+    assert e2._t["pool_occ"].data_ptr() == e1._t["pool_occ"].data_ptr()
+    e1.close()
+    e2.close()
+
+    class WrongShape(UserFloorMaps):
+        def get_data_point(self, idx):
+            return np.zeros((3, 3), bool)
+
+    with pytest.raises(ValueError, match="shape"):
+        ap.LIDARLocalization2DVectorEnv(num_envs=2, dataset=WrongShape(maps), device=gpu)
+    with pytest.raises(IndexError):
+        ap.LIDARLocalization2DVectorEnv(num_envs=2, dataset=UserFloorMaps(maps), static_map=True,
+                                        static_map_index=5, device=gpu)
+
+
+def test_pool_make_vec(gpu, oracle_mod):
+    """ap_gym_amd.make_vec over a user dataset (the registered ids take `dataset=`, registration.py:319-356)."""
+    import ap_gym_amd as ap
+
+    maps = random_pool(40, 48, 48, 8)
+    env = ap.make_vec("LIDARLocRooms-v0", num_envs=256, dataset=UserFloorMaps(maps), device=gpu)
+    ref = oracle_mod.OracleLidarVectorEnv(256, "pool", 0, False, 0, env.lidar_beam_count, pool=maps)
+    obs, _ = env.reset(seed=9)
+    ref.reset(9)
+    assert np.array_equal(obs["lidar"], ref.lidar)
+    rng = np.random.default_rng(3)
+    for t in range(30):
+        a = rng.uniform(-1, 1, (256, 2)).astype(np.float32)
+        p = rng.uniform(-1, 1, (256, 2)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        ref.step(a, p)
+        _compare(env, ref, obs, rew, term, t, False)
+    env.close()

@@ -86,6 +86,69 @@ def test_capi_validation_without_gpu():
         assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == -1
         assert b"out_row_bytes" in N.lib().apg_last_error()
     cfg.out_row_bytes = cfg.log_stats = cfg.sparse = 0
+    # pool maps (any FloorMapDataset): any H x W from 1 to 511, at least one map, static index inside the pool
+    cfg.map_kind, cfg.height, cfg.width, cfg.pool_len = N.APG_MAP_POOL, 40, 48, 37
+    assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0
+    assert sz.wpr == 1 and sz.stack_bytes == 0 and sz.prefetch_bytes == 0
+    cfg.height, cfg.width = 1, 511
+    assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0 and sz.wpr == 8
+    cfg.width = 512
+    assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == -1
+    cfg.width, cfg.pool_len = 48, 0
+    assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == -1
+    assert b"pool" in N.lib().apg_last_error()
+    cfg.pool_len, cfg.is_static, cfg.static_map_index = 37, 1, 37
+    assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == -1
+    cfg.static_map_index = 36
+    assert N.lib().apg_lidar_query_sizes(ctypes.byref(cfg), ctypes.byref(sz)) == 0
+    # the pool buffers are required before anything reaches the device
+    st = N.LidarState()
+    assert N.lib().apg_lidar_init(ctypes.byref(cfg), ctypes.byref(st), None) == -1
+    assert b"pool_occ" in N.lib().apg_last_error()
+
+
+def test_pool_floor_map_datasets_pack_the_maps():
+    """PoolFloorMapDataset.host_pool: bit x % 64 of word x // 64 of row y is map[y, x] (include/apgym_capi.h,
+    apg_lidar_state.pool_occ), free-cell counts per map; ForeignFloorMapView over the reference interface checks
+    shapes (lidar_localization2d.py:279) and dtypes like the reference env relies on them."""
+    import ap_gym_amd as ap
+    from ap_gym_amd.floor_map import as_floor_map_dataset
+
+    rng = np.random.default_rng(0)
+    maps = rng.random((7, 13, 130)) < 0.3
+    ds = ap.ArrayFloorMapDataset(maps)
+    bits, free = ds.host_pool()
+    assert bits.shape == (7, 13, 3) and bits.dtype == np.dtype("<u8")
+    y, x = np.nonzero(np.ones((13, 130), bool))
+    for i in range(7):
+        got = (bits[i][y, x // 64] >> (x % 64).astype(np.uint64)) & np.uint64(1)
+        assert np.array_equal(got.astype(bool), maps[i][y, x])
+        assert free[i] == (~maps[i]).sum()
+    assert np.all(bits[:, :, 2] >> np.uint64(2) == 0)  # no bits past W
+    assert np.array_equal(ds.get_data_point(3), maps[3]) and ds.get_data_point_batch([1, 2]).shape == (2, 13, 130)
+
+    class Ref:  # the reference FloorMapDataset interface
+        map_width, map_height = 130, 13
+
+        def __len__(self):
+            return 7
+
+        def get_data_point(self, i):
+            return maps[i]
+
+    view = as_floor_map_dataset(Ref())
+    assert isinstance(view, ap.ForeignFloorMapView) and len(view) == 7
+    assert np.array_equal(view.host_pool()[0], bits)
+    assert as_floor_map_dataset(ds) is ds
+
+    class Uint8Maps(Ref):
+        def get_data_point(self, i):
+            return maps[i].astype(np.uint8)
+
+    with pytest.raises(TypeError, match="boolean"):
+        as_floor_map_dataset(Uint8Maps()).host_pool()
+    with pytest.raises(TypeError, match="FloorMapDataset"):
+        as_floor_map_dataset(object())
 
 
 def test_mse_loss_matches_reference_golden():
@@ -278,7 +341,7 @@ def test_torch_ops_library_registers_the_ops():
     for name in ("lidar_reset", "lidar_step", "image_reset", "image_step"):
         assert callable(getattr(ops, name)), name
     assert torch.classes.apgym.LidarEnv is not None and torch.classes.apgym.ImageEnv is not None
-    with pytest.raises(RuntimeError, match="14 ints"):
+    with pytest.raises(RuntimeError, match="15 ints"):
         torch.classes.apgym.LidarEnv([1], [0.0], [], [])
 
 

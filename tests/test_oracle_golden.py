@@ -20,7 +20,18 @@ ENV_CASES = {
     "maze21_b8_grid": ("maze", 21, False, 8),
     "maze127_b64": ("maze", 127, False, 64),
     "maze21_b8_sparse": ("maze", 21, False, 8),  # LIDARLocMaze-sparse-v0 (SparsifyWrapper per sub-env)
+    # a user FloorMapDataset subclass of fixed maps (48 wide x 40 high; 36 x 36 with open borders)
+    "pool48x40_b16": ("pool", 0, False, 16),
+    "pool48x40_static_b8": ("pool", 0, True, 8),
+    "pool36_open_b8": ("pool", 0, False, 8),
 }
+POOL_STATIC_INDEX = 5  # make_golden.make_pool's static_map_index
+
+
+def pool_maps(d) -> np.ndarray:
+    """The fixture's dataset maps, bool [len, H, W]."""
+    h, w = (int(x) for x in d["pool_hw"])
+    return np.unpackbits(d["pool_bits"], axis=-1)[..., :w].astype(bool).reshape(-1, h, w)
 
 
 def _draws(O, seed, kind, a=0, b=0, p=0.0, n=8):
@@ -78,7 +89,11 @@ def test_vector_env_trace(oracle_mod, name):
     d = golden(f"lidar_env_{name}.npz")
     n = d["actions"].shape[1]
     sparse = name.endswith("_sparse")
-    env = oracle_mod.OracleLidarVectorEnv(n, kind, size, static, 0, beams, sparse=sparse)
+    if kind == "pool":
+        env = oracle_mod.OracleLidarVectorEnv(n, "pool", 0, static, POOL_STATIC_INDEX if static else 0, beams,
+                                              pool=pool_maps(d))
+    else:
+        env = oracle_mod.OracleLidarVectorEnv(n, kind, size, static, 0, beams, sparse=sparse)
     env.reset(int(d["seed"]))
     assert np.array_equal(env.lidar, d["reset_lidar"])
     assert np.array_equal(env.odometry, d["reset_odometry"])
