@@ -776,6 +776,10 @@ class _ImageVectorEnv(VectorEnv):
         if not getattr(self, "_closed", True):
             self._closed = True
             self.closed = True
+            if getattr(self, "_ahead_stream", None) is not None:
+                # the draw-ahead kernels on the side stream may still write the streams and ahead buffers, which
+                # the caching allocator would otherwise hand to a new allocation of the main stream
+                self._ahead_stream.synchronize()
             self._t = {}
             self._h = None  # the op handle keeps every state/output buffer alive
             self._c_args = None

@@ -96,13 +96,24 @@ def row_views(buf, layout) -> dict:
     return v
 
 
+_NP_DTYPES: dict = {}
+
+
+def np_dtype(dt) -> np.dtype:
+    """numpy dtype of a torch dtype (cached: the numpy backend builds its field views every step)."""
+    r = _NP_DTYPES.get(dt)
+    if r is None:
+        import torch
+
+        r = _NP_DTYPES[dt] = torch.empty((), dtype=dt).numpy().dtype
+    return r
+
+
 def row_views_np(buf: np.ndarray, layout) -> dict:
     """numpy field views of a packed [rows, row_bytes] uint8 host buffer (stats as [4, rows])."""
-    import torch
-
     v = {}
     for name, dt, sh, off in layout:
-        npdt = torch.empty((), dtype=dt).numpy().dtype
+        npdt = np_dtype(dt)
         nb = npdt.itemsize * int(np.prod(sh, dtype=np.int64))
         a = buf[:, off:off + nb].view(npdt)
         a = a[:, 0] if not sh else a.reshape(buf.shape[0], *sh)
@@ -137,9 +148,7 @@ def block_views(buf, layout) -> dict:
     v = {}
     for name, dt, sh, off in layout:
         if isinstance(buf, np.ndarray):
-            import torch
-
-            npdt = torch.empty((), dtype=dt).numpy().dtype
+            npdt = np_dtype(dt)
             v[name] = buf[off:off + npdt.itemsize * int(np.prod(sh, dtype=np.int64))].view(npdt).reshape(sh)
         else:
             nb = torch_elem(dt) * int(np.prod(sh, dtype=np.int64))
@@ -344,6 +353,7 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         self._err_pending = False
         self._autoreset_host = np.zeros(n, dtype=bool)
         self._rows_host = self._rows_np = self._map_host = None  # numpy backend: pinned host mirrors
+        self._ring, self._ring_copy = [], False  # numpy backend: pinned output blocks (_host_block)
         self._map_snapshot = None  # numpy backend, copy=True: read-only map obs shared until the next reset
         self._in_host = self._in_dev = None  # numpy backend: pinned input staging and its device copy
         self._seeded = False
@@ -587,12 +597,17 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
                 p = p.detach().cpu().numpy()
             a_np = np.ascontiguousarray(a, dtype=np.float32).reshape(self.num_envs, 2)
             p_np = np.ascontiguousarray(p, dtype=np.float32).reshape(self.num_envs, 2)
-            active = ~self._autoreset_host
-            bad_a = np.isnan(a_np).any(axis=1) & active
-            bad_p = np.isnan(p_np).any(axis=1) & active
-            if bad_a.any() or bad_p.any():  # first offending sub-env decides, action checked first
-                i = int(np.argmax(bad_a | bad_p))
-                raise ValueError(NAN_ACTION_MSG if bad_a[i] else NAN_PREDICTION_MSG)
+            # one summing pass per input finds that no NaN is present (a NaN or an inf makes the sum non-finite);
+            # only then the per-env check, which raises for the first offending active sub-env, action first
+            if not (np.isfinite(a_np.sum(dtype=np.float64)) and np.isfinite(p_np.sum(dtype=np.float64))):
+                active = ~self._autoreset_host
+                bad_a = np.isnan(a_np).view(np.uint16).reshape(-1) != 0
+                bad_p = np.isnan(p_np).view(np.uint16).reshape(-1) != 0
+                bad_a &= active
+                bad_p &= active
+                if bad_a.any() or bad_p.any():
+                    i = int(np.argmax(bad_a | bad_p))
+                    raise ValueError(NAN_ACTION_MSG if bad_a[i] else NAN_PREDICTION_MSG)
             # one H2D copy of both inputs from a pinned staging buffer (the previous step synchronized, so neither
             # the staging buffer nor the device copy is still in use)
             if self._in_host is None:
@@ -703,22 +718,54 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         obs["time_step"] = c(T["time_step"])
         return obs
 
-    def _host_rows(self) -> dict:
-        """numpy backend: the output block (or the packed output rows) and the error word copied D2H into pinned
-        host memory in one go, then one synchronize; returns numpy field views of the host copy (valid until the
-        next call)."""
+    HOST_RING = 4  # numpy backend, copy=True: pinned output blocks handed out as the returned arrays
+
+    def _host_block(self):
+        """A pinned host block for this step's outputs.  copy=True: a small ring of blocks whose field views ARE the
+        returned arrays (no per-field host copies); a block is reused only once no array of an earlier step still
+        refers to it (its numpy base has no outside references), else another block is pinned, up to HOST_RING;
+        past that (or with copy=False) the outputs land in a private block that is never handed out and the step
+        copies its fields from it (self._ring_copy)."""
+        import sys
+
         import torch
 
         src = self.output_rows if self._out_block is None else self._out_block
-        if self._rows_host is None:
+        if self.copy:
+            for blk in self._ring:
+                if sys.getrefcount(blk[1]) <= 2:  # the ring tuple and the call argument: no returned view is alive
+                    self._ring_copy = False
+                    return blk
+            if len(self._ring) < self.HOST_RING:
+                t = torch.empty(tuple(src.shape), dtype=torch.uint8).pin_memory()
+                self._ring.append((t, t.numpy()))
+                self._ring_copy = False
+                return self._ring[-1]
+        self._ring_copy = True
+        if self._rows_host is None:  # the private block
             self._rows_host = torch.empty(tuple(src.shape), dtype=torch.uint8).pin_memory()
-            self._rows_np = (row_views_np(self._rows_host.numpy(), self.output_layout) if self._out_block is None
-                             else block_views(self._rows_host.numpy(), self._block_layout))
-        self._rows_host.copy_(src, non_blocking=True)
+            self._rows_np = self._rows_host.numpy()
+        return self._rows_host, self._rows_np
+
+    def _host_rows(self) -> dict:
+        """numpy backend: the output block (or the packed output rows) and the error word copied D2H into a pinned
+        host block in one go, then one synchronize; returns fresh numpy field views of that block (copy=True: the
+        block is not written again while any of them is alive, see _host_block)."""
+        import torch
+
+        src = self.output_rows if self._out_block is None else self._out_block
+        blk_t, blk_np = self._host_block()
+        blk_t.copy_(src, non_blocking=True)
         self._err_host.copy_(self._t["err"], non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
         self._err_pending = False
-        return self._rows_np
+        return (row_views_np(blk_np, self.output_layout) if self._out_block is None
+                else block_views(blk_np, self._block_layout))
+
+    def _own(self, a: np.ndarray) -> np.ndarray:
+        """A returned output field: the block view itself, or a copy where the block is shared (copy=False keeps
+        the aliasing mirror semantics; a full ring falls back to copies)."""
+        return a.copy() if self._ring_copy else a
 
     def _map_refresh(self, reset_mask: np.ndarray | None):
         """The host mirror of the map observation, refreshed only for the sub-envs that reset (the map obs
@@ -753,10 +800,10 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
     def _to_numpy_obs(self, R: dict | None = None, reset_mask: np.ndarray | None = None):
         if R is None:
             R = self._host_rows()
-        obs = {"lidar": R["lidar"].copy(), "odometry": R["odometry"].copy()}
+        obs = {"lidar": self._own(R["lidar"]), "odometry": self._own(R["odometry"])}
         if not self.static_map:
             obs["map"] = self._map_refresh(reset_mask)
-        obs["time_step"] = R["time_step"].copy()
+        obs["time_step"] = self._own(R["time_step"])
         return obs
 
     def _numpy_step_result(self):
@@ -767,9 +814,9 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             self._raise_error_bits(bits)
         reset_mask = R["reset_mask"].copy()
         obs = self._to_numpy_obs(R, reset_mask)
-        reward = R["reward"].copy()
-        term = R["terminated"].copy()
-        trunc = R["truncated"].copy()
+        reward = self._own(R["reward"])
+        term = self._own(R["terminated"])
+        trunc = self._own(R["truncated"])
         mask = R["info_mask"].copy()
         info: dict[str, Any] = {}
         if mask.any():

@@ -110,6 +110,7 @@ class ShardedVectorEnv:
         self._index_full = None  # image envs: the gathered info["index"] (changes only with the batch)
         self._done_full = None  # image envs: gathered terminated / truncated / sparse weight constants
         self._tg_full = None  # image localization: the gathered target glimpses (change only with the batch)
+        self._inv_full = self._inv2_full = None  # randomly_invert_labels: gathered inversion flags / constant 2s
         self.time_gather = time_gather
         self.gather_events: list = []  # (begin, end) torch.cuda.Event pairs around each all-gather
 
@@ -181,6 +182,21 @@ class ShardedVectorEnv:
                                         device=local.device)
         return self._all_gather_into(self._tg_full, local.contiguous())
 
+    def _gathered_inverted(self, local):
+        """Image envs with randomly_invert_labels: obs["inverted_label"] of the whole batch.  It is the drawn
+        inversion (int32 0/1) on reset / autoreset steps -- gathered then -- and the constant 2 (int64) on every
+        other step (image_classification.py:130-141), which needs no collective."""
+        import torch
+
+        full = self.world * self.local_num_envs
+        if local.dtype == torch.int64:
+            if self._inv2_full is None:
+                self._inv2_full = torch.full((full,), 2, dtype=torch.int64, device=local.device)
+            return self._c(self._inv2_full)
+        if self._inv_full is None:
+            self._inv_full = torch.zeros(full, dtype=local.dtype, device=local.device)
+        return self._c(self._all_gather_into(self._inv_full, local.contiguous()))
+
     def _pack(self, fields: dict):
         import torch
 
@@ -238,7 +254,7 @@ class ShardedVectorEnv:
             if "target_glimpse" in obs:
                 gobs["target_glimpse"] = self._c(self._gathered_target_glimpse(obs["target_glimpse"]))
             if "inverted_label" in obs:
-                gobs["inverted_label"] = obs["inverted_label"]  # (local: drawn per shard like the index)
+                gobs["inverted_label"] = self._gathered_inverted(obs["inverted_label"])
             return gobs, {"index": self._c(self._gathered_index(info["index"])), "local_obs": obs,
                           "local_info": info}
         gobs = {"lidar": v["lidar"], "odometry": v["odometry"], "time_step": v["time_step"]}
@@ -310,7 +326,7 @@ class ShardedVectorEnv:
                 self._gathered_target_glimpse(obs["target_glimpse"])
             gobs["target_glimpse"] = self._c(self._tg_full)
         if "inverted_label" in obs:
-            gobs["inverted_label"] = obs["inverted_label"]
+            gobs["inverted_label"] = self._gathered_inverted(obs["inverted_label"])
         return gobs, v["reward"], g_term, g_trunc, ginfo
 
     def step(self, action):
@@ -344,6 +360,8 @@ class ShardedVectorEnv:
                 fields[k] = obs[k]
         full = self.all_gather(fields)
         gobs = {k: full[k] for k in ("glimpse", "glimpse_pos", "time_step", "target_glimpse") if k in full}
+        if "inverted_label" in obs:
+            gobs["inverted_label"] = self._gathered_inverted(obs["inverted_label"])
         ginfo = {"index": full["index"], "base_reward": full["base_reward"],
                  "prediction": {"target": full["target"], "loss": full["loss"]}, "local_obs": obs}
         return gobs, full["reward"], full["terminated"], full["truncated"], ginfo

@@ -85,10 +85,11 @@ def _stale() -> bool:
 OBJ_DIR = os.path.join(HERE, "build_obj")  # per-source objects (git- and gpurun-ignored)
 
 
-def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str | None = None) -> str:
+def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str | None = None, only=None) -> str:
     """Build the library; `extra_flags`/`out` make tuning variants (e.g. -DAPG_STEP_PROFILE into tune/).
     Each source compiles to its own object in parallel (the kernels are independent translation units), and only
-    objects older than their source or a shared header are rebuilt; then one link."""
+    objects older than their source or a shared header are rebuilt; then one link.  `only` (variants): the sources
+    that take `extra_flags`; the others link their default objects."""
     os.makedirs(OUT_DIR, exist_ok=True)
     variant = out is not None
     out = out or OUT
@@ -99,16 +100,19 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str |
     odir = os.path.join(OBJ_DIR, "default" + tag)
     os.makedirs(odir, exist_ok=True)
     compile_flags = [f for f in FLAGS if f != "-shared" and not f.startswith("-Wl,")]
-    shared = [os.path.join(CSRC, f) for f in HEADERS] + [os.path.join(INCLUDE, "apgym_capi.h"), os.path.abspath(__file__)]
+    shared = [os.path.join(CSRC, f) for f in HEADERS] + [os.path.join(INCLUDE, "apgym_capi.h")]
     newest_shared = max(os.path.getmtime(d) for d in shared)
     procs, objs = [], []
     for src in SOURCES:
         spath = os.path.join(CSRC, src)
-        obj = os.path.join(odir, os.path.splitext(src)[0] + ".o")
+        flags = extra_flags if only is None or src in only else ()
+        sdir = odir if flags else os.path.join(OBJ_DIR, "default")
+        os.makedirs(sdir, exist_ok=True)
+        obj = os.path.join(sdir, os.path.splitext(src)[0] + ".o")
         objs.append(obj)
         if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(spath), newest_shared):
             continue
-        cmd = [HIPCC, *compile_flags, *extra_flags, "-I", INCLUDE, "-c", "-o", obj + ".tmp", spath]
+        cmd = [HIPCC, *compile_flags, *flags, "-I", INCLUDE, "-c", "-o", obj + ".tmp", spath]
         if verbose:
             cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
             print(" ".join(cmd))
@@ -133,6 +137,7 @@ if __name__ == "__main__":
     args = sys.argv[1:]
     out_arg = next((a.split("=", 1)[1] for a in args if a.startswith("--out=")), None)
     defs = [a for a in args if a.startswith("-D")]
-    print(build(force="--force" in args, verbose="--verbose" in args, extra_flags=defs, out=out_arg))
+    only = next((a.split("=", 1)[1].split(",") for a in args if a.startswith("--only=")), None)
+    print(build(force="--force" in args, verbose="--verbose" in args, extra_flags=defs, out=out_arg, only=only))
     if out_arg is None:
         print(build_torch_ops(force="--force" in args))

@@ -562,7 +562,10 @@ __global__ __launch_bounds__(64) void k_maze_big(Geo g, apg_lidar_state S, const
 // (maze_paint), writes them out (occ, or S.occ), and for MZ_RESET writes the map obs (bool map / 255,
 // lidar_localization2d.py:299), draws the start cell like place_start (reset :304: the pick-th free cell in
 // row-major order, pick = integers(0, nfree) on the env's stream) and resets the env's state.
-constexpr int MP_THREADS = 256, MP_ENVS = 64;
+#ifndef APG_MP_ENVS
+#define APG_MP_ENVS 4  // mazes per k_maze_paint / k_pf_paint workgroup (64: 4.80 ms, 16: 4.51, 8: 4.49, 4: 4.44 at cfg 3)
+#endif
+constexpr int MP_THREADS = 256, MP_ENVS = APG_MP_ENVS;
 __global__ __launch_bounds__(MP_THREADS) void k_maze_paint(Geo g, apg_lidar_state S, const uint64_t *idx, int n,
                                                            uint64_t *occ, const uint8_t *scratch, int mode,
                                                            uint64_t seed, int use_seed, int all, int ng,
@@ -858,7 +861,7 @@ APG_DEV void log_episode_stats(const StepParams &P, const apg_lidar_outputs &O, 
 #define STEP_STOP(k)
 #endif
 #ifdef APG_STEP_PROFILE  // tuning builds only (tools/step_phase_profile.py): per-workgroup phase timestamps
-__device__ unsigned long long g_step_prof[16384][8];
+__device__ unsigned long long g_step_prof[16384][16];
 #define STEP_MARK(k) \
   if (threadIdx.x == 0 && blockIdx.x < 16384) g_step_prof[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();
 #else
@@ -941,7 +944,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   __shared__ int s_x0[EPB], s_y0[EPB];
   __shared__ uint16_t s_rlist[EPB];  // envs that reset this step (map obs pass)
   __shared__ uint32_t s_start[EPB];  // rooms autoreset: start cell y << 8 | x, or ~0u (no free cell)
-  __shared__ int s_cnt[4];           // 0: reset-list length, 1: queued walks, 2: walk cursor
+  __shared__ int s_cnt[4];           // 0: reset-list length, 1: queued walks, 2: walk / chunk cursor
   __shared__ float s_dirs[MAX_STAGED_BEAMS][2];  // beam_dirs, read inside the beam loops (LDS, not HBM latency)
 #if APG_SLIDE_SPLIT
   __shared__ float s_slide[EPB];  // phase 1: the second slide candidate's length, then its scan distance
@@ -981,6 +984,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
     s_cnt[0] = 0;
     s_cnt[1] = 0;
     s_cnt[2] = 0;
+    s_cnt[3] = 0;
   }
   // Phases 0 and 1 run lane = env on the first EPB / 64 waves (thread tid owns env base + tid).  Its
   // inputs are loaded here, before any barrier, so their latency overlaps phase R and the window loads
@@ -1017,7 +1021,11 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       const int el = r / MAX_WIN_ROWS, row = r - el * MAX_WIN_ROWS;
       wv[k] = 0;
       if (base + el < P.n && row >= P.wlo && row < P.whi) {  // rows outside [wlo, whi) are never read
+#ifdef APG_TIMING_NO_POSDEP  // timing experiment only (wrong results): window rows at a fixed origin, no pos load
+        const float wpx = 20.5f, wpy = 20.5f;
+#else
         const float wpx = S.pos[2 * (base + el)], wpy = S.pos[2 * (base + el) + 1];
+#endif
         const int y = (int)floorf(wpy) - 15 + row;
         if ((unsigned)y < (unsigned)P.h)
           wv[k] = extract_window_row(S.occ + (P.is_static ? 0 : (size_t)(base + el) * words) + (size_t)y * P.wpr,
@@ -1054,6 +1062,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
     } else {
       npend = __syncthreads_or(pend);
     }
+    STEP_MARK(8)
     if (npend) {
       if constexpr (GEN == GEN_PF) {
         // Prefetched mazes (the record written by the side stream's batch, k_pf_*): each wave copies the next
@@ -1112,7 +1121,10 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           S.init_pos[2 * my_e + 1] = py;
           S.elapsed[my_e] = 0;
           S.flags[my_e] = (uint8_t)((f0 & F_AUTORESET) | F_JUST_RESET | F_FIRST);
-          pf_store_gen(&V.gen[my_e], g0 + 1u);
+          // a consumed record moves the env to its next generation; a missing one (APG_ERR_PREFETCH, raised to the
+          // caller) leaves the generation alone, so the next batch still selects this env and later records stay
+          // in step with its resets
+          if (ready) pf_store_gen(&V.gen[my_e], g0 + 1u);
         }
       } else if constexpr (GEN == GEN_POOL) {
         // Maps of the resident pool (any FloorMapDataset, APG_MAP_POOL).  The env's lane draws the DatasetIterator
@@ -1388,6 +1400,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       s_win[el * WIN_STRIDE + row] = wv[k];
     }
   }
+  STEP_MARK(9)
   __syncthreads();
   STEP_MARK(1)
   STEP_STOP(1)

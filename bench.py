@@ -287,22 +287,38 @@ LIDAR_WORKLOADS = {
                     note="BASELINE config 3: 262144 envs in total, split over the GPUs (127x127: the reference "
                          "maze needs odd sizes, SURVEY §0.6)"),
 }
-KERNEL_SOURCES = {
-    "lidar": ["apg_lidar.hip", "apg_scan.hpp", "apg_device.hpp", "apg_maps.hpp", "apg_maze.hpp", "apg_rng.hpp",
-              "apg_pairwise.hpp"],
-    "image": ["apg_image.hip", "apg_device.hpp", "apg_rng.hpp", "apg_pairwise.hpp"],
-}
+KERNEL_ROOTS = {"lidar": "apg_lidar.hip", "image": "apg_image.hip"}  # the kernel family's translation unit
 HIP_CLOCK_HZ = 2.4e9  # MI355X max engine clock (MI355X_MICROARCH.md); capacity of the issue fractions
 SIMDS, CUS = 1024, 256
 
 
+def kernel_sources(family: str) -> list[str]:
+    """Every file the family's translation unit compiles: its .hip and the closure of its quoted #includes
+    (csrc headers and include/apgym_capi.h), as sorted paths."""
+    import re
+
+    todo = [os.path.join(ROOT, "active-perception-gym_amd", "csrc", KERNEL_ROOTS[family])]
+    seen = set()
+    while todo:
+        path = os.path.normpath(todo.pop())
+        if path in seen:
+            continue
+        seen.add(path)
+        with open(path) as fh:
+            for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', fh.read(), re.M):
+                todo.append(os.path.join(os.path.dirname(path), inc))
+    return sorted(seen)
+
+
 def kernel_source_sha(family: str) -> str:
-    """Hash of the kernel sources a PMC table was collected with (a stale table is never used)."""
+    """Hash of the kernel sources a PMC table was collected with (a stale table is never used): the translation
+    unit and every header it includes."""
     import hashlib
 
     h = hashlib.sha256()
-    for f in KERNEL_SOURCES[family]:
-        with open(os.path.join(ROOT, "active-perception-gym_amd", "csrc", f), "rb") as fh:
+    for path in kernel_sources(family):
+        h.update(os.path.relpath(path, ROOT).encode())
+        with open(path, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
 

@@ -636,8 +636,24 @@ def test_numpy_backend_copy_semantics(gpu, kind):
     assert not held[-1][0]["map"].flags.writeable
     assert not np.array_equal(held[0][1]["map"], held[-1][1]["map"])  # the maps did change at the resets
     assert np.shares_memory(oa["map"], obs0_a["map"])  # copy=False: one mirror, rewritten in place
+    assert env._ring_copy and len(env._ring) == env.HOST_RING  # 10 steps held: the ring is full, later steps copy
     env.close()
     alias.close()
+    # a loop that keeps only the latest step's arrays alternates between two pinned blocks and copies nothing:
+    # the returned fields are views of the block the outputs were copied into
+    env = ap.make_vec(env_id, num_envs=n, lidar_beam_count=8, dataset=ds, device=gpu, max_episode_steps=3)
+    env.reset(seed=3)
+    prev = None
+    for t in range(7):
+        o, r, te, tr, info = env.step({"action": np.zeros((n, 2), np.float32), "prediction": np.zeros((n, 2), np.float32)})
+        assert not env._ring_copy and o["lidar"].base is r.base is te.base
+        if prev is not None:
+            assert o["lidar"].base is not prev.base  # the previous step's arrays were alive during this step
+        prev = o["lidar"]
+        snap = (o["lidar"].copy(), r.copy())
+    assert len(env._ring) == 2
+    assert np.array_equal(prev, snap[0]) and np.array_equal(r, snap[1])
+    env.close()
 
 
 def test_numpy_vector_stats_array_mode(gpu):
@@ -668,6 +684,32 @@ def test_numpy_vector_stats_array_mode(gpu):
     assert seen > 0
     with pytest.raises(ValueError):
         ap.make_vec("LIDARLocRooms-v0", vector_stats="bad", **kw)
+
+
+def test_mazes_never_terminate_before_the_time_limit(gpu):
+    """The maze prefetch protocol (apg_lidar.hip pf_before_step) relies on an env not resetting again within
+    step_limit + 1 steps of its reset; mazes guarantee it because their border rows and columns are walls
+    (floor_map_dataset_maze.py:24-55 carves odd cells only), so no move leaves the map and only the TimeLimit
+    terminates.  Pushed at the border with oversized actions toward it, every env must run its 100 steps."""
+    import ap_gym_amd as ap
+
+    n = 2048
+    env = ap.make_vec("LIDARLocMaze-v0", num_envs=n, lidar_beam_count=8, dataset=ap.FloorMapDatasetMaze(21, 21),
+                      device=gpu)
+    obs, _ = env.reset(seed=4)
+    term_steps = []
+    rng = np.random.default_rng(0)
+    for t in range(205):
+        pos = env._t["pos"].cpu().numpy()  # push toward the nearest border, sometimes along it
+        a = np.where(pos < 10.5, -3.0, 3.0).astype(np.float32)
+        a[rng.random(n) < 0.3, rng.integers(0, 2)] = 0.0
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": np.zeros((n, 2), np.float32)})
+        if term.any():
+            term_steps.append((t, int(term.sum())))
+    # every episode ends exactly at step 100 of it: steps 99 and 200 (the autoreset step 100 in between)
+    assert term_steps == [(99, n), (200, n)], term_steps
+    assert env.prefetch_stats()["batches"] >= 2
+    env.close()
 
 
 def test_nan_action_raises(gpu):

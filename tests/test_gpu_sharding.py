@@ -28,6 +28,10 @@ def _make(kind, num_envs, env_offset=0, num_envs_total=None, **kw):
                            dataset=ap.FloorMapDatasetRooms(32, 32), device="cuda:0", array_backend="torch",
                            env_offset=env_offset, **kw)
     ds = ap.SyntheticImageClassificationDataset(64, (32, 32, 3), 10, 3, seed=3)
+    if kind == "image_cls_inv":  # classification with randomly_invert_labels (registration.py:391)
+        cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=(5, 5), step_limit=8, randomly_invert_labels=True)
+        return ap.ImageClassificationVectorEnv(num_envs, cfg, device="cuda:0", array_backend="torch",
+                                               num_envs_total=num_envs_total or num_envs, env_offset=env_offset, **kw)
     cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=(8, 8), step_limit=8)
     return ap.ImageLocalizationVectorEnv(num_envs, cfg, device="cuda:0", array_backend="torch",
                                          num_envs_total=num_envs_total or num_envs, env_offset=env_offset, **kw)
@@ -42,7 +46,7 @@ def _actions(kind, t, n):
 
     g = torch.Generator(device="cuda:0").manual_seed(1000 + t)
     return (torch.rand((n, 2), device="cuda:0", generator=g) * 2 - 1,
-            torch.rand((n, 2), device="cuda:0", generator=g) * 2 - 1)
+            torch.rand((n, 10 if kind == "image_cls_inv" else 2), device="cuda:0", generator=g) * 2 - 1)
 
 
 def _flat(kind, obs, rew, term, info):
@@ -57,7 +61,10 @@ def _flat(kind, obs, rew, term, info):
              "loss": info["prediction"]["loss"], "index": info["index"], "terminated": term}
         if "glimpse" in obs:
             d["glimpse"] = obs["glimpse"]
-            d["target_glimpse"] = obs["target_glimpse"]
+            if "target_glimpse" in obs:
+                d["target_glimpse"] = obs["target_glimpse"]
+        if "inverted_label" in obs:  # [num_envs_total]: drawn flags on reset steps, 2s after
+            d["inverted_label"] = obs["inverted_label"]
     return {k: v.detach().cpu().numpy().copy() for k, v in d.items()}
 
 
@@ -77,7 +84,7 @@ def _reference(kind, with_reset=False):
     return out
 
 
-@pytest.mark.parametrize("kind", ["lidar", "image"])
+@pytest.mark.parametrize("kind", ["lidar", "image", "image_cls_inv"])
 def test_shards_union_equals_unsharded(gpu, kind):
     import torch
 
@@ -138,7 +145,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("kind", ["lidar", "image"])
+@pytest.mark.parametrize("kind", ["lidar", "image", "image_cls_inv"])
 def test_two_rank_gather_on_gpu_equals_unsharded(gpu, kind, tmp_path):
     import torch.multiprocessing as mp
 
@@ -152,7 +159,7 @@ def test_two_rank_gather_on_gpu_equals_unsharded(gpu, kind, tmp_path):
                 assert np.array_equal(got[r][f"{t}_{k}"], v), f"rank {r} step {t}: {k}"
 
 
-@pytest.mark.parametrize("kind", ["lidar", "image"])
+@pytest.mark.parametrize("kind", ["lidar", "image", "image_cls_inv"])
 def test_rccl_gather_branch_single_rank(gpu, kind, tmp_path):
     """The RCCL branch of ShardedVectorEnv._all_gather_rows (dist.all_gather_into_tensor on the device rows;
     sharding.py) on a one-rank "nccl" group: RCCL refuses two ranks on one device, so this is the only way

@@ -452,3 +452,28 @@ def test_binomial_constant_table_matches_host_libm():
     assert [float.fromhex(v) for v in macro("APG_BINOM_QN")] == qn
     assert [int(v) for v in macro("APG_BINOM_BOUND")] == bound
     assert len(qn) == 64 and qn[1] == 0.7 and bound[:3] == [0, 1, 2]
+
+
+@pytest.mark.parametrize("family", ["lidar", "image"])
+def test_kernel_source_hash_covers_the_include_closure(family):
+    """bench.py keys its PMC / duration tables by a hash of the kernel sources; the hash must cover every file
+    the translation unit compiles (its quoted #include closure), which the compiler's own dependency list
+    (hipcc -MM) names."""
+    import os
+    import shutil
+    import subprocess
+
+    import bench
+
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    if not (os.path.exists(hipcc) or shutil.which("hipcc")):
+        pytest.skip("hipcc not available")
+    root = bench.ROOT
+    src = os.path.join(root, "active-perception-gym_amd", "csrc", bench.KERNEL_ROOTS[family])
+    out = subprocess.run([hipcc, "-MM", "--offload-arch=gfx950", "-I", os.path.join(root, "include"), src],
+                         capture_output=True, text=True, check=True).stdout
+    deps = {os.path.normpath(os.path.join(root, t)) for t in out.replace("\\\n", " ").split()
+            if t.endswith((".hip", ".hpp", ".h")) and not t.startswith("/opt")}
+    deps = {d if os.path.isabs(d) else os.path.join(root, d) for d in deps}
+    assert deps and deps == set(bench.kernel_sources(family))
+    assert any(p.endswith("apgym_capi.h") for p in deps)

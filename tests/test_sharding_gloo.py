@@ -165,13 +165,15 @@ def _img_pool():
 def _img_actions(kind):
     rng = np.random.default_rng(2)
     a = rng.uniform(-1, 1, (IMG_STEPS, IMG_N, 2)).astype(np.float32)
-    p = (rng.standard_normal((IMG_STEPS, IMG_N, 10)) if kind == "cls"
+    p = (rng.standard_normal((IMG_STEPS, IMG_N, 10)) if kind in ("cls", "cls_inv")
          else rng.uniform(-1, 1, (IMG_STEPS, IMG_N, 2))).astype(np.float32)
     return a, p
 
 
 class _ImageOracleShard:
     def __init__(self, kind, num_envs, env_offset, packed_outputs=False):
+        invert = kind == "cls_inv"  # randomly_invert_labels (the registered MNIST-style ids)
+        kind = "cls" if invert else kind
         from ap_gym_amd import _native as N
         from ap_gym_amd.image_env import image_output_row_layout, image_row_views
         from oracle import image_oracle as io
@@ -180,7 +182,8 @@ class _ImageOracleShard:
         self.kname, self.lo, self.n = kind, env_offset, num_envs
         self.kind = N.APG_IMAGE_CLASSIFY if kind == "cls" else N.APG_IMAGE_LOCALIZE
         self.single_observation_space = {"glimpse": np.zeros(IMG_SENSOR + (1,), np.float32)}  # .shape only
-        self.e = io.ImageVectorEnvOracle(kind, pool, labels, 10, 1, IMG_N, IMG_SENSOR, step_limit=IMG_LIMIT)
+        self.e = io.ImageVectorEnvOracle(kind, pool, labels, 10, 1, IMG_N, IMG_SENSOR, step_limit=IMG_LIMIT,
+                                         invert=invert)
         self.copy = False
         self._prev_done = False
         self.output_rows = self.output_layout = None
@@ -199,6 +202,8 @@ class _ImageOracleShard:
         out = {k: self._sl(o[k]) for k in ("glimpse", "glimpse_pos", "time_step")}
         if "target_glimpse" in o:
             out["target_glimpse"] = self._sl(o["target_glimpse"])
+        if "inverted_label" in o:  # int32 flags on reset steps, int64 2s after (image_env.py's torch outputs)
+            out["inverted_label"] = self._sl(o["inverted_label"])
         return out
 
     def reset(self, *, seed=None, options=None):
@@ -275,10 +280,12 @@ def _img_worker(rank, world, port, outdir, kind, packed):
     if packed:  # (the copying path gathers step outputs only)
         out["reset_glimpse"] = obs["glimpse"].numpy().copy()
         out["reset_index"] = info["index"].numpy().copy()
+        if "inverted_label" in obs:
+            out["reset_inverted_label"] = obs["inverted_label"].numpy().copy()
     for t in range(IMG_STEPS):
         obs, rew, term, trunc, info = senv.step({"action": torch.from_numpy(acts[t, lo:lo + n]),
                                                  "prediction": torch.from_numpy(preds[t, lo:lo + n])})
-        for k in ("glimpse", "glimpse_pos", "time_step", "target_glimpse"):
+        for k in ("glimpse", "glimpse_pos", "time_step", "target_glimpse", "inverted_label"):
             if k in obs:
                 out[f"{k}_{t}"] = obs[k].numpy().copy()
         out[f"reward_{t}"] = rew.numpy().copy()
@@ -296,7 +303,7 @@ def _img_worker(rank, world, port, outdir, kind, packed):
 
 
 @pytest.mark.parametrize("packed", [False, True], ids=["copying", "packed_rows"])
-@pytest.mark.parametrize("kind", ["cls", "loc"])
+@pytest.mark.parametrize("kind", ["cls", "loc", "cls_inv"])
 def test_two_rank_image_gather_equals_unsharded(tmp_path, kind, packed):
     from oracle import image_oracle as io
 
@@ -307,18 +314,23 @@ def test_two_rank_image_gather_equals_unsharded(tmp_path, kind, packed):
     for k in r0.files:
         assert np.array_equal(r0[k], r1[k], equal_nan=True), k  # every rank holds the full batch
     pool, labels = _img_pool()
-    full = io.ImageVectorEnvOracle(kind, pool, labels, 10, 1, IMG_N, IMG_SENSOR, step_limit=IMG_LIMIT)
+    full = io.ImageVectorEnvOracle("cls" if kind == "cls_inv" else kind, pool, labels, 10, 1, IMG_N, IMG_SENSOR,
+                                   step_limit=IMG_LIMIT, invert=kind == "cls_inv")
     o, info = full.reset(7)
     if packed:
         assert np.array_equal(r0["reset_glimpse"], o["glimpse"])
         assert np.array_equal(r0["reset_index"], info["index"])
+        if kind == "cls_inv":  # the whole batch's flags, not one shard's
+            got = r0["reset_inverted_label"]
+            assert got.shape == (IMG_N,) and got.dtype == np.int32 and np.array_equal(got, o["inverted_label"])
     acts, preds = _img_actions(kind)
     ends = 0
     for t in range(IMG_STEPS):
         o, r, te, tr, info = full.step(acts[t], preds[t])
-        for k in ("glimpse", "glimpse_pos", "time_step", "target_glimpse"):
+        for k in ("glimpse", "glimpse_pos", "time_step", "target_glimpse", "inverted_label"):
             if k in o:
                 assert np.array_equal(r0[f"{k}_{t}"], o[k]), (k, t)
+                assert r0[f"{k}_{t}"].dtype == np.asarray(o[k]).dtype, (k, t)
         assert np.array_equal(r0[f"reward_{t}"], np.asarray(r, np.float64)), t
         assert np.array_equal(r0[f"term_{t}"], te), t
         assert np.array_equal(r0[f"base_{t}"], np.asarray(info["base_reward"], np.float32)), t

@@ -47,7 +47,7 @@ for rep in range(3):
     print(f"rep {rep}: events around env.step {ev0.elapsed_time(ev1) * 1000:.1f} us")
     epb = int(os.environ.get("APG_STEP_EPB") or (256 if n >= 256 * 256 else 64))
     nwg = (n + epb - 1) // epb
-    buf = np.zeros((16384, 8), np.uint64)
+    buf = np.zeros((16384, 16), np.uint64)
     assert N.lib().apg_debug_step_profile(buf.ctypes.data, buf.nbytes) == 0
     b = buf[:nwg].astype(np.int64)
     t0 = b[:, 0].min()
@@ -59,6 +59,10 @@ for rep in range(3):
     print(f"rep {rep}: kernel span {us(b[:, 5].max() - t0):.1f} us; WG start offsets p50/p99/max "
           f"{us(np.percentile(off, 50)):.1f}/{us(np.percentile(off, 99)):.1f}/{us(off.max()):.1f}; "
           f"WG end p50/max {us(np.percentile(b[:, 5] - t0, 50)):.1f}/{us((b[:, 5] - t0).max()):.1f}")
+    if b[:, 8].any() and b[:, 9].any():  # sub-marks of the staging phase: 8 phase-R barrier, 9 windows in LDS
+        for nm, k0, k1 in (("  launch -> R barrier", 0, 8), ("  R barrier -> stored", 8, 9), ("  stored -> barrier", 9, 1)):
+            d = us(b[:, k1] - b[:, k0])
+            print(f"   {nm:22s} p50 {np.percentile(d, 50):6.2f}  p90 {np.percentile(d, 90):6.2f}")
     names = ["stage windows", "move (phase 1)", "pre-test (2a)", "walks (2b)", "store"]
     for k in range(5):
         d = us(b[:, k + 1] - b[:, k])
