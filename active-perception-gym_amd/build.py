@@ -85,6 +85,21 @@ def _stale() -> bool:
 OBJ_DIR = os.path.join(HERE, "build_obj")  # per-source objects (git- and gpurun-ignored)
 
 
+def _closure(path: str) -> list[str]:
+    """The source and every file of its quoted #include closure (an object is stale once any is newer)."""
+    import re
+
+    todo, seen = [path], set()
+    while todo:
+        p = os.path.normpath(todo.pop())
+        if p in seen:
+            continue
+        seen.add(p)
+        with open(p) as fh:
+            todo += [os.path.join(os.path.dirname(p), inc) for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', fh.read(), re.M)]
+    return sorted(seen)
+
+
 def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str | None = None, only=None) -> str:
     """Build the library; `extra_flags`/`out` make tuning variants (e.g. -DAPG_STEP_PROFILE into tune/).
     Each source compiles to its own object in parallel (the kernels are independent translation units), and only
@@ -100,8 +115,6 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str |
     odir = os.path.join(OBJ_DIR, "default" + tag)
     os.makedirs(odir, exist_ok=True)
     compile_flags = [f for f in FLAGS if f != "-shared" and not f.startswith("-Wl,")]
-    shared = [os.path.join(CSRC, f) for f in HEADERS] + [os.path.join(INCLUDE, "apgym_capi.h")]
-    newest_shared = max(os.path.getmtime(d) for d in shared)
     procs, objs = [], []
     for src in SOURCES:
         spath = os.path.join(CSRC, src)
@@ -110,18 +123,19 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str |
         os.makedirs(sdir, exist_ok=True)
         obj = os.path.join(sdir, os.path.splitext(src)[0] + ".o")
         objs.append(obj)
-        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(spath), newest_shared):
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(d) for d in _closure(spath)):
             continue
-        cmd = [HIPCC, *compile_flags, *flags, "-I", INCLUDE, "-c", "-o", obj + ".tmp", spath]
+        tmp = f"{obj}.{os.getpid()}.tmp"  # concurrent builds never share a temporary
+        cmd = [HIPCC, *compile_flags, *flags, "-I", INCLUDE, "-c", "-o", tmp, spath]
         if verbose:
             cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
             print(" ".join(cmd))
-        procs.append((subprocess.Popen(cmd), obj))
-    failed = [obj for p, obj in procs if p.wait() != 0]
+        procs.append((subprocess.Popen(cmd), obj, tmp))
+    failed = [obj for p, obj, _ in procs if p.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, f"hipcc -c ({', '.join(os.path.basename(f) for f in failed)})")
-    for _, obj in procs:
-        os.replace(obj + ".tmp", obj)
+    for _, obj, tmp in procs:
+        os.replace(tmp, obj)
     link = [HIPCC, *[f for f in FLAGS if f in ("--offload-arch=gfx950", "-fPIC", "-shared") or f.startswith("-Wl,")],
             "-o", out + ".tmp", *objs]
     subprocess.run(link, check=True)

@@ -153,12 +153,16 @@ APG_DEV uint32_t glimpse_pixel(const GlimpseGeo &g, const void *pool, const floa
 // A batch of n draws from ONE numpy stream, spread over the chip: every thread jumps to its own
 // stretch of FILL_PER_THREAD words of the stream (pcg_advance) and walks it.  integers() rejects
 // candidates (Lemire), so output i is the i-th accepted candidate: k_fill_count counts per thread,
-// k_fill_write places each thread's accepted draws at its prefix, and its last workgroup to finish (a
-// ticket counter in work[0], left at zero) advances the generator state past the consumed words (and, if
-// the candidates ran out, which is astronomically rare for the sizes used, finishes sequentially) once
-// every workgroup has read the state.  Uniform draws finish the same way when given a counter.
+// k_fill_write places each thread's accepted draws at its prefix, and its last workgroup to finish (a ticket
+// counter in work[0], left at zero; last_block_done) advances the generator state past the consumed words (and,
+// if the candidates ran out, which is astronomically rare for the sizes used, finishes sequentially) once every
+// workgroup has read the state; uniform draws finish the same way when given a counter.  Few outputs per thread:
+// the kernels' time is one thread's chain (the jump, then its outputs), not the chip's throughput.
 constexpr int FILL_THREADS = 256;
-constexpr int FILL_PER_THREAD = 32;
+#ifndef APG_FILL_PER_THREAD
+#define APG_FILL_PER_THREAD 8
+#endif
+constexpr int FILL_PER_THREAD = APG_FILL_PER_THREAD;
 constexpr int FILL_PER_BLOCK = FILL_THREADS * FILL_PER_THREAD;
 
 struct FillArgs {
@@ -181,22 +185,42 @@ int64_t fill_work_elems(int64_t cand) {
   return 1 + nb * (FILL_THREADS + 1) + 1;
 }
 
-// true in exactly one thread of the grid: thread 0 of the last workgroup to get here (every workgroup calls
-// it, all of its threads; the counter returns to zero).  Whatever the grid wrote before is visible to it.
-APG_DEV bool last_block_done(int64_t *counter) {
+// true in exactly one thread of the grid: thread 0 of the last workgroup to get here (every workgroup calls it, all
+// of its threads; the counter returns to zero).  No release / acquire fence (~3.5 us each on gfx950): what the last
+// workgroup relies on is (1) every workgroup has read the generator state -- its loads returned before its barrier --
+// and (2) the consumed-word count, written with an agent-scope (sc1) store and read with an agent-scope load, every
+// wave having drained its stores (vmcnt(0)) before the barrier behind which lane 0 takes the ticket
+// (MI355X_MICROARCH.md, inter-workgroup visibility: the sc1 store / load with a counter add form).
+// last_block: the same test, true in every thread of that workgroup (block-uniform)
+APG_DEV bool last_block(int64_t *counter) {
   __shared__ bool s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
-    const unsigned long long t = atomicAdd(reinterpret_cast<unsigned long long *>(counter), 1ULL);
+    const unsigned long long t = __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(counter), 1ULL,
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = t == (unsigned long long)(gridDim.x - 1);
-    if (s_last) {
-      __threadfence();
-      *counter = 0;
-    }
+    if (s_last) __hip_atomic_store(reinterpret_cast<unsigned long long *>(counter), 0ULL, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  return s_last && threadIdx.x == 0;
+  return s_last;
+}
+
+APG_DEV bool last_block_done(int64_t *counter) { return last_block(counter) && threadIdx.x == 0; }
+
+// sum of v[0, n) over the workgroup's threads (strided loads issued together, not one dependent round trip per
+// element), returned to every thread
+APG_DEV int64_t block_sum(const int64_t *v, int n) {
+  __shared__ int64_t s_red[FILL_THREADS / 64];
+  int64_t t = 0;
+  for (int k = threadIdx.x; k < n; k += FILL_THREADS) t += v[k];
+  for (int d = 32; d >= 1; d >>= 1) t += __shfl_xor(t, d, 64);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  t = 0;
+  for (int w = 0; w < FILL_THREADS / 64; w++) t += s_red[w];
+  return t;
 }
 
 struct LemireSpec {
@@ -221,7 +245,7 @@ APG_DEV int64_t lemire_value(const LemireSpec &l, uint32_t u) {
   return (int64_t)(l.full ? (uint64_t)u : (((uint64_t)u * l.rex) >> 32));
 }
 
-// counter != nullptr: the last workgroup advances the state (else k_fill_uniform_finish does)
+// counter != nullptr: the last workgroup advances the state (else k_fill_uniform_finish does, launched after)
 __global__ __launch_bounds__(FILL_THREADS) void k_fill_uniform(apg_pcg64 *st, FillArgs a, double *out,
                                                                int64_t *counter) {
   // random_uniform: off + scale * next_double, one next64 per value, C order over (n, cols)
@@ -278,13 +302,7 @@ __global__ __launch_bounds__(FILL_THREADS) void k_fill_write(apg_pcg64 *st, Fill
                                                              int64_t *work_all) {
   int64_t *work = work_all + 1;
   __shared__ int64_t s_wave[FILL_THREADS / 64];
-  __shared__ int64_t s_base;
   const LemireSpec l = lemire_spec(a.bound);
-  if (threadIdx.x == 0) {
-    int64_t b = 0;
-    for (int k = 0; k < (int)blockIdx.x; k++) b += work[k];
-    s_base = b;
-  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t cnt = work[a.nblocks + (size_t)blockIdx.x * FILL_THREADS + threadIdx.x];
   int64_t inc = cnt;
@@ -293,8 +311,8 @@ __global__ __launch_bounds__(FILL_THREADS) void k_fill_write(apg_pcg64 *st, Fill
     if (lane >= d) inc += o;
   }
   if (lane == 63) s_wave[wave] = inc;
-  __syncthreads();
-  int64_t q = s_base + inc - cnt;
+  // the accepted counts of the preceding workgroups (its barrier also publishes s_wave)
+  int64_t q = block_sum(work, (int)blockIdx.x) + inc - cnt;
   for (int w = 0; w < wave; w++) q += s_wave[w];
   const int64_t k0 = ((int64_t)blockIdx.x * FILL_THREADS + threadIdx.x) * FILL_PER_THREAD;
   if (cnt != 0 && q < a.n) {
@@ -304,22 +322,25 @@ __global__ __launch_bounds__(FILL_THREADS) void k_fill_write(apg_pcg64 *st, Fill
       const uint32_t u = wk.next();
       if (lemire_accept(l, u)) {
         out[q] = a.lo + lemire_value(l, u);
-        if (q == a.n - 1) *fill_consumed(work, a.nblocks) = k + 1;
+        if (q == a.n - 1)  // read by the last workgroup (last_block_done): an agent-scope store
+          __hip_atomic_store(reinterpret_cast<unsigned long long *>(fill_consumed(work, a.nblocks)),
+                             (unsigned long long)(k + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         q++;
       }
     }
   }
-  if (last_block_done(work_all)) fill_finish(st, a, out, work);
+  if (last_block(work_all)) fill_finish(st, a, out, work);  // block-uniform: the whole last workgroup
 }
 
 APG_DEV void fill_finish(apg_pcg64 *st, const FillArgs &a, int64_t *out, int64_t *work) {
+  const int64_t total = block_sum(work, a.nblocks);
+  if (threadIdx.x != 0) return;
   const LemireSpec l = lemire_spec(a.bound);
   const Pcg64 base = *reinterpret_cast<const Pcg64 *>(st);
-  int64_t total = 0;
-  for (int b = 0; b < a.nblocks; b++) total += work[b];
   Pcg64 r;
   if (total >= a.n) {
-    r = after_next32_words(base, (uint64_t)*fill_consumed(work, a.nblocks));
+    r = after_next32_words(base, (uint64_t)__hip_atomic_load(reinterpret_cast<unsigned long long *>(
+                                        fill_consumed(work, a.nblocks)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   } else {  // not enough accepted candidates: continue sequentially after all of them
     r = after_next32_words(base, (uint64_t)a.cand);
     for (int64_t i = total; i < a.n; i++) {

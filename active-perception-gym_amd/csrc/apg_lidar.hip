@@ -1233,6 +1233,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        STEP_MARK(10)  // (wave 0's view)
         // R2: each wave paints the maps of its own envs one after the other, lane = row: occupancy rows
         // out (coalesced), the f32 map obs from the wave's row copy in LDS, the free-cell count and the
         // start cell (place_start: the pick-th free cell in row-major order, drawn by the env's lane)
@@ -1307,6 +1308,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
             }
           }
         }
+        STEP_MARK(11)
         // R3: the env's lane finishes its reset (lidar_localization2d.py:293-315 tail)
         if (pend) {
           const uint32_t sc = s_start[my_el];
@@ -1333,6 +1335,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         if (pend) reset_one<GEN>(g, S, my_e, f0, false, 0, nullptr, O.map_idx, O.err, bt);
       }
       __syncthreads();
+      STEP_MARK(12)
       if (own && (pf_f & F_AUTORESET)) {  // this env was reset above
         pf_f = S.flags[oe];
         pf_px = S.pos[2 * oe];

@@ -31,8 +31,51 @@ APG_DEV U128 add128(U128 a, U128 b) {
   return r;
 }
 
+// Jumps of d = k * 256^i LCG steps (i < 4, k < 256): s -> A^d s + G(d) inc with G(d) = 1 + A + ... + A^(d-1)
+// (mod 2^128), tabulated at compile time, so an advance by d < 2^32 is at most four such maps (eight 128-bit
+// multiplies) instead of pcg_advance_lcg_128's square-and-multiply (four per bit of d: the per-thread jumps of
+// the parallel stream draws were their kernels' longest chain).
+struct PcgJump {
+  uint64_t m_hi, m_lo, g_hi, g_lo;
+};
+struct PcgJumpTable {
+  PcgJump e[4][256];
+};
+constexpr PcgJumpTable make_pcg_jump_table() {
+  PcgJumpTable t{};
+  using u128 = unsigned __int128;
+  u128 base_m = ((u128)PCG_MUL_HI << 64) | PCG_MUL_LO, base_g = 1;  // A^step, G(step) for step = 256^i
+  for (int i = 0; i < 4; i++) {
+    u128 m = 1, g = 0;  // A^(k step), G(k step)
+    for (int k = 0; k < 256; k++) {
+      t.e[i][k] = PcgJump{(uint64_t)(m >> 64), (uint64_t)m, (uint64_t)(g >> 64), (uint64_t)g};
+      g = g + m * base_g;  // G((k + 1) step) = G(k step) + A^(k step) G(step)
+      m = m * base_m;
+    }
+    base_m = m;  // A^(256 step), G(256 step)
+    base_g = g;
+  }
+  return t;
+}
+static __constant__ PcgJumpTable c_pcg_jump = make_pcg_jump_table();
+
 // state <- state advanced by `delta` LCG steps (numpy pcg64 advance / pcg_advance_lcg_128)
 APG_DEV void pcg_advance(Pcg64 &r, uint64_t delta) {
+  if ((delta >> 32) == 0ULL) {
+    U128 s{r.s_hi, r.s_lo};
+    const U128 inc{r.i_hi, r.i_lo};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int k = (int)((delta >> (8 * i)) & 255ULL);
+      if (k) {
+        const PcgJump j = c_pcg_jump.e[i][k];
+        s = add128(mul128(U128{j.m_hi, j.m_lo}, s), mul128(U128{j.g_hi, j.g_lo}, inc));
+      }
+    }
+    r.s_hi = s.hi;
+    r.s_lo = s.lo;
+    return;
+  }
   U128 acc_mult{0, 1}, acc_plus{0, 0}, cur_mult{PCG_MUL_HI, PCG_MUL_LO}, cur_plus{r.i_hi, r.i_lo};
   while (delta) {
     if (delta & 1ULL) {

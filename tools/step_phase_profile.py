@@ -4,7 +4,8 @@
     APG_LIBRARY=tune/libprof.so python tools/step_phase_profile.py
 
 Marks per workgroup (s_memrealtime, 100 MHz): 0 start, 1 windows staged, 2 move phase done,
-3 beam pre-test done, 4 queued walks done, 5 end; slot 6 = queued walks.
+3 beam pre-test done, 4 queued walks done, 5 end; slot 6 = queued walks.  WARM=100 profiles the rooms
+autoreset step (marks 8 phase R start, 10 / 11 wave 0's generation / paint done, 12 phase-R barrier).
 """
 import ctypes
 import os
@@ -59,7 +60,13 @@ for rep in range(3):
     print(f"rep {rep}: kernel span {us(b[:, 5].max() - t0):.1f} us; WG start offsets p50/p99/max "
           f"{us(np.percentile(off, 50)):.1f}/{us(np.percentile(off, 99)):.1f}/{us(off.max()):.1f}; "
           f"WG end p50/max {us(np.percentile(b[:, 5] - t0, 50)):.1f}/{us((b[:, 5] - t0).max()):.1f}")
-    if b[:, 8].any() and b[:, 9].any():  # sub-marks of the staging phase: 8 phase-R barrier, 9 windows in LDS
+    if b[:, 10].any():  # a rooms autoreset step: 10 generation done, 11 maps painted (wave 0), 12 phase-R barrier
+        for nm, k0, k1 in (("  launch -> R start", 0, 8), ("  R1 generate (wave 0)", 8, 10),
+                           ("  R2 paint (wave 0)", 10, 11), ("  R3 + R barrier", 11, 12),
+                           ("  windows reloaded", 12, 9), ("  stored -> barrier", 9, 1)):
+            d = us(b[:, k1] - b[:, k0])
+            print(f"   {nm:22s} p50 {np.percentile(d, 50):6.2f}  p90 {np.percentile(d, 90):6.2f}  max {d.max():6.2f}")
+    elif b[:, 8].any() and b[:, 9].any():  # sub-marks of the staging phase: 8 phase-R barrier, 9 windows in LDS
         for nm, k0, k1 in (("  launch -> R barrier", 0, 8), ("  R barrier -> stored", 8, 9), ("  stored -> barrier", 9, 1)):
             d = us(b[:, k1] - b[:, k0])
             print(f"   {nm:22s} p50 {np.percentile(d, 50):6.2f}  p90 {np.percentile(d, 90):6.2f}")
