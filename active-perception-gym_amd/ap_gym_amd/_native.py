@@ -3,7 +3,9 @@
 * `lib()` — ctypes over every entry point (setup, tests, render, utility calls);
 * `torch_ops()` — the TORCH_LIBRARY(apgym) custom ops of _lib/libapgym_torch.so
   (csrc/apg_torch_ops.cpp), which the envs' reset/step hot path calls: one C++ op call per step,
-  launched on PyTorch's current HIP stream (CUDA-graph capturable).
+  launched on PyTorch's current HIP stream (CUDA-graph capturable);
+* `fast()` — METH_FASTCALL wrappers of the per-step C-ABI calls (_lib/_apgfast*.so, csrc/apg_pyfast.cpp) that the
+  envs' eager steps use: ~0.1 us per call instead of ctypes' ~2.5 us of argument marshalling.
 
 The library is the ONLY compute path of this package: there is no CPU fallback.  Both loaders raise
 NativeLibraryError when their shared object is missing or cannot be loaded.
@@ -20,6 +22,7 @@ LIB_PATH = os.environ.get("APG_LIBRARY") or os.path.join(LIB_DIR, "libapgym_hip.
 TORCH_LIB_PATH = os.path.join(LIB_DIR, "libapgym_torch.so")
 
 APG_OK = 0
+APG_E_INVALID = -1  # apgym_capi.h: invalid argument / configuration (raised as ValueError)
 APG_ERR_NAN_ACTION = 1
 APG_ERR_NAN_PREDICTION = 2
 APG_ERR_MAPGEN = 4
@@ -216,6 +219,37 @@ def lib():
     return _lib
 
 
+_fast = None
+
+
+def fast():
+    """The CPython fast-call entry points of the per-step C-ABI calls (_lib/_apgfast*.so, csrc/apg_pyfast.cpp:
+    ~0.1 us per call against ~2.5 us through ctypes), loaded after the C-ABI library it links.  Raises when it is
+    missing, like lib()."""
+    global _fast
+    if _fast is None:
+        import importlib.machinery
+        import importlib.util
+        import sysconfig
+
+        lib()  # (an APG_LIBRARY variant, loaded first, also serves this module's libapgym_hip.so dependency)
+        path = os.path.join(LIB_DIR, "_apgfast" + sysconfig.get_config_var("EXT_SUFFIX"))
+        if not os.path.exists(path):
+            raise NativeLibraryError(f"{path} not found: build it with "
+                                     "`python -c 'import __graft_entry__ as g; g.build()'`")
+        loader = importlib.machinery.ExtensionFileLoader("_apgfast", path)
+        spec = importlib.util.spec_from_file_location("_apgfast", path, loader=loader)
+        mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(mod)
+        _fast = mod
+    return _fast
+
+
+def addr(obj) -> int:
+    """Address of a ctypes structure (the fast-call entry points take plain ints)."""
+    return ctypes.addressof(obj)
+
+
 _torch_ops = None
 
 
@@ -307,14 +341,54 @@ def stream_handle(device) -> int:
 _hip = None
 
 
-def event_record(event, stream) -> None:
-    """hipEventRecord(event, stream) through the HIP runtime torch already loaded (bench timing of
-    the step op on its own stream; torch.cuda.Event would only see torch's current stream object)."""
+def hip():
+    """The HIP runtime torch already loaded (ctypes: the event calls below)."""
     global _hip
     if _hip is None:
         h = ctypes.CDLL("libamdhip64.so")
         h.hipEventRecord.argtypes = [_vp, _vp]
         h.hipEventRecord.restype = ctypes.c_int
+        h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(_vp), ctypes.c_uint]
+        h.hipEventCreateWithFlags.restype = ctypes.c_int
+        h.hipStreamWaitEvent.argtypes = [_vp, _vp, ctypes.c_uint]
+        h.hipStreamWaitEvent.restype = ctypes.c_int
+        h.hipEventDestroy.argtypes = [_vp]
+        h.hipEventDestroy.restype = ctypes.c_int
         _hip = h
-    if _hip.hipEventRecord(event, stream) != 0:
+    return _hip
+
+
+def event_record(event, stream) -> None:
+    """hipEventRecord(event, stream) through the HIP runtime torch already loaded (bench timing of
+    the step op on its own stream; torch.cuda.Event would only see torch's current stream object)."""
+    if hip().hipEventRecord(event, stream) != 0:
         raise ApgError("hipEventRecord failed")
+
+
+class DeviceEvent:
+    """A hipEvent for ordering two streams of one device (no timing, no host inspection): recorded with a
+    device-scope release (hipEventReleaseToDevice), so the marker skips the system-scope cache writeback a
+    default event (torch.cuda.Event) pays on every record -- measured as a ~6-8 us idle gap on the recording
+    stream after the image env's batch-autoreset step.  record(stream) / wait(stream) take raw HIP streams."""
+
+    FLAGS = 0x2 | 0x40000000  # hipEventDisableTiming | hipEventReleaseToDevice
+
+    def __init__(self):
+        ev = _vp()
+        if hip().hipEventCreateWithFlags(ctypes.byref(ev), self.FLAGS) != 0:
+            raise ApgError("hipEventCreateWithFlags failed")
+        self.handle = ev.value
+
+    def record(self, stream: int) -> None:
+        if _hip.hipEventRecord(self.handle, stream) != 0:
+            raise ApgError("hipEventRecord failed")
+
+    def wait(self, stream: int) -> None:
+        """The stream's later work waits for the last record (none yet: no wait)."""
+        if _hip.hipStreamWaitEvent(stream, self.handle, 0) != 0:
+            raise ApgError("hipStreamWaitEvent failed")
+
+    def destroy(self) -> None:
+        if self.handle is not None:
+            _hip.hipEventDestroy(self.handle)
+            self.handle = None

@@ -300,7 +300,13 @@ class _ImageVectorEnv(VectorEnv):
         # autoreset step): that step then installs them in the fused step kernel, one launch instead of five.
         self.draw_ahead = bool(draw_ahead)
         self._ahead_stream = t.cuda.Stream(dev, priority=0) if self.draw_ahead else None
-        self._ahead_event = t.cuda.Event() if self.draw_ahead else None
+        # stream-ordering events (device-scope release: N.DeviceEvent): the draws made ahead -> the step installing
+        # them; the batch autoreset step -> the draws of the next batch
+        self._ahead_event = self._main_event = None
+        if self.draw_ahead:
+            with t.cuda.device(dev):
+                self._ahead_event, self._main_event = N.DeviceEvent(), N.DeviceEvent()
+        self._ahead_side = self._ahead_stream.cuda_stream if self.draw_ahead else None
         self._ahead = False  # draws made ahead and not yet installed
         self._err_host = t.zeros(1, dtype=t.int32).pin_memory()
         self._err_event = t.cuda.Event()
@@ -398,7 +404,7 @@ class _ImageVectorEnv(VectorEnv):
         if self._ahead:  # the batch is replaced here: the streams go back to before the draws made ahead
             import torch
 
-            torch.cuda.current_stream(self.device).wait_event(self._ahead_event)
+            self._ahead_event.wait(N.current_stream_ptr(self._dev))
             N.check(L.apg_image_discard_ahead(ctypes.byref(self._cfg), ctypes.byref(self._state), self._stream()),
                     "apg_image_discard_ahead")
             self._ahead = False
@@ -451,7 +457,7 @@ class _ImageVectorEnv(VectorEnv):
         if resetting:
             flags = 1
             if self._ahead:  # install the draws made ahead (the step's stream waits for the side stream)
-                torch.cuda.current_stream(self.device).wait_event(self._ahead_event)
+                self._ahead_event.wait(N.current_stream_ptr(self._dev))
                 flags |= 2
                 self._ahead = False
         self._track_render(p_np if numpy_mode else p_t, resetting)
@@ -492,20 +498,19 @@ class _ImageVectorEnv(VectorEnv):
             return
         import torch
 
-        main = torch.cuda.current_stream(self.device)
-        self._ahead_stream.wait_stream(main)
-        with torch.cuda.stream(self._ahead_stream):
-            N.check(N.lib().apg_image_draw_ahead(ctypes.byref(self._cfg), ctypes.byref(self._state),
-                                                 self._ahead_stream.cuda_stream), "apg_image_draw_ahead")
-        self._ahead_event.record(self._ahead_stream)
+        # (cached events and the side stream's raw handle: the C call takes the stream, no stream context needed)
+        self._main_event.record(N.current_stream_ptr(self._dev))
+        self._main_event.wait(self._ahead_side)
+        N.check(N.lib().apg_image_draw_ahead(ctypes.byref(self._cfg), ctypes.byref(self._state), self._ahead_side),
+                "apg_image_draw_ahead")
+        self._ahead_event.record(self._ahead_side)
         self._ahead = True
 
     def _c_step(self, a_t, p_t, flags):
-        if self._c_args is None:
-            self._c_args = (ctypes.byref(self._cfg), ctypes.byref(self._state), ctypes.byref(self._out))
-        cfg, st, out = self._c_args
-        rc = N.lib().apg_image_step(cfg, st, a_t.data_ptr(), p_t.data_ptr(), int(self._t_step), flags,
-                                    out, N.current_stream_ptr(self._dev))
+        if self._c_args is None:  # the fast-call entry point and the structures' addresses
+            self._c_args = (N.fast().image_step, N.addr(self._cfg), N.addr(self._state), N.addr(self._out))
+        fn, cfg, st, out = self._c_args
+        rc = fn(cfg, st, a_t.data_ptr(), p_t.data_ptr(), self._t_step, flags, out, N.current_stream_ptr(self._dev))
         if rc:
             N.check(rc, "apg_image_step")
 
@@ -780,6 +785,8 @@ class _ImageVectorEnv(VectorEnv):
                 # the draw-ahead kernels on the side stream may still write the streams and ahead buffers, which
                 # the caching allocator would otherwise hand to a new allocation of the main stream
                 self._ahead_stream.synchronize()
+                for ev in (self._ahead_event, self._main_event):
+                    ev.destroy()
             self._t = {}
             self._h = None  # the op handle keeps every state/output buffer alive
             self._c_args = None

@@ -499,10 +499,10 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
 
             with torch.cuda.device(self._dev):
                 return self._launch_step(a_t, p_t)
-        if self._c_args is None:
-            self._c_args = (ctypes.byref(self._cfg), ctypes.byref(self._state), ctypes.byref(self._out))
-        cfg, st, out = self._c_args
-        rc = N.lib().apg_lidar_step(cfg, st, a_t.data_ptr(), p_t.data_ptr(), out, N.current_stream_ptr(self._dev))
+        if self._c_args is None:  # (the structures' addresses: rebuilt whenever a structure is replaced)
+            self._c_args = (N.fast().lidar_step, N.addr(self._cfg), N.addr(self._state), N.addr(self._out))
+        fn, cfg, st, out = self._c_args
+        rc = fn(cfg, st, a_t.data_ptr(), p_t.data_ptr(), out, N.current_stream_ptr(self._dev))
         if rc:
             N.check(rc, "apg_lidar_step")
 

@@ -221,9 +221,8 @@ class LightDarkVectorEnv(VectorEnv):
             self.check_errors(block=False)
             a_t = torch.as_tensor(a, dtype=torch.float32, device=self.device).reshape(n, 2).contiguous()
             p_t = torch.as_tensor(p, dtype=torch.float32, device=self.device).reshape(n, 2).contiguous()
-        N.check(N.lib().apg_light_dark_step(ctypes.byref(self._cfg), ctypes.byref(self._state), N.ptr(a_t),
-                                            N.ptr(p_t), ctypes.byref(self._out), self._stream()),
-                "apg_light_dark_step")
+        N.check(N.fast().light_dark_step(N.addr(self._cfg), N.addr(self._state), a_t.data_ptr(), p_t.data_ptr(),
+                                         N.addr(self._out), self._stream() or 0), "apg_light_dark_step")
         self._track_render(p_np if numpy_mode else p_t)
         if numpy_mode:
             return self._numpy_step()

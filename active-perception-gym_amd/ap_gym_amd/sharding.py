@@ -24,6 +24,13 @@ gloo on CPU — for consumers that need the full batch (the north star's obs/rew
          reset and autoreset steps only, and terminated / truncated are the same for the whole batch (episodes
          end together), so they are not gathered at all
 (image_classification.py:117-151 and image_localization.py:131-181 are the outputs gathered).
+`sub_batches=S` (with gather=True and packed rows) overlaps the all-gather with the steps: each rank's envs form S
+sub-envs, sub-batch h of rank r holding global envs [(h*W + r)*m, +m) (m = N / (W*S)), so sub-batch h's all-gather
+fills the contiguous rows [h*W*m, (h+1)*W*m) of the receive buffer and the gathered batch stays in global env order.
+Each sub-env steps, then its gather is issued at once (RCCL: asynchronously on RCCL's stream, which waits for that
+step's kernel only), so RCCL moves sub-batch h's rows while sub-batch h+1's step kernel runs; the current stream
+waits for every gather before step() returns.  Bit-identical to S = 1 (the sub-envs are the same envs, seeded by
+their global ids; image sub-envs draw the whole batch and keep their slice).  Actions are in local_env_ids order.
 Envs without packed rows (e.g. test doubles) take the copying path (fields packed by copies, glimpses only with
 gather_glimpse=True).  Gathered tensors are views of the receive buffer, rewritten by the next step, unless the
 local env was built with copy=True (then they are cloned).
@@ -94,14 +101,28 @@ class ShardedVectorEnv:
 
     def __init__(self, make_local: Callable[..., object], num_envs_total: int, rank: int, world: int,
                  beams: int | None = None, gather: bool = False, group=None, gather_glimpse: bool = False,
-                 time_gather: bool = False):
+                 time_gather: bool = False, sub_batches: int = 1):
         self.rank, self.world, self.gather, self.group = rank, world, gather, group
         self.offset, self.local_num_envs = shard_bounds(num_envs_total, rank, world)
         self.num_envs = num_envs_total
+        self.sub_batches = S = int(sub_batches)
+        if S < 1:
+            raise ValueError("sub_batches must be >= 1")
+        if S > 1 and not gather:
+            raise ValueError("sub_batches > 1 overlaps the all-gather with the steps: it needs gather=True")
+        if num_envs_total % (world * S):
+            raise ValueError(f"num_envs ({num_envs_total}) must be divisible by world size x sub_batches ({world * S})")
+        # sub-batch h of rank r: global envs [(h*W + r)*m, +m), m = N / (W*S), so the all-gather of sub-batch h fills
+        # rows [h*W*m, (h+1)*W*m) of the receive buffer and the gathered batch is in global env order
+        self.sub_num_envs = m = num_envs_total // (world * S)
+        self.sub_offsets = [self.offset] if S == 1 else [(h * world + rank) * m for h in range(S)]
         kw = {"packed_outputs": True} if gather and _accepts(make_local, "packed_outputs") else {}
-        self.env = make_local(num_envs=self.local_num_envs, env_offset=self.offset, **kw)
+        self.envs = [make_local(num_envs=m, env_offset=o, **kw) for o in self.sub_offsets]
+        self.env = self.envs[0]
         self._lidar = _is_lidar(self.env, beams)
         self._packed = gather and getattr(self.env, "output_rows", None) is not None
+        if S > 1 and not self._packed:
+            raise ValueError("sub_batches > 1 needs envs with packed output rows (make_local(packed_outputs=True))")
         self._spec = _row_spec(self.env, beams, gather_glimpse)
         self._row = sum(_nbytes(dt, sh) for _, dt, sh in self._spec)
         self._row += (-self._row) % 8
@@ -115,41 +136,64 @@ class ShardedVectorEnv:
         self.gather_events: list = []  # (begin, end) torch.cuda.Event pairs around each all-gather
 
     # ------------------------------------------------------------------ collectives
-    def _all_gather_into(self, recv, send):
-        """All-gather of `send` ([n, ...]) into `recv` ([world * n, ...]): RCCL in place, gloo through host buffers
-        (CPU tests, or several ranks sharing one GPU)."""
+    def _all_gather_into(self, recv, send, async_op: bool = False):
+        """All-gather of `send` ([n, ...]) into `recv` ([world * n, ...]): RCCL in place (async_op: on RCCL's stream,
+        after the work queued so far on the current stream; returns the work to wait for), gloo through host buffers
+        (CPU tests, or several ranks sharing one GPU; always synchronous, returns None)."""
         import torch
         import torch.distributed as dist
 
         if dist.get_backend(self.group) == "nccl":
-            dist.all_gather_into_tensor(recv, send, group=self.group)
-        else:
-            parts = [torch.empty_like(send, device="cpu") for _ in range(self.world)]
-            dist.all_gather(parts, send.cpu(), group=self.group)
-            recv.copy_(torch.cat(parts))
-        return recv
+            return dist.all_gather_into_tensor(recv, send, group=self.group, async_op=async_op)
+        parts = [torch.empty_like(send, device="cpu") for _ in range(self.world)]
+        dist.all_gather(parts, send.cpu(), group=self.group)
+        recv.copy_(torch.cat(parts))
+        return None
 
-    def _all_gather_rows(self, send):
-        """All-gather of a [n, row] uint8 buffer into self._recv [world * n, row] (allocated once)."""
+    def _part(self, full, h: int):
+        """Sub-batch h's slice of a gathered buffer: rows [h*W*m, (h+1)*W*m) (the whole buffer without sub-batches)."""
+        if self.sub_batches == 1:
+            return full
+        k = self.world * self.sub_num_envs
+        return full[h * k:(h + 1) * k]
+
+    def _gather_parts(self, full, parts):
+        """All-gather each sub-batch's local part ([m, ...]) into its slice of `full` ([N, ...])."""
+        for h, p in enumerate(parts):
+            self._all_gather_into(self._part(full, h), p.contiguous())
+        return full
+
+    def _timing_begin(self, like):
         import torch
 
-        if self._recv is None:
-            self._recv = torch.zeros((self.world * send.shape[0], send.shape[1]), dtype=torch.uint8,
-                                     device=send.device)
-        ev = None
-        if self.time_gather and send.is_cuda:
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record()
-        self._all_gather_into(self._recv, send)
+        if not (self.time_gather and like.is_cuda):
+            return None
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        return ev
+
+    def _timing_end(self, ev):
         if ev is not None:
             ev[1].record()
             self.gather_events.append(ev)
+
+    def _rows_buffer(self, send):
+        """The receive buffer of the packed rows, [N, row] uint8 (allocated once)."""
+        import torch
+
+        if self._recv is None:
+            self._recv = torch.zeros((self.num_envs, send.shape[1]), dtype=torch.uint8, device=send.device)
         return self._recv
 
-    def _gathered_rows(self) -> dict:
-        """The packed path: gather the local env's output rows; field views of the receive buffer (cloned when
-        the local env copies its outputs)."""
-        recv = self._all_gather_rows(self.env.output_rows)
+    def _all_gather_rows(self, send):
+        """All-gather of a [n, row] uint8 buffer into self._recv [world * n, row] (allocated once)."""
+        recv = self._rows_buffer(send)
+        ev = self._timing_begin(send)
+        self._all_gather_into(recv, send)
+        self._timing_end(ev)
+        return recv
+
+    def _row_views(self, recv) -> dict:
         if self._views is None:
             if self._lidar:
                 from .lidar_env import row_views
@@ -163,24 +207,59 @@ class ShardedVectorEnv:
             return {k: v.clone() for k, v in self._views.items()}
         return self._views
 
+    def _gathered_rows(self) -> dict:
+        """The packed path: gather the local envs' output rows (every sub-batch, one after the other); field views
+        of the receive buffer (cloned when the local env copies its outputs)."""
+        recv = self._rows_buffer(self.env.output_rows)
+        ev = self._timing_begin(recv)
+        self._gather_parts(recv, [e.output_rows for e in self.envs])
+        self._timing_end(ev)
+        return self._row_views(recv)
+
+    def _split_step(self, action):
+        """Sub-batches: each sub-env steps, then its rows' all-gather is issued at once (RCCL: async on RCCL's
+        stream, which waits for that step's kernel only), so the gather of sub-batch h overlaps the step kernel of
+        sub-batch h+1; the current stream waits for every gather at the end.  Returns the sub-envs' step outputs and
+        the gathered row views."""
+        m = self.sub_num_envs
+        outs, works, recv, ev = [], [], None, None
+        for h, env in enumerate(self.envs):
+            outs.append(env.step({k: v[h * m:(h + 1) * m] for k, v in action.items()}))
+            if recv is None:
+                recv = self._rows_buffer(env.output_rows)
+                ev = self._timing_begin(recv)
+            works.append(self._all_gather_into(self._part(recv, h), env.output_rows, async_op=True))
+        for w in works:
+            if w is not None:
+                w.wait()
+        self._timing_end(ev)
+        return outs, self._row_views(recv)
+
+    @staticmethod
+    def _parts_of(x, key=None):
+        """The per-sub-batch list of a local output (a list with sub-batches, a single value without)."""
+        xs = x if isinstance(x, list) else [x]
+        return [v[key] for v in xs] if key is not None else xs
+
     def _gathered_index(self, local_index):
         """Image envs: info["index"] of the whole batch, gathered when the batch changes (reset, autoreset)."""
         import torch
 
+        parts = self._parts_of(local_index)
         if self._index_full is None:
-            self._index_full = torch.zeros(self.world * self.local_num_envs, dtype=torch.int64,
-                                           device=local_index.device)
-        return self._all_gather_into(self._index_full, local_index.contiguous())
+            self._index_full = torch.zeros(self.num_envs, dtype=torch.int64, device=parts[0].device)
+        return self._gather_parts(self._index_full, parts)
 
     def _gathered_target_glimpse(self, local):
         """Image localization: the target glimpses of the whole batch, gathered when the batch changes (reset,
         autoreset); not part of the packed rows."""
         import torch
 
+        parts = self._parts_of(local)
         if self._tg_full is None:
-            self._tg_full = torch.zeros((self.world * self.local_num_envs, *local.shape[1:]), dtype=local.dtype,
-                                        device=local.device)
-        return self._all_gather_into(self._tg_full, local.contiguous())
+            self._tg_full = torch.zeros((self.num_envs, *parts[0].shape[1:]), dtype=parts[0].dtype,
+                                        device=parts[0].device)
+        return self._gather_parts(self._tg_full, parts)
 
     def _gathered_inverted(self, local):
         """Image envs with randomly_invert_labels: obs["inverted_label"] of the whole batch.  It is the drawn
@@ -188,14 +267,14 @@ class ShardedVectorEnv:
         other step (image_classification.py:130-141), which needs no collective."""
         import torch
 
-        full = self.world * self.local_num_envs
-        if local.dtype == torch.int64:
+        parts = self._parts_of(local)
+        if parts[0].dtype == torch.int64:
             if self._inv2_full is None:
-                self._inv2_full = torch.full((full,), 2, dtype=torch.int64, device=local.device)
+                self._inv2_full = torch.full((self.num_envs,), 2, dtype=torch.int64, device=parts[0].device)
             return self._c(self._inv2_full)
         if self._inv_full is None:
-            self._inv_full = torch.zeros(full, dtype=local.dtype, device=local.device)
-        return self._c(self._all_gather_into(self._inv_full, local.contiguous()))
+            self._inv_full = torch.zeros(self.num_envs, dtype=parts[0].dtype, device=parts[0].device)
+        return self._c(self._gather_parts(self._inv_full, parts))
 
     def _pack(self, fields: dict):
         import torch
@@ -244,18 +323,23 @@ class ShardedVectorEnv:
         return obs
 
     def reset(self, *, seed=None, options=None):
-        obs, info = self.env.reset(seed=seed, options=options)
+        if self.sub_batches > 1:  # (lists of the sub-envs' local outputs below)
+            outs = [e.reset(seed=seed, options=options) for e in self.envs]
+            obs, info = [o[0] for o in outs], [o[1] for o in outs]
+        else:
+            obs, info = self.env.reset(seed=seed, options=options)
         if not (self.gather and self._packed):
             # the copying path gathers step outputs only (a reset has no reward / prediction fields)
             return obs, info
         v = self._gathered_rows()
+        first = self._parts_of(obs)[0]
         if not self._lidar:
             gobs = self._image_obs(v)
-            if "target_glimpse" in obs:
-                gobs["target_glimpse"] = self._c(self._gathered_target_glimpse(obs["target_glimpse"]))
-            if "inverted_label" in obs:
-                gobs["inverted_label"] = self._gathered_inverted(obs["inverted_label"])
-            return gobs, {"index": self._c(self._gathered_index(info["index"])), "local_obs": obs,
+            if "target_glimpse" in first:
+                gobs["target_glimpse"] = self._c(self._gathered_target_glimpse(self._parts_of(obs, "target_glimpse")))
+            if "inverted_label" in first:
+                gobs["inverted_label"] = self._gathered_inverted(self._parts_of(obs, "inverted_label"))
+            return gobs, {"index": self._c(self._gathered_index(self._parts_of(info, "index"))), "local_obs": obs,
                           "local_info": info}
         gobs = {"lidar": v["lidar"], "odometry": v["odometry"], "time_step": v["time_step"]}
         return gobs, {"map_idx": v["map_idx_out"], "_map_idx": v["reset_mask"], "local_obs": obs,
@@ -278,8 +362,9 @@ class ShardedVectorEnv:
                 scalar["_" + name] = done
             info["stats"] = {"scalar": scalar, "_scalar": done, "length": v["stats_len"]}
             info["_stats"] = done
-            local = local_info.get("stats") if local_info else None
-            if local is not None and "vector" in local:  # the per-step history stays local (this shard's envs)
+            # the per-step history stays local (this shard's envs; with sub-batches in each sub-env's info)
+            local = local_info.get("stats") if isinstance(local_info, dict) else None
+            if local is not None and "vector" in local:
                 info["stats"]["vector"] = local["vector"]
                 info["stats"]["_vector"] = local["_vector"]
         return info
@@ -288,8 +373,9 @@ class ShardedVectorEnv:
         import torch
 
         n = self.num_envs
+        first_obs, first_info = self._parts_of(obs)[0], self._parts_of(info)[0]
         if resetting or self._index_full is None:
-            self._gathered_index(info["index"])
+            self._gathered_index(self._parts_of(info, "index"))
         cls = "label_target" in v
         target = v["label_target"] if cls else v["target_out"]
         loss = v["loss_f64"] if cls else v["loss_f32"]
@@ -303,13 +389,13 @@ class ShardedVectorEnv:
                                torch.ones(n, dtype=torch.float32, device=dev))
         g_term = self._c(self._done_full[1 if tflag else 0])
         g_trunc = self._c(self._done_full[0])
-        pt = info["prediction"]["target"]
+        pt = first_info["prediction"]["target"]
         if isinstance(pt, dict):  # -sparse ids: weight = terminated as float32
             target = {"target": target, "weight": self._c(self._done_full[3 if tflag else 2])}
         ginfo = {"index": self._c(self._index_full), "base_reward": v["base_reward"],
                  "prediction": {"target": target, "loss": loss}, "local_obs": obs}
-        if "stats" in info:  # the vector log wrapper's scalars of the whole batch from the rows; the per-step
-            done = g_term  # history ("vector") stays local to this shard's envs
+        if "stats" in first_info:  # the vector log wrapper's scalars of the whole batch from the rows; the per-step
+            done = g_term  # history ("vector") stays local to this shard's envs (each sub-env's with sub-batches)
             scalar = {}
             for j, nm in enumerate(self.env._metric_names()):
                 scalar[f"final_{nm}"] = v["stats"][j]
@@ -318,24 +404,33 @@ class ShardedVectorEnv:
                 scalar[f"_avg_{nm}"] = done
             if cls:
                 scalar.update(first_correct=v["stats_idx"][0], last_incorrect=v["stats_idx"][1])
-            ginfo["stats"] = {"scalar": scalar, "_scalar": done, "vector": info["stats"]["vector"],
-                              "_vector": info["stats"]["_vector"]}
+            ginfo["stats"] = {"scalar": scalar, "_scalar": done}
+            if isinstance(info, dict):
+                ginfo["stats"].update(vector=info["stats"]["vector"], _vector=info["stats"]["_vector"])
         gobs = self._image_obs(v)
-        if "target_glimpse" in obs:  # gathered when the batch changed (this step's autoreset), else the last one
+        if "target_glimpse" in first_obs:  # gathered when the batch changed (this step's autoreset), else the last one
             if resetting or self._tg_full is None:
-                self._gathered_target_glimpse(obs["target_glimpse"])
+                self._gathered_target_glimpse(self._parts_of(obs, "target_glimpse"))
             gobs["target_glimpse"] = self._c(self._tg_full)
-        if "inverted_label" in obs:
-            gobs["inverted_label"] = self._gathered_inverted(obs["inverted_label"])
+        if "inverted_label" in first_obs:
+            gobs["inverted_label"] = self._gathered_inverted(self._parts_of(obs, "inverted_label"))
         return gobs, v["reward"], g_term, g_trunc, ginfo
 
     def step(self, action):
+        """`action` holds this rank's envs in local order (local_env_ids: with sub-batches, sub-batch 0's envs, then
+        sub-batch 1's, ...).  Gathered outputs are in global env order; local_obs (and the image envs' per-step
+        stats history) are per sub-batch lists with sub-batches."""
         resetting = bool(getattr(self.env, "_prev_done", False))
-        obs, rew, term, trunc, info = self.env.step(action)
-        if not self.gather:
-            return obs, rew, term, trunc, info
+        if self.sub_batches > 1:
+            outs, v = self._split_step(action)
+            obs, term, trunc, info = [o[0] for o in outs], outs[0][2], outs[0][3], [o[4] for o in outs]
+        else:
+            obs, rew, term, trunc, info = self.env.step(action)
+            if not self.gather:
+                return obs, rew, term, trunc, info
         if self._packed:
-            v = self._gathered_rows()
+            if self.sub_batches == 1:
+                v = self._gathered_rows()
             if not self._lidar:
                 return self._packed_image_step(v, obs, term, trunc, info, resetting)
             gobs = {"lidar": v["lidar"], "odometry": v["odometry"], "time_step": v["time_step"]}
@@ -366,5 +461,17 @@ class ShardedVectorEnv:
                  "prediction": {"target": full["target"], "loss": full["loss"]}, "local_obs": obs}
         return gobs, full["reward"], full["terminated"], full["truncated"], ginfo
 
+    @property
+    def local_env_ids(self):
+        """Global ids of this rank's envs in the local order of step()'s actions and the local outputs."""
+        import numpy as np
+
+        return np.concatenate([np.arange(o, o + self.sub_num_envs) for o in self.sub_offsets])
+
+    def check_errors(self):
+        for e in self.envs:
+            e.check_errors()
+
     def close(self):
-        self.env.close()
+        for e in self.envs:
+            e.close()

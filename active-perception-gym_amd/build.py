@@ -73,6 +73,32 @@ def build_torch_ops(force: bool = False) -> str:
     return TORCH_OUT
 
 
+FAST_SRC = os.path.join(CSRC, "apg_pyfast.cpp")
+
+
+def fast_module_path() -> str:
+    import sysconfig
+
+    return os.path.join(OUT_DIR, "_apgfast" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_fast_module(force: bool = False) -> str:
+    """The CPython fast-call entry points of the per-step C-ABI calls (csrc/apg_pyfast.cpp): g++ against the
+    interpreter's headers, linked to libapgym_hip.so next to it ($ORIGIN)."""
+    import sysconfig
+
+    out = fast_module_path()
+    deps = (FAST_SRC, OUT, os.path.join(INCLUDE, "apgym_capi.h"), os.path.abspath(__file__))
+    if not force and os.path.exists(out) and all(os.path.getmtime(d) <= os.path.getmtime(out) for d in deps):
+        return out
+    tmp = f"{out}.{os.getpid()}.tmp"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{sysconfig.get_paths()['include']}",
+                    "-I", INCLUDE, "-o", tmp, FAST_SRC, f"-L{OUT_DIR}", "-lapgym_hip", "-Wl,-rpath,$ORIGIN"],
+                   check=True)
+    os.replace(tmp, out)
+    return out
+
+
 def _stale() -> bool:
     if not os.path.exists(OUT):
         return True
@@ -143,8 +169,8 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str |
     return out
 
 
-def build_all(force: bool = False) -> tuple[str, str]:
-    return build(force=force), build_torch_ops(force=force)
+def build_all(force: bool = False) -> tuple[str, str, str]:
+    return build(force=force), build_torch_ops(force=force), build_fast_module(force=force)
 
 
 if __name__ == "__main__":
@@ -155,3 +181,4 @@ if __name__ == "__main__":
     print(build(force="--force" in args, verbose="--verbose" in args, extra_flags=defs, out=out_arg, only=only))
     if out_arg is None:
         print(build_torch_ops(force="--force" in args))
+        print(build_fast_module(force="--force" in args))

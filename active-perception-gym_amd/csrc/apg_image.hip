@@ -174,6 +174,11 @@ struct FillArgs {
   uint64_t bound;   // exclusive range of integers(lo, lo + bound)
   int64_t cand;     // candidate words examined in parallel (>= n)
   int nblocks;
+  // k_fill_count copies save_words words save_src -> save_dst first (apg_image_draw_ahead's snapshot of the streams,
+  // taken by the first kernel of the draws instead of a separate copy launch)
+  const uint64_t *save_src;
+  uint64_t *save_dst;
+  int save_words;
 };
 
 // work layout (int64): the finishing ticket counter, then (`wk` = work + 1) [nblocks] block totals,
@@ -276,6 +281,7 @@ __global__ void k_fill_uniform_finish(apg_pcg64 *st, int64_t m) {
 __global__ __launch_bounds__(FILL_THREADS) void k_fill_count(const apg_pcg64 *st, FillArgs a, int64_t *work_all) {
   int64_t *work = work_all + 1;
   __shared__ int s_sum[FILL_THREADS / 64];
+  if (blockIdx.x == 0 && (int)threadIdx.x < a.save_words) a.save_dst[threadIdx.x] = a.save_src[threadIdx.x];
   const LemireSpec l = lemire_spec(a.bound);
   const int64_t k0 = ((int64_t)blockIdx.x * FILL_THREADS + threadIdx.x) * FILL_PER_THREAD;
   int cnt = 0;
@@ -1524,14 +1530,26 @@ int64_t fill_candidates(int64_t n, uint64_t bound) {
   return cand < n ? n : cand;
 }
 
+// save_src / save_dst (optional): save_words words copied by the first kernel before any draw (or by a copy when no
+// kernel of this call reads the stream)
 int launch_integers(apg_pcg64 *state, int64_t n, int64_t lo, uint64_t bound, int64_t *out, int64_t *work,
-                    hipStream_t s) {
+                    hipStream_t s, const apg_pcg64 *save_src = nullptr, apg_pcg64 *save_dst = nullptr,
+                    int save_count = 0) {
+  if (save_dst && (n <= 0 || bound == 1) &&
+      hipMemcpyAsync(save_dst, save_src, save_count * sizeof(apg_pcg64), hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return fail(APG_E_LAUNCH, "hipMemcpyAsync (stream snapshot)");
   if (n <= 0) return APG_OK;
   if (bound == 1) {  // integers(lo, lo + 1): no draw at all
     hipLaunchKernelGGL(k_fill_const, dim3(grid_for(n, 256)), dim3(256), 0, s, n, lo, out);
     return check_launch("k_fill_const");
   }
   FillArgs a{};
+  if (save_dst) {
+    static_assert(sizeof(apg_pcg64) % 8 == 0, "apg_pcg64: whole 8-byte words");
+    a.save_src = reinterpret_cast<const uint64_t *>(save_src);
+    a.save_dst = reinterpret_cast<uint64_t *>(save_dst);
+    a.save_words = save_count * (int)(sizeof(apg_pcg64) / 8);
+  }
   a.kind = APG_DRAW_INTEGERS;
   a.n = n;
   a.cols = 1;
@@ -1937,11 +1955,12 @@ int apg_image_draw_ahead(const apg_image_config *c, const apg_image_state *st, a
   if (!st->ahead_i64 || !st->ahead_f64 || !st->rng_saved) return fail(APG_E_INVALID, "null ahead buffers");
   hipStream_t s = (hipStream_t)stream;
   const int nt = c->num_envs_total;
-  if (hipMemcpyAsync(st->rng_saved, st->rng, 3 * sizeof(apg_pcg64), hipMemcpyDeviceToDevice, s) != hipSuccess)
-    return fail(APG_E_LAUNCH, "hipMemcpyAsync (streams before the draws made ahead)");
   int rc;
-  // module_reset's draws in its order: next(DatasetBatchIterator), label inversions, start positions
-  if ((rc = launch_integers(st->rng + 2, nt, 0, (uint64_t)c->pool_len, st->ahead_i64, st->rng_work, s))) return rc;
+  // module_reset's draws in its order: next(DatasetBatchIterator), label inversions, start positions; the first
+  // kernel also keeps the three streams as they were before (rng_saved, for apg_image_discard_ahead)
+  if ((rc = launch_integers(st->rng + 2, nt, 0, (uint64_t)c->pool_len, st->ahead_i64, st->rng_work, s, st->rng,
+                            st->rng_saved, 3)))
+    return rc;
   if (c->invert_labels && (rc = launch_integers(st->rng + 1, nt, 0, 2, st->ahead_i64 + nt, st->rng_work, s))) return rc;
   const double low[2] = {-1.0, -1.0}, range[2] = {2.0, 2.0};
   if ((rc = launch_uniform(st->rng + 1, nt, 2, low, range, st->ahead_f64, s, st->rng_work))) return rc;

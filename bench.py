@@ -170,7 +170,7 @@ def run_image(args, world, rank, dev):
     senv = ShardedVectorEnv(lambda num_envs, env_offset, **kw: cls(num_envs, cfg, device=dev, array_backend="torch",
                                                                    num_envs_total=n_total, env_offset=env_offset,
                                                                    log_stats=log_stats, **kw),
-                            n_total, rank, world, gather=args.gather, time_gather=True)
+                            n_total, rank, world, gather=args.gather, time_gather=True, sub_batches=args.sub_batches)
     env = senv.env
     ring = 17
     g = torch.Generator(device=dev).manual_seed(1 + rank)
@@ -182,7 +182,7 @@ def run_image(args, world, rank, dev):
     inputs = [{"action": acts[k], "prediction": preds[k]} for k in range(ring)]  # prepared up front
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    env.reset(seed=0)
+    (senv if senv.sub_batches > 1 else env).reset(seed=0)  # (every sub-batch's env resets)
     torch.cuda.synchronize(dev)
     reset_ms = (time.perf_counter() - t0) * 1e3
     for t in range(args.warmup):
@@ -202,7 +202,7 @@ def run_image(args, world, rank, dev):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    env.check_errors()
+    senv.check_errors()
     # the kernel-time pass (roofline and gather_ms, not `value`): K more steps, hipEvents right around the step's
     # kernel launches (inside env.step) on every event_every-th, and around every all-gather
     senv.time_gather = True
@@ -216,7 +216,7 @@ def run_image(args, world, rank, dev):
             stepper(inputs[(args.warmup + args.steps + t) % ring])
     env.set_kernel_timing_events(None)
     torch.cuda.synchronize(dev)
-    env.check_errors()
+    senv.check_errors()
     step_ms = sum(ev.elapsed_ms(i) for i in timed) / len(timed)
     gather_ms = senv.gather_ms() or 0.0
     ev.close()
@@ -235,7 +235,7 @@ def run_image(args, world, rank, dev):
         events_ms = step_ms
         if dj is not None:
             step_ms = dj["per_class"]["step"]["median_us"] / 1e3
-        achieved = bpe * n_local / (step_ms * 1e-3) / 1e9
+        achieved = bpe * (n_local // args.sub_batches) / (step_ms * 1e-3) / 1e9  # (the timed launch: sub-batch 0's)
         tj, tpath = pmc_table(args.workload, "image", shape)
         traffic = issue = traffic_cal = None
         if tj is not None:
@@ -267,7 +267,7 @@ def run_image(args, world, rank, dev):
                          "kernel_ms": step_ms, "kernel_ms_source": dpath or "hip events",
                          "kernel_ms_events": events_ms,
                          "launches_timed": len(timed), "event_every": args.event_every,
-                         "bytes_per_launch": bpe * n_local, "issue": issue},
+                         "bytes_per_launch": bpe * (n_local // args.sub_batches), "issue": issue},
         }
         if world == 1 and not args.no_cpu_baseline:
             pool, labels = ds.device_pool()
@@ -435,7 +435,8 @@ def run_lidar(args, world, rank, dev):
         return apg.make_vec(w["env_id"], num_envs=num_envs, lidar_beam_count=beams, dataset=ds, device=dev,
                             array_backend=args.array_backend, env_offset=env_offset, **kw)
 
-    senv = ShardedVectorEnv(make_local, n_total, rank, world, beams, gather=args.gather, time_gather=True)
+    senv = ShardedVectorEnv(make_local, n_total, rank, world, beams, gather=args.gather, time_gather=True,
+                            sub_batches=args.sub_batches)
     env = senv.env
     ring = 128  # distinct synthetic action/prediction batches, cycled
     g = torch.Generator(device=dev).manual_seed(1 + rank)
@@ -476,7 +477,7 @@ def run_lidar(args, world, rank, dev):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    env.check_errors()
+    senv.check_errors()
     # the kernel-time pass (roofline and gather_ms, not `value`): K more steps, hipEvents around the step's
     # launches on every event_every-th (an event pair adds stream packets and +6..9 us of wall to its step) and
     # around every all-gather
@@ -487,7 +488,7 @@ def run_lidar(args, world, rank, dev):
         step(ev.pair(t) if t % args.event_every == args.event_every - 1 else (None, None))
     torch.cuda.synchronize(dev)
     env.set_kernel_timing_events(None)
-    env.check_errors()
+    senv.check_errors()
     per_step = [ev.elapsed_ms(i) for i in timed]
     gather_ms = senv.gather_ms() or 0.0
     kernel_ms = sum(per_step) / len(per_step)
@@ -510,7 +511,7 @@ def run_lidar(args, world, rank, dev):
         torch.cuda.synchronize(dev)
         ep_s = time.perf_counter() - te
         env.set_kernel_timing_events(None)
-        env.check_errors()
+        senv.check_errors()
         ep = [ev.elapsed_ms(args.steps + t) for t in ep_t]
         # mean kernel time of the episode: the ordinary steps' sampled mean over 100 steps + the reset step
         ep_mean = (statistics.mean(ep[:-1]) * (EPISODE_PERIOD - 1) + ep[-1]) / EPISODE_PERIOD
@@ -527,9 +528,9 @@ def run_lidar(args, world, rank, dev):
 
     if rank == 0:
         value = n_total * args.steps / elapsed
-        step_b = BYTES_PER_ENV_STEP(beams) * n_local
+        step_b = BYTES_PER_ENV_STEP(beams) * (n_local // args.sub_batches)  # (the timed launch: sub-batch 0's)
         # a reset step also writes each env's map obs (f32) and its bit-packed occupancy rows
-        reset_b = step_b + (MAP_OBS_BYTES(msize) + msize * ((msize + 63) // 64) * 8) * n_local
+        reset_b = step_b + (MAP_OBS_BYTES(msize) + msize * ((msize + 63) // 64) * 8) * (n_local // args.sub_batches)
         # the launches the kernel time averages over: the kernel-time pass's steps that carried events
         reset_ev = sum(1 for t in timed if (first_ev + t) % EPISODE_PERIOD == 0)
         bytes_per_launch = (step_b * (len(timed) - reset_ev) + reset_b * reset_ev) / len(timed)
@@ -674,7 +675,9 @@ def shard_plan(args, world: int) -> dict:
     return {"workload": name, "num_envs_per_gpu": n_local, "num_envs_total": n_local * world,
             "scaling": "strong" if "envs_total" in w else "weak", "row_bytes": row if args.gather else None,
             "gather_bytes_per_rank_step": row * n_local * (world - 1) if args.gather else 0,
-            "parallelism": f"env-shard x{world}" + (" + all-gather" if args.gather else "")}
+            "sub_batches": args.sub_batches,
+            "parallelism": f"env-shard x{world}" + (" + all-gather" if args.gather else "") + (
+                f" in {args.sub_batches} overlapped sub-batches" if args.sub_batches > 1 else "")}
 
 
 def run_dry(args, world, rank):
@@ -690,25 +693,33 @@ def run_dry(args, world, rank):
     if world > 1:
         dist.init_process_group("gloo")
         dist.barrier()
-    send = parts = None
-    if args.gather:
-        send = torch.empty((n_local, plan["row_bytes"]), dtype=torch.uint8)
-        send[:, 0] = rank
-        send[:, 8:16].view(torch.int64)[:, 0] = torch.arange(rank * n_local, (rank + 1) * n_local)  # env index
-        parts = [torch.empty_like(send) for _ in range(world)]
+    S = args.sub_batches
+    if n_local % S:
+        raise SystemExit(f"{n_local} envs per rank do not split into {S} sub-batches")
+    m = n_local // S
+    sends = parts = None
+    if args.gather:  # sub-batch h of rank r: global envs [(h*W + r)*m, +m) (ShardedVectorEnv's layout)
+        sends = []
+        for h in range(S):
+            snd = torch.empty((m, plan["row_bytes"]), dtype=torch.uint8)
+            snd[:, 0] = rank
+            snd[:, 8:16].view(torch.int64)[:, 0] = torch.arange((h * world + rank) * m, (h * world + rank + 1) * m)
+            sends.append(snd)
+        parts = [[torch.empty_like(sends[0]) for _ in range(world)] for _ in range(S)]
     t0 = time.perf_counter()
     for _ in range(args.steps):
         if args.gather:
-            if world > 1:
-                dist.all_gather(parts, send)
-            else:
-                parts[0].copy_(send)
+            for h in range(S):
+                if world > 1:
+                    dist.all_gather(parts[h], sends[h])
+                else:
+                    parts[h][0].copy_(sends[h])
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if args.gather:
-        got = torch.cat(parts)
-        ok = bool((got[:, 0] == torch.arange(world).repeat_interleave(n_local)).all()) and bool(
+        got = torch.cat([p for ps in parts for p in ps])
+        ok = bool((got[:, 0] == torch.arange(world).repeat_interleave(m).repeat(S)).all()) and bool(
             (got[:, 8:16].contiguous().view(torch.int64)[:, 0] == torch.arange(world * n_local)).all())
         if not ok:
             raise SystemExit(f"rank {rank}: gathered rows out of order")
@@ -736,6 +747,9 @@ def main():
     ap.add_argument("--beams", type=int, default=None)
     ap.add_argument("--map-size", type=int, default=None)
     ap.add_argument("--gather", action="store_true", help="all-gather step outputs across ranks (RCCL)")
+    ap.add_argument("--sub-batches", type=int, default=1,
+                    help="with --gather: each rank's envs in S sub-batches whose all-gathers are issued right after "
+                         "their steps, so RCCL gathers sub-batch h while sub-batch h+1 steps (ShardedVectorEnv)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-episode", action="store_true", help="skip the one-episode measurement after the timed steps")
     ap.add_argument("--cpu-envs", type=int, default=None)
@@ -772,6 +786,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.sub_batches > 1 and not args.gather:
+        raise SystemExit("--sub-batches overlaps the all-gather with the steps: it needs --gather")
     if args.dry_run:
         return run_dry(args, world, rank)
     # one rank per GPU; with fewer visible GPUs than ranks (rehearsals with --dist-backend gloo) ranks share them

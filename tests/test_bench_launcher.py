@@ -59,6 +59,19 @@ def test_dry_run_eight_ranks_maze127():
     assert cfg["parallelism"] == "env-shard x8"
 
 
+@pytest.mark.parametrize("workload,per_rank", [("lidar", 65536), ("maze127", 32768), ("tinyimagenet-loc", 4096)])
+def test_dry_run_eight_ranks_gather_in_sub_batches(workload, per_rank):
+    """BASELINE configs 2 / 3 / 5 at 8 ranks with the all-gather split into two sub-batches (ShardedVectorEnv's
+    overlapped layout: sub-batch h of rank r holds global envs [(h*W + r)*m, +m)): every rank receives every row,
+    in global env order (run_dry checks the env index carried in each row)."""
+    out = _run(["--gpus", "8", "--dry-run", "--workload", workload, "--gather", "--sub-batches", "2", "--steps", "2",
+                "--warmup", "0"], 300)
+    cfg = out["config"]
+    assert out["n_gpus"] == 8 and cfg["num_envs_per_gpu"] == per_rank and cfg["sub_batches"] == 2
+    assert cfg["gather_bytes_per_rank_step"] == 7 * per_rank * cfg["row_bytes"]
+    assert cfg["parallelism"] == "env-shard x8 + all-gather in 2 overlapped sub-batches"
+
+
 def test_dry_run_rejects_an_uneven_split():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--workload", "maze127",
                         "--gpus", "1"], capture_output=True, text=True, timeout=120, cwd=ROOT,

@@ -106,7 +106,7 @@ def test_shards_union_equals_unsharded(gpu, kind):
     torch.cuda.synchronize()
 
 
-def _worker(rank, world, port, kind, outdir, backend="gloo"):
+def _worker(rank, world, port, kind, outdir, backend="gloo", sub=1):
     import torch
     import torch.distributed as dist
 
@@ -120,9 +120,9 @@ def _worker(rank, world, port, kind, outdir, backend="gloo"):
 
     senv = ShardedVectorEnv(lambda num_envs, env_offset, **kw: _make(kind, num_envs, env_offset, N_TOTAL, **kw),
                             N_TOTAL, rank, world, beams=16 if kind == "lidar" else None, gather=True,
-                            gather_glimpse=True)
+                            gather_glimpse=True, sub_batches=sub)
     assert senv._packed  # the step kernels write the all-gather's send rows (LIDAR and image envs)
-    lo, n = senv.offset, senv.local_num_envs
+    ids = torch.as_tensor(senv.local_env_ids, device="cuda:0")
     obs0, info0 = senv.reset(seed=5)
     rows = []
     if kind == "lidar":  # reset returns the gathered batch too
@@ -130,7 +130,7 @@ def _worker(rank, world, port, kind, outdir, backend="gloo"):
         rows[-1]["map_idx"] = info0["map_idx"].cpu().numpy().copy()
     for t in range(_steps(kind)):
         a, p = _actions(kind, t, N_TOTAL)
-        obs, rew, term, trunc, info = senv.step({"action": a[lo:lo + n], "prediction": p[lo:lo + n]})
+        obs, rew, term, trunc, info = senv.step({"action": a[ids], "prediction": p[ids]})
         rows.append(_flat(kind, obs, rew, term, info))
     torch.cuda.synchronize()
     np.savez(os.path.join(outdir, f"rank{rank}.npz"),
@@ -159,14 +159,15 @@ def test_two_rank_gather_on_gpu_equals_unsharded(gpu, kind, tmp_path):
                 assert np.array_equal(got[r][f"{t}_{k}"], v), f"rank {r} step {t}: {k}"
 
 
-@pytest.mark.parametrize("kind", ["lidar", "image", "image_cls_inv"])
-def test_rccl_gather_branch_single_rank(gpu, kind, tmp_path):
+@pytest.mark.parametrize("kind,sub", [("lidar", 1), ("image", 1), ("image_cls_inv", 1), ("lidar", 2), ("image", 2)])
+def test_rccl_gather_branch_single_rank(gpu, kind, sub, tmp_path):
     """The RCCL branch of ShardedVectorEnv._all_gather_rows (dist.all_gather_into_tensor on the device rows;
     sharding.py) on a one-rank "nccl" group: RCCL refuses two ranks on one device, so this is the only way
-    one GPU runs that branch.  The gathered batch must equal the unsharded env."""
+    one GPU runs that branch.  The gathered batch must equal the unsharded env.  sub = 2: two sub-batches whose
+    all-gathers are issued asynchronously right after their steps (RCCL's stream overlaps the next step kernel)."""
     import torch.multiprocessing as mp
 
-    mp.start_processes(_worker, args=(1, _free_port(), kind, str(tmp_path), "nccl"), nprocs=1, join=True,
+    mp.start_processes(_worker, args=(1, _free_port(), kind, str(tmp_path), "nccl", sub), nprocs=1, join=True,
                        start_method="spawn")
     ref = _reference(kind, with_reset=kind == "lidar")
     got = np.load(tmp_path / "rank0.npz")

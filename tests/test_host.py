@@ -29,6 +29,33 @@ def test_capi_library_exports_every_declared_symbol():
     assert _native.lib().apg_version().startswith(b"apgym-mi355x")
 
 
+def test_fast_call_module_reaches_the_c_abi():
+    """_apgfast (csrc/apg_pyfast.cpp): the per-step C-ABI calls without ctypes marshalling.  Invalid configurations
+    return the C ABI's validation error before any HIP call, so this runs without a GPU."""
+    import ctypes
+
+    from ap_gym_amd import _native as N
+
+    F = N.fast()
+    assert os.path.dirname(F.__file__) == N.LIB_DIR
+    for name, args, cfg, st, out in (("lidar_step", 6, N.LidarConfig(), N.LidarState(), N.LidarOutputs()),
+                                     ("image_step", 8, N.ImageConfig(), N.ImageState(), N.ImageOutputs()),
+                                     ("light_dark_step", 6, N.LightDarkConfig(), N.LightDarkState(),
+                                      N.LightDarkOutputs())):
+        fn = getattr(F, name)
+        tail = [N.addr(out), 0] if args == 6 else [3, 0, N.addr(out), 0]
+        assert fn(N.addr(cfg), N.addr(st), 0, 0, *tail) == N.APG_E_INVALID, name
+        assert N.lib().apg_last_error()  # the C ABI's own message
+        with pytest.raises(TypeError):
+            fn(N.addr(cfg))
+        with pytest.raises(TypeError):
+            fn(N.addr(cfg), N.addr(st), "x", 0, *tail)
+        # the same validation result as the ctypes entry point
+        c_fn = getattr(N.lib(), "apg_" + name)
+        c_tail = [ctypes.byref(out), None] if args == 6 else [3, 0, ctypes.byref(out), None]
+        assert c_fn(ctypes.byref(cfg), ctypes.byref(st), None, None, *c_tail) == N.APG_E_INVALID
+
+
 def test_capi_validation_without_gpu():
     import ctypes
 

@@ -82,21 +82,22 @@ def _actions():
             rng.uniform(-1, 1, (STEPS, N_TOTAL, 2)).astype(np.float32))
 
 
-def _worker(rank, world, port, outdir, packed=False):
+def _worker(rank, world, port, outdir, packed=False, sub=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from ap_gym_amd.sharding import ShardedVectorEnv
 
     make = _PackedOracleShard if packed else (lambda num_envs, env_offset: _OracleShard(num_envs, env_offset))
-    senv = ShardedVectorEnv(make, N_TOTAL, rank, world, BEAMS, gather=True)
-    assert senv._packed == packed
+    senv = ShardedVectorEnv(make, N_TOTAL, rank, world, BEAMS, gather=True, sub_batches=sub)
+    assert senv._packed == packed and len(senv.envs) == sub
     acts, preds = _actions()
-    lo, n = senv.offset, senv.local_num_envs
+    ids = senv.local_env_ids  # sub-batches: rank r owns [(h*W + r)*m, +m) for each h
+    assert len(ids) == senv.local_num_envs and (sub > 1 or ids[0] == senv.offset)
     senv.reset(seed=7)
     rows = []
     for t in range(STEPS):
-        obs, rew, term, trunc, info = senv.step({"action": torch.from_numpy(acts[t, lo:lo + n]),
-                                                 "prediction": torch.from_numpy(preds[t, lo:lo + n])})
+        obs, rew, term, trunc, info = senv.step({"action": torch.from_numpy(acts[t, ids]),
+                                                 "prediction": torch.from_numpy(preds[t, ids])})
         rows.append(np.concatenate([np.ascontiguousarray(obs["lidar"].numpy()).view(np.uint8).ravel(),
                                     np.ascontiguousarray(obs["odometry"].numpy()).view(np.uint8).ravel(),
                                     np.ascontiguousarray(obs["time_step"].numpy()).view(np.uint8).ravel(),
@@ -125,9 +126,41 @@ def test_shard_bounds():
         shard_bounds(10, 0, 4)
 
 
-@pytest.mark.parametrize("packed", [False, True], ids=["copying", "packed_rows"])
-def test_two_rank_gather_equals_unsharded(tmp_path, oracle_mod, packed):
-    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), packed), nprocs=2, join=True,
+def test_sub_batch_layout_and_checks():
+    """Sub-batch h of rank r holds global envs [(h*W + r)*m, +m); every global env is in exactly one sub-batch."""
+    from ap_gym_amd.sharding import ShardedVectorEnv
+
+    made = []
+
+    def make(num_envs, env_offset, packed_outputs=False):
+        made.append((num_envs, env_offset))
+        env = type("E", (), {})()  # a stand-in: only the constructor's layout is checked here
+        env.output_rows = torch.zeros((num_envs, 8), dtype=torch.uint8) if packed_outputs else None
+        env.lidar_beam_count = BEAMS
+        return env
+
+    ids = []
+    for r in range(2):
+        made.clear()
+        s = ShardedVectorEnv(make, 16, r, 2, BEAMS, gather=True, sub_batches=4)
+        assert made == [(2, (h * 2 + r) * 2) for h in range(4)] and s.sub_num_envs == 2
+        ids.append(s.local_env_ids)
+    assert sorted(np.concatenate(ids).tolist()) == list(range(16))
+    with pytest.raises(ValueError, match="gather=True"):
+        ShardedVectorEnv(make, 16, 0, 2, BEAMS, gather=False, sub_batches=2)
+    with pytest.raises(ValueError, match="divisible"):
+        ShardedVectorEnv(make, 16, 0, 2, BEAMS, gather=True, sub_batches=3)
+    with pytest.raises(ValueError, match="packed"):
+        ShardedVectorEnv(lambda num_envs, env_offset: make(num_envs, env_offset), 16, 0, 2, BEAMS, gather=True,
+                         sub_batches=2)
+
+
+@pytest.mark.parametrize("packed,sub", [(False, 1), (True, 1), (True, 2), (True, 4)],
+                         ids=["copying", "packed_rows", "packed_rows_2sub", "packed_rows_4sub"])
+def test_two_rank_gather_equals_unsharded(tmp_path, oracle_mod, packed, sub):
+    """sub > 1: each rank's envs in sub-batches whose all-gathers are issued right after their steps (overlapping
+    the next sub-batch's step on RCCL); the gathered batch is still in global env order."""
+    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), packed, sub), nprocs=2, join=True,
                        start_method="spawn")
     r0, r1 = np.load(tmp_path / "rank0.npy"), np.load(tmp_path / "rank1.npy")
     assert np.array_equal(r0, r1)  # every rank holds the full batch
@@ -259,7 +292,7 @@ class _ImageOracleShard:
         pass
 
 
-def _img_worker(rank, world, port, outdir, kind, packed):
+def _img_worker(rank, world, port, outdir, kind, packed, sub=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from ap_gym_amd.sharding import ShardedVectorEnv
@@ -267,14 +300,14 @@ def _img_worker(rank, world, port, outdir, kind, packed):
     def make(num_envs, env_offset, packed_outputs=False):
         return _ImageOracleShard(kind, num_envs, env_offset, packed_outputs)
 
-    senv = ShardedVectorEnv(make, IMG_N, rank, world, gather=True, gather_glimpse=True)
+    senv = ShardedVectorEnv(make, IMG_N, rank, world, gather=True, gather_glimpse=True, sub_batches=sub)
     assert senv._packed == packed or not packed
     if not packed:  # the copying path: a factory without packed_outputs
         senv = ShardedVectorEnv(lambda num_envs, env_offset: _ImageOracleShard(kind, num_envs, env_offset), IMG_N, rank,
                                 world, gather=True, gather_glimpse=True)
         assert not senv._packed
     acts, preds = _img_actions(kind)
-    lo, n = senv.offset, senv.local_num_envs
+    ids = senv.local_env_ids
     obs, info = senv.reset(seed=7)
     out = {}
     if packed:  # (the copying path gathers step outputs only)
@@ -283,8 +316,8 @@ def _img_worker(rank, world, port, outdir, kind, packed):
         if "inverted_label" in obs:
             out["reset_inverted_label"] = obs["inverted_label"].numpy().copy()
     for t in range(IMG_STEPS):
-        obs, rew, term, trunc, info = senv.step({"action": torch.from_numpy(acts[t, lo:lo + n]),
-                                                 "prediction": torch.from_numpy(preds[t, lo:lo + n])})
+        obs, rew, term, trunc, info = senv.step({"action": torch.from_numpy(acts[t, ids]),
+                                                 "prediction": torch.from_numpy(preds[t, ids])})
         for k in ("glimpse", "glimpse_pos", "time_step", "target_glimpse", "inverted_label"):
             if k in obs:
                 out[f"{k}_{t}"] = obs[k].numpy().copy()
@@ -302,12 +335,13 @@ def _img_worker(rank, world, port, outdir, kind, packed):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("packed", [False, True], ids=["copying", "packed_rows"])
+@pytest.mark.parametrize("packed,sub", [(False, 1), (True, 1), (True, 2)],
+                         ids=["copying", "packed_rows", "packed_rows_2sub"])
 @pytest.mark.parametrize("kind", ["cls", "loc", "cls_inv"])
-def test_two_rank_image_gather_equals_unsharded(tmp_path, kind, packed):
+def test_two_rank_image_gather_equals_unsharded(tmp_path, kind, packed, sub):
     from oracle import image_oracle as io
 
-    mp.start_processes(_img_worker, args=(2, _free_port(), str(tmp_path), kind, packed), nprocs=2, join=True,
+    mp.start_processes(_img_worker, args=(2, _free_port(), str(tmp_path), kind, packed, sub), nprocs=2, join=True,
                        start_method="spawn")
     r0, r1 = np.load(tmp_path / "img_rank0.npz"), np.load(tmp_path / "img_rank1.npz")
     assert sorted(r0.files) == sorted(r1.files)
