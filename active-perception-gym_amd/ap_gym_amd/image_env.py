@@ -74,6 +74,17 @@ def unique_sampling_grid(image_hw, sensor_size, sensor_scale, rel=0.2):
     return np.ascontiguousarray(grid), cell
 
 
+def device_pool_u8(pool: np.ndarray, dev):
+    """A uint8 image pool on `dev` with N.APG_U8_POOL_PAD readable bytes after the last image (the glimpse kernels
+    read taps with whole-dword loads, apgym_capi.h); the returned tensor is the [M, H, W, C] view."""
+    import torch
+
+    nb = pool.nbytes
+    buf = torch.zeros(nb + N.APG_U8_POOL_PAD, dtype=torch.uint8, device=dev)
+    buf[:nb].copy_(torch.from_numpy(np.ascontiguousarray(pool).reshape(-1)))
+    return buf[:nb].view(pool.shape)
+
+
 def softmax_nan_rows(logits: np.ndarray) -> np.ndarray:
     """Rows where scipy.special.softmax(row)[label] is NaN: a NaN or +inf logit, or all -inf."""
     return np.isnan(logits).any(-1) | np.isposinf(logits).any(-1) | np.isneginf(logits).all(-1)
@@ -234,7 +245,8 @@ class _ImageVectorEnv(VectorEnv):
         gshape = (n, s0, s1, c)
         work = max(N.lib().apg_rng_fill_work_elems(nt, b) for b in (m, int(cfg.unique_sampling_top_k), 2))
         self._t = T = dict(
-            pool=pool_t if pool_t is not None else t.from_numpy(pool).to(dev),
+            pool=pool_t if pool_t is not None else device_pool_u8(pool, dev) if pool.dtype == np.uint8 else
+            t.from_numpy(pool).to(dev),
             pool_labels=labels_t if labels_t is not None else t.from_numpy(labels).to(dev),
             unique_grid=t.from_numpy(grid).to(dev),
             index=t.zeros(n, dtype=t.int64, device=dev), label=t.zeros(n, dtype=t.int32, device=dev),

@@ -477,6 +477,9 @@ struct U8Taps {
   uint32_t a00, a01, a02, a10, a11, a12;
   int o0, o1;
 };
+#ifndef APG_TAPS_WIDE
+#define APG_TAPS_WIDE 1  // (0: the per-dword tap loads of round 4, A/B knob)
+#endif
 
 template <bool F32, int PC, int C, int GT = GS_THREADS>
 APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, FastDiv per_div, FastDiv s1_div,
@@ -543,14 +546,27 @@ APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, 
       // pointer arithmetic (not integer round trips) keeps the loads global rather than flat
       const uint32_t *d0 = reinterpret_cast<const uint32_t *>(im + (r0 - t.o0)),
                      *d1 = reinterpret_cast<const uint32_t *>(im + (r1 - t.o1));
-      t.a00 = d0[0];
-      t.a10 = d1[0];
-      t.a01 = t.o0 + span > 4 ? d0[1] : 0u;
-      t.a11 = t.o1 + span > 4 ? d1[1] : 0u;
-      t.a02 = t.a12 = 0u;
-      if constexpr (span > 4) {
-        t.a02 = t.o0 + span > 8 ? d0[2] : 0u;
-        t.a12 = t.o1 + span > 8 ? d1[2] : 0u;
+      if constexpr (APG_TAPS_WIDE && span > 4) {
+        // RGB: one dwordx3 load per row instead of up to three dword loads (a third of the address work:
+        // TinyImageNetLoc 31.1-31.5 -> 30.6 us); it reads up to 6 bytes past the row's taps (u8 pools carry
+        // APG_U8_POOL_PAD bytes of slack after the last image, apgym_capi.h).  Grey pools keep the per-dword
+        // loads (an unconditional dwordx2 measured 11.4 -> 11.6 us at MNIST)
+        typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+        u32x3 v0, v1;
+        __builtin_memcpy(&v0, d0, 12);
+        __builtin_memcpy(&v1, d1, 12);
+        t.a00 = v0.x, t.a01 = v0.y, t.a02 = v0.z;
+        t.a10 = v1.x, t.a11 = v1.y, t.a12 = v1.z;
+      } else {
+        t.a00 = d0[0];
+        t.a10 = d1[0];
+        t.a01 = t.o0 + span > 4 ? d0[1] : 0u;
+        t.a11 = t.o1 + span > 4 ? d1[1] : 0u;
+        t.a02 = t.a12 = 0u;
+        if constexpr (span > 4) {
+          t.a02 = t.o0 + span > 8 ? d0[2] : 0u;
+          t.a12 = t.o1 + span > 8 ? d1[2] : 0u;
+        }
       }
       return t;
     };

@@ -319,8 +319,12 @@ typedef struct apg_image_config {
                                  stays dense [N][G0][G1][C] either way: it changes only with the batch */
 } apg_image_config;
 
+/* u8 pools are read with whole-dword loads that may run up to APG_U8_POOL_PAD - 1 bytes past the last image: the
+ * allocation must extend APG_U8_POOL_PAD readable bytes beyond [pool_len][H][W][pool_channels] */
+#define APG_U8_POOL_PAD 16
+
 typedef struct apg_image_state {
-  const void *pool;           /* [pool_len][H][W][pool_channels] u8 or f32 */
+  const void *pool;           /* [pool_len][H][W][pool_channels] u8 (+ APG_U8_POOL_PAD bytes) or f32 */
   const int32_t *pool_labels; /* [pool_len] */
   const double *unique_grid;  /* [P][2] sampling positions (localize) */
   int64_t *index;             /* [N] data point index of each env (info["index"]) */
@@ -384,7 +388,7 @@ int apg_image_draw_ahead(const apg_image_config *cfg, const apg_image_state *st,
 int apg_image_discard_ahead(const apg_image_config *cfg, const apg_image_state *st, apg_stream_t stream);
 
 /* Glimpses of npos positions per env: pos (f64 or f32, pos_is_f32) [N][npos][2] -> out
- * [N][npos][sensor_h][sensor_w][C]; index[N] selects the pool image of each env. */
+ * [N][npos][sensor_h][sensor_w][C]; index[N] selects the pool image of each env (u8 pools: + APG_U8_POOL_PAD). */
 int apg_image_glimpse(const apg_image_config *cfg, const void *pool, const int64_t *index, const void *pos,
                       int pos_is_f32, int32_t npos, float *out, uint32_t *err, apg_stream_t stream);
 

@@ -117,6 +117,15 @@ def _pool(rng, m, h, w, pc, dtype):
     return rng.uniform(-0.2, 1.2, (m, h, w, pc)).astype(np.float32)
 
 
+def _dev_pool(pool, dev):
+    """The pool on the device as the envs upload it: u8 pools with APG_U8_POOL_PAD bytes of slack (apgym_capi.h)."""
+    import torch
+
+    from ap_gym_amd.image_env import device_pool_u8
+
+    return device_pool_u8(pool, dev) if pool.dtype == np.uint8 else torch.as_tensor(pool, device=dev)
+
+
 @pytest.mark.parametrize("case", range(len(GLIMPSE_CASES)))
 def test_glimpse_matches_oracle(gpu, case):
     import torch
@@ -137,7 +146,8 @@ def test_glimpse_matches_oracle(gpu, case):
     cfg = _cfg(N, n, N.APG_IMAGE_CLASSIFY, h, w, pc, c, sensor, scale, dtype, m)
     out = torch.zeros((n, npos, sensor[0], sensor[1], c), dtype=torch.float32, device=gpu)
     err = torch.zeros(1, dtype=torch.int32, device=gpu)
-    pool_t, idx_t, pos_t = (torch.as_tensor(x, device=gpu) for x in (pool, index, pos))
+    idx_t, pos_t = (torch.as_tensor(x, device=gpu) for x in (index, pos))
+    pool_t = _dev_pool(pool, gpu)
     N.check(N.lib().apg_image_glimpse(ctypes.byref(cfg), N.ptr(pool_t), N.ptr(idx_t), N.ptr(pos_t), 0, npos,
                                       N.ptr(out), N.ptr(err), N.stream_handle(gpu)))
     imgs = io.images_f32(pool, c)[index]
@@ -169,7 +179,7 @@ def test_glimpse_out_of_bounds_flags_like_scipy(gpu):
         cfg = _cfg(N, 1, N.APG_IMAGE_CLASSIFY, h, w, 1, 1, sensor, scale, np.uint8, 2)
         out = torch.zeros((1, 1, 5, 5, 1), dtype=torch.float32, device=gpu)
         err = torch.zeros(1, dtype=torch.int32, device=gpu)
-        keep = [torch.as_tensor(pool, device=gpu), torch.zeros(1, dtype=torch.int64, device=gpu),
+        keep = [_dev_pool(pool, gpu), torch.zeros(1, dtype=torch.int64, device=gpu),
                 torch.as_tensor(pos, device=gpu)]  # device buffers must outlive the async launch
         N.check(N.lib().apg_image_glimpse(ctypes.byref(cfg), *[N.ptr(x) for x in keep], 0, 1, N.ptr(out), N.ptr(err),
                                           N.stream_handle(gpu)))
@@ -206,7 +216,7 @@ def test_unique_top_k_matches_oracle(gpu, h, w, c, sensor, n, knob, monkeypatch)
     cfg = _cfg(N, n, N.APG_IMAGE_LOCALIZE, h, w, c, c, sensor, 1.0, np.uint8, n, top_k=10, points=p)
     top_d = torch.zeros((n, 10), dtype=torch.int32, device=gpu)
     uniq = torch.zeros((n, p), dtype=torch.float32, device=gpu)
-    keep = [torch.as_tensor(x, device=gpu) for x in (pool, index, grid)]
+    keep = [_dev_pool(pool, gpu)] + [torch.as_tensor(x, device=gpu) for x in (index, grid)]
     N.check(N.lib().apg_image_unique_top_k(ctypes.byref(cfg), *[N.ptr(x) for x in keep], p, 10, N.ptr(top_d),
                                            N.ptr(uniq), N.stream_handle(gpu)))
     assert np.array_equal(uniq.cpu().numpy().astype(np.float64), u)
