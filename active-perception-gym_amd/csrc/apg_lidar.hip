@@ -819,6 +819,7 @@ struct StepParams {
   int lidar16;  // dense lidar rows 16-byte aligned (base pointer and row pitch): vector stores
   int pretest;  // phase 2a's bounding-box pre-test (rooms: ~1/3 of the beams walk); 0: every beam walks (mazes:
                 // ~98 % of the beams touch a wall, the pre-test only delays them)
+  int p4;       // the pre-test reads a 4-row OR table of the windows (built by phase 1's idle waves; step_lds_bytes)
   float range, loss_scale, loss_offset;
 };
 
@@ -958,6 +959,8 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   float *s_lid = reinterpret_cast<float *>(s_dyn + EPB * WIN_STRIDE);
   uint16_t *s_queue = reinterpret_cast<uint16_t *>(s_lid + EPB * LS);
   float *s_tab = reinterpret_cast<float *>(s_queue + EPB * P.beams);  // EMPTY_TAB entries (staged instances)
+  // (P.p4) s_win4[el * WIN_STRIDE + r] = OR of window rows r .. r + 3 of env slot el, for r in [wlo, whi - 3)
+  uint32_t *s_win4 = reinterpret_cast<uint32_t *>(s_tab + EMPTY_TAB);
   // first table entry's bit pattern (recomputed where used: nothing stays live across the phases)
   auto tab_base = [&]() { return __float_as_uint(__fmul_rn(P.range, P.range)) - (uint32_t)(EMPTY_TAB / 2); };
   // the occupancy rows a scan of env slot el from x = ax to x = bx reads
@@ -1459,6 +1462,26 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
     }
   }
   float d0 = 0.0f, d1 = 0.0f;
+  if (!GR && P.p4 && tid >= 2 * EPB) {
+    // waves idle in phase 1 (beyond the env lanes and the second slide scans): phase 2a's 4-row OR table, each
+    // thread sliding down half of an env's staged rows (one LDS read and one write per entry; lanes = envs, so
+    // the row reads of a wave hit distinct banks)
+    const int hi = min(P.whi, MAX_WIN_ROWS) - 3, mid = (P.wlo + hi + 1) / 2;
+    for (int q = tid - 2 * EPB; q < 2 * EPB; q += T - 2 * EPB) {
+      const int sl = q & (EPB - 1), r0 = q < EPB ? P.wlo : mid, r1 = q < EPB ? mid : hi;
+      const uint32_t *w = s_win + sl * WIN_STRIDE;
+      uint32_t *w4 = s_win4 + sl * WIN_STRIDE;
+      if (r0 >= r1) continue;
+      uint32_t a = w[r0], b = w[r0 + 1], c = w[r0 + 2];
+      for (int r = r0; r < r1; r++) {
+        const uint32_t d = w[r + 3];
+        w4[r] = a | b | c | d;
+        a = b;
+        b = c;
+        c = d;
+      }
+    }
+  }
 #if APG_SLIDE_SPLIT
   if (tid < EPB) {
     s_pos[tid][0] = pos0;
@@ -1614,7 +1637,27 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
       // the box spans <= floor(|qy - py|) + 2 <= floor(|dy| + 1e-4) + 2 rows (positions < 1024): a bound
       // uniform per wave
       const int hmax = __builtin_amdgcn_readfirstlane((int)floorf(fabsf(dy) + 1e-4f) + 2);
-      walk = scan_may_hit(rows_of(el, px, qx), px, py, qx, qy, hmax);
+      if (!GR && P.p4) {
+        // the box's rows [j0, j1] (h = j1 - j0 + 1 <= hmax) from the 4-row table: two reads when h >= 4 (rows
+        // j0..j0+3 and j1-3..j1), the rows themselves below; a lane with h < 4 in a wave with hmax >= 4 reads
+        // directly too (branch-free selects)
+        const int i0 = (int)ceilf(fminf(px, qx)) - 1, i1 = (int)floorf(fmaxf(px, qx));
+        const int j0 = (int)ceilf(fminf(py, qy)) - 1, j1 = (int)floorf(fmaxf(py, qy));
+        const int h = j1 - j0 + 1, o = el * WIN_STRIDE + (j0 - s_y0[el]);
+        uint32_t acc;
+        if (hmax >= 4) {  // (wave-uniform)
+          const bool t4 = h >= 4;
+          acc = (t4 ? s_win4[o] : s_win[o]) | (t4 ? s_win4[o + h - 4] : (h > 1 ? s_win[o + 1] : 0u)) |
+                (!t4 && h > 2 ? s_win[o + 2] : 0u);
+          for (int t = 8; t < h; t += 4) acc |= s_win4[o + min(t, h - 4)];  // (boxes taller than 8: lidar_range > 6)
+        } else {
+          acc = s_win[o] | (h > 1 ? s_win[o + 1] : 0u) | (h > 2 ? s_win[o + 2] : 0u);
+        }
+        const uint32_t mask = ((1u << (i1 - i0 + 1)) - 1u) << (i0 - s_x0[el]);
+        walk = (acc & mask) != 0u;
+      } else {
+        walk = scan_may_hit(rows_of(el, px, qx), px, py, qx, qy, hmax);
+      }
       if (!walk) {  // SCAN_EMPTY: |q - p| (f32 norm), its value from the table
         const float ex = __fsub_rn(qx, px), ey = __fsub_rn(qy, py);
         const float s2 = __fadd_rn(__fmul_rn(ex, ex), __fmul_rn(ey, ey));
@@ -1994,12 +2037,14 @@ int launch_map_generate_any(const Geo &g, const uint64_t *idx, int n, uint64_t *
 
 // Dynamic LDS of a k_lidar_step instance: windows + staged lidar rows + walk queue; fused rooms resets
 // use the same bytes first for the primitives and each wave's map rows.
-size_t step_lds_bytes(int epb, int beams) {
+size_t step_lds_bytes(int epb, int beams, bool p4 = false) {
   size_t b = ((size_t)epb * WIN_STRIDE + 8) * sizeof(uint32_t);  // + RowsWindow::or_rows's over-read
   if (beams <= MAX_STAGED_BEAMS)
     b += (size_t)epb * (beams + 1) * sizeof(float) + (size_t)epb * beams * sizeof(uint16_t) + EMPTY_TAB * sizeof(float);
+  if (p4 && beams <= MAX_STAGED_BEAMS) b += (size_t)epb * WIN_STRIDE * sizeof(uint32_t);  // s_win4
   return b;
 }
+constexpr size_t STEP_LDS_P4_MAX = 144 * 1024;  // the 4-row table only while the dynamic LDS stays below this
 
 bool big_rooms(const apg_lidar_config *c) {
   return c->map_kind == APG_MAP_ROOMS && !c->is_static && (c->max_rooms > 17 || c->height > MAX_MAP_ROWS);
@@ -2043,9 +2088,13 @@ int step_epb(int n) {
 }
 
 template <int GEN, bool FUSED, int EPB, bool GR = false>
-int launch_step_t(const StepParams &P, const Geo &g, const apg_lidar_state *st, const float *act, const float *pred,
+int launch_step_t(const StepParams &P_in, const Geo &g, const apg_lidar_state *st, const float *act, const float *pred,
                   const apg_lidar_outputs *out, hipStream_t s, const PfView &V) {
-  size_t lds = step_lds_bytes(EPB, P.beams);
+  StepParams P = P_in;
+  static const int p4_knob = getenv("APG_STEP_P4") ? atoi(getenv("APG_STEP_P4")) : 1;  // (A/B knob)
+  P.p4 = !GR && P.pretest && p4_knob && P.beams <= MAX_STAGED_BEAMS &&
+         step_lds_bytes(EPB, P.beams, true) <= STEP_LDS_P4_MAX;
+  size_t lds = step_lds_bytes(EPB, P.beams, P.p4 != 0);
   if (FUSED && GEN == GEN_ROOMS && RoomsLds<EPB>::bytes > lds) lds = RoomsLds<EPB>::bytes;
   if (FUSED && GEN == GEN_PF) lds = std::max(lds, (size_t)(4 * EPB / 64) * PF_WAVE_WORDS * sizeof(uint64_t));
   auto kern = P.row ? k_lidar_step<GEN, FUSED, EPB, GR, true> : k_lidar_step<GEN, FUSED, EPB, GR, false>;
