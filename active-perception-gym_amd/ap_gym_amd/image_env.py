@@ -129,7 +129,7 @@ def image_row_views(buf, layout) -> dict:
 
 class _ImageVectorEnv(VectorEnv):
     metadata = {"render_modes": ["rgb_array"], "render_fps": 2, "autoreset_mode": "NextStep"}
-    ERROR_POLL_INTERVAL = 32
+    ERROR_POLL_INTERVAL = 128  # steps between the lazy error-word copies (each costs the stream a blit + marker)
     kind: int
 
     def __init__(self, num_envs: int, image_perception_config: ImagePerceptionConfig,

@@ -190,7 +190,7 @@ def lidar_spaces(num_envs: int, height: int, width: int, beams: int, static_map:
 
 class LIDARLocalization2DVectorEnv(VectorEnv):
     metadata = {"render_modes": ["rgb_array"], "render_fps": 4, "autoreset_mode": "NextStep"}
-    ERROR_POLL_INTERVAL = 32
+    ERROR_POLL_INTERVAL = 128  # steps between the lazy error-word copies (each costs the stream a blit + marker)
 
     def __init__(self, num_envs: int = 1, dataset: FloorMapDataset | None = None, render_mode: str = "rgb_array",
                  static_map: bool = False, lidar_beam_count: int = 8, lidar_range: float = 5,

@@ -39,7 +39,7 @@ NAN_PREDICTION_MSG = "NaN values detected in prediction."
 
 class LightDarkVectorEnv(VectorEnv):
     metadata = {"render_modes": ["rgb_array"], "render_fps": 4, "autoreset_mode": "NextStep"}
-    ERROR_POLL_INTERVAL = 32
+    ERROR_POLL_INTERVAL = 128  # steps between the lazy error-word copies (each costs the stream a blit + marker)
     STAT_NAMES = ("avg_euclidean_distance", "avg_mse", "final_euclidean_distance", "final_mse")
 
     def __init__(self, num_envs: int = 1, render_mode: str = "rgb_array", max_episode_steps: int = 50, device=None,
