@@ -820,13 +820,21 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         mask = R["info_mask"].copy()
         info: dict[str, Any] = {}
         if mask.any():
-            info["base_reward"] = np.where(mask, R["base_reward"], np.float32(0))
+            full = bool(mask.all())
+
+            def masked(a):  # np.where(mask, a, 0) along the env axis: the field itself when every env reports
+                if full:
+                    return self._own(a)
+                out = a.copy()  # (a copy plus a masked store: np.where broadcasting the [N, 2] target costs ~10x)
+                out[~mask] = 0
+                return out
+
+            info["base_reward"] = masked(R["base_reward"])
             info["_base_reward"] = mask.copy()
-            tgt = np.where(mask[:, None], R["target"], np.float32(0))
-            loss = np.where(mask, R["loss"], np.float32(0))
+            tgt = masked(R["target"])
+            loss = masked(R["loss"])
             if self.sparse:
-                tgt = {"target": tgt, "_target": mask.copy(),
-                       "weight": np.where(mask, R["weight"], 0.0), "_weight": mask.copy()}
+                tgt = {"target": tgt, "_target": mask.copy(), "weight": masked(R["weight"]), "_weight": mask.copy()}
             info["prediction"] = {"target": tgt, "_target": mask.copy(), "loss": loss, "_loss": mask.copy()}
             info["_prediction"] = mask.copy()
         if self.log_stats:
