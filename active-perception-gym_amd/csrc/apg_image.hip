@@ -658,6 +658,60 @@ struct EnvArgs {
 };
 
 
+// numpy's float32 exp and log (the AVX-512F loops np.exp / np.log run on contiguous float32 arrays, numpy 2.2:
+// simd_exp_f32 / simd_log_f32), restated operation by operation so that the CE loss (scipy.special.log_softmax:
+// np.exp of x - max, np.log of the pairwise sum) is bit-exact.  The constants are numpy's float32 coefficients (read
+// from the loops' constant pool of the installed numpy); checked bit for bit against np.exp on every float32 in
+// [-103.97, 0] and np.log on every float32 in [1, 65536] (the ranges a log-softmax feeds them), tests/test_host.py.
+// exp: x = q ln2 + r with q = rint(x log2e) (the 1.5 * 2^23 magic), r by two Cody-Waite fmas; exp(r) as a [5/2]
+// rational in fmas and one correctly rounded division; scaled by 2^q with one rounding (vscalefps); x >= 88.72 -> inf,
+// x <= -103.97 -> 0.
+APG_DEV float np_expf(float x) {
+  if (x != x) return x;
+  if (x >= 88.72283935546875f) return __int_as_float(0x7f800000);
+  if (x <= -103.97208404541015625f) return 0.0f;
+  const float q = __fsub_rn(__fadd_rn(__fmul_rn(x, 1.4426950216293335f), 12582912.0f), 12582912.0f);
+  float r = __fmaf_rn(q, -0.693145751953125f, x);
+  r = __fmaf_rn(q, -1.428606765330187e-06f, r);
+  r = __fmaf_rn(q, 0.0f, r);
+  float num = __fmaf_rn(5.082762800157070e-04f, r, 6.757896859198809e-03f);
+  num = __fmaf_rn(num, r, 5.1145121455192566e-02f);
+  num = __fmaf_rn(num, r, 2.4736154079437256e-01f);
+  num = __fmaf_rn(num, r, 7.2576647996902466e-01f);
+  num = __fmaf_rn(num, r, 1.0f);
+  float den = __fmaf_rn(2.1595094352960587e-02f, r, -2.7423354983329773e-01f);
+  den = __fmaf_rn(den, r, 1.0f);
+  const float poly = f32_div(num, den);
+  // poly * 2^q (q integral in [-150, 128]): exact in f64, one rounding to f32 (subnormal results included)
+  return __double2float_rn(__dmul_rn((double)poly, __longlong_as_double((long long)(1023 + (int)q) << 52)));
+}
+// log: x = m 2^e with m in [0.5, 1) (vgetmantps / vgetexpps); m <= sqrt(1/2) is doubled (e - 1); log(m) as a [5/5]
+// rational of m - 1 in fmas and one correctly rounded division, + e ln2 by one fma.  0 -> -inf, < 0 / NaN -> NaN,
+// inf -> inf.
+APG_DEV float np_logf(float x) {
+  if (!(x > 0.0f)) return x == 0.0f ? __int_as_float(0xff800000) : __int_as_float(0x7fc00000);
+  if (x == __int_as_float(0x7f800000)) return x;
+  int e;
+  float m = frexpf(x, &e);
+  float ex = (float)e;
+  if (m <= 0.70710676908493042f) {
+    m = __fadd_rn(m, m);
+    ex = __fsub_rn(ex, 1.0f);
+  }
+  const float r = __fsub_rn(m, 1.0f);
+  float num = __fmaf_rn(2.5899792090058327e-02f, r, 3.8088378310203552e-01f);
+  num = __fmaf_rn(num, r, 1.4800006151199341f);
+  num = __fmaf_rn(num, r, 2.1126775741577148f);
+  num = __fmaf_rn(num, r, 1.0f);
+  num = __fmaf_rn(num, r, 0.0f);
+  float den = __fmaf_rn(5.8750952593982220e-03f, r, 1.5464763343334198e-01f);
+  den = __fmaf_rn(den, r, 9.8649430274963379e-01f);
+  den = __fmaf_rn(den, r, 2.4530060291290283f);
+  den = __fmaf_rn(den, r, 2.6126775741577148f);
+  den = __fmaf_rn(den, r, 1.0f);
+  return __fmaf_rn(ex, 0.69314718246459961f, f32_div(num, den));
+}
+
 // scipy.special.log_softmax(row)[target] in float32 (x_max zeroed when not finite); -> -value
 APG_DEV float ce_f32(const float *row, int k, int target) {
   float m = row[0];
@@ -668,9 +722,9 @@ APG_DEV float ce_f32(const float *row, int k, int target) {
     m = v > m ? v : m;
   }
   if (nan || isinf(m)) m = 0.0f;  // np.amax propagates NaN; x_max[~isfinite] = 0
-  auto ex = [&](int i) { return expf(__fsub_rn(row[i], m)); };
+  auto ex = [&](int i) { return np_expf(__fsub_rn(row[i], m)); };
   const float s = pw_sum<MAX_PW_DEPTH>(ex, 0, k);
-  const float out = __fsub_rn(__fsub_rn(row[target], m), logf(s));
+  const float out = __fsub_rn(__fsub_rn(row[target], m), np_logf(s));
   return -out;
 }
 
@@ -929,13 +983,13 @@ __global__ __launch_bounds__(256) void k_image_env_cls(EnvArgs a, int envs_per_b
   const float xt = row[lc];
   __syncthreads();
   if (live)  // lanes of the tail groups (grp >= ne) alias row 0 and must not write it
-    for (int i = j; i < k; i += CLS_LANES) row[i] = expf(__fsub_rn(row[i], m));
+    for (int i = j; i < k; i += CLS_LANES) row[i] = np_expf(__fsub_rn(row[i], m));
   __syncthreads();
   const float sum = pw_sum8<MAX_PW_DEPTH>(row, 0, k, j);
   if (!live || j != 0) return;
   const int e = e0 + grp;
   uint32_t err = (nan || pos_inf || all_neg_inf) ? APG_ERR_NAN_PREDICTION : 0u;
-  const float ce = -__fsub_rn(__fsub_rn(xt, m), logf(sum));
+  const float ce = -__fsub_rn(__fsub_rn(xt, m), np_logf(sum));
   const double loss_d = __dadd_rn(__dmul_rn((double)ce, a.ce_scale), a.ce_offset);
   ro(out.loss_f64, a.row, e, 1) = loss_d;
   ro(out.label_target, a.row, e, 1) = l;
@@ -992,7 +1046,7 @@ APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const EnvIn &in, doub
   const int32_t l = in.label;
   const int lc = l < 0 ? 0 : (l >= k ? k - 1 : l);
   const float xt = row[lc];
-  for (int i = 0; i < k; i++) row[i] = expf(__fsub_rn(row[i], m));
+  for (int i = 0; i < k; i++) row[i] = np_expf(__fsub_rn(row[i], m));
   float sum = 0.0f;
   if (k < 8) {
     for (int i = 0; i < k; i++) sum = __fadd_rn(sum, row[i]);
@@ -1010,7 +1064,7 @@ APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const EnvIn &in, doub
     for (; i < k; i++) sum = __fadd_rn(sum, row[i]);
   }
   uint32_t err = (nan || pos_inf || all_neg_inf) ? APG_ERR_NAN_PREDICTION : 0u;
-  const float ce = -__fsub_rn(__fsub_rn(xt, m), logf(sum));
+  const float ce = -__fsub_rn(__fsub_rn(xt, m), np_logf(sum));
   const double loss_d = __dadd_rn(__dmul_rn((double)ce, a.ce_scale), a.ce_offset);
   ro(out.loss_f64, a.row, e, 1) = loss_d;
   ro(out.label_target, a.row, e, 1) = l;

@@ -504,3 +504,56 @@ def test_kernel_source_hash_covers_the_include_closure(family):
     deps = {d if os.path.isabs(d) else os.path.join(root, d) for d in deps}
     assert deps and deps == set(bench.kernel_sources(family))
     assert any(p.endswith("apgym_capi.h") for p in deps)
+
+
+def _np_fma(a, b, c):
+    # float32 fma: the float32 product is exact in float64, the sum rounded there and then to float32 (no case in
+    # the ranges below rounds differently from a single rounding: the sweep matches numpy bit for bit)
+    return (np.asarray(a, np.float64) * np.asarray(b, np.float64) + np.asarray(c, np.float64)).astype(np.float32)
+
+
+def _np_exp_restated(x):
+    """apg_image.hip's np_expf in numpy (normal-range outputs)."""
+    f = np.float32
+    q = ((x * f(1.4426950216293335)).astype(f) + f(12582912.0)).astype(f) - f(12582912.0)
+    r = _np_fma(q, f(-0.693145751953125), x)
+    r = _np_fma(q, f(-1.428606765330187e-06), r)
+    num = _np_fma(f(5.082762800157070e-04), r, f(6.757896859198809e-03))
+    for c in (5.1145121455192566e-02, 2.4736154079437256e-01, 7.2576647996902466e-01, 1.0):
+        num = _np_fma(num, r, f(c))
+    den = _np_fma(_np_fma(f(2.1595094352960587e-02), r, f(-2.7423354983329773e-01)), r, f(1.0))
+    poly = (num.astype(np.float64) / den.astype(np.float64)).astype(f)
+    return np.ldexp(poly.astype(np.float64), q.astype(np.int32)).astype(f)
+
+
+def _np_log_restated(x):
+    """apg_image.hip's np_logf in numpy (positive finite inputs)."""
+    f = np.float32
+    m, e = np.frexp(x)
+    m, ex = m.astype(f), e.astype(f)
+    low = m <= f(0.70710676908493042)
+    m = np.where(low, (m + m).astype(f), m)
+    ex = np.where(low, ex - f(1), ex).astype(f)
+    r = (m - f(1)).astype(f)
+    num = _np_fma(f(2.5899792090058327e-02), r, f(3.8088378310203552e-01))
+    for c in (1.4800006151199341, 2.1126775741577148, 1.0, 0.0):
+        num = _np_fma(num, r, f(c))
+    den = _np_fma(f(5.8750952593982220e-03), r, f(1.5464763343334198e-01))
+    for c in (9.8649430274963379e-01, 2.4530060291290283, 2.6126775741577148, 1.0):
+        den = _np_fma(den, r, f(c))
+    return _np_fma(ex, f(0.69314718246459961), (num.astype(np.float64) / den.astype(np.float64)).astype(f))
+
+
+def test_numpy_float32_exp_log_restatement():
+    """The float32 exp / log algorithms the cross-entropy kernels run (apg_image.hip np_expf / np_logf: numpy's
+    AVX-512F loops, its coefficients) against np.exp / np.log on a strided sweep of every float32 a log-softmax feeds
+    them: exp on [-87.3, 0] (normal results), log on [1, 65536].  (The full sweeps, 1.1e9 and 1.3e8 inputs, matched
+    bit for bit when the restatement was written; the GPU suite checks the kernels against numpy the same way.)"""
+    f = np.float32
+    lo = np.array([-87.3], f).view(np.uint32)[0]
+    bits = np.arange(0x80000000, int(lo) + 1, 101, dtype=np.uint64).astype(np.uint32)
+    x = bits.view(f)
+    assert np.array_equal(_np_exp_restated(x).view(np.uint32), np.exp(x).view(np.uint32))
+    a, b = np.array([1.0, 65536.0], f).view(np.uint32)
+    x = np.arange(a, b + 1, 13, dtype=np.uint64).astype(np.uint32).view(f)
+    assert np.array_equal(_np_log_restated(x).view(np.uint32), np.log(x).view(np.uint32))
