@@ -136,13 +136,16 @@ class _ImageVectorEnv(VectorEnv):
                  render_mode: str = "rgb_array", device=None, copy: bool = False, strict_errors: bool = False,
                  array_backend: str = "numpy", num_envs_total: int | None = None, env_offset: int = 0,
                  log_stats: bool = False, sparse: bool = False, render_envs=None, packed_outputs: bool = False,
-                 draw_ahead: bool = True):
+                 draw_ahead: bool = True, vector_stats: str = "list"):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
             raise ValueError(f"Unsupported render mode: {render_mode}")
         if array_backend not in ("numpy", "torch"):
             raise ValueError("array_backend must be 'numpy' or 'torch'")
+        if vector_stats not in ("list", "array"):
+            raise ValueError("vector_stats must be 'list' (the reference's lists of np.float32) or 'array'")
+        self.vector_stats = vector_stats  # numpy backend: form of info["stats"]["vector"] entries (as the LIDAR env)
         cfg = image_perception_config
         self.config = cfg
         self.num_envs = n = int(num_envs)
@@ -681,8 +684,13 @@ class _ImageVectorEnv(VectorEnv):
         vector: dict[str, Any] = {}
         for j, nm in enumerate(names):
             arr = np.empty(n, dtype=object)
-            for i in range(n):
-                arr[i] = list(hist[i, j, :lim])
+            hj = hist[:, j, :lim]
+            if self.vector_stats == "array":  # float32 row views of one host block (opt-in: ndarray, not list)
+                for i in range(n):
+                    arr[i] = hj[i]
+            else:  # the reference's list of np.float32 per env (update_info_metrics_vec, util.py:68-77)
+                for i in range(n):
+                    arr[i] = list(hj[i])
             vector[nm] = arr
         for nm in names:
             vector[f"_{nm}"] = done

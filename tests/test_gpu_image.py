@@ -471,6 +471,43 @@ def test_image_env_nan_errors(gpu):
         env.close()
 
 
+@pytest.mark.parametrize("gname", ["image_cls_mnist.npz"])
+def test_image_numpy_vector_stats_array_mode(gpu, gname):
+    """vector_stats="array" on the image envs: float32 row views holding the values of the reference's
+    np.float32 lists (update_info_metrics_vec, util.py:68-77); anything else is a ValueError."""
+    import ap_gym_amd as ap
+
+    g = golden(gname)
+    h, w, c, k, s0, s1, lim, inv, n_g, _ = (int(v) for v in g["config"])
+    ds = ap.ArrayImageClassificationDataset(g["pool"], g["labels"], k, c)
+    cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=(s0, s1), sensor_scale=float(g["sensor_scale"]),
+                                   step_limit=lim, randomly_invert_labels=bool(inv))
+    e1 = ap.ImageClassificationVectorEnv(n_g, cfg, log_stats=True)
+    e2 = ap.ImageClassificationVectorEnv(n_g, cfg, log_stats=True, vector_stats="array")
+    e1.reset(seed=0)
+    e2.reset(seed=0)
+    seen = 0
+    for t in range(len(g["actions"])):
+        act = {"action": g["actions"][t], "prediction": g["predictions"][t]}
+        i1, i2 = e1.step(act)[4], e2.step(act)[4]
+        assert ("stats" in i1) == ("stats" in i2)
+        if "stats" in i1:
+            for name, v1 in i1["stats"]["vector"].items():
+                if name.startswith("_"):
+                    continue
+                v2 = i2["stats"]["vector"][name]
+                for j in range(n_g):
+                    assert isinstance(v1[j], list) and isinstance(v1[j][0], np.float32)
+                    assert isinstance(v2[j], np.ndarray) and v2[j].dtype == np.float32
+                    assert np.array_equal(np.array(v1[j], np.float32), v2[j], equal_nan=True)
+                    seen += 1
+    assert seen > 0
+    e1.close()
+    e2.close()
+    with pytest.raises(ValueError):
+        ap.ImageClassificationVectorEnv(n_g, cfg, vector_stats="bad")
+
+
 def test_image_cls_full_size_properties(gpu):
     """BASELINE config 4 (MNIST-shaped classification, N = 65536, 5x5 glimpse): bounded glimpses,
     clipped positions, reset cadence, label targets from the pool."""
