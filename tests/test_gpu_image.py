@@ -348,6 +348,21 @@ def test_image_env_matches_reference_trace(gpu, name):
                                                          ("cls", 2000, (28, 28), (5, 5), 13, 20),
                                                          ("cls", 2000, (28, 28), (5, 5), 16, 20)])
 def test_image_env_matches_oracle_at_scale(gpu, kind, n, shape, sensor, k, steps):
+    _env_vs_oracle(kind, n, shape, sensor, k, steps)
+
+
+@pytest.mark.parametrize("kind,n,shape,sensor,k,steps,scale", [
+    ("loc", 300, (33, 29, 3), (6, 6), 5, 20, 1.7),    # odd row pitch (87 B): per-row dword alignment of the box
+    ("cls", 300, (31, 27), (5, 5), 10, 20, 1.3),      # grey, odd pitch
+    ("cls", 200, (17, 19, 3), (5, 5), 4, 20, 2.0),    # box rows clipped to the image (min(h, ...))
+    ("cls", 130, (12, 14), (4, 4), 5, 20, 3.0)])      # box rows = the whole image (h = 12)
+def test_image_env_box_staging_edges(gpu, kind, n, shape, sensor, k, steps, scale):
+    """The fused step's LDS box staging (u8 pools): odd pitches, scales != 1, boxes clipped at the image border;
+    bit-exact vs the oracle like every other configuration."""
+    _env_vs_oracle(kind, n, shape, sensor, k, steps, scale)
+
+
+def _env_vs_oracle(kind, n, shape, sensor, k, steps, scale=1.0):
     import ap_gym_amd as ap
     from oracle import image_oracle as io
 
@@ -356,9 +371,9 @@ def test_image_env_matches_oracle_at_scale(gpu, kind, n, shape, sensor, k, steps
     labels = rng.integers(0, k, 300)
     c = 1 if len(shape) == 2 else shape[-1]
     ds = ap.ArrayImageClassificationDataset(pool, labels, k, c)
-    cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=sensor, step_limit=16)
+    cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=sensor, sensor_scale=scale, step_limit=16)
     env = (ap.ImageClassificationVectorEnv if kind == "cls" else ap.ImageLocalizationVectorEnv)(n, cfg)
-    ref = io.ImageVectorEnvOracle(kind, pool, labels, k, c, n, sensor, 1.0, 16)
+    ref = io.ImageVectorEnvOracle(kind, pool, labels, k, c, n, sensor, scale, 16)
     obs, info = env.reset(seed=11)
     robs, rinfo = ref.reset(11)
     for key in robs:
