@@ -1954,7 +1954,30 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
     // do not depend on it).
     static const int envw_knob = getenv("APG_IMAGE_ENV_WAVE") ? atoi(getenv("APG_IMAGE_ENV_WAVE")) : -1;
     const bool envw = envw_knob >= 0 ? envw_knob != 0 : true;
-    const int upb = envw ? std::min(ENV_WAVE, glimpse_units_per_block(per, 8)) : glimpse_units_per_block(per, 4);
+    static const int gt_knob = getenv("APG_IMAGE_GT") ? atoi(getenv("APG_IMAGE_GT")) : 448;
+    const bool gt448 = gt_knob == 448;
+    int upb = envw ? std::min(ENV_WAVE, glimpse_units_per_block(per, 8)) : glimpse_units_per_block(per, 4);
+    // Whole generations: four eight-wave workgroups are resident per CU, and a grid of 2.13 such generations
+    // leaves the chip mostly idle in its last one.  From one full generation up, the units per workgroup are
+    // re-chosen so the grid is the nearest whole number of generations (TinyImageNetLoc: 15 units, 2185
+    // workgroups, 31.3 / 30.8 us -> 16 units, 2048 workgroups, 30.2 / 29.8 us, rocprof medians of two rounds).
+    // Not when APG_GLIMPSE_PPT forces the size (A/B knob); results do not depend on it.
+    static const bool ppt_forced = getenv("APG_GLIMPSE_PPT") != nullptr;
+    if (envw && gt448 && !ppt_forced) {
+      static int resident = 0;
+      if (!resident) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+          cus = 256;
+        resident = 4 * cus;
+      }
+      const double gens = (double)n / ((double)upb * resident);
+      if (gens >= 1.0) {
+        const int whole = (int)std::lround(gens);
+        upb = std::min(ENV_WAVE, (int)(((int64_t)n + (int64_t)whole * resident - 1) / ((int64_t)whole * resident)));
+      }
+    }
     size_t dyn = (size_t)upb * (g.s0 + g.s1) * sizeof(Axis);
     if (c->kind == APG_IMAGE_CLASSIFY) dyn += (size_t)upb * (c->num_classes + 2) * sizeof(float);
     const dim3 grid(grid_for(n, upb)), block(GS_THREADS);
@@ -1963,8 +1986,6 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
     // one instance per env kind and pool format (u8 / f32, pool channels, glimpse channels)
     // glimpse threads of the env-wave instances: 448 (eight-wave workgroups) unless APG_IMAGE_GT=256 (A/B knob;
     // results do not depend on it)
-    static const int gt_knob = getenv("APG_IMAGE_GT") ? atoi(getenv("APG_IMAGE_GT")) : 448;
-    const bool gt448 = gt_knob == 448;
     const dim3 block_e((gt448 ? 448 : GS_THREADS) + ENV_WAVE);
     // one instance per env kind and pool format (u8 / f32, pool channels, glimpse channels)
 #define APG_FUSED(K, F, P, C)                                                                                    \
