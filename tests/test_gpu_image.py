@@ -630,19 +630,20 @@ def test_tuning_knobs_do_not_change_results(gpu, tmp_path, knobs):
         assert np.array_equal(base[key], got[key]), key
 
 
-@pytest.mark.parametrize("kind,invert,backend", [("cls", True, "torch"), ("loc", False, "torch"), ("cls", False, "numpy"),
-                                                 ("loc", False, "numpy")])
-def test_draw_ahead_matches_drawing_at_the_autoreset(gpu, kind, invert, backend):
+@pytest.mark.parametrize("kind,invert,backend,limit", [("cls", True, "torch", 5), ("loc", False, "torch", 5),
+                                                       ("cls", False, "numpy", 5), ("loc", False, "numpy", 5),
+                                                       ("cls", True, "torch", 1), ("loc", False, "numpy", 2)])
+def test_draw_ahead_matches_drawing_at_the_autoreset(gpu, kind, invert, backend, limit):
     """The next batch's draws made ahead on the side stream (apg_image_draw_ahead, installed by the fused step
     kernel) give the outputs of drawing them in the autoreset step, across autoresets, a reset() (the streams are
-    restored from before the draws made ahead) and a reset(seed)."""
+    restored from before the draws made ahead) and a reset(seed); also with episodes of 1 and 2 steps."""
     import torch
 
     import ap_gym_amd as ap
 
     ch = 3 if kind == "loc" else 1
     ds = ap.SyntheticImageClassificationDataset(64, (32, 32, 3) if ch == 3 else (28, 28), 10, ch, seed=3)
-    cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=(8, 8) if kind == "loc" else (5, 5), step_limit=5,
+    cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=(8, 8) if kind == "loc" else (5, 5), step_limit=limit,
                                    randomly_invert_labels=invert)
     cls = ap.ImageLocalizationVectorEnv if kind == "loc" else ap.ImageClassificationVectorEnv
     n = 300
