@@ -66,7 +66,8 @@ class LidarConfig(ctypes.Structure):
                 ("beams", ctypes.c_int32), ("step_limit", ctypes.c_int32), ("max_rooms", ctypes.c_int32),
                 ("door_width", ctypes.c_int32), ("lidar_range", ctypes.c_float), ("loss_scale", ctypes.c_float),
                 ("loss_offset", ctypes.c_float), ("branching_prob", ctypes.c_double), ("log_stats", ctypes.c_int32),
-                ("sparse", ctypes.c_int32), ("out_row_bytes", ctypes.c_int32), ("pool_len", ctypes.c_int32)]
+                ("sparse", ctypes.c_int32), ("out_row_bytes", ctypes.c_int32), ("pool_len", ctypes.c_int32),
+                ("stream_len", ctypes.c_int64)]
 
 
 class LidarState(ctypes.Structure):
@@ -159,6 +160,8 @@ SYMBOLS = [
     ("apg_lidar_prefetcher_create", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(_vp)]),
     ("apg_lidar_prefetcher_destroy", ctypes.c_int, [_vp]),
     ("apg_lidar_prefetcher_stats", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64)]),
+    ("apg_lidar_peek_map_index", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(LidarState),
+                                                ctypes.c_uint64, ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
     ("apg_maze_frames", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     ("apg_map_generate", ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp]),

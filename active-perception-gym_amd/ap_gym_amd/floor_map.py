@@ -89,6 +89,9 @@ class PoolFloorMapDataset(FloorMapDataset):
 
     map_kind = N.APG_MAP_POOL
     FETCH_CHUNK = 1024
+    POOL_MAX_MAPS = 2**31 - 1  # apg_lidar_config.pool_len
+    POOL_AUTO_MAPS = 2**16     # frozen_maps=None: larger datasets are streamed
+    POOL_AUTO_BYTES = 2 << 30
 
     def native_params(self) -> dict:
         return dict(max_rooms=10, door_width=3, branching_prob=1.0)  # unused by pool maps
@@ -107,22 +110,49 @@ class PoolFloorMapDataset(FloorMapDataset):
         (lidar_localization2d.py:279: shape (map_height, map_width)); maps must be boolean arrays (the reference
         indexes its coordinate grids with them, :282-284)."""
         n = len(self)
-        if n < 1 or n > 2**31 - 1:
-            raise ValueError(f"pool maps: the dataset must hold 1 .. 2**31 - 1 maps, got {n}")
-        h, w = self.map_height, self.map_width
-        wpr = (w + 63) // 64
-        bits = np.zeros((n, h, wpr * 8), np.uint8)
+        if n < 1 or n > self.POOL_MAX_MAPS:
+            raise ValueError(f"pool maps: a frozen pool holds 1 .. {self.POOL_MAX_MAPS} maps, got {n} "
+                             "(larger datasets are streamed: frozen_maps=False)")
+        bits = np.zeros((n, self.map_height, self.words_per_row * 8), np.uint8)
         free = np.zeros(n, np.int32)
         for lo in range(0, n, self.FETCH_CHUNK):
-            for i in range(lo, min(n, lo + self.FETCH_CHUNK)):
-                m = np.asarray(self.map_array(i))
-                if m.shape != (h, w):
-                    raise ValueError(f"map {i} has shape {m.shape}, expected (map_height, map_width) = {(h, w)}")
-                if m.dtype != np.bool_:
-                    raise TypeError(f"map {i} has dtype {m.dtype}: floor maps are boolean arrays (True = wall)")
-                bits[i, :, :(w + 7) // 8] = np.packbits(m, axis=-1, bitorder="little")
-                free[i] = h * w - int(np.count_nonzero(m))
-        return bits.view("<u8").reshape(n, h, wpr), free
+            hi = min(n, lo + self.FETCH_CHUNK)
+            pack_maps([self.map_array(i) for i in range(lo, hi)], self.map_height, self.map_width,
+                      bits[lo:hi], free[lo:hi], first=lo)
+        return bits.view("<u8").reshape(n, self.map_height, self.words_per_row), free
+
+    @property
+    def words_per_row(self) -> int:
+        return (self.map_width + 63) // 64
+
+    def pool_bytes(self) -> int:
+        return len(self) * self.map_height * self.words_per_row * 8
+
+    def prefers_streaming(self) -> bool:
+        """Default map source of a dynamic env (frozen_maps=None): the pool when it is small enough to read at
+        construction (<= POOL_AUTO_MAPS maps and POOL_AUTO_BYTES of bit rows), else streamed per episode."""
+        n = len(self)
+        return n > self.POOL_AUTO_MAPS or self.pool_bytes() > self.POOL_AUTO_BYTES
+
+    def static_pool(self, index: int, device):
+        """(pool_occ int64 [1, H, wpr], pool_free int32 [1]) holding dataset[index] alone: a static env reads
+        only its map (lidar_localization2d.py:177-178), whatever the dataset's size."""
+        import torch
+
+        cache = self.__dict__.setdefault("_static_pools", {})
+        key = (str(torch.device(device)), int(index))
+        if key not in cache:
+            h, wpr = self.map_height, self.words_per_row
+            bits = np.zeros((1, h, wpr * 8), np.uint8)
+            free = np.zeros(1, np.int32)
+            pack_maps([self.static_map_array(int(index))], h, self.map_width, bits, free, first=int(index))
+            cache[key] = (torch.as_tensor(bits.view(np.int64).reshape(1, h, wpr), device=device).contiguous(),
+                          torch.as_tensor(free, device=device))
+        return cache[key]
+
+    def static_map_array(self, idx: int) -> np.ndarray:
+        """dataset[static_map_index] (lidar_localization2d.py:177-178)."""
+        return self.map_array(idx)
 
     def device_pool(self, device):
         """(pool_occ int64 [len, H, wpr], pool_free int32 [len]) on `device`, uploaded on first use."""
@@ -158,10 +188,9 @@ class ArrayFloorMapDataset(PoolFloorMapDataset):
 class ForeignFloorMapView(PoolFloorMapDataset):
     """Any object with the reference's FloorMapDataset interface (`map_width`, `map_height`, `load`, `__len__`,
     `get_data_point`) -- e.g. a user subclass of ap_gym.envs.floor_map.FloorMapDataset
-    (floor_map_dataset.py:10-22) -- seen as a pool dataset: `get_data_point(i)` is called once for every index
-    and the maps are frozen on the device.  The reference env calls `get_data_point(idx)` at every draw, so a
-    dataset that randomizes per fetch or does not fit in device memory behaves differently here (every draw of
-    index i sees the first fetch); parity for such datasets is unpinned."""
+    (floor_map_dataset.py:10-22).  The env reads its maps either once into a frozen pool (small datasets; every draw
+    of index i then sees the first fetch) or per episode (streamed: `get_data_point(idx)` at every draw, like the
+    reference's DatasetIterator, dataset_iterator.py:26-32); see LIDARLocalization2DVectorEnv(frozen_maps=...)."""
 
     def __init__(self, inner):
         self.inner = inner
@@ -177,11 +206,66 @@ class ForeignFloorMapView(PoolFloorMapDataset):
     def map_array(self, idx: int) -> np.ndarray:
         return np.asarray(self.inner.get_data_point(idx))
 
+    def static_map_array(self, idx: int) -> np.ndarray:
+        getitem = getattr(type(self.inner), "__getitem__", None)
+        return np.asarray(self.inner[idx] if getitem is not None else self.inner.get_data_point(idx))
+
+
+def pack_maps(maps, h: int, w: int, bits_out: np.ndarray, free_out: np.ndarray, first: int = 0):
+    """Maps (bool [H, W] each) into bit rows (bits_out u8 [k, H, 8 * wpr], bit x % 8 of byte x / 8) and free-cell
+    counts, checked like LIDARLocalization2DEnv.__set_map (lidar_localization2d.py:279) and the boolean indexing
+    that follows it (:282-284).  `first`: the dataset index of maps[0] (error messages)."""
+    nb = (w + 7) // 8
+    for j, m in enumerate(maps):
+        m = np.asarray(m)
+        if m.shape != (h, w):
+            raise ValueError(f"map {first + j} has shape {m.shape}, expected (map_height, map_width) = {(h, w)}")
+        if m.dtype != np.bool_:
+            raise TypeError(f"map {first + j} has dtype {m.dtype}: floor maps are boolean arrays (True = wall)")
+        bits_out[j, :, :nb] = np.packbits(m, axis=-1, bitorder="little")
+        free_out[j] = h * w - int(np.count_nonzero(m))
+
+
+_REFERENCE_PROCEDURAL = ("FloorMapDatasetRooms", "FloorMapDatasetMaze")
+
+
+def procedural_equivalent(ds):
+    """The device generator for a reference procedural dataset or a subclass of one that keeps its maps:
+    FloorMapDatasetRooms / FloorMapDatasetMaze (floor_map_dataset_rooms.py:10-24, floor_map_dataset_maze.py:10-22)
+    found in the MRO, with `get_data_point` and the length (2**32) not overridden; the generator's parameters from
+    the reference's private attributes.  None otherwise."""
+    t = type(ds)
+    for cls in t.__mro__:
+        if cls.__name__ not in _REFERENCE_PROCEDURAL or not cls.__module__.startswith("ap_gym."):
+            continue
+        if getattr(t, "get_data_point", None) is not getattr(cls, "get_data_point", None):
+            return None  # maps of the user's own (a streamed or pooled foreign dataset)
+        try:
+            if len(ds) != 2**32:
+                return None
+        except TypeError:
+            return None
+        if cls.__name__ == "FloorMapDatasetRooms":
+            return FloorMapDatasetRooms(ds.map_width, ds.map_height,
+                                        getattr(ds, "_FloorMapDatasetRooms__max_rooms", 10),
+                                        getattr(ds, "_FloorMapDatasetRooms__door_width", 3))
+        return FloorMapDatasetMaze(ds.map_width, ds.map_height, getattr(ds, "_FloorMapDatasetMaze__branching_prob", 1.0))
+    return None
+
 
 def as_floor_map_dataset(ds):
-    """`ds` itself when the LIDAR envs can use it directly (procedural or pool), else a ForeignFloorMapView."""
+    """`ds` itself when the LIDAR envs can use it directly (procedural or pool), the device generator for a reference
+    procedural dataset (procedural_equivalent), else a ForeignFloorMapView.  A subclass of ap_gym_amd's own
+    procedural datasets that overrides get_data_point is foreign too (its maps are its own)."""
+    if isinstance(ds, (FloorMapDatasetRooms, FloorMapDatasetMaze)):
+        if type(ds).get_data_point is FloorMapDataset.get_data_point:
+            return ds
+        return ForeignFloorMapView(ds)
     if isinstance(ds, FloorMapDataset):
         return ds
+    proc = procedural_equivalent(ds)
+    if proc is not None:
+        return proc
     for attr in ("map_width", "map_height", "get_data_point"):
         if not hasattr(ds, attr):
             raise TypeError(f"dataset {type(ds).__name__} is not a FloorMapDataset (no {attr})")

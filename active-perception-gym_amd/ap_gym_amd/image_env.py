@@ -16,8 +16,11 @@ generators) runs on the device through the C ABI (include/apgym_capi.h: apg_imag
   episode all envs terminate together after step_limit steps; the next step resets the batch
           (NEXT_STEP autoreset inside the module, base_reward = zeros(N) float64)
 
-array_backend="numpy" (default) returns numpy exactly like the reference; "torch" returns
-persistent device tensors without host synchronisation (errors raised lazily, like the LIDAR env).
+array_backend="numpy" (default) returns numpy exactly like the reference: every step's arrays are the caller's own
+(writable, never written again by the env), obs["target_glimpse"] included (the reference computes it anew every step,
+image_localization.py:142-146, 170-174); obs_snapshot="shared" (opt-in) hands out the target glimpse as one read-only
+array shared by the steps of a batch instead (it changes only with the batch).  "torch" returns persistent device
+tensors without host synchronisation (errors raised lazily, like the LIDAR env).
 """
 
 from __future__ import annotations
@@ -85,6 +88,21 @@ def device_pool_u8(pool: np.ndarray, dev):
     return buf[:nb].view(pool.shape)
 
 
+def padded_device_pool_u8(pool_t):
+    """A device uint8 pool (e.g. from a dataset's device_pool_tensors) as the glimpse kernels need it: contiguous with
+    N.APG_U8_POOL_PAD readable bytes after the last image in its own allocation (apgym_capi.h).  The tensor itself
+    when its storage already extends that far, else a padded copy."""
+    import torch
+
+    nb = pool_t.numel()
+    if (pool_t.is_contiguous() and
+            pool_t.untyped_storage().nbytes() - pool_t.storage_offset() >= nb + N.APG_U8_POOL_PAD):
+        return pool_t
+    buf = torch.zeros(nb + N.APG_U8_POOL_PAD, dtype=torch.uint8, device=pool_t.device)
+    buf[:nb].copy_(pool_t.reshape(-1))
+    return buf[:nb].view(tuple(pool_t.shape))
+
+
 def softmax_nan_rows(logits: np.ndarray) -> np.ndarray:
     """Rows where scipy.special.softmax(row)[label] is NaN: a NaN or +inf logit, or all -inf."""
     return np.isnan(logits).any(-1) | np.isposinf(logits).any(-1) | np.isneginf(logits).all(-1)
@@ -136,7 +154,7 @@ class _ImageVectorEnv(VectorEnv):
                  render_mode: str = "rgb_array", device=None, copy: bool = False, strict_errors: bool = False,
                  array_backend: str = "numpy", num_envs_total: int | None = None, env_offset: int = 0,
                  log_stats: bool = False, sparse: bool = False, render_envs=None, packed_outputs: bool = False,
-                 draw_ahead: bool = True, vector_stats: str = "list"):
+                 draw_ahead: bool = True, vector_stats: str = "list", obs_snapshot: str = "copy"):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -146,6 +164,9 @@ class _ImageVectorEnv(VectorEnv):
         if vector_stats not in ("list", "array"):
             raise ValueError("vector_stats must be 'list' (the reference's lists of np.float32) or 'array'")
         self.vector_stats = vector_stats  # numpy backend: form of info["stats"]["vector"] entries (as the LIDAR env)
+        if obs_snapshot not in ("copy", "shared"):
+            raise ValueError("obs_snapshot must be 'copy' (a writable target glimpse per step) or 'shared'")
+        self.obs_snapshot = obs_snapshot  # numpy backend: obs["target_glimpse"] per step or a shared snapshot
         cfg = image_perception_config
         self.config = cfg
         self.num_envs = n = int(num_envs)
@@ -172,12 +193,23 @@ class _ImageVectorEnv(VectorEnv):
         ds.load()
         if hasattr(ds, "device_pool_tensors"):  # procedural datasets render their pool on the device
             pool_t, labels_t = ds.device_pool_tensors(self.device)
+            pool = None
             pool_is_u8 = pool_t.dtype == torch.uint8
+            if pool_is_u8:  # the kernels' dword tap loads read up to APG_U8_POOL_PAD - 1 bytes past the last image
+                pool_t = padded_device_pool_u8(pool_t)
         else:
-            pool, labels = ds.device_pool()
-            pool_t, labels_t = None, None
-            pool_is_u8 = pool.dtype == np.uint8
-        m, h, w, pc = (pool_t if pool_t is not None else pool).shape
+            # one upload per dataset and device, shared by every env built on it (ShardedVectorEnv's sub-batches, a
+            # train and an eval env): the pool is read-only on the device
+            cache = ds.__dict__.setdefault("_apg_device_pools", {}) if hasattr(ds, "__dict__") else {}
+            key = str(self.device)
+            if key not in cache:
+                pool, labels = ds.device_pool()
+                cache[key] = (device_pool_u8(pool, self.device) if pool.dtype == np.uint8
+                              else torch.from_numpy(np.ascontiguousarray(pool)).to(self.device),
+                              torch.from_numpy(np.ascontiguousarray(labels)).to(self.device), pool)
+            pool_t, labels_t, pool = cache[key]
+            pool_is_u8 = pool_t.dtype == torch.uint8
+        m, h, w, pc = pool_t.shape
         c = int(ds.num_channels)
         if c not in (1, 3):
             raise ValueError(f"Target channels must be either 1 or 3 but is {c}.")
@@ -248,9 +280,7 @@ class _ImageVectorEnv(VectorEnv):
         gshape = (n, s0, s1, c)
         work = max(N.lib().apg_rng_fill_work_elems(nt, b) for b in (m, int(cfg.unique_sampling_top_k), 2))
         self._t = T = dict(
-            pool=pool_t if pool_t is not None else device_pool_u8(pool, dev) if pool.dtype == np.uint8 else
-            t.from_numpy(pool).to(dev),
-            pool_labels=labels_t if labels_t is not None else t.from_numpy(labels).to(dev),
+            pool=pool_t, pool_labels=labels_t,
             unique_grid=t.from_numpy(grid).to(dev),
             index=t.zeros(n, dtype=t.int64, device=dev), label=t.zeros(n, dtype=t.int32, device=dev),
             inverted=t.zeros(n, dtype=t.int32, device=dev), pos=t.zeros((n, 2), dtype=t.float64, device=dev),
@@ -340,7 +370,7 @@ class _ImageVectorEnv(VectorEnv):
         from .render import tracked_envs
 
         self.render_envs = tracked_envs(render_envs, n)
-        self._pool_host = pool if pool_t is None else None  # render: images of the tracked envs
+        self._pool_host = pool  # render: images of the tracked envs (host pools)
         self._visits = [[] for _ in self.render_envs]  # (pre-step position f64 [2], quality) since the reset
         self._last_prediction = None
 
@@ -589,7 +619,8 @@ class _ImageVectorEnv(VectorEnv):
         f8 = [("reward", T["reward"]), ("index", T["index"])] + ([] if loc else [("loss", T["loss_f64"])])
         f4 = [("glimpse", T["glimpse"]), ("glimpse_pos", T["glimpse_pos"]), ("time_step", T["time_step"]),
               ("base_reward", T["base_reward"]), ("target", T["target_out"] if loc else T["label_target"])] + (
-            [("loss", T["loss_f32"])] if loc else []) + [("err", T["err"])]
+            [("loss", T["loss_f32"])] if loc else []) + [("err", T["err"])] + (
+            [("target_glimpse", T["target_glimpse"])] if loc and self.obs_snapshot == "copy" else [])
         return f8 + f4
 
     def _np_block(self):
@@ -640,7 +671,9 @@ class _ImageVectorEnv(VectorEnv):
         if self.config.randomly_invert_labels:
             obs["inverted_label"] = (np.full(n, 2) if self._t_step > 0
                                      else T["inverted"].cpu().numpy().astype(np.int32))
-        if self.kind == N.APG_IMAGE_LOCALIZE:
+        if self.kind == N.APG_IMAGE_LOCALIZE and self.obs_snapshot == "copy":
+            obs["target_glimpse"] = v["target_glimpse"]  # (a field of this step's host block: the caller's own)
+        elif self.kind == N.APG_IMAGE_LOCALIZE:
             # the target glimpse changes only with the batch: a read-only host snapshot refreshed on batch changes
             if resetting or self._tg_host is None:
                 self._tg_host = T["target_glimpse"].cpu().numpy()

@@ -152,13 +152,12 @@ def convert_dataset(ds):
     if ds is None or type(ds).__module__.startswith("ap_gym_amd"):
         return ds
     name = type(ds).__name__
-    if name == "FloorMapDatasetRooms":  # floor_map_dataset_rooms.py:10-24
-        return fm.FloorMapDatasetRooms(ds.map_width, ds.map_height,
-                                       getattr(ds, "_FloorMapDatasetRooms__max_rooms", 10),
-                                       getattr(ds, "_FloorMapDatasetRooms__door_width", 3))
-    if name == "FloorMapDatasetMaze":  # floor_map_dataset_maze.py:10-22
-        return fm.FloorMapDatasetMaze(ds.map_width, ds.map_height,
-                                      getattr(ds, "_FloorMapDatasetMaze__branching_prob", 1.0))
+    # FloorMapDatasetRooms / FloorMapDatasetMaze (floor_map_dataset_rooms.py:10-24, floor_map_dataset_maze.py:10-22)
+    # and subclasses that keep their maps (found in the MRO): the device generators; other floor-map datasets are
+    # read through ForeignFloorMapView by the env (a frozen pool or streamed per episode)
+    proc = fm.procedural_equivalent(ds)
+    if proc is not None:
+        return proc
     if name == "CircleSquareDataset":  # circle_square_dataset.py:80-89
         return cs.CircleSquareDataset(show_gradient=ds._show_gradient, image_shape=tuple(ds._image_shape),
                                       object_extents=ds._object_extents)

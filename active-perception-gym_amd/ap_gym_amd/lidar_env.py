@@ -27,11 +27,13 @@ HBM plus one fused kernel launch per step (include/apgym_capi.h):
 
 Two I/O modes (constructor `array_backend`), inputs of either type are accepted:
   "numpy" (default) -> numpy out, host copies and host-side NaN checks, like the reference.  By default
-                       (copy=None -> True, SyncVectorEnv's default) no returned array is ever written
-                       again: obs["map"] is a read-only array shared by the steps between two steps with
-                       resets (the map obs changes only at resets; a step with resets returns a new
-                       array), every other field is a fresh copy.  copy=False returns the pinned host
-                       mirror of the map obs itself (writable, refreshed in place at resets)
+                       (copy=None -> True, SyncVectorEnv's default, which deep-copies the observations) every
+                       returned array is the caller's own: writable, never written again by the env, obs["map"]
+                       included (a full copy of the map obs per step, 4*H*W bytes per env).
+                       obs_snapshot="shared" (opt-in) hands out obs["map"] as one read-only array shared by
+                       the steps between two steps with resets instead (no per-step copy: the map obs changes
+                       only at resets).  copy=False returns the pinned host mirror of the map obs itself
+                       (writable, refreshed in place at resets)
   "torch"           -> torch out on the env's device, no host synchronisation.  Returned tensors
                        are persistent buffers overwritten by the next step (gymnasium's copy=False
                        contract, the default here: copy=None -> False); pass copy=True to get fresh
@@ -198,7 +200,7 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
                  max_episode_steps: int = 100, device=None, env_offset: int = 0, copy: bool | None = None,
                  strict_errors: bool = False, array_backend: str = "numpy", log_stats: bool = False,
                  sparse: bool = False, render_envs=None, sparse_reset_info: bool = False, packed_outputs: bool = False,
-                 vector_stats: str = "list"):
+                 vector_stats: str = "list", frozen_maps: bool | None = None, obs_snapshot: str = "copy"):
         import torch
 
         if render_mode not in self.metadata["render_modes"]:
@@ -224,6 +226,9 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         if vector_stats not in ("list", "array"):
             raise ValueError("vector_stats must be 'list' (the reference's lists of np.float32) or 'array'")
         self.vector_stats = vector_stats  # numpy backend: form of info["stats"]["vector"] entries
+        if obs_snapshot not in ("copy", "shared"):
+            raise ValueError("obs_snapshot must be 'copy' (writable arrays, SyncVectorEnv(copy=True)) or 'shared'")
+        self.obs_snapshot = obs_snapshot  # numpy backend, copy=True: obs["map"] per step or a shared snapshot
         self.sparse = bool(sparse)
         self.sparse_reset_info = bool(sparse_reset_info)
         self.array_backend = array_backend
@@ -240,23 +245,34 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         # ---- native configuration
         p = dataset.native_params()
         pool_occ = pool_free = None
-        if dataset.map_kind == N.APG_MAP_POOL:  # every map of the dataset, once per device
-            pool_occ, pool_free = dataset.device_pool(self.device)
-            if self.static_map and not 0 <= int(static_map_index) < len(dataset):
-                raise IndexError(f"static_map_index {static_map_index} is out of range for a dataset of "
-                                 f"{len(dataset)} maps")
+        self._streamer = None
+        cfg_static_index, pool_len, stream_len = int(static_map_index), 0, 0
+        if dataset.map_kind == N.APG_MAP_POOL:
+            if self.static_map:  # dataset[static_map_index] alone (lidar_localization2d.py:177-178), any dataset size
+                pool_occ, pool_free = dataset.static_pool(int(static_map_index), self.device)
+                cfg_static_index, pool_len = 0, 1
+            elif frozen_maps is True or (frozen_maps is None and not dataset.prefers_streaming()):
+                pool_occ, pool_free = dataset.device_pool(self.device)  # every map of the dataset, once per device
+                pool_len = len(dataset)
+            else:  # get_data_point(idx) at every draw, fetched one episode ahead (map_stream.py)
+                from .map_stream import MapStreamer
+
+                self._streamer = MapStreamer(dataset, self.num_envs, self.device)
+                pool_occ, pool_free = self._streamer.slots_occ, self._streamer.slots_free
+                pool_len, stream_len = self.num_envs, len(dataset)
+        self.frozen_maps = None if dataset.map_kind != N.APG_MAP_POOL or self.static_map else self._streamer is None
         scale, offset = affine_f32(inner_loss)
         self.output_layout, row_bytes = lidar_output_row_layout(self.lidar_beam_count, self.log_stats, self.sparse)
         if not packed_outputs:
             self.output_layout, row_bytes = None, 0
         self._cfg = N.LidarConfig(num_envs=self.num_envs, height=h, width=w, map_kind=dataset.map_kind,
-                                  is_static=int(self.static_map), static_map_index=int(static_map_index),
+                                  is_static=int(self.static_map), static_map_index=cfg_static_index,
                                   beams=self.lidar_beam_count, step_limit=self.max_episode_steps,
                                   max_rooms=p["max_rooms"], door_width=p["door_width"],
                                   lidar_range=float(np.float32(lidar_range)), loss_scale=scale, loss_offset=offset,
                                   branching_prob=p["branching_prob"], log_stats=int(self.log_stats),
                                   sparse=int(self.sparse), out_row_bytes=row_bytes,
-                                  pool_len=len(dataset) if pool_occ is not None else 0)
+                                  pool_len=pool_len, stream_len=stream_len)
         L = N.lib()
         sizes = N.LidarSizes()
         N.check(L.apg_lidar_query_sizes(ctypes.byref(self._cfg), ctypes.byref(sizes)), "apg_lidar_query_sizes")
@@ -340,7 +356,8 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         self._c_args = None
         self._h = t.classes.apgym.LidarEnv(
             [c.num_envs, c.height, c.width, c.map_kind, c.is_static, c.static_map_index, c.beams, c.step_limit,
-             c.max_rooms, c.door_width, c.log_stats, c.sparse, c.out_row_bytes, self._prefetcher or 0, c.pool_len],
+             c.max_rooms, c.door_width, c.log_stats, c.sparse, c.out_row_bytes, self._prefetcher or 0, c.pool_len,
+             c.stream_len],
             [c.lidar_range, c.loss_scale, c.loss_offset, c.branching_prob],
             N.op_buffers([T[k] for k in ("pos", "init_pos", "elapsed", "flags", "rng", "it_rng", "occ", "scratch",
                                          "stack", "map_idx", "beam_dirs", "stats_hist", "prefetch")] + [None] +
@@ -354,7 +371,8 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         self._autoreset_host = np.zeros(n, dtype=bool)
         self._rows_host = self._rows_np = self._map_host = None  # numpy backend: pinned host mirrors
         self._ring, self._ring_copy = [], False  # numpy backend: pinned output blocks (_host_block)
-        self._map_snapshot = None  # numpy backend, copy=True: read-only map obs shared until the next reset
+        self._map_snapshot = None  # numpy backend, copy=True, obs_snapshot="shared": read-only map obs until a reset
+        self._map_copies = []  # numpy backend, copy=True, obs_snapshot="copy": host blocks handed out as obs["map"]
         self._in_host = self._in_dev = None  # numpy backend: pinned input staging and its device copy
         self._seeded = False
         self._closed = False
@@ -469,6 +487,9 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
 
         if not self._seeded:
             raise RuntimeError("capture_step_graph() needs reset() first")
+        if self._streamer is not None:
+            raise RuntimeError("capture_step_graph(): streamed maps (frozen_maps=False) are fetched by the host "
+                               "between steps; a captured step cannot do that")
         for name, x in (("action", action), ("prediction", prediction)):
             if not (isinstance(x, torch.Tensor) and x.dtype == torch.float32 and x.is_contiguous()
                     and x.device == self.device and x.numel() == 2 * self.num_envs):
@@ -566,7 +587,11 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         s = (int(seed) + self.env_offset) if use_seed else 0
         if s < 0 or s + self.num_envs > 2**64:
             raise ValueError("seed must be a non-negative int")
+        if self._streamer is not None:
+            self._streamer.before_reset(self, s, use_seed)
         self._ops.lidar_reset(self._h, s if s < 2**63 else s - 2**64, bool(use_seed))
+        if self._streamer is not None:
+            self._streamer.after_reset(self)
         self._track_render(None)
         self._seeded = True
         self._autoreset_host[:] = False
@@ -622,6 +647,8 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             self.check_errors(block=False)
             a_t = N.as_device_f32(a, self._dev, 2 * self.num_envs, name="action")
             p_t = N.as_device_f32(p, self._dev, 2 * self.num_envs, name="prediction")
+        if self._streamer is not None:
+            self._streamer.before_step()
         if self._kernel_events is None:
             self._launch_step(a_t, p_t)
         else:  # bench timing: hipEvents on the op's stream around the step launch(es)
@@ -630,6 +657,8 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             N.event_record(ev_b, s)
             self._launch_step(a_t, p_t)
             N.event_record(ev_e, s)
+        if self._streamer is not None:
+            self._streamer.after_step(self, N.ptr(self._t["reset_mask"]))
         self._track_render(p_t)
         if numpy_mode:
             return self._numpy_step_result()
@@ -767,12 +796,16 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         the aliasing mirror semantics; a full ring falls back to copies)."""
         return a.copy() if self._ring_copy else a
 
+    MAP_COPIES = 3  # obs_snapshot="copy": host blocks kept for reuse once no returned obs["map"] refers to them
+
     def _map_refresh(self, reset_mask: np.ndarray | None):
         """The host mirror of the map observation, refreshed only for the sub-envs that reset (the map obs
-        changes only then); None refreshes every sub-env.  copy=False: the mirror itself.  copy=True: a
-        read-only snapshot of it, taken again only when the mirror changed, so an array returned at step t
-        keeps its values after later autoresets (SyncVectorEnv(copy=True)) without a 4*H*W-byte host copy per
-        env on every step."""
+        changes only then); None refreshes every sub-env.  copy=False: the mirror itself.  copy=True: the caller's
+        own copy of it, like SyncVectorEnv(copy=True)'s deepcopy -- a block no earlier returned array refers to any
+        more (sys.getrefcount), rewritten whole from the mirror on torch's intra-op threads, or
+        (obs_snapshot="shared") one read-only snapshot of the mirror taken again only when the mirror changed."""
+        import sys
+
         import torch
 
         if self.static_map:
@@ -790,6 +823,19 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         m = self._map_host.numpy()
         if not self.copy:
             return m
+        if self.obs_snapshot == "copy":
+            blk = None
+            for b in self._map_copies:
+                if sys.getrefcount(b[1]) <= 2:  # the list's tuple and the call argument: no returned array is alive
+                    blk = b
+                    break
+            if blk is None:
+                t = torch.empty(tuple(self._map_host.shape), dtype=torch.float32)
+                blk = (t, t.numpy())
+                if len(self._map_copies) < self.MAP_COPIES:
+                    self._map_copies.append(blk)
+            blk[0].copy_(self._map_host)  # whole: the caller may have written into an earlier hand-out of it
+            return blk[1]
         if changed or self._map_snapshot is None:
             # torch's CPU copy runs on the intra-op thread pool (numpy's m.copy() is one thread: 3-4x slower at
             # the 1 GB of a cfg-2 episode end)
@@ -861,6 +907,9 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             if getattr(self, "_prefetcher", None):
                 N.lib().apg_lidar_prefetcher_destroy(self._prefetcher)  # synchronizes its side stream
                 self._prefetcher = None
+            if getattr(self, "_streamer", None) is not None:
+                self._streamer.close()
+                self._streamer = None
             self._t = {}
             self._h = None  # the op handle keeps every state/output buffer alive
             self._c_args = None

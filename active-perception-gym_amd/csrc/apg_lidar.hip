@@ -67,6 +67,7 @@ constexpr int EMPTY_TAB = 1024;
 struct Geo {
   int n, h, w, wpr, is_static, kind, max_rooms, door_width, frames, row, pool_len;
   double bp;
+  int64_t stream_len;  // APG_MAP_POOL streamed maps: len(dataset) of the draw; the map is slot e of the pool (0: pool)
 };
 
 // Output element j of env e: a dense [N][k] array, or (row > 0: apg_lidar_config.out_row_bytes) a field of env
@@ -91,6 +92,7 @@ Geo make_geo(const apg_lidar_config *c) {
   g.bp = c->branching_prob;
   g.row = c->out_row_bytes;
   g.pool_len = c->map_kind == APG_MAP_POOL ? c->pool_len : 0;
+  g.stream_len = c->map_kind == APG_MAP_POOL && !c->is_static ? c->stream_len : 0;
   return g;
 }
 
@@ -110,6 +112,9 @@ int validate(const apg_lidar_config *c) {
     if (c->pool_len < 1) return fail(APG_E_INVALID, "the map pool must hold at least one map");
     if (c->is_static && (c->static_map_index < 0 || c->static_map_index >= c->pool_len))
       return fail(APG_E_INVALID, "static_map_index is outside the map pool");
+    if (c->stream_len < 0) return fail(APG_E_INVALID, "stream_len must be >= 0");
+    if (c->stream_len > 0 && !c->is_static && c->pool_len != c->num_envs)
+      return fail(APG_E_INVALID, "streamed maps need one pool slot per env (pool_len == num_envs)");
   } else if (c->height < 3 || c->width < 3) {
     return fail(APG_E_INVALID, "map size must be at least 3");
   }
@@ -251,10 +256,11 @@ APG_DEV uint8_t reset_one(const Geo &g, const apg_lidar_state &S, int e, uint8_t
   float px = 0.5f, py = 0.5f;
   if constexpr (GEN == GEN_POOL) {
     // DatasetIterator: integers(0, len(dataset)) (dataset_iterator.py:26-32), then get_data_point(idx) is pool map idx
-    midx = (uint64_t)integers(it, 0, g.pool_len);
+    // (streamed maps: the host fetched get_data_point(idx) of this very draw into slot e ahead of the reset)
+    midx = (uint64_t)integers(it, 0, g.stream_len ? g.stream_len : (int64_t)g.pool_len);
     const size_t words = (size_t)g.h * g.wpr;
     uint64_t *rows = S.occ + (size_t)e * words;
-    const uint64_t *src = S.pool_occ + midx * words;
+    const uint64_t *src = S.pool_occ + (g.stream_len ? (uint64_t)e : midx) * words;
     for (size_t q = 0; q < words; q++) rows[q] = src[q];
     if (place_start(rng, rows, g.h, g.w, g.wpr, px, py) != 0) atomicOr(err, APG_ERR_NO_FREE_CELL);
     *reinterpret_cast<Pcg64 *>(&S.it_rng[e]) = it;
@@ -1141,8 +1147,8 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         if (pend) {
           rng = *reinterpret_cast<const Pcg64 *>(&S.rng[my_e]);
           it = *reinterpret_cast<const Pcg64 *>(&S.it_rng[my_e]);
-          midx = (uint64_t)integers(it, 0, g.pool_len);
-          const int nfree = S.pool_free[midx];
+          midx = (uint64_t)integers(it, 0, g.stream_len ? g.stream_len : (int64_t)g.pool_len);
+          const int nfree = S.pool_free[g.stream_len ? (uint64_t)my_e : midx];  // (streamed: slot = env)
           if (nfree > 0) pick = (long long)integers(rng, 0, nfree);
         }
         const int wpr = P.wpr;
@@ -1152,7 +1158,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           const uint64_t mj = ((uint64_t)(uint32_t)__shfl((int)(midx >> 32), j) << 32) | (uint32_t)__shfl((int)midx, j);
           const long long pj = ((long long)__shfl((int)((unsigned long long)pick >> 32), j) << 32) |
                                (uint32_t)__shfl((int)pick, j);
-          const uint64_t *src = S.pool_occ + mj * words;
+          const uint64_t *src = S.pool_occ + (g.stream_len ? (uint64_t)e : mj) * words;
           uint64_t *dst = S.occ + (size_t)e * words;
           if (lane == 0) s_start[el] = ~0u;
           int off = 0;
@@ -1649,7 +1655,9 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           const bool t4 = h >= 4;
           acc = (t4 ? s_win4[o] : s_win[o]) | (t4 ? s_win4[o + h - 4] : (h > 1 ? s_win[o + 1] : 0u)) |
                 (!t4 && h > 2 ? s_win[o + 2] : 0u);
-          for (int t = 8; t < h; t += 4) acc |= s_win4[o + min(t, h - 4)];  // (boxes taller than 8: lidar_range > 6)
+          // the middle rows of boxes taller than 8 (lidar_range > 6): rows 4.. in 4-row steps, the last group
+          // overlapping the tail read above
+          for (int t = 4; t < h - 4; t += 4) acc |= s_win4[o + t];
         } else {
           acc = s_win[o] | (h > 1 ? s_win[o + 1] : 0u) | (h > 2 ? s_win[o + 2] : 0u);
         }
@@ -2178,6 +2186,43 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
 
 // One prefetch batch on the prefetcher's side stream (k_pf_select .. k_pf_paint), after `after` (an event of the
 // env's stream): the next mazes of every env whose record is stale by then.
+// Streamed maps (apgym_capi.h, apg_lidar_peek_map_index): the dataset index the NEXT reset of each selected env
+// will draw, integers(0, len) of a copy of its DatasetIterator stream (dataset_iterator.py:26-32), or (use_seed) of
+// the stream reset(seed) gives it (the _np_random setter, lidar_localization2d.py:547-557).  Nothing is advanced.
+// out_env NULL: out_idx[e] for every selected env; else the selected envs compacted (any order) with their count.
+__global__ __launch_bounds__(256) void k_peek_map_index(int n, const apg_pcg64 *it_state, int64_t len, uint64_t seed,
+                                                        int use_seed, const uint8_t *mask, int mask_stride,
+                                                        int64_t *out_idx, int32_t *out_env, int32_t *count) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const bool sel = e < n && (!mask || mask[(size_t)e * mask_stride]);
+  int64_t idx = 0;
+  if (sel) {
+    Pcg64 it;
+    if (use_seed) {
+      Pcg64 r = seed_pcg64(seed + (uint64_t)e);
+      it = seed_pcg64(bounded_u64(r, 0x100000000ULL));  // integers(0, 2**32, endpoint=True)
+    } else {
+      it = *reinterpret_cast<const Pcg64 *>(&it_state[e]);
+    }
+    idx = integers(it, 0, len);
+  }
+  if (!out_env) {
+    if (sel) out_idx[e] = idx;
+    return;
+  }
+  const unsigned long long m = __ballot(sel);
+  if (m == 0ULL) return;
+  const int lane = threadIdx.x & 63, first = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == first) base = atomicAdd(count, __popcll(m));
+  base = __shfl(base, first);
+  if (sel) {
+    const int k = base + __popcll(m & ((1ULL << lane) - 1ULL));
+    out_env[k] = e;
+    out_idx[k] = idx;
+  }
+}
+
 int pf_batch_kernels(const apg_lidar_config *cfg, const apg_lidar_state *st, const apg_lidar_outputs *out,
                      hipStream_t side) {
   const Geo g = make_geo(cfg);
@@ -2514,6 +2559,24 @@ int apg_lidar_prefetcher_destroy(apg_lidar_prefetcher *p) {
   if (dev >= 0) hipSetDevice(dev);
   delete p;
   return APG_OK;
+}
+
+int apg_lidar_peek_map_index(const apg_lidar_config *cfg, const apg_lidar_state *st, uint64_t seed, int use_seed,
+                             const uint8_t *mask, int64_t *out_idx, int32_t *out_env, int32_t *out_count,
+                             apg_stream_t stream) {
+  int rc = validate(cfg);
+  if (rc) return rc;
+  if (cfg->map_kind != APG_MAP_POOL || cfg->is_static || cfg->stream_len <= 0)
+    return fail(APG_E_INVALID, "peek_map_index: streamed pool maps only (stream_len > 0, dynamic maps)");
+  if (!st || !out_idx || (!use_seed && !st->it_rng) || (out_env && !out_count))
+    return fail(APG_E_INVALID, "peek_map_index: null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  if (out_env && hipMemsetAsync(out_count, 0, sizeof(int32_t), s) != hipSuccess)
+    return fail(APG_E_LAUNCH, "hipMemsetAsync (peek count)");
+  const int n = cfg->num_envs;
+  hipLaunchKernelGGL(k_peek_map_index, dim3(grid_for(n, 256)), dim3(256), 0, s, n, st->it_rng, cfg->stream_len, seed,
+                     use_seed, mask, cfg->out_row_bytes ? cfg->out_row_bytes : 1, out_idx, out_env, out_count);
+  return check_launch("k_peek_map_index");
 }
 
 int apg_lidar_prefetcher_stats(const apg_lidar_prefetcher *p, int64_t out[4]) {

@@ -67,12 +67,12 @@ struct LidarEnv : torch::CustomClassHolder {
 
   // ints: num_envs, height, width, map_kind, is_static, static_map_index, beams, step_limit, max_rooms,
   // door_width, log_stats, sparse, out_row_bytes, prefetcher handle (apg_lidar_prefetcher_create's pointer or 0:
-  // owned by the Python env), pool_len; reals: lidar_range, loss_scale, loss_offset, branching_prob.  The state
+  // owned by the Python env), pool_len, stream_len; reals: lidar_range, loss_scale, loss_offset, branching_prob.  The state
   // buffers are the struct's fields in order: ..., the prefetch buffer, a 0-element placeholder for the prefetcher
   // field, the map pool (pool_occ, pool_free: 0-element tensors for the procedural kinds).
   LidarEnv(std::vector<int64_t> ints, std::vector<double> reals, std::vector<at::Tensor> state,
            std::vector<at::Tensor> outputs) {
-    TORCH_CHECK(ints.size() == 15 && reals.size() == 4, "LidarEnv: 15 ints and 4 reals expected");
+    TORCH_CHECK(ints.size() == 16 && reals.size() == 4, "LidarEnv: 16 ints and 4 reals expected");
     cfg.num_envs = (int32_t)ints[0];
     cfg.height = (int32_t)ints[1];
     cfg.width = (int32_t)ints[2];
@@ -87,6 +87,7 @@ struct LidarEnv : torch::CustomClassHolder {
     cfg.sparse = (int32_t)ints[11];
     cfg.out_row_bytes = (int32_t)ints[12];
     cfg.pool_len = (int32_t)ints[14];
+    cfg.stream_len = ints[15];
     cfg.lidar_range = (float)reals[0];
     cfg.loss_scale = (float)reals[1];
     cfg.loss_offset = (float)reals[2];

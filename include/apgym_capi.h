@@ -125,6 +125,14 @@ typedef struct apg_lidar_config {
                                    map is pool map integers(0, pool_len) of the env's DatasetIterator stream
                                    (dataset_iterator.py:26-32), the static map pool map static_map_index.
                                    Other kinds: ignored (ABI 0.3) */
+  int64_t stream_len;           /* APG_MAP_POOL, dynamic maps: 0 = the pool holds every map of the dataset (above).
+                                   > 0 = streamed maps (ABI 0.4): len(dataset) (any size, e.g. 2**32); the episode's
+                                   map index is integers(0, stream_len) of the env's DatasetIterator stream and its
+                                   map is pool slot e (pool_len == num_envs), which the host filled with
+                                   dataset.get_data_point(that index) before the reset -- the reference's per-draw
+                                   fetch (dataset_iterator.py:26-32) through its prefetch thread
+                                   (buffered_iterator.py:11-61).  apg_lidar_peek_map_index tells the host which index
+                                   each env's next reset draws.  Callers built against ABI <= 0.3 must zero it. */
 } apg_lidar_config;
 
 /* Persistent per-env state.  Sizes come from apg_lidar_query_sizes(). */
@@ -224,6 +232,19 @@ int apg_lidar_prefetcher_destroy(apg_lidar_prefetcher *p); /* synchronizes its s
 /* per-prefetcher counters: [0] batches launched, [1] steps whose main stream had to wait for a batch that was still
  * running, [2] resets observed, [3] step calls since the last reset (diagnostics, host memory) */
 int apg_lidar_prefetcher_stats(const apg_lidar_prefetcher *p, int64_t out[4]);
+
+/* ---------------------------------------------------------------- streamed maps (APG_MAP_POOL, stream_len > 0)
+ * The dataset index the NEXT reset of each selected env will draw (integers(0, stream_len) of a copy of its
+ * DatasetIterator stream, dataset_iterator.py:26-32; use_seed: of the stream reset(seed=seed) gives sub-env e, i.e.
+ * default_rng(seed + e).integers(0, 2**32, endpoint=True), the _np_random setter of lidar_localization2d.py:547-557).
+ * No stream is advanced.  mask: NULL = every env, else the envs whose reset_mask output is 1 (the step that just ran
+ * reset them: their slots were consumed; mask is read with the output row stride when out_row_bytes > 0).
+ * out_env NULL: out_idx[e] for every selected env.  Else the selected envs compacted (in no particular order) into
+ * out_env[k] / out_idx[k], k < *out_count (zeroed by the call).  Replaces next(DataLoader(DatasetIterator)) of
+ * lidar_localization2d.py:296-298 on the host side: the host fetches get_data_point(idx) into the env's slot. */
+int apg_lidar_peek_map_index(const apg_lidar_config *cfg, const apg_lidar_state *st, uint64_t seed, int use_seed,
+                             const uint8_t *mask, int64_t *out_idx, int32_t *out_env, int32_t *out_count,
+                             apg_stream_t stream);
 
 /* u16 units of maze scratch per map (apg_lidar_state.stack / apg_map_generate's stack) for an h x w maze;
  * replaces the reference's recursion stack of carve() (floor_map_dataset_maze.py:31-45). */

@@ -65,6 +65,10 @@ void orc_lidar_destroy(orc_lidar_env *e);
 void orc_lidar_set_rooms(orc_lidar_env *e, int max_rooms, int door_width);
 /* kind 2: the maps of any finite FloorMapDataset, [pool_len][h][w] 0/1 bytes (borrowed), before reset */
 int orc_lidar_set_pool(orc_lidar_env *e, const uint8_t *maps, int64_t pool_len, int static_map_index);
+/* kind 2, dynamic maps fetched at every draw: fn(ctx, idx, out) writes get_data_point(idx) as [h][w] 0/1 bytes and
+   returns 0; len = len(dataset), any size (streamed maps) */
+typedef int (*orc_map_fn)(void *ctx, uint64_t idx, uint8_t *out);
+int orc_lidar_set_map_source(orc_lidar_env *e, orc_map_fn fn, void *ctx, int64_t len);
 int orc_lidar_no_free(const orc_lidar_env *e);
 /* reset(seed=seed): sub-env i seeded with seed+i. Writes obs. */
 void orc_lidar_reset(orc_lidar_env *e, uint64_t seed, float *lidar, float *odometry,

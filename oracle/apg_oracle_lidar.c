@@ -338,6 +338,8 @@ struct orc_lidar_env {
   int max_rooms, door_width; /* FloorMapDatasetRooms parameters of the dynamic maps (default 10, 3) */
   const uint8_t *pool;       /* kind 2: the dataset's maps [pool_len][h][w] (borrowed), any FloorMapDataset */
   int64_t pool_len;
+  orc_map_fn map_fn;         /* kind 2 without a pool: get_data_point(idx) called at every draw (any len) */
+  void *map_ctx;
   float range;
   float *dirs;        /* [beams][2] scaled beam vectors (lidar_directions) */
   orc_pcg64 *rng;     /* env np_random */
@@ -435,7 +437,12 @@ static void env_reset_one(orc_lidar_env *e, int i) {
     /* DatasetIterator.__next__ (dataset_iterator.py:26-32): idx = rng.integers(0, len(dataset)), then
        dataset.get_data_point(idx) -- the pool's map idx */
     uint64_t idx = (uint64_t)orc_integers(&e->it_rng[i], 0, e->pool_len);
-    memcpy(e->maps + (size_t)i * e->h * e->w, e->pool + (size_t)idx * e->h * e->w, (size_t)e->h * e->w);
+    uint8_t *m = e->maps + (size_t)i * e->h * e->w;
+    if (e->map_fn) {
+      if (e->map_fn(e->map_ctx, idx, m) != 0) e->no_free = 1; /* (the callback failed: flagged like a bad map) */
+    } else {
+      memcpy(m, e->pool + (size_t)idx * e->h * e->w, (size_t)e->h * e->w);
+    }
     e->map_idx[i] = idx;
   } else if (!e->is_static) {
     uint64_t idx = (uint64_t)orc_next32(&e->it_rng[i]); /* integers(0, 2**32) */
@@ -636,6 +643,18 @@ int orc_lidar_set_pool(orc_lidar_env *e, const uint8_t *maps, int64_t pool_len, 
     if (static_map_index < 0 || static_map_index >= pool_len) return -1;
     memcpy(e->maps, maps + (size_t)static_map_index * e->h * e->w, (size_t)e->h * e->w);
   }
+  return 0;
+}
+
+/* kind 2, dynamic maps, fetched per draw: fn(ctx, idx, out[h][w] 0/1 bytes) is the dataset's get_data_point(idx)
+   (dataset_iterator.py:26-32), called at every reset with idx = integers(0, len) of the env's DatasetIterator stream.
+   Any len >= 1 (e.g. 2**32). */
+int orc_lidar_set_map_source(orc_lidar_env *e, orc_map_fn fn, void *ctx, int64_t len) {
+  if (e->kind != 2 || e->is_static || !fn || len < 1) return -1;
+  e->map_fn = fn;
+  e->map_ctx = ctx;
+  e->pool = NULL;
+  e->pool_len = len;
   return 0;
 }
 

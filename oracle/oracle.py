@@ -16,6 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 _lib = None
+MAP_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p)
 
 
 def build(force: bool = False) -> str:
@@ -49,6 +50,8 @@ def lib():
         L.orc_lidar_get_state.argtypes = [vp, vp, vp, vp, vp]
         L.orc_lidar_set_pool.restype = i32
         L.orc_lidar_set_pool.argtypes = [vp, vp, ctypes.c_int64, i32]
+        L.orc_lidar_set_map_source.restype = i32
+        L.orc_lidar_set_map_source.argtypes = [vp, MAP_FN, vp, ctypes.c_int64]
         L.orc_lidar_no_free.restype = i32
         L.orc_lidar_no_free.argtypes = [vp]
         _lib = L
@@ -92,9 +95,28 @@ class OracleLidarVectorEnv:
     """SyncVectorEnv(TimeLimit(LIDARLocalization2DEnv)) restated in C; numpy in/out."""
 
     def __init__(self, num_envs, map_kind="rooms", size=32, static_map=False, static_map_index=0, beams=8,
-                 lidar_range=5, step_limit=100, sparse=False, max_rooms=10, door_width=3, pool=None):
-        """map_kind "pool": `pool` holds the maps of a finite FloorMapDataset, bool [len, H, W] (any H x W)."""
-        if map_kind == "pool":
+                 lidar_range=5, step_limit=100, sparse=False, max_rooms=10, door_width=3, pool=None,
+                 map_fn=None, map_len=None, map_hw=None):
+        """map_kind "pool": `pool` holds the maps of a finite FloorMapDataset, bool [len, H, W] (any H x W).
+        map_kind "stream": `map_fn(idx) -> bool [H, W]` is the dataset's get_data_point, called at every draw
+        (dataset_iterator.py:26-32), `map_len` its len (any size), `map_hw` = (H, W)."""
+        self._map_cb = None
+        if map_kind == "stream":
+            size_hw = tuple(map_hw)
+            h_, w_ = size_hw
+
+            def cb(_ctx, idx, out):
+                try:
+                    m = np.asarray(map_fn(int(idx)), dtype=bool)
+                    if m.shape != (h_, w_):
+                        return 1
+                    ctypes.memmove(out, np.ascontiguousarray(m.view(np.uint8)).ctypes.data, h_ * w_)
+                    return 0
+                except Exception:  # noqa: BLE001 (reported as a failed draw)
+                    return 1
+
+            self._map_cb = MAP_FN(cb)
+        elif map_kind == "pool":
             self._pool = np.ascontiguousarray(np.asarray(pool, dtype=bool).view(np.uint8))
             size_hw = self._pool.shape[1:]
         else:
@@ -104,12 +126,15 @@ class OracleLidarVectorEnv:
         size = self.h
         self.static = static_map
         self.dirs = beam_directions(beams, lidar_range)
-        kind = {"rooms": 0, "maze": 1, "pool": 2}[map_kind]
+        kind = {"rooms": 0, "maze": 1, "pool": 2, "stream": 2}[map_kind]
         self._e = lib().orc_lidar_create(num_envs, kind, self.h, self.w, int(static_map),
                                          static_map_index, beams, float(lidar_range), step_limit, _p(self.dirs))
         if not self._e:
             raise ValueError("invalid map configuration")
-        if kind == 2 and lib().orc_lidar_set_pool(self._e, _p(self._pool), len(self._pool), static_map_index) != 0:
+        if map_kind == "stream":
+            if static_map or lib().orc_lidar_set_map_source(self._e, self._map_cb, None, int(map_len)) != 0:
+                raise ValueError("streamed maps: dynamic maps and map_len >= 1")
+        elif kind == 2 and lib().orc_lidar_set_pool(self._e, _p(self._pool), len(self._pool), static_map_index) != 0:
             raise ValueError("invalid map pool / static_map_index")
         if (max_rooms, door_width) != (10, 3):
             lib().orc_lidar_set_rooms(self._e, max_rooms, door_width)

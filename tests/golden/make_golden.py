@@ -811,10 +811,35 @@ def make_hf():
     save("hf_dataset.npz", **out)
 
 
+def make_stream():
+    """LIDAR envs over a user FloorMapDataset of len 2**32 whose maps come from default_rng(idx) (tests/stream_maps.py):
+    too large for any pool, the backend streams it (get_data_point at every draw, like the reference's DatasetIterator,
+    dataset_iterator.py:26-32).  The fixture records the maps of every reset (reset_map / map) and their indices."""
+    fm = refload.load("envs.floor_map")
+    sys.path.insert(0, os.path.dirname(HERE))
+    from stream_maps import STREAM_LEN, rng_floor_map
+
+    class RngFloorMaps(fm.FloorMapDataset):
+        def __init__(self):
+            super().__init__(40, 40)
+
+        def _get_length(self):
+            return STREAM_LEN
+
+        def get_data_point(self, idx):
+            return rng_floor_map(int(idx))
+
+        def get_data_point_batch(self, idx):
+            return np.stack([rng_floor_map(int(i)) for i in idx])
+
+    run_lidar_env("stream40_b16", RngFloorMaps(), False, 16, 64, 110, 42, "wide")
+
+
 SECTIONS = {"rng": make_rng, "maps": make_maps, "loss": make_loss, "scan": make_lidar_scan,
             "lidar": make_lidar_env, "image": make_image_env,
             "sparse": make_sparse_env, "circle_square": make_circle_square,
-            "light_dark": make_light_dark, "render": make_render, "hf": make_hf, "pool": make_pool}
+            "light_dark": make_light_dark, "render": make_render, "hf": make_hf, "pool": make_pool,
+            "stream": make_stream}
 
 
 def main(argv):

@@ -684,3 +684,41 @@ def test_draw_ahead_matches_drawing_at_the_autoreset(gpu, kind, invert, backend,
     for e in envs:
         e.check_errors()
         e.close()
+
+
+@pytest.mark.parametrize("snapshot", ["copy", "shared"])
+def test_image_numpy_returned_arrays_are_writable(gpu, snapshot):
+    """The reference computes every observation anew each step (image_localization.py:142-146, 170-174): a caller
+    may write into them.  Writes into every returned array on consecutive steps (target glimpse included) leave the
+    next steps' values unaffected (checked against the oracle across a batch change); obs_snapshot="shared" (opt-in)
+    returns the target glimpse as a read-only array shared by a batch's steps."""
+    import ap_gym_amd as ap
+    from oracle import image_oracle as io
+
+    n, k, sensor, shape = 96, 10, (5, 5), (28, 28)
+    rng = np.random.default_rng(4)
+    pool = rng.integers(0, 256, (64, *shape), dtype=np.uint8)
+    labels = rng.integers(0, k, 64)
+    ds = ap.ArrayImageClassificationDataset(pool, labels, k, 1)
+    cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=sensor, step_limit=4)
+    env = ap.ImageLocalizationVectorEnv(n, cfg, obs_snapshot=snapshot)
+    ref = io.ImageVectorEnvOracle("loc", pool, labels, k, 1, n, sensor, 1.0, 4)
+    env.reset(seed=2)
+    ref.reset(2)
+    arng = np.random.default_rng(1)
+    for t in range(11):  # two batch changes
+        a = arng.uniform(-1.5, 1.5, (n, 2)).astype(np.float32)
+        p = arng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        want = ref.step(a, p)
+        for key in want[0]:
+            assert np.array_equal(obs[key], want[0][key]), (t, key)
+        assert np.array_equal(rew, want[1]), t
+        for key, v in obs.items():
+            if key == "target_glimpse" and snapshot == "shared":
+                assert not v.flags.writeable
+                continue
+            v[...] = 5
+        rew[...] = -1
+        info["prediction"]["target"][...] = 9
+    env.close()

@@ -399,7 +399,12 @@ def test_vector_env_matches_oracle(gpu, oracle_mod, kind, size, beams, n, steps,
     env.close()
 
 
-@pytest.mark.parametrize("kind,size,static,beams,lidar_range,n", [("rooms", 64, False, 16, 12.0, 512),
+@pytest.mark.parametrize("kind,size,static,beams,lidar_range,n", [("rooms", 64, False, 32, 8.0, 1024),
+                                                                   ("rooms", 64, True, 32, 9.5, 512),
+                                                                   ("rooms", 64, False, 16, 9.9, 512),
+                                                                   ("rooms", 32, False, 16, 6.5, 512),
+                                                                   ("maze", 63, False, 32, 9.0, 512),
+                                                                   ("rooms", 64, False, 16, 12.0, 512),
                                                                    ("maze", 63, False, 32, 20.0, 256),
                                                                    ("rooms", 32, True, 8, 10.5, 256),
                                                                    ("rooms", 64, False, 8, 28.0, 128),
@@ -407,8 +412,10 @@ def test_vector_env_matches_oracle(gpu, oracle_mod, kind, size, beams, n, steps,
                                                                    ("maze", 63, False, 16, 60.0, 128),
                                                                    ("rooms", 128, False, 16, 45.5, 128)])
 def test_long_range_matches_oracle(gpu, oracle_mod, kind, size, static, beams, lidar_range, n):
-    """lidar_range > 10 (the step kernel's rows-from-global-memory instance, 64-column row windows: ranges up to
-    60): observations, rewards and terminations of 110 steps (one autoreset) against the oracle env."""
+    """Ranges past the default 5: 6.5-10 (the staged-window instance with bounding boxes 9-12 rows tall, whose
+    pre-test ORs the middle rows of the 4-row table) and > 10 (the rows-from-global-memory instance, 64-column row
+    windows: ranges up to 60): observations, rewards and terminations of 110 steps (one autoreset) against the
+    oracle env."""
     import ap_gym_amd as ap
 
     env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_ds(ap, kind, size), lidar_beam_count=beams,
@@ -633,7 +640,7 @@ def test_numpy_backend_copy_semantics(gpu, kind):
     for o, snap in held:  # nothing handed out by the copying env changed afterwards
         for k in snap:
             assert np.array_equal(o[k], snap[k]), k
-    assert not held[-1][0]["map"].flags.writeable
+    assert held[-1][0]["map"].flags.writeable  # the caller's own copy (SyncVectorEnv(copy=True) deep-copies)
     assert not np.array_equal(held[0][1]["map"], held[-1][1]["map"])  # the maps did change at the resets
     assert np.shares_memory(oa["map"], obs0_a["map"])  # copy=False: one mirror, rewritten in place
     assert env._ring_copy and len(env._ring) == env.HOST_RING  # 10 steps held: the ring is full, later steps copy
@@ -832,3 +839,33 @@ def test_step_through_ops_and_graph_replay(gpu, kind, size, beams, use_torch_op)
         assert torch.equal(graphed._t["map_obs"], obs["map"]), t
     eager.check_errors()
     graphed.check_errors()
+
+
+@pytest.mark.parametrize("snapshot", ["copy", "shared"])
+def test_numpy_backend_returned_arrays_are_writable(gpu, oracle_mod, snapshot):
+    """SyncVectorEnv(copy=True) deep-copies the observations it returns: a caller may normalise them in place.
+    Writes into every returned array (obs["map"] included) on consecutive steps leave the next steps' values
+    unaffected (checked against the oracle).  obs_snapshot="shared" (opt-in) returns obs["map"] read-only."""
+    import ap_gym_amd as ap
+
+    n = 64
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=ap.FloorMapDatasetRooms(32, 32), lidar_beam_count=8,
+                                          device=gpu, max_episode_steps=4, obs_snapshot=snapshot)
+    ref = oracle_mod.OracleLidarVectorEnv(n, "rooms", 32, False, 0, 8, step_limit=4)
+    obs, _ = env.reset(seed=1)
+    ref.reset(1)
+    rng = np.random.default_rng(3)
+    for t in range(12):
+        a = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        p = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        ref.step(a, p)
+        assert np.array_equal(obs["lidar"], ref.lidar) and np.array_equal(obs["map"][..., 0], ref.map), t
+        assert np.array_equal(rew, ref.reward), t
+        for k, v in obs.items():
+            if k == "map" and snapshot == "shared":
+                assert not v.flags.writeable
+                continue
+            v[...] = -7  # in-place "normalisation" by the caller
+        rew[...] = 123.0
+    env.close()

@@ -49,7 +49,8 @@ def _compare(env, ref, obs, rew, term, t, static):
         assert np.array_equal(obs["map"][..., 0], ref.map), t
 
 
-@pytest.mark.parametrize("case", ["golden48x40_n1024", "wide100x70_r12", "tall300x257", "tiny5x7", "open64"])
+@pytest.mark.parametrize("case", ["golden48x40_n1024", "wide100x70_r12", "tall300x257", "tiny5x7", "open64",
+                                  "wide100x70_r8", "sq80_r9_5"])
 def test_pool_env_matches_oracle(gpu, oracle_mod, case):
     import ap_gym_amd as ap
 
@@ -62,6 +63,10 @@ def test_pool_env_matches_oracle(gpu, oracle_mod, case):
         maps, beams, n = random_pool(17, 257, 300, 2), 8, 64
     elif case == "tiny5x7":  # maps smaller than the scan window, most beams leave the map
         maps, beams, n = random_pool(9, 7, 5, 3, open_every=2, density=0.1), 8, 256
+    elif case == "wide100x70_r8":  # staged windows with 10-row beam boxes (the pre-test's middle 4-row groups)
+        maps, beams, rng_, n = random_pool(300, 70, 100, 11, density=0.01), 32, 8.0, 1024
+    elif case == "sq80_r9_5":  # 11-12-row beam boxes
+        maps, beams, rng_, n = random_pool(50, 80, 80, 12, density=0.005), 32, 9.5, 1024
     else:  # square maps with open borders: early terminations, autoresets every few steps
         maps, n, a_scale = random_pool(64, 64, 64, 4, open_every=2), 1024, 2.5
     env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=UserFloorMaps(maps), lidar_beam_count=beams,
@@ -178,4 +183,140 @@ def test_pool_make_vec(gpu, oracle_mod):
         obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
         ref.step(a, p)
         _compare(env, ref, obs, rew, term, t, False)
+    env.close()
+
+
+# ---------------------------------------------------------------------------------------------- streamed maps
+def _stream_ds(**kw):
+    from stream_maps import StreamFloorMaps
+
+    return StreamFloorMaps(**kw)
+
+
+@pytest.mark.parametrize("backend", ["numpy", "torch"])
+def test_stream_env_matches_reference_golden(gpu, backend):
+    """A user dataset of len 2**32 (maps from default_rng(idx)): no pool can hold it, so the env streams it,
+    get_data_point(idx) at every draw one episode ahead (map_stream.py), and matches the reference env's own trace
+    over the same dataset (tests/golden/lidar_env_stream40_b16.npz: 64 envs, 110 steps, one TimeLimit autoreset)."""
+    import torch
+
+    import ap_gym_amd as ap
+
+    d = golden("lidar_env_stream40_b16.npz")
+    n = d["actions"].shape[1]
+    ds = _stream_ds()
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=ds, lidar_beam_count=16, device=gpu,
+                                          array_backend=backend, log_stats=True)
+    assert env.frozen_maps is False and ds.fetches == 0
+    to_np = (lambda x: x.cpu().numpy()) if backend == "torch" else (lambda x: x)
+    obs, info = env.reset(seed=int(d["seed"]))
+    assert np.array_equal(to_np(obs["lidar"]), d["reset_lidar"])
+    assert np.array_equal(to_np(info["map_idx"]), d["reset_map_idx"])
+    assert np.array_equal(np.packbits(to_np(obs["map"])[..., 0] > 0, axis=-1), d["reset_map"])
+    for t in range(d["actions"].shape[0]):
+        a, p = d["actions"][t], d["predictions"][t]
+        if backend == "torch":
+            a, p = torch.as_tensor(a, device=gpu), torch.as_tensor(p, device=gpu)
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        assert np.array_equal(to_np(obs["lidar"]), d["lidar"][t]), t
+        assert np.array_equal(to_np(obs["odometry"]), d["odometry"][t]), t
+        assert np.array_equal(to_np(rew), d["reward"][t]), t
+        assert np.array_equal(to_np(term), d["terminated"][t]), t
+        assert np.array_equal(np.packbits(to_np(obs["map"])[..., 0] > 0, axis=-1), d["map"][t]), t
+    env.close()
+    # one fetch per episode start (reset + the next episode fetched ahead + its successor after the autoreset)
+    assert n <= ds.fetches <= 3 * n
+
+
+def test_stream_env_matches_oracle_n4096(gpu, oracle_mod):
+    """The same dataset at N = 4096 over 110 steps against the oracle fetching per draw (oracle stream mode)."""
+    from stream_maps import STREAM_LEN, rng_floor_map
+
+    import ap_gym_amd as ap
+
+    n = 4096
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=_stream_ds(), lidar_beam_count=16, device=gpu)
+    ref = oracle_mod.OracleLidarVectorEnv(n, "stream", 0, False, 0, 16, map_fn=rng_floor_map, map_len=STREAM_LEN,
+                                          map_hw=(40, 40))
+    obs, info = env.reset(seed=2024)
+    ref.reset(2024)
+    assert np.array_equal(obs["lidar"], ref.lidar)
+    assert np.array_equal(info["map_idx"], ref.map_idx.astype(np.int64))
+    rng = np.random.default_rng(8)
+    for t in range(110):
+        a = rng.uniform(-1.5, 1.5, (n, 2)).astype(np.float32)
+        p = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        ref.step(a, p)
+        _compare(env, ref, obs, rew, term, t, False)
+        if "map_idx" in info:
+            m = info["_map_idx"]
+            assert np.array_equal(info["map_idx"][m], ref.map_idx.astype(np.int64)[m]), t
+    assert not ref.no_free_cell()
+    env.close()
+
+
+@pytest.mark.parametrize("backend", ["numpy", "torch"])
+def test_stream_two_step_episodes_match_oracle(gpu, oracle_mod, backend):
+    """frozen_maps=False on a small dataset with max_episode_steps=2 and open maps: envs reset every second or third
+    step, the tightest the one-episode-ahead fetch allows (a slot consumed at step t is needed again at t + 2),
+    against the pool oracle (same maps, same draws)."""
+    import torch
+
+    import ap_gym_amd as ap
+
+    maps, n = random_pool(40, 36, 36, 21, open_every=2), 2048
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=n, dataset=UserFloorMaps(maps), lidar_beam_count=8, device=gpu,
+                                          frozen_maps=False, max_episode_steps=2, array_backend=backend)
+    assert env.frozen_maps is False
+    ref = oracle_mod.OracleLidarVectorEnv(n, "pool", 0, False, 0, 8, step_limit=2, pool=maps)
+    to_np = (lambda x: x.cpu().numpy()) if backend == "torch" else (lambda x: x)
+    obs, _ = env.reset(seed=77)
+    ref.reset(77)
+    assert np.array_equal(to_np(obs["lidar"]), ref.lidar)
+    rng = np.random.default_rng(5)
+    for t in range(40):
+        a = rng.uniform(-2.5, 2.5, (n, 2)).astype(np.float32)
+        p = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        if backend == "torch":
+            obs, rew, term, trunc, info = env.step({"action": torch.as_tensor(a, device=gpu),
+                                                    "prediction": torch.as_tensor(p, device=gpu)})
+        else:
+            obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        ref.step(a, p)
+        _compare(env, ref, {k: to_np(v) for k, v in obs.items()}, to_np(rew), to_np(term), t, False)
+    env.close()
+
+
+def test_stream_static_map_of_a_huge_dataset(gpu, oracle_mod):
+    """static_map=True reads dataset[static_map_index] alone (lidar_localization2d.py:177-178): a static env over
+    the 2**32-map dataset builds in well under a second with one fetch and matches the oracle on that map."""
+    import time
+
+    import torch
+
+    import ap_gym_amd as ap
+    from stream_maps import rng_floor_map
+
+    ap.LIDARLocalization2DVectorEnv(num_envs=8, dataset=_stream_ds(), static_map=True, device=gpu).close()  # warm-up
+    torch.cuda.synchronize()
+    idx = 2**32 - 7
+    ds = _stream_ds()
+    t0 = time.perf_counter()
+    env = ap.LIDARLocalization2DVectorEnv(num_envs=1024, dataset=ds, static_map=True, static_map_index=idx,
+                                          lidar_beam_count=16, device=gpu)
+    built = time.perf_counter() - t0
+    assert built < 1.0 and ds.fetches == 1, (built, ds.fetches)
+    ref = oracle_mod.OracleLidarVectorEnv(1024, "pool", 0, True, 0, 16, pool=rng_floor_map(idx)[None])
+    obs, info = env.reset(seed=3)
+    ref.reset(3)
+    assert np.array_equal(obs["lidar"], ref.lidar)
+    assert np.all(info["map_idx"] == idx)
+    rng = np.random.default_rng(1)
+    for t in range(30):
+        a = rng.uniform(-1, 1, (1024, 2)).astype(np.float32)
+        p = rng.uniform(-1, 1, (1024, 2)).astype(np.float32)
+        obs, rew, term, trunc, info = env.step({"action": a, "prediction": p})
+        ref.step(a, p)
+        _compare(env, ref, obs, rew, term, t, True)
     env.close()

@@ -368,7 +368,7 @@ def test_torch_ops_library_registers_the_ops():
     for name in ("lidar_reset", "lidar_step", "image_reset", "image_step"):
         assert callable(getattr(ops, name)), name
     assert torch.classes.apgym.LidarEnv is not None and torch.classes.apgym.ImageEnv is not None
-    with pytest.raises(RuntimeError, match="15 ints"):
+    with pytest.raises(RuntimeError, match="16 ints"):
         torch.classes.apgym.LidarEnv([1], [0.0], [], [])
 
 
@@ -557,3 +557,121 @@ def test_numpy_float32_exp_log_restatement():
     a, b = np.array([1.0, 65536.0], f).view(np.uint32)
     x = np.arange(a, b + 1, 13, dtype=np.uint64).astype(np.uint32).view(f)
     assert np.array_equal(_np_log_restated(x).view(np.uint32), np.log(x).view(np.uint32))
+
+
+def test_procedural_subclasses_recognised_through_the_mro():
+    """A subclass of the reference's FloorMapDatasetRooms / FloorMapDatasetMaze that keeps get_data_point and the
+    2**32 length runs on the device generators with its parameters; one that overrides get_data_point (or the
+    length) is a foreign dataset read through ForeignFloorMapView.  Stand-ins carry the reference's class names,
+    module and private attributes (floor_map_dataset_rooms.py:10-24, floor_map_dataset_maze.py:10-22)."""
+    import ap_gym_amd as ap
+    from ap_gym_amd.floor_map import as_floor_map_dataset, procedural_equivalent
+
+    class FloorMapDatasetRooms:  # the reference's public surface, under its own module name
+        def __init__(self, width=32, height=32, max_rooms=10, door_width=3):
+            self.map_width, self.map_height = width, height
+            self._FloorMapDatasetRooms__max_rooms = max_rooms
+            self._FloorMapDatasetRooms__door_width = door_width
+
+        def __len__(self):
+            return 2**32
+
+        def get_data_point(self, idx):
+            raise AssertionError("the device generator must be used")
+
+    FloorMapDatasetRooms.__module__ = "ap_gym.envs.floor_map.floor_map_dataset_rooms"
+
+    class FloorMapDatasetMaze(FloorMapDatasetRooms):
+        def __init__(self, width=21, height=21, branching_prob=1.0):
+            super().__init__(width, height)
+            self._FloorMapDatasetMaze__branching_prob = branching_prob
+
+    FloorMapDatasetMaze.__module__ = "ap_gym.envs.floor_map.floor_map_dataset_maze"
+
+    class MyRooms(FloorMapDatasetRooms):  # a user subclass that only changes defaults
+        def __init__(self):
+            super().__init__(64, 64, max_rooms=7, door_width=2)
+
+    class MyMaps(FloorMapDatasetRooms):  # its own maps
+        def get_data_point(self, idx):
+            return np.zeros((self.map_height, self.map_width), bool)
+
+    class Finite(FloorMapDatasetRooms):  # a finite length changes the DatasetIterator's draws
+        def __len__(self):
+            return 1000
+
+    p = procedural_equivalent(MyRooms())
+    assert isinstance(p, ap.FloorMapDatasetRooms) and (p.map_width, p.max_rooms, p.door_width) == (64, 7, 2)
+    q = procedural_equivalent(FloorMapDatasetMaze(31, 31, 0.5))
+    assert isinstance(q, ap.FloorMapDatasetMaze) and q.branching_prob == 0.5 and q.map_height == 31
+    assert procedural_equivalent(MyMaps()) is None and procedural_equivalent(Finite()) is None
+    assert isinstance(as_floor_map_dataset(MyMaps()), ap.ForeignFloorMapView)
+    assert isinstance(as_floor_map_dataset(MyRooms()), ap.FloorMapDatasetRooms)
+
+    class NotReference(FloorMapDatasetRooms):
+        pass
+
+    NotReference.__module__ = "user_module"  # (the MRO still holds the reference class: recognised)
+    assert isinstance(procedural_equivalent(NotReference()), ap.FloorMapDatasetRooms)
+
+    class OwnGen(ap.FloorMapDatasetRooms):  # ap_gym_amd's own class with user maps
+        def get_data_point(self, idx, device=None):
+            return np.zeros((self.map_height, self.map_width), bool)
+
+    assert isinstance(as_floor_map_dataset(OwnGen(16, 16)), ap.ForeignFloorMapView)
+    assert isinstance(as_floor_map_dataset(ap.FloorMapDatasetRooms(16, 16)), ap.FloorMapDatasetRooms)
+
+
+def test_map_source_choice_and_static_pool():
+    """frozen_maps=None: datasets up to POOL_AUTO_MAPS maps (and POOL_AUTO_BYTES of bit rows) are read once into a
+    frozen pool, larger ones are streamed per episode; a static env reads dataset[static_map_index] alone."""
+    import ap_gym_amd as ap
+    from ap_gym_amd.floor_map import ForeignFloorMapView, pack_maps
+
+    class Big:
+        map_width = map_height = 40
+
+        def __init__(self, n):
+            self.n, self.fetched = n, []
+
+        def __len__(self):
+            return self.n
+
+        def get_data_point(self, idx):
+            self.fetched.append(int(idx))
+            m = np.zeros((40, 40), bool)
+            m[0] = True
+            return m
+
+    assert ForeignFloorMapView(Big(2**32)).prefers_streaming()
+    assert ForeignFloorMapView(Big(2**16 + 1)).prefers_streaming()
+    assert not ForeignFloorMapView(Big(1000)).prefers_streaming()
+    inner = Big(2**32)
+    occ, free = ForeignFloorMapView(inner).static_pool(2**32 - 3, "cpu")
+    assert inner.fetched == [2**32 - 3] and tuple(occ.shape) == (1, 40, 1) and int(free[0]) == 40 * 39
+    assert int(occ[0, 0, 0]) == (1 << 40) - 1 and int(occ[0, 1, 0]) == 0
+    bits, fr = np.zeros((1, 3, 8), np.uint8), np.zeros(1, np.int32)
+    with pytest.raises(ValueError, match="shape"):
+        pack_maps([np.zeros((4, 3), bool)], 3, 4, bits, fr)
+    with pytest.raises(TypeError, match="boolean"):
+        pack_maps([np.zeros((3, 4), np.uint8)], 3, 4, bits, fr)
+    with pytest.raises(ValueError, match="streamed"):
+        ap.ArrayFloorMapDataset.host_pool(ForeignFloorMapView(Big(2**31)))
+
+
+def test_device_u8_pools_are_padded_for_the_dword_taps():
+    """apgym_capi.h: the glimpse kernels read u8 taps with whole-dword loads up to APG_U8_POOL_PAD - 1 bytes past the
+    last image; a pool handed over as a tensor (a dataset's device_pool_tensors) is re-homed into a padded
+    allocation unless its storage already extends that far (CPU tensors stand in for device ones here)."""
+    import torch
+
+    from ap_gym_amd import _native as N
+    from ap_gym_amd.image_env import padded_device_pool_u8
+
+    pool = torch.arange(10 * 4 * 5 * 3, dtype=torch.int64).remainder(251).to(torch.uint8).reshape(10, 4, 5, 3)
+    padded = padded_device_pool_u8(pool)
+    assert padded is not pool and torch.equal(padded, pool)
+    assert padded.untyped_storage().nbytes() >= pool.numel() + N.APG_U8_POOL_PAD
+    assert padded_device_pool_u8(padded) is padded  # already padded: used as is
+    sliced = padded_device_pool_u8(torch.zeros(64, dtype=torch.uint8)[:48].view(2, 4, 6, 1))
+    assert sliced.untyped_storage().nbytes() == 64  # 16 spare bytes behind the view: kept

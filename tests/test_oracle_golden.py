@@ -24,6 +24,8 @@ ENV_CASES = {
     "pool48x40_b16": ("pool", 0, False, 16),
     "pool48x40_static_b8": ("pool", 0, True, 8),
     "pool36_open_b8": ("pool", 0, False, 8),
+    # a user FloorMapDataset of len 2**32, maps from default_rng(idx) (tests/stream_maps.py): fetched per draw
+    "stream40_b16": ("stream", 0, False, 16),
 }
 POOL_STATIC_INDEX = 5  # make_golden.make_pool's static_map_index
 
@@ -92,6 +94,11 @@ def test_vector_env_trace(oracle_mod, name):
     if kind == "pool":
         env = oracle_mod.OracleLidarVectorEnv(n, "pool", 0, static, POOL_STATIC_INDEX if static else 0, beams,
                                               pool=pool_maps(d))
+    elif kind == "stream":
+        from stream_maps import STREAM_LEN, rng_floor_map
+
+        env = oracle_mod.OracleLidarVectorEnv(n, "stream", 0, False, 0, beams, map_fn=rng_floor_map,
+                                              map_len=STREAM_LEN, map_hw=(40, 40))
     else:
         env = oracle_mod.OracleLidarVectorEnv(n, kind, size, static, 0, beams, sparse=sparse)
     env.reset(int(d["seed"]))
