@@ -31,6 +31,11 @@ Each sub-env steps, then its gather is issued at once (RCCL: asynchronously on R
 step's kernel only), so RCCL moves sub-batch h's rows while sub-batch h+1's step kernel runs; the current stream
 waits for every gather before step() returns.  Bit-identical to S = 1 (the sub-envs are the same envs, seeded by
 their global ids; image sub-envs draw the whole batch and keep their slice).  Actions are in local_env_ids order.
+`gather_lag=1` (LIDAR envs with packed rows) pipelines the all-gather instead: step(a_t) launches step t, snapshots its
+rows into one of two send buffers and issues their all-gather asynchronously into one of two receive buffers, then
+returns the gathered outputs of step t - 1 (None on the first step after a reset; flush() returns the last step's), so
+RCCL moves step t's rows while the caller works and step t + 1's kernel runs.  The outputs are those of gather=True
+shifted by one call.
 Envs without packed rows (e.g. test doubles) take the copying path (fields packed by copies, glimpses only with
 gather_glimpse=True).  Gathered tensors are views of the receive buffer, rewritten by the next step, unless the
 local env was built with copy=True (then they are cloned).
@@ -101,8 +106,13 @@ class ShardedVectorEnv:
 
     def __init__(self, make_local: Callable[..., object], num_envs_total: int, rank: int, world: int,
                  beams: int | None = None, gather: bool = False, group=None, gather_glimpse: bool = False,
-                 time_gather: bool = False, sub_batches: int = 1):
+                 time_gather: bool = False, sub_batches: int = 1, gather_lag: int = 0):
         self.rank, self.world, self.gather, self.group = rank, world, gather, group
+        self.gather_lag = int(gather_lag)
+        if self.gather_lag not in (0, 1):
+            raise ValueError("gather_lag must be 0 or 1")
+        if self.gather_lag and (not gather or sub_batches != 1):
+            raise ValueError("gather_lag=1 pipelines the all-gather: it needs gather=True and sub_batches=1")
         self.offset, self.local_num_envs = shard_bounds(num_envs_total, rank, world)
         self.num_envs = num_envs_total
         self.sub_batches = S = int(sub_batches)
@@ -134,6 +144,11 @@ class ShardedVectorEnv:
         self._inv_full = self._inv2_full = None  # randomly_invert_labels: gathered inversion flags / constant 2s
         self.time_gather = time_gather
         self.gather_events: list = []  # (begin, end) torch.cuda.Event pairs around each all-gather
+        if self.gather_lag and not (self._packed and self._lidar):
+            raise ValueError("gather_lag=1 needs LIDAR envs with packed output rows (make_local(packed_outputs=True))")
+        self._lag = None  # gather_lag: ([send] * 2, [recv] * 2, [views] * 2), allocated on the first step
+        self._pending = None  # gather_lag: (all-gather work or None, buffer index) of the last step
+        self._lag_t = 0
 
     # ------------------------------------------------------------------ collectives
     def _all_gather_into(self, recv, send, async_op: bool = False):
@@ -322,7 +337,50 @@ class ShardedVectorEnv:
         obs = {k: v[k] for k in ("glimpse", "glimpse_pos", "time_step", "target_glimpse") if k in v}
         return obs
 
+    # ------------------------------------------------------------------ gather_lag=1
+    def _lag_step(self, action):
+        """Step t, its rows' all-gather issued asynchronously; returns step t - 1's gathered outputs (None at first)."""
+        import torch
+
+        from .lidar_env import row_views
+
+        self.env.step(action)
+        rows = self.env.output_rows
+        if self._lag is None:
+            send = [torch.empty_like(rows) for _ in range(2)]
+            recv = [torch.zeros((self.num_envs, rows.shape[1]), dtype=torch.uint8, device=rows.device) for _ in range(2)]
+            self._lag = (send, recv, [row_views(r, self.env.output_layout) for r in recv])
+        send, recv, _ = self._lag
+        k = self._lag_t & 1
+        # the kernel of step t + 1 rewrites output_rows while this all-gather may still read: a snapshot is sent.
+        # send[k] / recv[k] are free: step t - 2's gather was waited for when step t - 1's call returned it
+        send[k].copy_(rows)
+        ev = self._timing_begin(rows)
+        work = self._all_gather_into(recv[k], send[k], async_op=True)
+        self._timing_end(ev)
+        prev, self._pending = self._pending, (work, k)
+        self._lag_t += 1
+        return None if prev is None else self._lag_result(prev)
+
+    def _lag_result(self, pend):
+        work, k = pend
+        if work is not None:
+            work.wait()  # (the current stream waits for RCCL's; no host synchronization)
+        v = self._lag[2][k]
+        if getattr(self.env, "copy", False):
+            v = {key: t.clone() for key, t in v.items()}
+        gobs = {"lidar": v["lidar"], "odometry": v["odometry"], "time_step": v["time_step"]}
+        info = self._packed_step_info(v, None)
+        del info["local_obs"]  # (the local buffers already hold the next step)
+        return gobs, v["reward"], v["terminated"], v["truncated"], info
+
+    def flush(self):
+        """gather_lag=1: the gathered outputs of the last step (None when none is pending)."""
+        pend, self._pending = self._pending, None
+        return None if pend is None else self._lag_result(pend)
+
     def reset(self, *, seed=None, options=None):
+        self._pending, self._lag_t = None, 0  # (gather_lag: a pending step's outputs are dropped with its episode)
         if self.sub_batches > 1:  # (lists of the sub-envs' local outputs below)
             outs = [e.reset(seed=seed, options=options) for e in self.envs]
             obs, info = [o[0] for o in outs], [o[1] for o in outs]
@@ -420,6 +478,8 @@ class ShardedVectorEnv:
         """`action` holds this rank's envs in local order (local_env_ids: with sub-batches, sub-batch 0's envs, then
         sub-batch 1's, ...).  Gathered outputs are in global env order; local_obs (and the image envs' per-step
         stats history) are per sub-batch lists with sub-batches."""
+        if self.gather_lag:
+            return self._lag_step(action)
         resetting = bool(getattr(self.env, "_prev_done", False))
         if self.sub_batches > 1:
             outs, v = self._split_step(action)

@@ -436,7 +436,7 @@ def run_lidar(args, world, rank, dev):
                             array_backend=args.array_backend, env_offset=env_offset, **kw)
 
     senv = ShardedVectorEnv(make_local, n_total, rank, world, beams, gather=args.gather, time_gather=True,
-                            sub_batches=args.sub_batches)
+                            sub_batches=args.sub_batches, gather_lag=args.gather_lag)
     env = senv.env
     ring = 128  # distinct synthetic action/prediction batches, cycled
     g = torch.Generator(device=dev).manual_seed(1 + rank)
@@ -473,6 +473,8 @@ def run_lidar(args, world, rank, dev):
     first_timed = steps_done + 1
     for t in range(args.steps):
         step()
+    if senv.gather_lag:  # (the last step's all-gather, returned one call late, is part of the window)
+        senv.flush()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -508,6 +510,8 @@ def run_lidar(args, world, rank, dev):
                 if t % args.event_every == args.event_every - 1 or t == EPISODE_PERIOD - 1]
         for t in range(EPISODE_PERIOD):
             step(ev.pair(args.steps + t) if t in ep_t else (None, None))
+        if senv.gather_lag:
+            senv.flush()
         torch.cuda.synchronize(dev)
         ep_s = time.perf_counter() - te
         env.set_kernel_timing_events(None)
@@ -567,8 +571,9 @@ def run_lidar(args, world, rank, dev):
                        "num_envs_total": n_total,
                        "beams": beams, "map": f"{msize}x{msize} {w['kind']}", "max_episode_steps": 100,
                        "reset_ms": reset_ms, "note": w["note"], "gather_ms": gather_ms if senv.gather else None,
-                       "packed_rows": bool(senv._packed),
-                       "parallelism": f"env-shard x{world}" + (" + all-gather" if senv.gather else "")},
+                       "packed_rows": bool(senv._packed), "gather_lag": senv.gather_lag,
+                       "parallelism": f"env-shard x{world}" + (" + all-gather" if senv.gather else "") + (
+                           " (pipelined: step t's batch returned with step t+1)" if senv.gather_lag else "")},
             "roofline": {"bound": bound, "bound_basis": basis, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_calibrated": traffic_cal,
@@ -675,9 +680,10 @@ def shard_plan(args, world: int) -> dict:
     return {"workload": name, "num_envs_per_gpu": n_local, "num_envs_total": n_local * world,
             "scaling": "strong" if "envs_total" in w else "weak", "row_bytes": row if args.gather else None,
             "gather_bytes_per_rank_step": row * n_local * (world - 1) if args.gather else 0,
-            "sub_batches": args.sub_batches,
+            "sub_batches": args.sub_batches, "gather_lag": args.gather_lag,
             "parallelism": f"env-shard x{world}" + (" + all-gather" if args.gather else "") + (
-                f" in {args.sub_batches} overlapped sub-batches" if args.sub_batches > 1 else "")}
+                f" in {args.sub_batches} overlapped sub-batches" if args.sub_batches > 1 else "") + (
+                " (pipelined: step t's batch returned with step t+1)" if args.gather_lag else "")}
 
 
 def run_dry(args, world, rank):
@@ -750,6 +756,9 @@ def main():
     ap.add_argument("--sub-batches", type=int, default=1,
                     help="with --gather: each rank's envs in S sub-batches whose all-gathers are issued right after "
                          "their steps, so RCCL gathers sub-batch h while sub-batch h+1 steps (ShardedVectorEnv)")
+    ap.add_argument("--gather-lag", type=int, default=0, choices=[0, 1],
+                    help="with --gather (LIDAR): 1 = pipelined all-gather, step t's gathered batch returned with step "
+                         "t+1's call (two send / receive buffers), so RCCL moves step t's rows while step t+1 runs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-episode", action="store_true", help="skip the one-episode measurement after the timed steps")
     ap.add_argument("--cpu-envs", type=int, default=None)
@@ -788,6 +797,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.sub_batches > 1 and not args.gather:
         raise SystemExit("--sub-batches overlaps the all-gather with the steps: it needs --gather")
+    if args.gather_lag and (not args.gather or args.sub_batches > 1 or args.workload in IMAGE_WORKLOADS):
+        raise SystemExit("--gather-lag 1 pipelines the LIDAR all-gather: it needs --gather and --sub-batches 1")
     if args.dry_run:
         return run_dry(args, world, rank)
     # one rank per GPU; with fewer visible GPUs than ranks (rehearsals with --dist-backend gloo) ranks share them

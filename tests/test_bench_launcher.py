@@ -72,6 +72,20 @@ def test_dry_run_eight_ranks_gather_in_sub_batches(workload, per_rank):
     assert cfg["parallelism"] == "env-shard x8 + all-gather in 2 overlapped sub-batches"
 
 
+def test_dry_run_eight_ranks_pipelined_gather():
+    """BASELINE config 2 at 8 ranks with the pipelined all-gather (--gather-lag 1: step t's batch returned with step
+    t+1's call): the same per-rank rows and traffic as the plain gather; the flag is refused without --gather."""
+    out = _run(["--gpus", "8", "--dry-run", "--workload", "lidar", "--gather", "--gather-lag", "1", "--steps", "2",
+                "--warmup", "0"], 300)
+    cfg = out["config"]
+    assert out["n_gpus"] == 8 and cfg["gather_lag"] == 1 and cfg["num_envs_per_gpu"] == 65536
+    assert cfg["gather_bytes_per_rank_step"] == 7 * 65536 * cfg["row_bytes"]
+    assert cfg["parallelism"] == "env-shard x8 + all-gather (pipelined: step t's batch returned with step t+1)"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--gather-lag", "1"],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and "needs --gather" in p.stderr
+
+
 def test_dry_run_rejects_an_uneven_split():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--workload", "maze127",
                         "--gpus", "1"], capture_output=True, text=True, timeout=120, cwd=ROOT,

@@ -106,7 +106,7 @@ def test_shards_union_equals_unsharded(gpu, kind):
     torch.cuda.synchronize()
 
 
-def _worker(rank, world, port, kind, outdir, backend="gloo", sub=1):
+def _worker(rank, world, port, kind, outdir, backend="gloo", sub=1, lag=0):
     import torch
     import torch.distributed as dist
 
@@ -120,7 +120,7 @@ def _worker(rank, world, port, kind, outdir, backend="gloo", sub=1):
 
     senv = ShardedVectorEnv(lambda num_envs, env_offset, **kw: _make(kind, num_envs, env_offset, N_TOTAL, **kw),
                             N_TOTAL, rank, world, beams=16 if kind == "lidar" else None, gather=True,
-                            gather_glimpse=True, sub_batches=sub)
+                            gather_glimpse=True, sub_batches=sub, gather_lag=lag)
     assert senv._packed  # the step kernels write the all-gather's send rows (LIDAR and image envs)
     ids = torch.as_tensor(senv.local_env_ids, device="cuda:0")
     obs0, info0 = senv.reset(seed=5)
@@ -130,7 +130,15 @@ def _worker(rank, world, port, kind, outdir, backend="gloo", sub=1):
         rows[-1]["map_idx"] = info0["map_idx"].cpu().numpy().copy()
     for t in range(_steps(kind)):
         a, p = _actions(kind, t, N_TOTAL)
-        obs, rew, term, trunc, info = senv.step({"action": a[ids], "prediction": p[ids]})
+        out = senv.step({"action": a[ids], "prediction": p[ids]})
+        if lag:  # the pipelined gather: step t's call returns step t - 1's batch (None first)
+            assert (out is None) == (t == 0)
+            if out is None:
+                continue
+        obs, rew, term, trunc, info = out
+        rows.append(_flat(kind, obs, rew, term, info))
+    if lag:
+        obs, rew, term, trunc, info = senv.flush()
         rows.append(_flat(kind, obs, rew, term, info))
     torch.cuda.synchronize()
     np.savez(os.path.join(outdir, f"rank{rank}.npz"),
@@ -159,15 +167,17 @@ def test_two_rank_gather_on_gpu_equals_unsharded(gpu, kind, tmp_path):
                 assert np.array_equal(got[r][f"{t}_{k}"], v), f"rank {r} step {t}: {k}"
 
 
-@pytest.mark.parametrize("kind,sub", [("lidar", 1), ("image", 1), ("image_cls_inv", 1), ("lidar", 2), ("image", 2)])
-def test_rccl_gather_branch_single_rank(gpu, kind, sub, tmp_path):
+@pytest.mark.parametrize("kind,sub,lag", [("lidar", 1, 0), ("image", 1, 0), ("image_cls_inv", 1, 0), ("lidar", 2, 0),
+                                          ("image", 2, 0), ("lidar", 1, 1)])
+def test_rccl_gather_branch_single_rank(gpu, kind, sub, lag, tmp_path):
     """The RCCL branch of ShardedVectorEnv._all_gather_rows (dist.all_gather_into_tensor on the device rows;
     sharding.py) on a one-rank "nccl" group: RCCL refuses two ranks on one device, so this is the only way
     one GPU runs that branch.  The gathered batch must equal the unsharded env.  sub = 2: two sub-batches whose
-    all-gathers are issued asynchronously right after their steps (RCCL's stream overlaps the next step kernel)."""
+    all-gathers are issued asynchronously right after their steps (RCCL's stream overlaps the next step kernel).
+    lag = 1: the pipelined gather (gather_lag=1), the same batches one call late."""
     import torch.multiprocessing as mp
 
-    mp.start_processes(_worker, args=(1, _free_port(), kind, str(tmp_path), "nccl", sub), nprocs=1, join=True,
+    mp.start_processes(_worker, args=(1, _free_port(), kind, str(tmp_path), "nccl", sub, lag), nprocs=1, join=True,
                        start_method="spawn")
     ref = _reference(kind, with_reset=kind == "lidar")
     got = np.load(tmp_path / "rank0.npz")

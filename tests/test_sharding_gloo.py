@@ -82,31 +82,36 @@ def _actions():
             rng.uniform(-1, 1, (STEPS, N_TOTAL, 2)).astype(np.float32))
 
 
-def _worker(rank, world, port, outdir, packed=False, sub=1):
+def _worker(rank, world, port, outdir, packed=False, sub=1, lag=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from ap_gym_amd.sharding import ShardedVectorEnv
 
     make = _PackedOracleShard if packed else (lambda num_envs, env_offset: _OracleShard(num_envs, env_offset))
-    senv = ShardedVectorEnv(make, N_TOTAL, rank, world, BEAMS, gather=True, sub_batches=sub)
+    senv = ShardedVectorEnv(make, N_TOTAL, rank, world, BEAMS, gather=True, sub_batches=sub, gather_lag=lag)
     assert senv._packed == packed and len(senv.envs) == sub
     acts, preds = _actions()
     ids = senv.local_env_ids  # sub-batches: rank r owns [(h*W + r)*m, +m) for each h
     assert len(ids) == senv.local_num_envs and (sub > 1 or ids[0] == senv.offset)
     senv.reset(seed=7)
     rows = []
+
+    def row(out):  # the gathered batch as bytes (the packed path's views are rewritten by the next call)
+        obs, rew, term, trunc, info = out
+        parts = [obs["lidar"], obs["odometry"], obs["time_step"], rew, info["base_reward"],
+                 info["prediction"]["target"], info["prediction"]["loss"], term, trunc, info["_base_reward"]]
+        return np.concatenate([np.ascontiguousarray(x.numpy()).view(np.uint8).ravel() for x in parts])
+
     for t in range(STEPS):
-        obs, rew, term, trunc, info = senv.step({"action": torch.from_numpy(acts[t, ids]),
-                                                 "prediction": torch.from_numpy(preds[t, ids])})
-        rows.append(np.concatenate([np.ascontiguousarray(obs["lidar"].numpy()).view(np.uint8).ravel(),
-                                    np.ascontiguousarray(obs["odometry"].numpy()).view(np.uint8).ravel(),
-                                    np.ascontiguousarray(obs["time_step"].numpy()).view(np.uint8).ravel(),
-                                    np.ascontiguousarray(rew.numpy()).view(np.uint8).ravel(),
-                                    np.ascontiguousarray(info["base_reward"].numpy()).view(np.uint8).ravel(),
-                                    np.ascontiguousarray(info["prediction"]["target"].numpy()).view(np.uint8).ravel(),
-                                    np.ascontiguousarray(info["prediction"]["loss"].numpy()).view(np.uint8).ravel(),
-                                    np.ascontiguousarray(term.numpy()).view(np.uint8).ravel(), np.ascontiguousarray(trunc.numpy()).view(np.uint8).ravel(),
-                                    np.ascontiguousarray(info["_base_reward"].numpy()).view(np.uint8).ravel()]))
+        out = senv.step({"action": torch.from_numpy(acts[t, ids]), "prediction": torch.from_numpy(preds[t, ids])})
+        if lag:  # step t's call returns step t - 1's gathered batch (None first); flush() the last one
+            assert (out is None) == (t == 0)
+            if out is None:
+                continue
+        rows.append(row(out))
+    if lag:
+        rows.append(row(senv.flush()))
+        assert senv.flush() is None
     np.save(os.path.join(outdir, f"rank{rank}.npy"), np.stack(rows))
     senv.close()
     dist.destroy_process_group()
@@ -153,14 +158,21 @@ def test_sub_batch_layout_and_checks():
     with pytest.raises(ValueError, match="packed"):
         ShardedVectorEnv(lambda num_envs, env_offset: make(num_envs, env_offset), 16, 0, 2, BEAMS, gather=True,
                          sub_batches=2)
+    with pytest.raises(ValueError, match="gather=True"):
+        ShardedVectorEnv(make, 16, 0, 2, BEAMS, gather=False, gather_lag=1)
+    with pytest.raises(ValueError, match="sub_batches=1"):
+        ShardedVectorEnv(make, 16, 0, 2, BEAMS, gather=True, sub_batches=2, gather_lag=1)
+    with pytest.raises(ValueError, match="0 or 1"):
+        ShardedVectorEnv(make, 16, 0, 2, BEAMS, gather=True, gather_lag=2)
 
 
-@pytest.mark.parametrize("packed,sub", [(False, 1), (True, 1), (True, 2), (True, 4)],
-                         ids=["copying", "packed_rows", "packed_rows_2sub", "packed_rows_4sub"])
-def test_two_rank_gather_equals_unsharded(tmp_path, oracle_mod, packed, sub):
+@pytest.mark.parametrize("packed,sub,lag", [(False, 1, 0), (True, 1, 0), (True, 2, 0), (True, 4, 0), (True, 1, 1)],
+                         ids=["copying", "packed_rows", "packed_rows_2sub", "packed_rows_4sub", "packed_rows_lag1"])
+def test_two_rank_gather_equals_unsharded(tmp_path, oracle_mod, packed, sub, lag):
     """sub > 1: each rank's envs in sub-batches whose all-gathers are issued right after their steps (overlapping
-    the next sub-batch's step on RCCL); the gathered batch is still in global env order."""
-    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), packed, sub), nprocs=2, join=True,
+    the next sub-batch's step on RCCL); the gathered batch is still in global env order.  lag = 1: the pipelined
+    gather (step t's call returns step t - 1's batch, flush() the last): the same batches shifted by one call."""
+    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), packed, sub, lag), nprocs=2, join=True,
                        start_method="spawn")
     r0, r1 = np.load(tmp_path / "rank0.npy"), np.load(tmp_path / "rank1.npy")
     assert np.array_equal(r0, r1)  # every rank holds the full batch
