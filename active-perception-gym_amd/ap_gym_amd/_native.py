@@ -39,6 +39,7 @@ APG_IMAGE_CLASSIFY = 0
 APG_IMAGE_LOCALIZE = 1
 APG_POOL_U8 = 0
 APG_POOL_F32 = 1
+APG_POOL_U8_TILED = 2  # RGBX in 8 x 4-pixel 128-byte tiles (apgym_capi.h)
 APG_U8_POOL_PAD = 16  # readable bytes after a u8 image pool (apgym_capi.h)
 APG_DS_CIRCLE_SQUARE = 0
 APG_DS_DOUBLE_CIRCLE_SQUARE = 1

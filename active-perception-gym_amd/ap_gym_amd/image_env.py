@@ -88,6 +88,40 @@ def device_pool_u8(pool: np.ndarray, dev):
     return buf[:nb].view(pool.shape)
 
 
+def tiled_pool_bytes(h: int, w: int) -> int:
+    """Bytes of one image of an APG_POOL_U8_TILED pool (apgym_capi.h): ceil(H/4) x ceil(W/8) tiles of 128 bytes."""
+    return ((h + 3) // 4) * ((w + 7) // 8) * 128
+
+
+def use_tiled_pools() -> bool:
+    """RGB u8 pools go to the device as RGBX 8 x 4-pixel tiles (APG_POOL_U8_TILED) unless APG_IMAGE_TILED=0 (A/B)."""
+    import os
+
+    return os.environ.get("APG_IMAGE_TILED", "1") != "0"
+
+
+def device_pool_u8_tiled(pool: np.ndarray, dev, chunk: int = 4096):
+    """An RGB uint8 pool [M, H, W, 3] laid out on `dev` as APG_POOL_U8_TILED: pixel (y, x) of image m at byte
+    m * img + (y // 4) * ceil(W/8) * 128 + (x // 8) * 128 + (y % 4) * 32 + (x % 8) * 4 + channel (the 4th byte 0),
+    re-tiled on the device in chunks of images; N.APG_U8_POOL_PAD spare bytes after the last image.  Returned as the
+    flat byte tensor of the M images (the kernels address it through apg_image_config.pool_dtype)."""
+    import torch
+
+    m, h, w, c = pool.shape
+    assert c == 3 and pool.dtype == np.uint8
+    th, tw = (h + 3) // 4, (w + 7) // 8
+    img = th * tw * 128
+    buf = torch.zeros(m * img + N.APG_U8_POOL_PAD, dtype=torch.uint8, device=dev)
+    for lo in range(0, m, chunk):
+        hi = min(m, lo + chunk)
+        src = torch.from_numpy(np.ascontiguousarray(pool[lo:hi])).to(dev)
+        padded = torch.zeros((hi - lo, th * 4, tw * 8, 4), dtype=torch.uint8, device=dev)
+        padded[:, :h, :w, :3] = src
+        tiles = padded.view(hi - lo, th, 4, tw, 8, 4).permute(0, 1, 3, 2, 4, 5).reshape(-1)
+        buf[lo * img:hi * img].copy_(tiles)
+    return buf[:m * img]
+
+
 def padded_device_pool_u8(pool_t):
     """A device uint8 pool (e.g. from a dataset's device_pool_tensors) as the glimpse kernels need it: contiguous with
     N.APG_U8_POOL_PAD readable bytes after the last image in its own allocation (apgym_capi.h).  The tensor itself
@@ -193,7 +227,7 @@ class _ImageVectorEnv(VectorEnv):
         ds.load()
         if hasattr(ds, "device_pool_tensors"):  # procedural datasets render their pool on the device
             pool_t, labels_t = ds.device_pool_tensors(self.device)
-            pool = None
+            pool, pool_tiled = None, False
             pool_is_u8 = pool_t.dtype == torch.uint8
             if pool_is_u8:  # the kernels' dword tap loads read up to APG_U8_POOL_PAD - 1 bytes past the last image
                 pool_t = padded_device_pool_u8(pool_t)
@@ -201,15 +235,17 @@ class _ImageVectorEnv(VectorEnv):
             # one upload per dataset and device, shared by every env built on it (ShardedVectorEnv's sub-batches, a
             # train and an eval env): the pool is read-only on the device
             cache = ds.__dict__.setdefault("_apg_device_pools", {}) if hasattr(ds, "__dict__") else {}
-            key = str(self.device)
+            key = (str(self.device), use_tiled_pools())
             if key not in cache:
                 pool, labels = ds.device_pool()
-                cache[key] = (device_pool_u8(pool, self.device) if pool.dtype == np.uint8
+                tiled = key[1] and pool.dtype == np.uint8 and pool.shape[-1] == 3
+                cache[key] = (device_pool_u8_tiled(pool, self.device) if tiled else
+                              device_pool_u8(pool, self.device) if pool.dtype == np.uint8
                               else torch.from_numpy(np.ascontiguousarray(pool)).to(self.device),
-                              torch.from_numpy(np.ascontiguousarray(labels)).to(self.device), pool)
-            pool_t, labels_t, pool = cache[key]
+                              torch.from_numpy(np.ascontiguousarray(labels)).to(self.device), pool, tiled)
+            pool_t, labels_t, pool, pool_tiled = cache[key]
             pool_is_u8 = pool_t.dtype == torch.uint8
-        m, h, w, pc = pool_t.shape
+        m, h, w, pc = pool.shape if pool_tiled else pool_t.shape
         c = int(ds.num_channels)
         if c not in (1, 3):
             raise ValueError(f"Target channels must be either 1 or 3 but is {c}.")
@@ -264,7 +300,8 @@ class _ImageVectorEnv(VectorEnv):
             mse_scale, mse_offset = affine_f32(inner_loss)
         self._cfg = N.ImageConfig(
             num_envs=n, kind=self.kind, height=h, width=w, pool_channels=pc, channels=c,
-            pool_dtype=N.APG_POOL_U8 if pool_is_u8 else N.APG_POOL_F32, sensor_h=s0, sensor_w=s1,
+            pool_dtype=(N.APG_POOL_U8_TILED if pool_tiled else N.APG_POOL_U8 if pool_is_u8 else N.APG_POOL_F32),
+            sensor_h=s0, sensor_w=s1,
             step_limit=int(cfg.step_limit), num_classes=k, invert_labels=int(bool(cfg.randomly_invert_labels)),
             top_k=int(cfg.unique_sampling_top_k), unique_points=int(grid.shape[0]), num_envs_total=nt,
             env_offset=self.env_offset, pool_len=m,

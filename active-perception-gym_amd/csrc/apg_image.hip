@@ -37,7 +37,9 @@ struct GlimpseGeo {
   double lim_x, lim_y;  // sensor_pos_lim_pixels (x first, like the reference)
   double scale, cy, cx;  // grid centres (h - 1) / 2, (w - 1) / 2
   int pool_f32;
-  int64_t img_elems;     // h * w * pc
+  int tiled;             // APG_POOL_U8_TILED: RGBX pixels in 8 x 4-pixel 128-byte tiles
+  int64_t trow;          // tiled: bytes per row of tiles, ceil(w / 8) * 128
+  int64_t img_elems;     // h * w * pc (tiled: ceil(h / 4) * trow bytes)
   int64_t pitch;         // output floats per glimpse unit: s0 * s1 * c (dense), out_row_bytes / 4 (packed env rows)
 };
 
@@ -56,7 +58,9 @@ GlimpseGeo make_geo(const apg_image_config *c) {
   g.cy = ((double)c->height - 1.0) / 2.0;
   g.cx = ((double)c->width - 1.0) / 2.0;
   g.pool_f32 = c->pool_dtype == APG_POOL_F32;
-  g.img_elems = (int64_t)c->height * c->width * c->pool_channels;
+  g.tiled = c->pool_dtype == APG_POOL_U8_TILED;
+  g.trow = (int64_t)((c->width + 7) / 8) * 128;
+  g.img_elems = g.tiled ? (int64_t)((c->height + 3) / 4) * g.trow : (int64_t)c->height * c->width * c->pool_channels;
   g.pitch = (int64_t)c->sensor_h * c->sensor_w * c->channels;
   return g;
 }
@@ -103,9 +107,16 @@ APG_DEV void load_u8_table(float *lut) {
   __syncthreads();
 }
 
+// byte offsets of image row y / column x in a tiled pool (APG_POOL_U8_TILED): separable, pixel = row_off + col_off
+APG_DEV int64_t tile_row_off(const GlimpseGeo &g, int y) { return (int64_t)(y >> 2) * g.trow + ((y & 3) << 5); }
+APG_DEV int tile_col_off(int x) { return ((x >> 3) << 7) + ((x & 7) << 2); }
+
 APG_DEV float pool_value(const GlimpseGeo &g, const void *pool, const float *lut, int64_t base, int y, int x, int ch) {
-  const int64_t i = base + (int64_t)((y * g.w + x) * g.pc + (g.pc == 1 ? 0 : ch));
-  return g.pool_f32 ? static_cast<const float *>(pool)[i] : lut[static_cast<const uint8_t *>(pool)[i]];
+  const int64_t i = g.tiled ? base + tile_row_off(g, y) + tile_col_off(x) + ch
+                            : base + (int64_t)((y * g.w + x) * g.pc + (g.pc == 1 ? 0 : ch));
+  if (g.pool_f32) return static_cast<const float *>(pool)[i];
+  const uint32_t v = static_cast<const uint8_t *>(pool)[i];
+  return APG_U8_ARITH ? u8_value_f32(v) : lut[v];  // (random table reads conflict on the LDS banks)
 }
 
 // grid interval of v on the unit grid k - c (k = 0..n-1): g[i] <= v < g[i+1], clipped to [0, n-2]
@@ -438,9 +449,9 @@ FastDiv make_fastdiv(uint32_t d) {
   return f;
 }
 
-struct Axis {  // one sampling coordinate: pool offset of its grid interval (rows: idx * w * pc, columns:
-  int off;      // idx * pc), fractional weight, 1 - weight
-  double w, nw;
+struct Axis {     // one sampling coordinate: pool offsets of its grid interval's two ends (rows: idx * w * pc and
+  int off, off1;  // (idx + 1) * w * pc, columns: idx * pc and (idx + 1) * pc; tiled pools: tile_row_off /
+  double w, nw;   // tile_col_off of idx and idx + 1), fractional weight, 1 - weight
 };
 
 // Separable glimpse of `nu` units (env x position) starting at unit u0, in two passes over a workgroup:
@@ -462,7 +473,14 @@ APG_DEV uint32_t gs_axes(const GlimpseGeo &g, const int64_t *index, PosAt pos_at
     const double lim = row ? g.cy : g.cx;
     if (!(c >= -lim && c <= lim)) bad |= row ? APG_ERR_OOB_Y : APG_ERR_OOB_X;
     Axis ax;
-    ax.off = grid_interval(c, lim, row ? g.h : g.w, ax.w) * (row ? g.w * g.pc : g.pc);
+    const int iv = grid_interval(c, lim, row ? g.h : g.w, ax.w);
+    if (g.tiled) {
+      ax.off = row ? (int)tile_row_off(g, iv) : tile_col_off(iv);
+      ax.off1 = row ? (int)tile_row_off(g, iv + 1) : tile_col_off(iv + 1);
+    } else {
+      ax.off = iv * (row ? g.w * g.pc : g.pc);
+      ax.off1 = ax.off + (row ? g.w * g.pc : g.pc);
+    }
     ax.nw = __dsub_rn(1.0, ax.w);
     s_ax[q] = ax;
     if (k == 0 && index) s_base[u] = index[(u0 + u) / npos] * g.img_elems;  // index == nullptr: s_base is set
@@ -481,7 +499,7 @@ struct U8Taps {
 #define APG_TAPS_WIDE 1  // (0: the per-dword tap loads of round 4, A/B knob)
 #endif
 
-template <bool F32, int PC, int C, int GT = GS_THREADS>
+template <bool F32, int PC, int C, int GT = GS_THREADS, bool TILED = false>
 APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, FastDiv per_div, FastDiv s1_div,
                          const Axis *s_ax, const int64_t *s_base, const float *s_lut, float *out) {
   const int side = g.s0 + g.s1;
@@ -510,7 +528,35 @@ APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, 
       __builtin_nontemporal_store(res[0], dst);  // the glimpses are read by the consumer, not by this kernel
     }
   };
-  if constexpr (F32) {
+  if constexpr (TILED) {
+    // RGBX tiles (APG_POOL_U8_TILED): each tap one aligned dword, its channels at fixed byte positions; the four
+    // taps from the axes' two row and two column offsets (a tap pair may straddle a tile edge)
+    static_assert(PC == 3 && C == 3, "tiled pools are RGB");
+    const uint8_t *im = static_cast<const uint8_t *>(pool);
+    for (int q = threadIdx.x; q < total; q += GT) {
+      int u, i, j;
+      coords(q, u, i, j);
+      const Axis ay = s_ax[u * side + i], axx = s_ax[u * side + g.s0 + j];
+      const uint8_t *b = im + s_base[u];
+      const uint32_t t00 = *reinterpret_cast<const uint32_t *>(b + (ay.off + axx.off)),
+                     t01 = *reinterpret_cast<const uint32_t *>(b + (ay.off + axx.off1)),
+                     t10 = *reinterpret_cast<const uint32_t *>(b + (ay.off1 + axx.off)),
+                     t11 = *reinterpret_cast<const uint32_t *>(b + (ay.off1 + axx.off1));
+      double w00, w01, w10, w11;
+      weights(ay, axx, w00, w01, w10, w11);
+      auto tap = [&](uint32_t t, int ch) { return u8_value_f32((t >> (8 * ch)) & 0xffu); };
+      float res[3];
+#pragma unroll
+      for (int ch = 0; ch < 3; ch++) {
+        double v = __dmul_rn((double)tap(t00, ch), w00);
+        v = __dadd_rn(v, __dmul_rn((double)tap(t01, ch), w01));
+        v = __dadd_rn(v, __dmul_rn((double)tap(t10, ch), w10));
+        v = __dadd_rn(v, __dmul_rn((double)tap(t11, ch), w11));
+        res[ch] = (float)fmin(v, 1.0);
+      }
+      store(q, u, res);
+    }
+  } else if constexpr (F32) {
     const float *im = static_cast<const float *>(pool);
     for (int q = threadIdx.x; q < total; q += GT) {
       int u, i, j;
@@ -606,7 +652,9 @@ APG_DEV void gs_pixels_t(const GlimpseGeo &g, const void *pool, int u0, int nu, 
 APG_DEV void gs_pixels(const GlimpseGeo &g, const void *pool, int u0, int nu, FastDiv per_div, FastDiv s1_div,
                        const Axis *s_ax, const int64_t *s_base, const float *s_lut, float *out) {
 #define APG_GS_PIXELS(F, P, C) gs_pixels_t<F, P, C>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out)
-  if (g.pool_f32) {
+  if (g.tiled) {
+    gs_pixels_t<false, 3, 3, GS_THREADS, true>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out);
+  } else if (g.pool_f32) {
     if (g.pc == 3) APG_GS_PIXELS(true, 3, 3);
     else if (g.c == 3) APG_GS_PIXELS(true, 1, 3);
     else APG_GS_PIXELS(true, 1, 1);
@@ -1089,7 +1137,7 @@ APG_DEV void cls1_env(const EnvArgs &a, int e, float *row, const EnvIn &in, doub
 #define APG_FUSED_MIN_WAVES 8  // <= 64 VGPRs: every workgroup of the grid resident at once
 #endif
 constexpr int ENV_WAVE = 64;
-template <int KIND, bool F32, int PC, int C, bool ENVW, int GT = GS_THREADS>
+template <int KIND, bool F32, int PC, int C, bool ENVW, int GT = GS_THREADS, bool TILED = false>
 __global__ __launch_bounds__(ENVW ? GT + ENV_WAVE : GT)
 __attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fused(EnvArgs a, GlimpseGeo g, const void *pool, const int64_t *index, const float *__restrict__ act,
                    const float *__restrict__ pred, const int32_t *label, double *pos, apg_image_outputs out,
@@ -1157,7 +1205,7 @@ __attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fuse
     const uint32_t bad =
         gs_axes<GT>(g, nullptr, [&](int u, int c) { return s_npos[u][c]; }, u0, nu, 1, side_div, s_ax, s_base);
     __syncthreads();
-    gs_pixels_t<F32, PC, C, GT>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
+    gs_pixels_t<F32, PC, C, GT, TILED>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
     if (bad) atomicOr(out.err, bad);
   } else {
     if (!APG_U8_ARITH) for (int v = tid; v < 256; v += GT) s_lut[v] = u8_value((unsigned)v);
@@ -1168,7 +1216,7 @@ __attribute__((amdgpu_waves_per_eu(APG_FUSED_MIN_WAVES))) void k_image_step_fuse
     const uint32_t bad =
         gs_axes<GT>(g, nullptr, [&](int u, int c) { return s_npos[u][c]; }, u0, nu, 1, side_div, s_ax, s_base);
     __syncthreads();
-    gs_pixels_t<F32, PC, C, GT>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
+    gs_pixels_t<F32, PC, C, GT, TILED>(g, pool, u0, nu, per_div, s1_div, s_ax, s_base, s_lut, out.glimpse);
     env_step(tid, in);
     if (bad) atomicOr(out.err, bad);
   }
@@ -1347,7 +1395,11 @@ __global__ __launch_bounds__(UQ_THREADS, 3) void k_unique_blk(GlimpseGeo g, cons
 #pragma unroll
             for (int rr = 0; rr < NPASS; rr++) {
               const int r = r0 + RPASS * rr;
-              if (c < ln) *reinterpret_cast<f4 *>(s_dyn + r * ls + c) = v[rr];
+              // 16-byte aligned (ls and c are multiples of 4): one ds_write_b128 per row piece, 8 lanes per 128 B;
+              // without the assumption the store splits into ds_write2_b32 pairs whose lanes (4 dwords apart)
+              // meet on every fourth bank
+              f4 *dst = static_cast<f4 *>(__builtin_assume_aligned(s_dyn + r * ls + c, 16));
+              if (c < ln) *dst = v[rr];
             }
           }
           __syncthreads();
@@ -1573,6 +1625,10 @@ int validate(const apg_image_config *c) {
   if (c->channels != 1 && c->channels != 3) return fail(APG_E_INVALID, "Target channels must be either 1 or 3");
   if (c->pool_channels == 3 && c->channels == 1)
     return fail(APG_E_INVALID, "Invalid image format. Expected 1 channels but got 3");
+  if (c->pool_dtype != APG_POOL_U8 && c->pool_dtype != APG_POOL_F32 && c->pool_dtype != APG_POOL_U8_TILED)
+    return fail(APG_E_INVALID, "unknown pool_dtype");
+  if (c->pool_dtype == APG_POOL_U8_TILED && c->pool_channels != 3)
+    return fail(APG_E_INVALID, "tiled pools (APG_POOL_U8_TILED) hold RGB images (pool_channels 3)");
   if (c->sensor_h <= 0 || c->sensor_w <= 0) return fail(APG_E_INVALID, "sensor size must be positive");
   if ((int64_t)c->sensor_h * c->sensor_w * c->channels > MAX_PW_N)
     return fail(APG_E_INVALID, "glimpse too large");
@@ -1988,29 +2044,33 @@ int apg_image_step(const apg_image_config *c, const apg_image_state *st, const f
     // results do not depend on it)
     const dim3 block_e((gt448 ? 448 : GS_THREADS) + ENV_WAVE);
     // one instance per env kind and pool format (u8 / f32, pool channels, glimpse channels)
-#define APG_FUSED(K, F, P, C)                                                                                    \
+#define APG_FUSED(K, F, P, C, TL)                                                                                \
   do {                                                                                                           \
     if (envw && gt448)                                                                                           \
-      hipLaunchKernelGGL((k_image_step_fused<K, F, P, C, true, 448>), grid, block_e, dyn, s, a, g, st->pool,     \
+      hipLaunchKernelGGL((k_image_step_fused<K, F, P, C, true, 448, TL>), grid, block_e, dyn, s, a, g, st->pool, \
                          st->index, action, prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, sd, sid, \
                          kd);                                                                                    \
     else if (envw)                                                                                               \
-      hipLaunchKernelGGL((k_image_step_fused<K, F, P, C, true>), grid, block_e, dyn, s, a, g, st->pool, st->index, \
-                         action, prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, sd, sid, kd);    \
+      hipLaunchKernelGGL((k_image_step_fused<K, F, P, C, true, GS_THREADS, TL>), grid, block_e, dyn, s, a, g,    \
+                         st->pool, st->index, action, prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, \
+                         sd, sid, kd);                                                                           \
     else                                                                                                         \
-      hipLaunchKernelGGL((k_image_step_fused<K, F, P, C, false>), grid, block, dyn, s, a, g, st->pool, st->index,\
-                         action, prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, sd, sid, kd);    \
+      hipLaunchKernelGGL((k_image_step_fused<K, F, P, C, false, GS_THREADS, TL>), grid, block, dyn, s, a, g,     \
+                         st->pool, st->index, action, prediction, st->label, st->pos, *out, st->stats_hist, upb, pd, \
+                         sd, sid, kd);                                                                           \
   } while (0)
 #define APG_FUSED_KIND(K)                                   \
   do {                                                      \
-    if (g.pool_f32) {                                       \
-      if (g.pc == 3) APG_FUSED(K, true, 3, 3);              \
-      else if (g.c == 3) APG_FUSED(K, true, 1, 3);          \
-      else APG_FUSED(K, true, 1, 1);                        \
+    if (g.tiled) {                                          \
+      APG_FUSED(K, false, 3, 3, true);                      \
+    } else if (g.pool_f32) {                                \
+      if (g.pc == 3) APG_FUSED(K, true, 3, 3, false);       \
+      else if (g.c == 3) APG_FUSED(K, true, 1, 3, false);   \
+      else APG_FUSED(K, true, 1, 1, false);                 \
     } else {                                                \
-      if (g.pc == 3) APG_FUSED(K, false, 3, 3);             \
-      else if (g.c == 3) APG_FUSED(K, false, 1, 3);         \
-      else APG_FUSED(K, false, 1, 1);                       \
+      if (g.pc == 3) APG_FUSED(K, false, 3, 3, false);      \
+      else if (g.c == 3) APG_FUSED(K, false, 1, 3, false);  \
+      else APG_FUSED(K, false, 1, 1, false);                \
     }                                                       \
   } while (0)
     if (c->kind == APG_IMAGE_LOCALIZE) APG_FUSED_KIND(APG_IMAGE_LOCALIZE);

@@ -877,6 +877,9 @@ __device__ unsigned long long g_step_prof[16384][16];
 #ifndef APG_SLIDE_SPLIT
 #define APG_SLIDE_SPLIT 1  // phase 1: second slide scan on the idle waves (0: both on the env's lane; A/B 36.4 -> 35.8 us)
 #endif
+#ifndef APG_MAPOBS_NT
+#define APG_MAPOBS_NT 1  // the fused rooms autoreset's f32 map obs as non-temporal 16-byte stores (0: plain; A/B knob)
+#endif
 #ifndef APG_STEP_MIN_WAVES
 #define APG_STEP_MIN_WAVES 4  // keep k_lidar_step at <= 128 VGPRs: 4 waves per SIMD
 #endif
@@ -1307,7 +1310,11 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
               v.y = (bits & 2u) ? wall : 0.0f;
               v.z = (bits & 4u) ? wall : 0.0f;
               v.w = (bits & 8u) ? wall : 0.0f;
+#if APG_MAPOBS_NT
               __builtin_nontemporal_store(v, reinterpret_cast<f4 *>(mo) + k4);
+#else
+              reinterpret_cast<f4 *>(mo)[k4] = v;
+#endif
             }
           } else if (O.map_obs) {
             float *mo = O.map_obs + (size_t)e * m * P.w;

@@ -306,6 +306,12 @@ int apg_rng_fill(apg_pcg64 *state, int kind, int64_t n, int cols, const double *
 #define APG_IMAGE_LOCALIZE 1 /* ImageLocalizationVectorEnv */
 #define APG_POOL_U8 0        /* pool values v -> float32(v) / 255 (_process_imgs_np) */
 #define APG_POOL_F32 1
+#define APG_POOL_U8_TILED 2  /* u8 RGB pools (pool_channels 3) as RGBX, 4 bytes per pixel (the 4th unused), in tiles of
+                                8 x 4 pixels = one 128-byte line, tiles row-major: pixel (y, x) of an image at byte
+                                (y / 4) * ceil(W / 8) * 128 + (y % 4) * 32 + (x / 8) * 128 + (x % 8) * 4 + channel;
+                                an image takes ceil(H / 4) * ceil(W / 8) * 128 bytes.  A
+                                glimpse's tap box then spans ~40 % fewer cache lines than in row-major HWC, and every tap
+                                is one aligned dword.  Same values as APG_POOL_U8 (v -> float32(v) / 255) (ABI 0.4) */
 
 typedef struct apg_image_config {
   int32_t num_envs;
@@ -313,7 +319,7 @@ typedef struct apg_image_config {
   int32_t height, width;      /* image size of the dataset */
   int32_t pool_channels;      /* channels stored in the pool (1 or 3) */
   int32_t channels;           /* observation channels (1 or 3; 1 -> 3 repeats the grey channel) */
-  int32_t pool_dtype;         /* APG_POOL_U8 | APG_POOL_F32 */
+  int32_t pool_dtype;         /* APG_POOL_U8 | APG_POOL_F32 | APG_POOL_U8_TILED */
   int32_t sensor_h, sensor_w; /* sensor_size[0], sensor_size[1] */
   int32_t step_limit;
   int32_t num_classes;

@@ -722,3 +722,43 @@ def test_image_numpy_returned_arrays_are_writable(gpu, snapshot):
         rew[...] = -1
         info["prediction"]["target"][...] = 9
     env.close()
+
+
+@pytest.mark.parametrize("kind,shape,sensor,scale", [("loc", (64, 64, 3), (12, 12), 1.0),
+                                                     ("cls", (33, 29, 3), (6, 6), 1.7),
+                                                     ("loc", (17, 19, 3), (5, 5), 2.0)])
+def test_tiled_rgb_pool_matches_row_major(gpu, monkeypatch, kind, shape, sensor, scale):
+    """RGB u8 pools run as RGBX 8 x 4-pixel tiles (APG_POOL_U8_TILED) by default: every output of reset (the unique
+    sampler's targets included) and of 40 steps across batch changes equals the row-major pool's (APG_IMAGE_TILED=0),
+    which the oracle suites pin."""
+    import torch
+
+    import ap_gym_amd as ap
+    from ap_gym_amd import _native as N
+
+    rng = np.random.default_rng(7)
+    pool = rng.integers(0, 256, (50, *shape), dtype=np.uint8)
+    labels = rng.integers(0, 10, 50)
+    envs = []
+    for tiled in ("1", "0"):
+        monkeypatch.setenv("APG_IMAGE_TILED", tiled)
+        ds = ap.ArrayImageClassificationDataset(pool, labels, 10, 3)
+        cfg = ap.ImagePerceptionConfig(dataset=ds, sensor_size=sensor, sensor_scale=scale, step_limit=16)
+        cls = ap.ImageClassificationVectorEnv if kind == "cls" else ap.ImageLocalizationVectorEnv
+        envs.append(cls(512, cfg, array_backend="torch"))
+    assert envs[0]._cfg.pool_dtype == N.APG_POOL_U8_TILED and envs[1]._cfg.pool_dtype == N.APG_POOL_U8
+    outs = [e.reset(seed=3) for e in envs]
+    for k in outs[0][0]:
+        assert torch.equal(outs[0][0][k], outs[1][0][k]), k
+    arng = np.random.default_rng(2)
+    for t in range(40):
+        a = torch.as_tensor(arng.uniform(-1.5, 1.5, (512, 2)).astype(np.float32), device=gpu)
+        p = torch.as_tensor((arng.standard_normal((512, 10)) if kind == "cls" else arng.uniform(-1, 1, (512, 2)))
+                            .astype(np.float32), device=gpu)
+        r = [e.step({"action": a, "prediction": p}) for e in envs]
+        for k in r[0][0]:
+            assert torch.equal(r[0][0][k], r[1][0][k]), (t, k)
+        assert torch.equal(r[0][1], r[1][1]), t
+    for e in envs:
+        e.check_errors()
+        e.close()

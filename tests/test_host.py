@@ -675,3 +675,23 @@ def test_device_u8_pools_are_padded_for_the_dword_taps():
     assert padded_device_pool_u8(padded) is padded  # already padded: used as is
     sliced = padded_device_pool_u8(torch.zeros(64, dtype=torch.uint8)[:48].view(2, 4, 6, 1))
     assert sliced.untyped_storage().nbytes() == 64  # 16 spare bytes behind the view: kept
+
+
+@pytest.mark.parametrize("h,w", [(64, 64), (33, 29), (5, 6)])
+def test_tiled_rgb_pool_layout(h, w):
+    """APG_POOL_U8_TILED (apgym_capi.h): pixel (y, x) of image m at m * img + (y // 4) * ceil(W/8) * 128 +
+    (y % 4) * 32 + (x // 8) * 128 + (x % 8) * 4 + channel, the 4th byte zero; built here on CPU tensors in chunks."""
+    from ap_gym_amd import _native as N
+    from ap_gym_amd.image_env import device_pool_u8_tiled, tiled_pool_bytes
+
+    rng = np.random.default_rng(h * w)
+    pool = rng.integers(0, 256, (5, h, w, 3), dtype=np.uint8)
+    t = device_pool_u8_tiled(pool, "cpu", chunk=2)
+    img, trow = tiled_pool_bytes(h, w), ((w + 7) // 8) * 128
+    assert t.numel() == 5 * img and t.untyped_storage().nbytes() >= 5 * img + N.APG_U8_POOL_PAD
+    b = t.numpy()
+    m, y, x = np.meshgrid(np.arange(5), np.arange(h), np.arange(w), indexing="ij")
+    off = m * img + (y // 4) * trow + (y % 4) * 32 + (x // 8) * 128 + (x % 8) * 4
+    for ch in range(3):
+        assert np.array_equal(b[off + ch], pool[..., ch])
+    assert not b[off + 3].any()

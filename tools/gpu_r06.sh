@@ -30,7 +30,7 @@ case $1 in
     case $WL in lidar | maze127) REGEX="k_lidar_step|k_maze" ;; *) REGEX='k_image_step|k_glimpse|k_unique' ;; esac
     R=$PWD
     cd /tmp
-    rm -rf $O/pmc_$TAG
+    rm -rf $O/pmc_$TAG && mkdir -p $O/pmc_$TAG
     for C in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES"; do
       D=$O/pmc_$TAG/$(echo $C | cut -d' ' -f1)
       timeout -s KILL 150 rocprofv3 --pmc $C --kernel-include-regex "$REGEX" -d $D -o run \
