@@ -18,7 +18,7 @@ for path in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
             per[key] += float(row["Counter_Value"])
             names[row["Dispatch_Id"]] = row["Kernel_Name"]
     for (disp, cname), v in per.items():
-        k = names[disp].split("(")[0].replace("void ", "")
+        k = names[disp].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         if filt in k:
             acc[k][cname].append(v)
 for k, cs in sorted(acc.items()):
