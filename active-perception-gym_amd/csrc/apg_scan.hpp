@@ -139,6 +139,18 @@ APG_DEV ScanOut scan_runs_result(const Rows &rows, float fpx, float fpy, float f
 // only: SCAN_POINT / SCAN_MULTIPOINT at distance 0 (the first point is p when p is one).  Returns false
 // (the caller runs the general walk) when a crossing turns out to be a lattice point or the segment is
 // collinear with a grid line; the exact orientation decides near-ties as in the general walk.
+#ifndef APG_WALK_INC
+#define APG_WALK_INC 0  // 1: crossing order from the incrementally updated f64 orientation (A/B: noise-level, not kept)
+#endif
+// APG_WALK_INC: the orientation of the next lattice point, O(a, b) = (px - a)(qy - b) - (py - b)(qx - a), is affine
+// in (a, b): O(a + sx, b) = O + sx (py - qy), O(a, b + sy) = O + sy (qx - px).  The walk keeps it in f64 and adds one
+// increment per crossing.  Error bound: coordinates lie in [0, 512] and segments are < 64 long, so every |O| and
+// partial product stays below 2^13 and each f64 operation errs by < 2^-40; the initial value (five operations) plus
+// at most 128 increments (each also carrying the < 2^-47 rounding of its increment) stay below 2^-32 in all.  A
+// magnitude above ORDER_EPS = 2^-30 therefore has the exact sign; below it the exact predicate decides, as the f32
+// filter's undecided band did.
+constexpr double ORDER_EPS = 0x1p-30;
+
 template <class W>
 struct FastWalk {
   float px, py, qx, qy, sxy;
@@ -146,6 +158,9 @@ struct FastWalk {
   W r_c, r_o, r_p;
   bool cur0, cur, bail;
   int n_runs, n_x, na, nb;
+#if APG_WALK_INC
+  double O, DA, DB;  // orientation of lattice point (a, b) (times sx * sy), its increments for a += sx / b += sy
+#endif
 
   // false when the segment runs along a grid line (the general walk's case)
   template <class Rows>
@@ -181,11 +196,23 @@ struct FastWalk {
     n_x = 0, na = 0, nb = 0;  // the first run's entry crossing: lines (na, nb) ahead of it, x-line or not
     sxy = (float)(sx * sy);
     left = bail ? 0 : nxl + nyl;
+#if APG_WALK_INC
+    {
+      const double dpx = fpx, dpy = fpy, dqx = fqx, dqy = fqy, da = (double)a, db = (double)b, s = (double)(sx * sy);
+      O = __dmul_rn(__dsub_rn(__dmul_rn(__dsub_rn(dpx, da), __dsub_rn(dqy, db)),
+                              __dmul_rn(__dsub_rn(dpy, db), __dsub_rn(dqx, da))), s);
+      DA = __dmul_rn(__dsub_rn(dpy, dqy), (double)(sx * sx * sy));  // sx * (py - qy), times sx * sy
+      DB = __dmul_rn(__dsub_rn(dqx, dpx), (double)(sy * sx * sy));  // sy * (qx - px), times sx * sy
+    }
+#endif
     return !bail;
   }
 
   // f32 filter of the crossing order at (a, b): < 0 x-line first, > 0 y-line first, 0 undecided
   APG_DEV int order() const {
+#if APG_WALK_INC
+    return O > ORDER_EPS ? -1 : (O < -ORDER_EPS ? 1 : 0);
+#endif
     const float fa = (float)a, fb = (float)b;
     const float dl = __fmul_rn(__fsub_rn(px, fa), __fsub_rn(qy, fb));
     const float dr = __fmul_rn(__fsub_rn(py, fb), __fsub_rn(qx, fa));
@@ -210,6 +237,9 @@ struct FastWalk {
     const int pa = a, pb = b;
     a += takex ? sx : 0;
     b += takex ? 0 : sy;
+#if APG_WALK_INC
+    O = __dadd_rn(O, takex ? DA : DB);
+#endif
     r_c = takex ? r_c : r_o;
     r_o = takex ? r_o : r_p;
     const int ry = b - vy + 2 * sd;  // unchanged after an x-crossing; consumed a crossing later at the earliest

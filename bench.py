@@ -432,6 +432,8 @@ def run_lidar(args, world, rank, dev):
     ds = (apg.FloorMapDatasetRooms(msize, msize) if w["kind"] == "rooms" else apg.FloorMapDatasetMaze(msize, msize))
 
     def make_local(num_envs, env_offset, **kw):  # kw: packed_outputs=True when gathering
+        if args.array_backend == "numpy":
+            kw["obs_snapshot"] = args.obs_snapshot
         return apg.make_vec(w["env_id"], num_envs=num_envs, lidar_beam_count=beams, dataset=ds, device=dev,
                             array_backend=args.array_backend, env_offset=env_offset, **kw)
 
@@ -567,7 +569,9 @@ def run_lidar(args, world, rank, dev):
             "data": "synthetic (uniform(-1,1) actions/predictions generated on device; maps generated on device)"
                     + ("; array_backend=numpy: host arrays in/out of every step (PCIe included)"
                        if args.array_backend == "numpy" else ""),
-            "config": {"workload": w["env_id"], "array_backend": args.array_backend, "num_envs_per_gpu": n_local,
+            "config": {"workload": w["env_id"], "array_backend": args.array_backend,
+                       "obs_snapshot": args.obs_snapshot if args.array_backend == "numpy" else None,
+                       "num_envs_per_gpu": n_local,
                        "num_envs_total": n_total,
                        "beams": beams, "map": f"{msize}x{msize} {w['kind']}", "max_episode_steps": 100,
                        "reset_ms": reset_ms, "note": w["note"], "gather_ms": gather_ms if senv.gather else None,
@@ -772,6 +776,9 @@ def main():
     ap.add_argument("--array-backend", default="torch", choices=["torch", "numpy"],
                     help="LIDAR workloads: torch = device tensors in/out (the hot path, default); numpy = the "
                          "drop-in default of make_vec (host arrays, one packed D2H copy per step)")
+    ap.add_argument("--obs-snapshot", default="copy", choices=["copy", "shared"],
+                    help="--array-backend numpy: obs['map'] as the caller's own writable copy per step (copy: "
+                         "SyncVectorEnv(copy=True), the default) or one read-only snapshot shared until a reset")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend of multi-rank runs (nccl = RCCL; gloo for rehearsals with "
                          "several ranks on one GPU)")
