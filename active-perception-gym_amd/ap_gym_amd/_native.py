@@ -40,7 +40,6 @@ APG_IMAGE_LOCALIZE = 1
 APG_POOL_U8 = 0
 APG_POOL_F32 = 1
 APG_POOL_U8_TILED = 2  # RGBX in 8 x 4-pixel 128-byte tiles (apgym_capi.h)
-APG_STEP_DEFER_MAP_OBS = 1  # apg_lidar_step_flags: the mass autoreset's map obs from a streaming kernel (apgym_capi.h)
 APG_U8_POOL_PAD = 16  # readable bytes after a u8 image pool (apgym_capi.h)
 APG_DS_CIRCLE_SQUARE = 0
 APG_DS_DOUBLE_CIRCLE_SQUARE = 1
@@ -159,8 +158,6 @@ SYMBOLS = [
                                       ctypes.POINTER(LidarOutputs), _vp]),
     ("apg_lidar_step_profiled", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(LidarState), _vp, _vp,
                                                ctypes.POINTER(LidarOutputs), _vp, _vp, _vp]),
-    ("apg_lidar_step_flags", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(LidarState), _vp, _vp,
-                                            ctypes.POINTER(LidarOutputs), ctypes.c_int, _vp]),
     ("apg_lidar_prefetcher_create", ctypes.c_int, [ctypes.POINTER(LidarConfig), ctypes.POINTER(_vp)]),
     ("apg_lidar_prefetcher_destroy", ctypes.c_int, [_vp]),
     ("apg_lidar_prefetcher_stats", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64)]),

@@ -43,7 +43,6 @@ Two I/O modes (constructor `array_backend`), inputs of either type are accepted:
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Any
 
 import numpy as np
@@ -355,10 +354,6 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         # torch.ops.apgym.lidar_step instead, which capture_step_graph always uses.
         self.use_torch_op = False
         self._c_args = None
-        # the TimeLimit autoreset hint of _launch_step (A/B switch: False never defers, "always" on every call; the
-        # outputs are identical either way)
-        self.defer_map_obs = os.environ.get("APG_DEFER_MAP_OBS", "1") != "0"
-        self._calls = 0  # step calls since reset()
         self._h = t.classes.apgym.LidarEnv(
             [c.num_envs, c.height, c.width, c.map_kind, c.is_static, c.static_map_index, c.beams, c.step_limit,
              c.max_rooms, c.door_width, c.log_stats, c.sparse, c.out_row_bytes, self._prefetcher or 0, c.pool_len,
@@ -517,7 +512,6 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         return out
 
     def _launch_step(self, a_t, p_t):
-        self._calls += 1
         if self.use_torch_op:
             self._step_op(self._h, a_t, p_t)
             return
@@ -525,18 +519,11 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
             import torch
 
             with torch.cuda.device(self._dev):
-                self._calls -= 1
                 return self._launch_step(a_t, p_t)
         if self._c_args is None:  # (the structures' addresses: rebuilt whenever a structure is replaced)
             self._c_args = (N.fast().lidar_step, N.addr(self._cfg), N.addr(self._state), N.addr(self._out))
         fn, cfg, st, out = self._c_args
-        # every env that started its episode at reset() reaches the TimeLimit on the same call, and the next call
-        # autoresets them all (NEXT_STEP): that call's map obs come from a streaming kernel after the step kernel
-        # (apg_lidar_step_flags; outputs identical, only the reset envs are written whatever the hint)
-        lim = self._cfg.step_limit
-        d = self.defer_map_obs
-        flags = N.APG_STEP_DEFER_MAP_OBS if (d == "always" or (d and lim > 0 and self._calls % (lim + 1) == 0)) else 0
-        rc = fn(cfg, st, a_t.data_ptr(), p_t.data_ptr(), out, flags, N.current_stream_ptr(self._dev))
+        rc = fn(cfg, st, a_t.data_ptr(), p_t.data_ptr(), out, N.current_stream_ptr(self._dev))
         if rc:
             N.check(rc, "apg_lidar_step")
 
@@ -603,7 +590,6 @@ class LIDARLocalization2DVectorEnv(VectorEnv):
         if self._streamer is not None:
             self._streamer.before_reset(self, s, use_seed)
         self._ops.lidar_reset(self._h, s if s < 2**63 else s - 2**64, bool(use_seed))
-        self._calls = 0
         if self._streamer is not None:
             self._streamer.after_reset(self)
         self._track_render(None)

@@ -826,35 +826,8 @@ struct StepParams {
   int pretest;  // phase 2a's bounding-box pre-test (rooms: ~1/3 of the beams walk); 0: every beam walks (mazes:
                 // ~98 % of the beams touch a wall, the pre-test only delays them)
   int p4;       // the pre-test reads a 4-row OR table of the windows (built by phase 1's idle waves; step_lds_bytes)
-  int defer_obs;  // APG_STEP_DEFER_MAP_OBS: the autoresets' f32 map obs left to k_map_obs_deferred (after this kernel)
   float range, loss_scale, loss_offset;
 };
-
-// An env's f32 map obs from its occupancy bit rows: bool map / 255 (lidar_localization2d.py:299), threads tid of
-// nt; W % 4 == 0: 4 cells of one row per float4 (one row-word load, non-temporal 16-byte stores)
-APG_DEV void map_obs_from_rows(const uint64_t *rows, int h, int w, int wpr, float *dst, int tid, int nt) {
-  const float wall = 1.0f / 255.0f;
-  const int cells = h * w;
-  if ((w & 3) == 0) {
-    const int q = w >> 2;
-    for (int k4 = tid; k4 < cells / 4; k4 += nt) {
-      const int y = k4 / q, x = (k4 - y * q) * 4;
-      const uint32_t b = (uint32_t)(rows[y * wpr + (x >> 6)] >> (x & 63));
-      typedef float f4 __attribute__((ext_vector_type(4)));
-      f4 v;
-      v.x = (b & 1u) ? wall : 0.0f;
-      v.y = (b & 2u) ? wall : 0.0f;
-      v.z = (b & 4u) ? wall : 0.0f;
-      v.w = (b & 8u) ? wall : 0.0f;
-      __builtin_nontemporal_store(v, reinterpret_cast<f4 *>(dst) + k4);
-    }
-  } else {
-    for (int k = tid; k < cells; k += nt) {
-      const int y = k / w, x = k - y * w;
-      dst[k] = ((rows[y * wpr + (x >> 6)] >> (x & 63)) & 1ULL) ? wall : 0.0f;
-    }
-  }
-}
 
 // ActiveRegressionLogWrapper (active_regression_env.py:131-159): per step |target - prediction| and
 // mean((target - prediction)^2) in float32; at the episode end avg = float(np.mean(list)) (numpy's
@@ -1131,8 +1104,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          if (O.map_obs && !P.defer_obs)
-            bitmap_map_obs<64>(mrow, m, P.w, wpr, O.map_obs + (size_t)e * m * P.w, lane, mrow + words);
+          if (O.map_obs) bitmap_map_obs<64>(mrow, m, P.w, wpr, O.map_obs + (size_t)e * m * P.w, lane, mrow + words);
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();  // mrow is rewritten by the next env
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1325,9 +1297,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
             }
             off = __shfl(incl, 63);
           }
-          if (P.defer_obs) {
-            // written by k_map_obs_deferred after this kernel
-          } else if (O.map_obs && (P.w & 3) == 0) {  // bool map / 255 (lidar_localization2d.py:299), float4 stores
+          if (O.map_obs && (P.w & 3) == 0) {  // bool map / 255 (lidar_localization2d.py:299), float4 stores
             const float wall = 1.0f / 255.0f;
             typedef float f4 __attribute__((ext_vector_type(4)));
             float *mo = O.map_obs + (size_t)e * m * P.w;
@@ -1405,12 +1375,32 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
   if constexpr (kMapObsHere) __syncthreads();
   // map obs of the envs that reset this step: bool map / 255 (lidar_localization2d.py:299), written by
   // the whole workgroup with float4 stores
-  if (kMapObsHere && s_cnt[0] != 0 && O.map_obs && !P.is_static && !P.defer_obs) {
+  if (kMapObsHere && s_cnt[0] != 0 && O.map_obs && !P.is_static) {
+    const float wall = 1.0f / 255.0f;
     const int cells = P.h * P.w, nr = s_cnt[0];
     for (int r = 0; r < nr; r++) {
       const int j = s_rlist[r];
-      map_obs_from_rows(S.occ + (size_t)(base + j) * words, P.h, P.w, P.wpr, O.map_obs + (size_t)(base + j) * cells,
-                        tid, T);
+      const uint64_t *rows = S.occ + (size_t)(base + j) * words;
+      float *dst = O.map_obs + (size_t)(base + j) * cells;
+      if ((P.w & 3) == 0) {  // 4 cells of one row per float4: one row-word load, non-temporal stores
+        const int q = P.w >> 2;
+        for (int k4 = tid; k4 < cells / 4; k4 += T) {
+          const int y = k4 / q, x = (k4 - y * q) * 4;
+          const uint32_t b = (uint32_t)(rows[y * P.wpr + (x >> 6)] >> (x & 63));
+          typedef float f4 __attribute__((ext_vector_type(4)));
+          f4 v;
+          v.x = (b & 1u) ? wall : 0.0f;
+          v.y = (b & 2u) ? wall : 0.0f;
+          v.z = (b & 4u) ? wall : 0.0f;
+          v.w = (b & 8u) ? wall : 0.0f;
+          __builtin_nontemporal_store(v, reinterpret_cast<f4 *>(dst) + k4);
+        }
+      } else {
+        for (int k = tid; k < cells; k += T) {
+          const int y = k / P.w, x = k - y * P.w;
+          dst[k] = ((rows[y * P.wpr + (x >> 6)] >> (x & 63)) & 1ULL) ? wall : 0.0f;
+        }
+      }
     }
   }
   {
@@ -2160,23 +2150,10 @@ __global__ __launch_bounds__(256) void k_episode_stats(StepParams P, const float
   if (len > PW_PTR_MAX_N) log_episode_stats<true>(P, O, e, hist, len);
 }
 
-// APG_STEP_DEFER_MAP_OBS: the f32 map obs of the envs the step kernel just reset (reset_mask), which it left
-// unwritten; one 256-thread workgroup per env (the others exit at once).  A mass autoreset (every env at the
-// TimeLimit) writes 4 * H * W bytes per env: from a streaming kernel at full occupancy instead of behind the
-// generation inside the step kernel, whose one 1024-thread workgroup per CU also has the step phases to run.
-__global__ __launch_bounds__(256) void k_map_obs_deferred(StepParams P, const uint64_t *__restrict__ occ,
-                                                          apg_lidar_outputs O) {
-  const int e = blockIdx.x;
-  if (e >= P.n || !oat(O.reset_mask, P.row, e, 1)) return;
-  map_obs_from_rows(occ + (size_t)e * P.h * P.wpr, P.h, P.w, P.wpr, O.map_obs + (size_t)e * P.h * P.w,
-                    (int)threadIdx.x, 256);
-}
-
 int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *act,
                        const float *pred, const apg_lidar_outputs *out, hipStream_t s, bool fused,
-                       const PfView *pf = nullptr, bool defer_obs = false) {
+                       const PfView *pf = nullptr) {
   StepParams P;
-  P.defer_obs = defer_obs && fused && out->map_obs && out->reset_mask && !cfg->is_static ? 1 : 0;
   P.n = cfg->num_envs;
   P.h = cfg->height;
   P.w = cfg->width;
@@ -2209,14 +2186,9 @@ int launch_step_kernel(const apg_lidar_config *cfg, const apg_lidar_state *st, c
     case 256: rc = launch_step_epb<256>(P, g, st, act, pred, out, s, fused, pf); break;
     default: rc = launch_step_epb<64>(P, g, st, act, pred, out, s, fused, pf); break;
   }
-  if (rc) return rc;
-  if (P.log_stats && P.step_limit > PW_PTR_MAX_N) {
-    hipLaunchKernelGGL(k_episode_stats, dim3(grid_for(P.n, 256)), dim3(256), 0, s, P, st->stats_hist, *out);
-    if ((rc = check_launch("k_episode_stats"))) return rc;
-  }
-  if (!P.defer_obs) return APG_OK;
-  hipLaunchKernelGGL(k_map_obs_deferred, dim3(P.n), dim3(256), 0, s, P, (const uint64_t *)st->occ, *out);
-  return check_launch("k_map_obs_deferred");
+  if (rc || !P.log_stats || P.step_limit <= PW_PTR_MAX_N) return rc;
+  hipLaunchKernelGGL(k_episode_stats, dim3(grid_for(P.n, 256)), dim3(256), 0, s, P, st->stats_hist, *out);
+  return check_launch("k_episode_stats");
 }
 
 // One prefetch batch on the prefetcher's side stream (k_pf_select .. k_pf_paint), after `after` (an event of the
@@ -2491,13 +2463,11 @@ int apg_lidar_reset(const apg_lidar_config *cfg, const apg_lidar_state *st, uint
   return APG_OK;
 }
 
-static int lidar_step(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
-                      const float *prediction, const apg_lidar_outputs *out, apg_stream_t stream, void *ev_begin,
-                      void *ev_end, int flags) {
+int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
+                            const float *prediction, const apg_lidar_outputs *out, apg_stream_t stream,
+                            void *ev_begin, void *ev_end) {
   int rc = validate(cfg);
   if (rc) return rc;
-  if (flags & ~APG_STEP_DEFER_MAP_OBS) return fail(APG_E_INVALID, "unknown step flags");
-  const bool defer = (flags & APG_STEP_DEFER_MAP_OBS) != 0;
   if (!action || !prediction) return fail(APG_E_INVALID, "null action/prediction");
   if (cfg->log_stats && (!st->stats_hist || !out->stats || !out->stats_len))
     return fail(APG_E_INVALID, "log_stats needs stats_hist, stats and stats_len buffers");
@@ -2522,7 +2492,7 @@ static int lidar_step(const apg_lidar_config *cfg, const apg_lidar_state *st, co
   }
   if (ev_begin && hipEventRecord((hipEvent_t)ev_begin, s) != hipSuccess) return fail(APG_E_LAUNCH, "hipEventRecord");
   if (use_pf) {
-    rc = launch_step_kernel(cfg, st, action, prediction, out, s, true, &V, defer);
+    rc = launch_step_kernel(cfg, st, action, prediction, out, s, true, &V);
   } else if (big_rooms(cfg)) {
     // rooms the fused step kernel's LDS generator does not hold (max_rooms > 17, maps > 128): the pending
     // autoresets in k_lidar_reset, then the unfused step kernel (it writes their map obs)
@@ -2538,24 +2508,13 @@ static int lidar_step(const apg_lidar_config *cfg, const apg_lidar_state *st, co
     o2.map_obs = nullptr;  // written by k_maze
     if (rc == APG_OK) rc = launch_step_kernel(cfg, st, action, prediction, &o2, s, false);
   } else {
-    rc = launch_step_kernel(cfg, st, action, prediction, out, s, true, nullptr, defer);
+    rc = launch_step_kernel(cfg, st, action, prediction, out, s, true);
   }
   if (rc == APG_OK && ev_end && hipEventRecord((hipEvent_t)ev_end, s) != hipSuccess)
     return fail(APG_E_LAUNCH, "hipEventRecord");
   if (rc == APG_OK && use_pf && hipEventRecord(p->main_ev[p->c % p->R], s) != hipSuccess)
     return fail(APG_E_LAUNCH, "hipEventRecord (prefetch)");
   return rc;
-}
-
-int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
-                            const float *prediction, const apg_lidar_outputs *out, apg_stream_t stream,
-                            void *ev_begin, void *ev_end) {
-  return lidar_step(cfg, st, action, prediction, out, stream, ev_begin, ev_end, 0);
-}
-
-int apg_lidar_step_flags(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
-                         const float *prediction, const apg_lidar_outputs *out, int flags, apg_stream_t stream) {
-  return lidar_step(cfg, st, action, prediction, out, stream, nullptr, nullptr, flags);
 }
 
 int apg_lidar_prefetcher_create(const apg_lidar_config *cfg, apg_lidar_prefetcher **out) {

@@ -1,6 +1,6 @@
 // apg_pyfast.cpp — CPython METH_FASTCALL entry points for the C-ABI calls made once per env step.
 //
-// The eager step of a vector env is one C-ABI call (apg_lidar_step_flags / apg_image_step / apg_light_dark_step).  Through
+// The eager step of a vector env is one C-ABI call (apg_lidar_step / apg_image_step / apg_light_dark_step).  Through
 // ctypes, marshalling its 6-8 arguments costs ~2.5 us per call (measured in this container: 2.94 us for an
 // apg_image_step that returns at validate(), 0.39 us for a call without arguments), a quarter of the image env's
 // host time per step, and the MNIST step loop is host-bound (10 us of host per 12 us kernel).  These wrappers take
@@ -27,19 +27,17 @@ bool nargs_ok(Py_ssize_t n, Py_ssize_t want, const char *name) {
   return false;
 }
 
-// lidar_step(cfg, state, action, prediction, outputs, flags, stream) -> rc    (apg_lidar_step_flags)
+// lidar_step(cfg, state, action, prediction, outputs, stream) -> rc    (apg_lidar_step)
 PyObject *lidar_step(PyObject *, PyObject *const *args, Py_ssize_t n) {
-  if (!nargs_ok(n, 7, "lidar_step")) return nullptr;
-  static const int w[6] = {0, 1, 2, 3, 4, 6};
+  if (!nargs_ok(n, 6, "lidar_step")) return nullptr;
+  static const int w[6] = {0, 1, 2, 3, 4, 5};
   void *v[6];
   if (!addr_args(args, w, 6, v)) return nullptr;
-  const long flags = PyLong_AsLong(args[5]);
-  if (PyErr_Occurred()) return nullptr;
   int rc;
   Py_BEGIN_ALLOW_THREADS
-  rc = apg_lidar_step_flags(static_cast<const apg_lidar_config *>(v[0]), static_cast<const apg_lidar_state *>(v[1]),
-                            static_cast<const float *>(v[2]), static_cast<const float *>(v[3]),
-                            static_cast<const apg_lidar_outputs *>(v[4]), (int)flags, v[5]);
+  rc = apg_lidar_step(static_cast<const apg_lidar_config *>(v[0]), static_cast<const apg_lidar_state *>(v[1]),
+                      static_cast<const float *>(v[2]), static_cast<const float *>(v[3]),
+                      static_cast<const apg_lidar_outputs *>(v[4]), v[5]);
   Py_END_ALLOW_THREADS
   return PyLong_FromLong(rc);
 }
@@ -78,7 +76,7 @@ PyObject *light_dark_step(PyObject *, PyObject *const *args, Py_ssize_t n) {
 
 PyMethodDef kMethods[] = {
     {"lidar_step", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(lidar_step)), METH_FASTCALL,
-     "apg_lidar_step_flags(cfg, state, action, prediction, outputs, flags, stream) with addresses as ints"},
+     "apg_lidar_step(cfg, state, action, prediction, outputs, stream) with addresses as ints"},
     {"image_step", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(image_step)), METH_FASTCALL,
      "apg_image_step(cfg, state, action, prediction, t, flags, outputs, stream) with addresses as ints"},
     {"light_dark_step", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(light_dark_step)),

@@ -213,15 +213,6 @@ int apg_lidar_step_profiled(const apg_lidar_config *cfg, const apg_lidar_state *
                             const float *prediction, const apg_lidar_outputs *out, apg_stream_t stream,
                             void *ev_begin, void *ev_end);
 
-/* apg_lidar_step with per-call flags (0 = apg_lidar_step; same reference interface,
- * lidar_localization2d.py:317-389 under SyncVectorEnv.step).  APG_STEP_DEFER_MAP_OBS: a hint that many envs
- * auto-reset in this call (every env at the TimeLimit); the f32 map obs of the envs that reset are then written by
- * a streaming kernel after the step kernel instead of inside it.  Outputs are identical either way; needs the
- * reset_mask output (otherwise ignored).  Unknown bits: APG_E_INVALID. */
-#define APG_STEP_DEFER_MAP_OBS 1
-int apg_lidar_step_flags(const apg_lidar_config *cfg, const apg_lidar_state *st, const float *action,
-                         const float *prediction, const apg_lidar_outputs *out, int flags, apg_stream_t stream);
-
 /* ---------------------------------------------------------------- map prefetch (dynamic mazes)
  * The reference builds each sub-env's DataLoader(prefetch=True, prefetch_buffer_size=128): a background thread
  * generates the next maps while the env steps (ap_gym/envs/lidar_localization2d.py:130-131, 296-298;

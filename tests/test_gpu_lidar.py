@@ -869,54 +869,3 @@ def test_numpy_backend_returned_arrays_are_writable(gpu, oracle_mod, snapshot):
             v[...] = -7  # in-place "normalisation" by the caller
         rew[...] = 123.0
     env.close()
-
-
-@pytest.mark.parametrize("case", ["rooms64", "rooms64_packed", "maze21_prefetch", "pool_open"])
-def test_deferred_map_obs_matches_in_kernel(gpu, case):
-    """apg_lidar_step_flags(APG_STEP_DEFER_MAP_OBS): the autoreset envs' map obs written by k_map_obs_deferred after
-    the step kernel equal the step kernel's own (defer_map_obs=False), bit for bit, for every output, whether the
-    hint is right (the TimeLimit mass reset), wrong ("always": steps with no or few resets) or stale (a NaN-delayed
-    env and open-border maps whose early terminations desynchronize the episodes); fused rooms (phase R paint),
-    packed output rows, prefetched mazes (GEN_PF) and pool maps (the phase-0 map-obs pass)."""
-    import torch
-
-    import ap_gym_amd as ap
-    from test_gpu_lidar_pool import random_pool
-
-    limit, n, a_scale = 7, 512, 1.5
-    kw = dict(device=gpu, array_backend="torch", max_episode_steps=limit, log_stats=True)
-    if case.startswith("rooms"):
-        kw.update(dataset=ap.FloorMapDatasetRooms(64, 64), lidar_beam_count=32,
-                  packed_outputs=case.endswith("packed"))
-    elif case == "maze21_prefetch":
-        kw.update(dataset=ap.FloorMapDatasetMaze(21, 21), lidar_beam_count=8, prefetch=True)
-    else:
-        kw.update(dataset=UserFloorMaps(random_pool(32, 40, 40, 7, open_every=2)), lidar_beam_count=16)
-        a_scale = 2.5
-    envs = [ap.LIDARLocalization2DVectorEnv(num_envs=n, **kw) for _ in range(3)]
-    for e, mode in zip(envs, (True, False, "always")):
-        e.defer_map_obs = mode
-        e.reset(seed=77)
-    g = torch.Generator(device=gpu).manual_seed(3)
-    deferred_resets = 0
-    for t in range(4 * (limit + 1) + 2):
-        a = (torch.rand((n, 2), generator=g, device=gpu) * 2 - 1) * a_scale
-        p = torch.rand((n, 2), generator=g, device=gpu) * 2 - 1
-        if t == limit + 2:
-            a[3, 1] = float("nan")  # env 3's step refused: its episode ends one step after the others'
-        for e in envs:
-            e.step({"action": a, "prediction": p})
-        outs = [_torch_outputs(e) for e in envs]
-        for o in outs[1:]:
-            for k in outs[0]:
-                assert torch.equal(outs[0][k], o[k]), (t, k)
-        if envs[0]._calls % (limit + 1) == 0:
-            deferred_resets += int(outs[0]["reset_mask"].sum())
-        if t == limit + 2:
-            for e in envs:
-                with pytest.raises(ValueError, match="NaN values detected in action."):
-                    e.check_errors()
-    assert deferred_resets > n  # the hinted calls did reset envs (the mass resets)
-    for e in envs:
-        e.check_errors()
-        e.close()

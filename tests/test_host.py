@@ -38,12 +38,12 @@ def test_fast_call_module_reaches_the_c_abi():
 
     F = N.fast()
     assert os.path.dirname(F.__file__) == N.LIB_DIR
-    for name, args, cfg, st, out in (("lidar_step", 7, N.LidarConfig(), N.LidarState(), N.LidarOutputs()),
+    for name, args, cfg, st, out in (("lidar_step", 6, N.LidarConfig(), N.LidarState(), N.LidarOutputs()),
                                      ("image_step", 8, N.ImageConfig(), N.ImageState(), N.ImageOutputs()),
                                      ("light_dark_step", 6, N.LightDarkConfig(), N.LightDarkState(),
                                       N.LightDarkOutputs())):
         fn = getattr(F, name)
-        tail = {6: [N.addr(out), 0], 7: [N.addr(out), N.APG_STEP_DEFER_MAP_OBS, 0], 8: [3, 0, N.addr(out), 0]}[args]
+        tail = [N.addr(out), 0] if args == 6 else [3, 0, N.addr(out), 0]
         assert fn(N.addr(cfg), N.addr(st), 0, 0, *tail) == N.APG_E_INVALID, name
         assert N.lib().apg_last_error()  # the C ABI's own message
         with pytest.raises(TypeError):
@@ -51,9 +51,8 @@ def test_fast_call_module_reaches_the_c_abi():
         with pytest.raises(TypeError):
             fn(N.addr(cfg), N.addr(st), "x", 0, *tail)
         # the same validation result as the ctypes entry point
-        c_fn = getattr(N.lib(), "apg_" + name + ("_flags" if args == 7 else ""))
-        c_tail = {6: [ctypes.byref(out), None], 7: [ctypes.byref(out), N.APG_STEP_DEFER_MAP_OBS, None],
-                  8: [3, 0, ctypes.byref(out), None]}[args]
+        c_fn = getattr(N.lib(), "apg_" + name)
+        c_tail = [ctypes.byref(out), None] if args == 6 else [3, 0, ctypes.byref(out), None]
         assert c_fn(ctypes.byref(cfg), ctypes.byref(st), None, None, *c_tail) == N.APG_E_INVALID
 
 
