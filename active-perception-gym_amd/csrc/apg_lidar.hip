@@ -871,14 +871,23 @@ APG_DEV void log_episode_stats(const StepParams &P, const apg_lidar_outputs &O, 
 __device__ unsigned long long g_step_prof[16384][16];
 #define STEP_MARK(k) \
   if (threadIdx.x == 0 && blockIdx.x < 16384) g_step_prof[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();
+// per wave (lane 0): [0] phase R1 (generation) done, [1] phase R2 (paint) done
+__device__ unsigned long long g_step_prof_w[16384][16][2];
+#define STEP_MARK_W(k)                                    \
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 16384) \
+    g_step_prof_w[blockIdx.x][threadIdx.x >> 6][k] = __builtin_amdgcn_s_memrealtime();
 #else
 #define STEP_MARK(k)
+#define STEP_MARK_W(k)
 #endif
 #ifndef APG_SLIDE_SPLIT
 #define APG_SLIDE_SPLIT 1  // phase 1: second slide scan on the idle waves (0: both on the env's lane; A/B 36.4 -> 35.8 us)
 #endif
 #ifndef APG_MAPOBS_NT
 #define APG_MAPOBS_NT 1  // the fused rooms autoreset's f32 map obs as non-temporal 16-byte stores (0: plain; A/B knob)
+#endif
+#ifndef APG_R2_LANES
+#define APG_R2_LANES 1  // rooms autoreset paint: primitives via v_readlane (scalar decode); 0: per-lane LDS reads (A/B)
 #endif
 #ifndef APG_STEP_MIN_WAVES
 #define APG_STEP_MIN_WAVES 4  // keep k_lidar_step at <= 128 VGPRs: 4 waves per SIMD
@@ -914,6 +923,33 @@ APG_DEV uint64_t rooms_row_word(const uint32_t *pr, int st, int m, int y, int k)
   for (int i = 0; i < nd; i++) {
     const Door d = RoomsFmt<false>::door_of(pr[(17 + i) * st]);
     if (y >= d.r0 && y < d.r0 + d.hh) v &= ~span_mask(d.c0, d.ww, k);
+  }
+  return v;
+}
+
+// rooms_row_word with the env's primitives held one per lane (prv = pr[lane * st] on lanes 0 .. ROOMS_PRIM_WORDS - 1)
+// and taken into scalar registers with v_readlane: the primitives' decode and span masks run on the scalar unit,
+// and each lane keeps a range compare and a masked OR / AND per primitive (the reset step's paint is VALU-bound
+// with four waves per SIMD)
+APG_DEV uint64_t rooms_row_word_lanes(uint32_t prv, int m, int y, int k) {
+  const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)prv, 0);
+  const int nw = (int)(p0 & 255u), nd = (int)(p0 >> 8);
+  const uint64_t full = span_mask(0, m, k), side = span_mask(0, 1, k) | span_mask(m - 1, 1, k);
+  uint64_t v = (y == 0 || y == m - 1) ? full : side;
+  for (int i = 0; i < nw; i++) {
+    const Wall wl = RoomsFmt<false>::wall_of((uint32_t)__builtin_amdgcn_readlane((int)prv, 1 + i));
+    if (wl.vertical) {
+      const uint64_t bit = (wl.fixed >> 6) == k ? 1ULL << (wl.fixed & 63) : 0ULL;
+      if (y >= wl.start && y < wl.start + wl.len) v |= bit;
+    } else {
+      const uint64_t sm = span_mask(wl.start, wl.len, k);
+      if (y == wl.fixed) v |= sm;
+    }
+  }
+  for (int i = 0; i < nd; i++) {
+    const Door d = RoomsFmt<false>::door_of((uint32_t)__builtin_amdgcn_readlane((int)prv, 17 + i));
+    const uint64_t keep = ~span_mask(d.c0, d.ww, k);
+    if (y >= d.r0 && y < d.r0 + d.hh) v &= keep;
   }
   return v;
 }
@@ -1246,6 +1282,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         STEP_MARK(10)  // (wave 0's view)
+        STEP_MARK_W(0)
         // R2: each wave paints the maps of its own envs one after the other, lane = row: occupancy rows
         // out (coalesced), the f32 map obs from the wave's row copy in LDS, the free-cell count and the
         // start cell (place_start: the pick-th free cell in row-major order, drawn by the env's lane)
@@ -1255,6 +1292,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           if (!__shfl((int)pend, j)) continue;  // wave-uniform
           const int el = j * W + wave, e = base + el;
           const uint32_t *pr = s_prims + el;
+          const uint32_t prv = lane < ROOMS_PRIM_WORDS ? pr[lane * EPB] : 0u;
           uint64_t *dst = S.occ + (size_t)e * words;
           int fr[2] = {0, 0};
           uint64_t rw[2][2] = {{0ULL, 0ULL}, {0ULL, 0ULL}};
@@ -1264,7 +1302,11 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
             if (y < m) {
               int occ = 0;
               for (int k = 0; k < wpr; k++) {
+#if APG_R2_LANES
+                const uint64_t v = rooms_row_word_lanes(prv, m, y, k);
+#else
                 const uint64_t v = rooms_row_word(pr, EPB, m, y, k);
+#endif
                 rw[rr][k] = v;
                 dst[y * wpr + k] = v;
                 mrow[y * 2 + k] = v;
@@ -1325,6 +1367,7 @@ __global__ __launch_bounds__(4 * EPB, APG_STEP_MIN_WAVES) void k_lidar_step(Step
           }
         }
         STEP_MARK(11)
+        STEP_MARK_W(1)
         // R3: the env's lane finishes its reset (lidar_localization2d.py:293-315 tail)
         if (pend) {
           const uint32_t sc = s_start[my_el];
@@ -2670,6 +2713,9 @@ int apg_rng_draws(const uint64_t *seeds, int m, int kind, int64_t a, int64_t b, 
 #ifdef APG_STEP_PROFILE
 int apg_debug_step_profile(void *dst, size_t bytes) {
   return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_step_prof), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+int apg_debug_step_profile_waves(void *dst, size_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_step_prof_w), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
 }  // extern "C"

@@ -2,7 +2,7 @@
 # Reset-step A/B at cfg 2 (on the GPU box): per variant and round, the bench line's synchronized episode (100 steps +
 # the NEXT_STEP autoreset step) under a rocprof kernel trace: its reset_step_kernel_ms (hipEvents around the step
 # call: every launch of the reset step) and env-steps/s, and the traced k_lidar_step / k_map_obs_deferred durations.
-#   bash tools/ab_reset_step.sh <default|env:NAME=VALUE>...       outputs under gpurun_out/ab/
+#   bash tools/ab_reset_step.sh <default|env:NAME=VALUE|variant.so>...       outputs under gpurun_out/ab/
 set -o pipefail
 R=$PWD
 O=$R/gpurun_out/ab
@@ -10,9 +10,11 @@ mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 for round in 1 2; do
   for V in "$@"; do
+    unset APG_LIBRARY
     case "$V" in
       default) tag=reset_default_$round; ENVSET="" ;;
       env:*) ENVSET=${V#env:}; tag=reset_$(echo $ENVSET | tr '=' '_')_$round ;;
+      *) export APG_LIBRARY=$R/$V; ENVSET=""; tag=reset_$(basename $V .so)_$round ;;
     esac
     rm -rf $O/kt_$tag
     [ -n "$ENVSET" ] && export "$ENVSET"

@@ -70,6 +70,21 @@ for rep in range(3):
         for nm, k0, k1 in (("  launch -> R barrier", 0, 8), ("  R barrier -> stored", 8, 9), ("  stored -> barrier", 9, 1)):
             d = us(b[:, k1] - b[:, k0])
             print(f"   {nm:22s} p50 {np.percentile(d, 50):6.2f}  p90 {np.percentile(d, 90):6.2f}")
+    if b[:, 10].any() and hasattr(N.lib(), "apg_debug_step_profile_waves"):  # per-wave R1 / R2 ends (lane 0)
+        wv = np.zeros((16384, 16, 2), np.uint64)
+        N.lib().apg_debug_step_profile_waves.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        assert N.lib().apg_debug_step_profile_waves(wv.ctypes.data, wv.nbytes) == 0
+        w = wv[:nwg].astype(np.int64)
+        r0 = b[:, 8][:, None]
+        g1 = us(w[:, :, 0] - r0)  # R start -> wave's generation done
+        p2 = us(w[:, :, 1] - w[:, :, 0])  # wave's paint
+        e2 = us(w[:, :, 1] - r0)  # R start -> wave's paint done
+        for nm, d in (("R1 generate, per wave", g1), ("R2 paint, per wave", p2), ("R start -> R2 done, per wave", e2)):
+            print(f"   {nm:30s} all-wave p50 {np.percentile(d, 50):6.1f} p90 {np.percentile(d, 90):6.1f}  "
+                  f"per-WG max: p50 {np.percentile(d.max(1), 50):6.1f} max {d.max():6.1f}")
+        slow = np.argmax(e2, axis=1)
+        print(f"   slowest wave of a WG: its R1 p50 {np.percentile(g1[np.arange(nwg), slow], 50):.1f}, "
+              f"its R2 p50 {np.percentile(p2[np.arange(nwg), slow], 50):.1f} us")
     names = ["stage windows", "move (phase 1)", "pre-test (2a)", "walks (2b)", "store"]
     for k in range(5):
         d = us(b[:, k + 1] - b[:, k])
