@@ -1321,6 +1321,12 @@ __global__ __launch_bounds__(UNIQ_THREADS) void k_unique(GlimpseGeo g, const voi
 // results are combined in the recursion's post order through a small shifting stack (the combine
 // counts come from the host, UniqPlan).  Per-point minima are kept on the pair TOTALS and divided
 // by L at the end: rounding x / L is monotone, so min(x) / L == min(x / L) bit for bit.
+#ifndef APG_UQ_STAGED
+X
+#endif
+#ifndef APG_UQ_WAVES
+#define APG_UQ_WAVES 3  // k_unique_blk's occupancy bound (waves per SIMD; A/B knob)
+#endif
 constexpr int UQ_TA = 32, UQ_TB = 64, UQ_THREADS = 256, UQ_MAX_LEAVES = 16, UQ_MAX_L = 2048;
 struct UniqPlan {
   int nleaves, ls;  // leaves of the pairwise sum over L; LDS row stride (>= longest leaf, ls % 8 == 4)
@@ -1331,7 +1337,7 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 template <int SD>
-__global__ __launch_bounds__(UQ_THREADS, 3) void k_unique_blk(GlimpseGeo g, const void *pool, const int64_t *index,
+__global__ __launch_bounds__(UQ_THREADS, APG_UQ_WAVES) void k_unique_blk(GlimpseGeo g, const void *pool, const int64_t *index,
                                                            const double *grid, int n, int P, int k, int32_t *top_k,
                                                            float *uniq, float *scratch, UniqPlan plan) {
   extern __shared__ float s_dyn[];  // [UQ_TA + UQ_TB][ls] leaf tiles, then s_min[P]
@@ -1437,6 +1443,20 @@ __global__ __launch_bounds__(UQ_THREADS, 3) void k_unique_blk(GlimpseGeo g, cons
               bv[j][2] = hi4.xy;
               bv[j][3] = hi4.zw;
             }
+#if APG_UQ_STAGED
+            // per column pair h: the 8 pairs' differences, then their squares, then the adds (independent
+            // chains side by side instead of sub -> mul -> add back to back on one temporary)
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+              f2 d[8];
+#pragma unroll
+              for (int q = 0; q < 8; q++) d[q] = bv[q & 3][h] - av[q >> 2][h];
+#pragma unroll
+              for (int q = 0; q < 8; q++) d[q] = d[q] * d[q];
+#pragma unroll
+              for (int q = 0; q < 8; q++) acc[q >> 2][q & 3][h] = acc[q >> 2][q & 3][h] + d[q];
+            }
+#else
 #pragma unroll
             for (int i = 0; i < 2; i++)
 #pragma unroll
@@ -1446,6 +1466,7 @@ __global__ __launch_bounds__(UQ_THREADS, 3) void k_unique_blk(GlimpseGeo g, cons
                   const f2 d = bv[j][h] - av[i][h];
                   acc[i][j][h] = acc[i][j][h] + d * d;
                 }
+#endif
           }
           // leaf sums: ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) (0 for a leaf shorter than 8), in-order tail
           float res[8];
