@@ -1322,7 +1322,7 @@ __global__ __launch_bounds__(UNIQ_THREADS) void k_unique(GlimpseGeo g, const voi
 // counts come from the host, UniqPlan).  Per-point minima are kept on the pair TOTALS and divided
 // by L at the end: rounding x / L is monotone, so min(x) / L == min(x / L) bit for bit.
 #ifndef APG_UQ_STAGED
-X
+#define APG_UQ_STAGED 1  // k_unique_blk's pair loop in stage order (0: per pair; A/B 189.5 -> 187.6 ms, ab/unique_staged.txt)
 #endif
 #ifndef APG_UQ_WAVES
 #define APG_UQ_WAVES 3  // k_unique_blk's occupancy bound (waves per SIMD; A/B knob)
