@@ -23,6 +23,12 @@ SOURCES = ["apg_lidar.hip", "apg_image.hip", "apg_circle_square.hip", "apg_light
 HEADERS = ["apg_device.hpp", "apg_maps.hpp", "apg_scan.hpp", "apg_rng.hpp", "apg_host.hpp", "apg_pairwise.hpp",
            "apg_ziggurat.hpp", "apg_maze.hpp", "apg_binom_table.hpp"]
 
+# per-source compiler options, each measured: k_lidar_step's latency-bound phases schedule better under the
+# memory-clause strategy (same-box A/B over six interleaved pairs of 300-step runs: median 32.53 -> 32.35 us, mean
+# 36.27 -> 36.05 us, profiles/r06/ab/lidar_sched_strategy.txt; max-ilp measured slower).  bench.kernel_source_sha
+# hashes these with the sources, so tables collected under other options are not used.
+SOURCE_FLAGS = {"apg_lidar.hip": ("-mllvm", "-amdgpu-sched-strategy=max-memory-clause")}
+
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = [
     "--offload-arch=gfx950",
@@ -149,10 +155,11 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str |
         os.makedirs(sdir, exist_ok=True)
         obj = os.path.join(sdir, os.path.splitext(src)[0] + ".o")
         objs.append(obj)
-        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(os.path.getmtime(d) for d in _closure(spath)):
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(
+                os.path.getmtime(d) for d in _closure(spath) + [os.path.abspath(__file__)]):
             continue
         tmp = f"{obj}.{os.getpid()}.tmp"  # concurrent builds never share a temporary
-        cmd = [HIPCC, *compile_flags, *flags, "-I", INCLUDE, "-c", "-o", tmp, spath]
+        cmd = [HIPCC, *compile_flags, *SOURCE_FLAGS.get(src, ()), *flags, "-I", INCLUDE, "-c", "-o", tmp, spath]
         if verbose:
             cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
             print(" ".join(cmd))

@@ -312,14 +312,19 @@ def kernel_sources(family: str) -> list[str]:
 
 def kernel_source_sha(family: str) -> str:
     """Hash of the kernel sources a PMC table was collected with (a stale table is never used): the translation
-    unit and every header it includes."""
+    unit, every header it includes and its per-source compiler options (build.SOURCE_FLAGS)."""
     import hashlib
+
+    import build  # active-perception-gym_amd/build.py: the per-source compiler options
 
     h = hashlib.sha256()
     for path in kernel_sources(family):
         h.update(os.path.relpath(path, ROOT).encode())
         with open(path, "rb") as fh:
             h.update(fh.read())
+    opts = build.SOURCE_FLAGS.get(KERNEL_ROOTS[family])
+    if opts:  # (a family compiled without extra options keeps its sources-only hash)
+        h.update(" ".join(opts).encode())
     return h.hexdigest()[:16]
 
 
